@@ -1,0 +1,359 @@
+// Python binding of the gfx950 kernels: adapts at::Tensor arguments to the extern "C" launchers in
+// csrc/kernels/*.hip and launches them on torch's current HIP stream (so they order with hipBLASLt
+// GEMMs and RCCL work issued by torch, and are captured by torch.cuda.graphs).
+//
+// Every entry point validates device, dtype, contiguity and the shape assumptions of its kernel on
+// the host before launching -- a wrong shape must be a Python exception, never a GPU fault.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+extern "C" {
+int ftc_rmsnorm_fwd(const void* x, const void* res, const void* w, void* h_out, void* y, float* rstd, int rows, int d,
+                    float eps, hipStream_t stream);
+int ftc_rmsnorm_bwd_grid(int rows);
+int ftc_rmsnorm_bwd(const void* dy, const void* h, const void* w, const float* rstd, const void* dres, void* dx,
+                    float* dw_part, float* dw, int rows, int d, hipStream_t stream);
+int ftc_rope(void* qkv, const float* cosT, const float* sinT, const int* positions, long long rows, int ld,
+             int n_rot_heads, int head_dim, int seq_len, int inverse, hipStream_t stream);
+int ftc_swiglu_fwd(const void* gu, void* a, long long rows, int F, hipStream_t stream);
+int ftc_swiglu_bwd(const void* da, const void* gu, void* dgu, long long rows, int F, hipStream_t stream);
+int ftc_ce_fwd_bwd(void* logits, const long long* labels, float* loss, float* lse, long long rows, int V, long long ld,
+                   float gscale, long long ignore_index, hipStream_t stream);
+int ftc_adamw(void* param_bf16, float* master, float* m, float* v, const void* grad, int grad_is_fp32, long long n,
+              float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, const float* gscale,
+              hipStream_t stream);
+int ftc_sumsq_partials();
+int ftc_sumsq(const void* x, int is_fp32, long long n, float* partial, float* out, float* coef, float max_norm,
+              float scale, hipStream_t stream);
+int ftc_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H, int KV, int D,
+                  long long q_row_stride, long long kv_row_stride, long long o_row_stride, float scale, int causal,
+                  int window, hipStream_t stream);
+int ftc_flash_bwd_workspace(int B, int S, int H, int D, long long* bytes);
+int ftc_flash_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
+                  void* dq, void* dk, void* dv, void* workspace, int B, int S, int H, int KV, int D,
+                  long long q_row_stride, long long kv_row_stride, long long o_row_stride, long long dq_row_stride,
+                  long long dkv_row_stride, float scale, int causal, int window, hipStream_t stream);
+int ftc_nf4_dequant(const uint8_t* packed, const uint8_t* absmax_q, const float* absmax_scale, float absmax_offset,
+                    void* out, long long n, int block, int block2, hipStream_t stream);
+int ftc_nf4_quant(const void* w, uint8_t* packed, float* absmax, long long n, int block, hipStream_t stream);
+int ftc_nf4_gemm(const void* x, const uint8_t* packed, const uint8_t* absmax_q, const float* absmax_scale,
+                 float absmax_offset, void* y, int M, int N, int K, int block, int block2, hipStream_t stream);
+int ftc_lora_merge(void* w, const void* a, const void* b, int out_f, int in_f, int r, int seg_rows, float scale,
+                   hipStream_t stream);
+}
+
+namespace {
+
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+inline void check(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, what, " failed with code ", rc, (rc > 0 ? std::string(": ") + hipGetErrorString((hipError_t)rc) : std::string(" (shape/argument rejected)")));
+}
+
+inline void need(const at::Tensor& t, at::ScalarType dt, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+}
+
+inline void need_rows(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.dim() == 2, name, " must be 2-D");
+  TORCH_CHECK(t.stride(1) == 1 && t.stride(0) == t.size(1), name, " must be contiguous");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
+// ---------------- RMSNorm ----------------
+std::vector<at::Tensor> rmsnorm_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& res, const at::Tensor& w,
+                                    double eps) {
+  need(x, at::kBFloat16, "x");
+  need(w, at::kBFloat16, "w");
+  need_rows(x, "x");
+  const int rows = (int)x.size(0), d = (int)x.size(1);
+  TORCH_CHECK(w.numel() == d && w.is_contiguous(), "w must be [d] contiguous");
+  TORCH_CHECK(d % 8 == 0 && d <= 8192, "rmsnorm: d must be a multiple of 8 and <= 8192");
+  auto y = at::empty_like(x);
+  auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
+  at::Tensor h;
+  const void* rp = nullptr;
+  if (res.has_value()) {
+    need(*res, at::kBFloat16, "res");
+    need_rows(*res, "res");
+    TORCH_CHECK(res->sizes() == x.sizes(), "res shape mismatch");
+    h = at::empty_like(x);
+    rp = res->data_ptr();
+  } else {
+    h = x;
+  }
+  check(ftc_rmsnorm_fwd(x.data_ptr(), rp, w.data_ptr(), rp ? h.data_ptr() : nullptr, y.data_ptr(),
+                        rstd.data_ptr<float>(), rows, d, (float)eps, cur_stream()),
+        "rmsnorm_fwd");
+  return {y, rstd, h};
+}
+
+std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Tensor& w,
+                                    const at::Tensor& rstd, const c10::optional<at::Tensor>& dres, bool need_dw) {
+  need(dy, at::kBFloat16, "dy");
+  need(h, at::kBFloat16, "h");
+  need(w, at::kBFloat16, "w");
+  need(rstd, at::kFloat, "rstd");
+  need_rows(dy, "dy");
+  need_rows(h, "h");
+  TORCH_CHECK(dy.sizes() == h.sizes(), "dy/h shape mismatch");
+  const int rows = (int)h.size(0), d = (int)h.size(1);
+  TORCH_CHECK(rstd.numel() == rows && w.numel() == d, "rstd/w shape mismatch");
+  TORCH_CHECK(d % 8 == 0 && d <= 8192, "rmsnorm: bad d");
+  const void* drp = nullptr;
+  if (dres.has_value()) {
+    need(*dres, at::kBFloat16, "dres");
+    need_rows(*dres, "dres");
+    TORCH_CHECK(dres->sizes() == h.sizes(), "dres shape mismatch");
+    drp = dres->data_ptr();
+  }
+  auto dx = at::empty_like(h);
+  at::Tensor dw, part;
+  if (need_dw) {
+    const int g = ftc_rmsnorm_bwd_grid(rows);
+    part = at::empty({g, d}, h.options().dtype(at::kFloat));
+    dw = at::empty({d}, h.options().dtype(at::kFloat));
+  }
+  check(ftc_rmsnorm_bwd(dy.data_ptr(), h.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), drp, dx.data_ptr(),
+                        need_dw ? part.data_ptr<float>() : nullptr, need_dw ? dw.data_ptr<float>() : nullptr, rows, d,
+                        cur_stream()),
+        "rmsnorm_bwd");
+  if (need_dw) return {dx, dw};
+  return {dx};
+}
+
+// ---------------- RoPE (in place) ----------------
+void rope_(at::Tensor& qkv, const at::Tensor& cos, const at::Tensor& sin, const c10::optional<at::Tensor>& positions,
+           int64_t n_rot_heads, int64_t head_dim, int64_t seq_len, bool inverse) {
+  need(qkv, at::kBFloat16, "qkv");
+  need(cos, at::kFloat, "cos");
+  need(sin, at::kFloat, "sin");
+  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1, "qkv must be 2-D with unit column stride");
+  TORCH_CHECK(head_dim % 16 == 0, "rope: head_dim must be a multiple of 16");
+  TORCH_CHECK(qkv.size(1) >= n_rot_heads * head_dim, "rope: qkv too narrow");
+  TORCH_CHECK(qkv.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(qkv.data_ptr()) % 16 == 0, "rope: alignment");
+  TORCH_CHECK(cos.is_contiguous() && sin.is_contiguous() && cos.size(1) == head_dim / 2, "rope: tables [P, D/2]");
+  const int* pp = nullptr;
+  const long long rows = qkv.size(0);
+  if (positions.has_value()) {
+    need(*positions, at::kInt, "positions");
+    TORCH_CHECK(positions->numel() == rows, "positions length");
+    auto mx = positions->max().item<int>();
+    TORCH_CHECK(mx < cos.size(0), "rope: position beyond table");
+    pp = positions->data_ptr<int>();
+  } else {
+    TORCH_CHECK(seq_len <= cos.size(0), "rope: seq_len beyond table");
+  }
+  check(ftc_rope(qkv.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(), pp, rows, (int)qkv.stride(0),
+                 (int)n_rot_heads, (int)head_dim, (int)seq_len, inverse ? 1 : 0, cur_stream()),
+        "rope");
+}
+
+// ---------------- SwiGLU ----------------
+at::Tensor swiglu_fwd(const at::Tensor& gu) {
+  need(gu, at::kBFloat16, "gu");
+  need_rows(gu, "gu");
+  const long long rows = gu.size(0);
+  const int F = (int)(gu.size(1) / 2);
+  TORCH_CHECK(gu.size(1) % 16 == 0, "swiglu: 2F must be a multiple of 16");
+  auto a = at::empty({rows, F}, gu.options());
+  check(ftc_swiglu_fwd(gu.data_ptr(), a.data_ptr(), rows, F, cur_stream()), "swiglu_fwd");
+  return a;
+}
+
+at::Tensor swiglu_bwd(const at::Tensor& da, const at::Tensor& gu) {
+  need(da, at::kBFloat16, "da");
+  need(gu, at::kBFloat16, "gu");
+  need_rows(da, "da");
+  need_rows(gu, "gu");
+  TORCH_CHECK(da.size(0) == gu.size(0) && gu.size(1) == 2 * da.size(1), "swiglu_bwd shapes");
+  auto dgu = at::empty_like(gu);
+  check(ftc_swiglu_bwd(da.data_ptr(), gu.data_ptr(), dgu.data_ptr(), gu.size(0), (int)da.size(1), cur_stream()),
+        "swiglu_bwd");
+  return dgu;
+}
+
+// ---------------- cross entropy (in place on logits) ----------------
+at::Tensor ce_fwd_bwd_(at::Tensor& logits, const at::Tensor& labels, double gscale, int64_t ignore_index) {
+  need(logits, at::kBFloat16, "logits");
+  need(labels, at::kLong, "labels");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be 2-D row-major");
+  TORCH_CHECK(labels.numel() == logits.size(0) && labels.is_contiguous(), "labels length");
+  auto loss = at::empty({logits.size(0)}, logits.options().dtype(at::kFloat));
+  check(ftc_ce_fwd_bwd(logits.data_ptr(), (const long long*)labels.data_ptr<int64_t>(), loss.data_ptr<float>(), nullptr, logits.size(0),
+                       (int)logits.size(1), logits.stride(0), (float)gscale, ignore_index, cur_stream()),
+        "ce_fwd_bwd");
+  return loss;
+}
+
+// ---------------- AdamW / grad norm ----------------
+void adamw_(const c10::optional<at::Tensor>& param, at::Tensor& master, at::Tensor& m, at::Tensor& v,
+            const at::Tensor& grad, double lr, double b1, double b2, double eps, double wd, int64_t step,
+            const c10::optional<at::Tensor>& gscale) {
+  need(master, at::kFloat, "master");
+  need(m, at::kFloat, "m");
+  need(v, at::kFloat, "v");
+  TORCH_CHECK(master.is_contiguous() && m.is_contiguous() && v.is_contiguous() && grad.is_contiguous(),
+              "adamw: flat contiguous buffers required");
+  const long long n = master.numel();
+  TORCH_CHECK(m.numel() == n && v.numel() == n && grad.numel() == n, "adamw: size mismatch");
+  TORCH_CHECK(grad.scalar_type() == at::kFloat || grad.scalar_type() == at::kBFloat16, "adamw: grad dtype");
+  void* pp = nullptr;
+  if (param.has_value()) {
+    need(*param, at::kBFloat16, "param");
+    TORCH_CHECK(param->is_contiguous() && param->numel() == n, "adamw: param size");
+    pp = param->data_ptr();
+  }
+  const float* gs = nullptr;
+  if (gscale.has_value()) {
+    need(*gscale, at::kFloat, "gscale");
+    gs = gscale->data_ptr<float>();
+  }
+  const double bc1 = 1.0 - std::pow(b1, (double)step);
+  const double bc2 = 1.0 - std::pow(b2, (double)step);
+  check(ftc_adamw(pp, master.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), grad.data_ptr(),
+                  grad.scalar_type() == at::kFloat, n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd,
+                  (float)bc1, (float)bc2, gs, cur_stream()),
+        "adamw");
+}
+
+// returns [sumsq, coef] (fp32, on device): coef = scale * min(1, max_norm/||scale*g||)
+at::Tensor grad_sumsq(const at::Tensor& g, double max_norm, double scale) {
+  TORCH_CHECK(g.is_cuda() && g.is_contiguous(), "grad_sumsq: contiguous GPU tensor");
+  TORCH_CHECK(g.scalar_type() == at::kFloat || g.scalar_type() == at::kBFloat16, "grad_sumsq: dtype");
+  auto part = at::empty({ftc_sumsq_partials()}, g.options().dtype(at::kFloat));
+  auto out = at::empty({2}, g.options().dtype(at::kFloat));
+  check(ftc_sumsq(g.data_ptr(), g.scalar_type() == at::kFloat, g.numel(), part.data_ptr<float>(),
+                  out.data_ptr<float>(), out.data_ptr<float>() + 1, (float)max_norm, (float)scale, cur_stream()),
+        "grad_sumsq");
+  return out;
+}
+
+// ---------------- flash attention ----------------
+// q: [B*S, >=H*D] view (row stride q_rs), k/v: [B*S, >=KV*D] views; all bf16 with unit column stride.
+std::vector<at::Tensor> flash_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, int64_t B, int64_t S,
+                                  int64_t H, int64_t KV, int64_t D, double scale, bool causal, int64_t window) {
+  need(q, at::kBFloat16, "q");
+  need(k, at::kBFloat16, "k");
+  need(v, at::kBFloat16, "v");
+  TORCH_CHECK(q.dim() == 2 && k.dim() == 2 && v.dim() == 2, "flash_fwd: 2-D row views");
+  TORCH_CHECK(q.stride(1) == 1 && k.stride(1) == 1 && v.stride(1) == 1, "flash_fwd: unit column stride");
+  TORCH_CHECK(q.size(0) == B * S && k.size(0) == B * S && v.size(0) == B * S, "flash_fwd: rows != B*S");
+  TORCH_CHECK(q.size(1) >= H * D && k.size(1) >= KV * D && v.size(1) >= KV * D, "flash_fwd: width");
+  TORCH_CHECK(k.stride(0) == v.stride(0), "flash_fwd: k/v strides must match");
+  TORCH_CHECK(D == 128 || D == 64, "flash_fwd: head_dim 64 or 128");
+  TORCH_CHECK(H % KV == 0, "flash_fwd: H % KV");
+  TORCH_CHECK(S % 64 == 0, "flash_fwd: S must be a multiple of 64");
+  TORCH_CHECK(q.stride(0) % 8 == 0 && k.stride(0) % 8 == 0, "flash_fwd: row strides must be 16B multiples");
+  auto o = at::empty({B * S, H * D}, q.options());
+  auto lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
+  check(ftc_flash_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), (int)B, (int)S,
+                      (int)H, (int)KV, (int)D, q.stride(0), k.stride(0), o.stride(0), (float)scale, causal ? 1 : 0,
+                      (int)window, cur_stream()),
+        "flash_fwd");
+  return {o, lse};
+}
+
+// writes dq/dk/dv into the given views (packed dqkv buffer)
+void flash_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
+               const at::Tensor& dout, const at::Tensor& lse, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv,
+               int64_t B, int64_t S, int64_t H, int64_t KV, int64_t D, double scale, bool causal, int64_t window) {
+  for (auto* t : {&q, &k, &v, &o, &dout}) need(*t, at::kBFloat16, "flash_bwd input");
+  need(lse, at::kFloat, "lse");
+  TORCH_CHECK(D == 128 || D == 64, "flash_bwd: head_dim");
+  TORCH_CHECK(S % 64 == 0 && H % KV == 0, "flash_bwd: shapes");
+  TORCH_CHECK(o.stride(0) == dout.stride(0), "flash_bwd: o/dout strides");
+  TORCH_CHECK(dk.stride(0) == dv.stride(0) && k.stride(0) == v.stride(0), "flash_bwd: k/v strides");
+  TORCH_CHECK(lse.numel() == B * H * S, "flash_bwd: lse size");
+  long long ws = 0;
+  check(ftc_flash_bwd_workspace((int)B, (int)S, (int)H, (int)D, &ws), "flash_bwd_workspace");
+  auto work = at::empty({ws}, q.options().dtype(at::kByte));
+  check(ftc_flash_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
+                      dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), work.data_ptr(), (int)B, (int)S, (int)H, (int)KV,
+                      (int)D, q.stride(0), k.stride(0), o.stride(0), dq.stride(0), dk.stride(0), (float)scale,
+                      causal ? 1 : 0, (int)window, cur_stream()),
+        "flash_bwd");
+}
+
+// ---------------- NF4 (QLoRA) ----------------
+std::vector<at::Tensor> nf4_quantize(const at::Tensor& w, int64_t block) {
+  need(w, at::kBFloat16, "w");
+  TORCH_CHECK(w.is_contiguous() && w.numel() % block == 0 && block % 2 == 0, "nf4_quantize: shape");
+  const long long n = w.numel();
+  auto packed = at::empty({n / 2}, w.options().dtype(at::kByte));
+  auto absmax = at::empty({n / block}, w.options().dtype(at::kFloat));
+  check(ftc_nf4_quant(w.data_ptr(), packed.data_ptr<uint8_t>(), absmax.data_ptr<float>(), n, (int)block,
+                      cur_stream()),
+        "nf4_quant");
+  return {packed, absmax};
+}
+
+at::Tensor nf4_dequantize(const at::Tensor& packed, const at::Tensor& absmax_q, const at::Tensor& absmax_scale,
+                          double absmax_offset, int64_t rows, int64_t cols, int64_t block, int64_t block2) {
+  need(packed, at::kByte, "packed");
+  need(absmax_q, at::kByte, "absmax_q");
+  need(absmax_scale, at::kFloat, "absmax_scale");
+  const long long n = rows * cols;
+  TORCH_CHECK(packed.numel() * 2 == n && absmax_q.numel() * block == n, "nf4_dequantize: sizes");
+  TORCH_CHECK(absmax_scale.numel() * block2 >= absmax_q.numel(), "nf4_dequantize: second-level scales");
+  auto out = at::empty({rows, cols}, packed.options().dtype(at::kBFloat16));
+  check(ftc_nf4_dequant(packed.data_ptr<uint8_t>(), absmax_q.data_ptr<uint8_t>(), absmax_scale.data_ptr<float>(),
+                        (float)absmax_offset, out.data_ptr(), n, (int)block, (int)block2, cur_stream()),
+        "nf4_dequant");
+  return out;
+}
+
+// y[M,N] = x[M,K] @ dequant(W)[N,K]^T  with the NF4 decode fused into the MFMA operand load
+at::Tensor nf4_linear(const at::Tensor& x, const at::Tensor& packed, const at::Tensor& absmax_q,
+                      const at::Tensor& absmax_scale, double absmax_offset, int64_t N, int64_t block, int64_t block2) {
+  need(x, at::kBFloat16, "x");
+  need_rows(x, "x");
+  const int M = (int)x.size(0), K = (int)x.size(1);
+  TORCH_CHECK(packed.numel() * 2 == (long long)N * K, "nf4_linear: packed size");
+  TORCH_CHECK(K % 64 == 0 && N % 64 == 0 && block == 64, "nf4_linear: K,N multiples of 64, block 64");
+  auto y = at::empty({M, N}, x.options());
+  check(ftc_nf4_gemm(x.data_ptr(), packed.data_ptr<uint8_t>(), absmax_q.data_ptr<uint8_t>(),
+                     absmax_scale.data_ptr<float>(), (float)absmax_offset, y.data_ptr(), M, (int)N, K, (int)block,
+                     (int)block2, cur_stream()),
+        "nf4_gemm");
+  return y;
+}
+
+// ---------------- LoRA merge ----------------
+// W[out,in] += scale * B[out, r_total] @ A[r_total, in]; with seg_rows > 0 the product is block diagonal:
+// output rows [s*seg_rows, (s+1)*seg_rows) only see rank slice s (packed qkv / gate_up projections)
+void lora_merge_(at::Tensor& w, const at::Tensor& a, const at::Tensor& b, double scale, int64_t seg_rows) {
+  need(w, at::kBFloat16, "w");
+  need(a, at::kBFloat16, "a");
+  need(b, at::kBFloat16, "b");
+  need_rows(w, "w");
+  TORCH_CHECK(a.is_contiguous() && b.is_contiguous(), "lora_merge: contiguous A/B");
+  const int out_f = (int)w.size(0), in_f = (int)w.size(1), r = (int)a.size(0);
+  TORCH_CHECK(a.size(1) == in_f && b.size(0) == out_f && b.size(1) == r, "lora_merge: shapes");
+  TORCH_CHECK(in_f % 8 == 0, "lora_merge: in_features % 8");
+  check(ftc_lora_merge(w.data_ptr(), a.data_ptr(), b.data_ptr(), out_f, in_f, r, (int)seg_rows, (float)scale,
+                       cur_stream()),
+        "lora_merge");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "finetune_controller_amd gfx950 kernels";
+  m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("rope_", &rope_);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("ce_fwd_bwd_", &ce_fwd_bwd_);
+  m.def("adamw_", &adamw_);
+  m.def("grad_sumsq", &grad_sumsq);
+  m.def("flash_fwd", &flash_fwd);
+  m.def("flash_bwd", &flash_bwd);
+  m.def("nf4_quantize", &nf4_quantize);
+  m.def("nf4_dequantize", &nf4_dequantize);
+  m.def("nf4_linear", &nf4_linear);
+  m.def("lora_merge_", &lora_merge_);
+}

@@ -1,0 +1,105 @@
+// Shared device helpers for the gfx950 (CDNA4, MI355X) kernels of finetune_controller_amd.
+//
+// Conventions used by every kernel in csrc/kernels:
+//   * wave64: lane = threadIdx.x & 63, wave reductions over 64 lanes with __shfl_xor;
+//   * bf16 is moved as raw 16-bit words, 8 per 16-byte vector (uint4) -- hipcc does not
+//     auto-vectorise bf16 loads (guide: Guideline 13), so every memory-bound kernel loads
+//     16 B per lane;
+//   * float -> bf16 goes through the __bf16 cast, which hipcc lowers to v_cvt_pk_bf16_f32
+//     (round-to-nearest-even, NaN preserving);
+//   * launchers are extern "C" host functions taking raw pointers + hipStream_t so that the
+//     kernels compile without torch headers; csrc/binding.cpp adapts them to at::Tensor.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define FTC_DEV __device__ __forceinline__
+
+namespace ftc {
+
+constexpr int kWave = 64;
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+FTC_DEV float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
+FTC_DEV float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+FTC_DEV float bf2f(uint16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
+
+FTC_DEV uint16_t f2bf(float x) {
+  __bf16 b = (__bf16)x;
+  return __builtin_bit_cast(uint16_t, b);
+}
+// pack two floats into one dword of 2 x bf16 (lo in bits 0..15)
+FTC_DEV uint32_t pack_bf2(float lo, float hi) {
+  f32x2 v = {lo, hi};
+  bf16x2 b = __builtin_convertvector(v, bf16x2);
+  return __builtin_bit_cast(uint32_t, b);
+}
+
+// 8 bf16 <-> 8 floats
+FTC_DEV void unpack8(const uint4& v, float* f) {
+  f[0] = bf_lo(v.x); f[1] = bf_hi(v.x);
+  f[2] = bf_lo(v.y); f[3] = bf_hi(v.y);
+  f[4] = bf_lo(v.z); f[5] = bf_hi(v.z);
+  f[6] = bf_lo(v.w); f[7] = bf_hi(v.w);
+}
+FTC_DEV uint4 pack8(const float* f) {
+  uint4 v;
+  v.x = pack_bf2(f[0], f[1]);
+  v.y = pack_bf2(f[2], f[3]);
+  v.z = pack_bf2(f[4], f[5]);
+  v.w = pack_bf2(f[6], f[7]);
+  return v;
+}
+
+FTC_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+FTC_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+// Block-wide sum for blockDim.x == NT (multiple of 64). `red` needs NT/64 floats of LDS.
+template <int NT>
+FTC_DEV float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r += red[i];
+  __syncthreads();
+  return r;
+}
+template <int NT>
+FTC_DEV float block_max(float v, float* red) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float r = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r = fmaxf(r, red[i]);
+  __syncthreads();
+  return r;
+}
+
+// Grid size for grid-stride memory-bound kernels: enough blocks to fill 256 CUs x 8,
+// never more than the work needs (guide Guideline 11).
+inline int stream_grid(long long work_items, int block) {
+  long long g = (work_items + block - 1) / block;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace ftc

@@ -1,0 +1,117 @@
+// K4 RoPE (in place, forward and inverse rotation) and K9 SwiGLU forward/backward.
+// Memory-bound: 16-byte vector loads per lane, cos/sin from host-precomputed fp32 tables
+// (no on-device trig: guide Appendix B "Element-wise"), grid-stride capped at 2048 blocks.
+#include "common.h"
+
+using namespace ftc;
+
+// qkv: [rows, ld] bf16; the first (n_rot_heads * head_dim) columns are rotated in place, half-split
+// (rotate_half) convention: (x1, x2) -> (x1 c - x2 s, x2 c + x1 s) with x1 = x[:D/2], x2 = x[D/2:].
+// pos = positions ? positions[row] : row % seq_len.  cos/sin tables: [max_pos, D/2] fp32.
+__global__ __launch_bounds__(256) void rope_kernel(uint16_t* __restrict__ qkv, const float* __restrict__ cosT,
+                                                   const float* __restrict__ sinT,
+                                                   const int* __restrict__ positions, long long rows, int ld,
+                                                   int n_rot_heads, int head_dim, int seq_len, float sign) {
+  const int half = head_dim >> 1;
+  const int chunks = half >> 3;  // 8 pairs per work item
+  const long long per_row = (long long)n_rot_heads * chunks;
+  const long long total = rows * per_row;
+  for (long long it = (long long)blockIdx.x * 256 + threadIdx.x; it < total; it += (long long)gridDim.x * 256) {
+    const long long row = it / per_row;
+    const int rem = (int)(it - row * per_row);
+    const int head = rem / chunks;
+    const int c = rem - head * chunks;
+    const int pos = positions ? positions[row] : (int)(row % seq_len);
+    uint16_t* base = qkv + row * ld + (long long)head * head_dim + c * 8;
+    uint4* p1 = reinterpret_cast<uint4*>(base);
+    uint4* p2 = reinterpret_cast<uint4*>(base + half);
+    float x1[8], x2[8], cs[8], sn[8];
+    unpack8(*p1, x1);
+    unpack8(*p2, x2);
+    const float4* cr = reinterpret_cast<const float4*>(cosT + (long long)pos * half + c * 8);
+    const float4* sr = reinterpret_cast<const float4*>(sinT + (long long)pos * half + c * 8);
+    float4 c0 = cr[0], c1 = cr[1], s0 = sr[0], s1 = sr[1];
+    cs[0] = c0.x; cs[1] = c0.y; cs[2] = c0.z; cs[3] = c0.w; cs[4] = c1.x; cs[5] = c1.y; cs[6] = c1.z; cs[7] = c1.w;
+    sn[0] = s0.x; sn[1] = s0.y; sn[2] = s0.z; sn[3] = s0.w; sn[4] = s1.x; sn[5] = s1.y; sn[6] = s1.z; sn[7] = s1.w;
+    float o1[8], o2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float s = sign * sn[j];
+      o1[j] = x1[j] * cs[j] - x2[j] * s;
+      o2[j] = x2[j] * cs[j] + x1[j] * s;
+    }
+    *p1 = pack8(o1);
+    *p2 = pack8(o2);
+  }
+}
+
+extern "C" int ftc_rope(void* qkv, const float* cosT, const float* sinT, const int* positions, long long rows,
+                        int ld, int n_rot_heads, int head_dim, int seq_len, int inverse, hipStream_t stream) {
+  if (head_dim % 16 != 0 || ld % 8 != 0) return -1;
+  const long long total = rows * n_rot_heads * (head_dim / 16);
+  const int grid = ftc::stream_grid(total, 256);
+  hipLaunchKernelGGL(rope_kernel, dim3(grid), dim3(256), 0, stream, (uint16_t*)qkv, cosT, sinT, positions, rows, ld,
+                     n_rot_heads, head_dim, seq_len, inverse ? -1.0f : 1.0f);
+  return (int)hipGetLastError();
+}
+
+FTC_DEV float silu_f(float g) { return g / (1.0f + __expf(-g)); }
+
+// gu: [rows, 2F] (gate | up), a: [rows, F]
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ a,
+                                                         long long rows, int F) {
+  const int fv = F >> 3;
+  const long long total = rows * fv;
+  for (long long it = (long long)blockIdx.x * 256 + threadIdx.x; it < total; it += (long long)gridDim.x * 256) {
+    const long long row = it / fv;
+    const int c = (int)(it - row * fv);
+    const uint4* r = reinterpret_cast<const uint4*>(gu + row * 2 * F);
+    float g[8], u[8], o[8];
+    unpack8(r[c], g);
+    unpack8(r[fv + c], u);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = silu_f(g[j]) * u[j];
+    reinterpret_cast<uint4*>(a + row * F)[c] = pack8(o);
+  }
+}
+
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const uint16_t* __restrict__ da,
+                                                         const uint16_t* __restrict__ gu, uint16_t* __restrict__ dgu,
+                                                         long long rows, int F) {
+  const int fv = F >> 3;
+  const long long total = rows * fv;
+  for (long long it = (long long)blockIdx.x * 256 + threadIdx.x; it < total; it += (long long)gridDim.x * 256) {
+    const long long row = it / fv;
+    const int c = (int)(it - row * fv);
+    const uint4* r = reinterpret_cast<const uint4*>(gu + row * 2 * F);
+    float g[8], u[8], d[8], dg[8], du[8];
+    unpack8(r[c], g);
+    unpack8(r[fv + c], u);
+    unpack8(reinterpret_cast<const uint4*>(da + row * F)[c], d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float sg = 1.0f / (1.0f + __expf(-g[j]));
+      const float sl = g[j] * sg;
+      du[j] = d[j] * sl;
+      dg[j] = d[j] * u[j] * sg * (1.0f + g[j] * (1.0f - sg));
+    }
+    uint4* o = reinterpret_cast<uint4*>(dgu + row * 2 * F);
+    o[c] = pack8(dg);
+    o[fv + c] = pack8(du);
+  }
+}
+
+extern "C" int ftc_swiglu_fwd(const void* gu, void* a, long long rows, int F, hipStream_t stream) {
+  if (F % 8 != 0) return -1;
+  const int grid = ftc::stream_grid(rows * (F / 8), 256);
+  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(grid), dim3(256), 0, stream, (const uint16_t*)gu, (uint16_t*)a, rows, F);
+  return (int)hipGetLastError();
+}
+
+extern "C" int ftc_swiglu_bwd(const void* da, const void* gu, void* dgu, long long rows, int F, hipStream_t stream) {
+  if (F % 8 != 0) return -1;
+  const int grid = ftc::stream_grid(rows * (F / 8), 256);
+  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid), dim3(256), 0, stream, (const uint16_t*)da, (const uint16_t*)gu,
+                     (uint16_t*)dgu, rows, F);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,106 @@
+// K8 (part 1): NF4 quantisation / dequantisation for QLoRA base weights.
+//
+// Format: 4-bit NormalFloat codes, blocks of `block` (=64) consecutive
+// elements share an fp32 absmax; two codes per byte, FIRST element in the HIGH nibble (the
+// bitsandbytes packing order).  Double quantisation stores the absmax vector itself as uint8:
+//     absmax[i] = offset + (q2[i] - 128) / 127 * scale2[i / block2]        (block2 = 256)
+// The nested step is done on the host-side tensor (finetune_controller_amd/ops/nf4.py) because it
+// is a one-time O(n/64) operation; these kernels do the O(n) parts.
+#include "common.h"
+
+using namespace ftc;
+
+__constant__ float kNF4[16] = {-1.0f,
+                               -0.6961928009986877f,
+                               -0.5250730514526367f,
+                               -0.39491748809814453f,
+                               -0.28444138169288635f,
+                               -0.18477343022823334f,
+                               -0.09105003625154495f,
+                               0.0f,
+                               0.07958029955625534f,
+                               0.16093020141124725f,
+                               0.24611230194568634f,
+                               0.33791524171829224f,
+                               0.44070982933044434f,
+                               0.5626170039176941f,
+                               0.7229568362236023f,
+                               1.0f};
+
+FTC_DEV int nf4_encode(float x) {
+  // nearest codebook entry (midpoints between consecutive codes)
+  int best = 0;
+  float bd = fabsf(x - kNF4[0]);
+#pragma unroll
+  for (int i = 1; i < 16; ++i) {
+    const float dd = fabsf(x - kNF4[i]);
+    if (dd < bd) { bd = dd; best = i; }
+  }
+  return best;
+}
+
+// one wave per block of 64 elements: lane j handles element j
+__global__ __launch_bounds__(256) void nf4_quant_kernel(const uint16_t* __restrict__ w, uint8_t* __restrict__ packed,
+                                                        float* __restrict__ absmax, long long nblocks, int block) {
+  const int lane = threadIdx.x & 63;
+  for (long long b = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); b < nblocks; b += (long long)gridDim.x * 4) {
+    float mx = 0.f;
+    for (int i = lane; i < block; i += 64) mx = fmaxf(mx, fabsf(bf2f(w[b * block + i])));
+    mx = wave_max(mx);
+    const float inv = mx > 0.f ? 1.0f / mx : 0.f;
+    for (int i = lane * 2; i < block; i += 128) {
+      const int q0 = nf4_encode(bf2f(w[b * block + i]) * inv);
+      const int q1 = nf4_encode(bf2f(w[b * block + i + 1]) * inv);
+      packed[(b * block + i) >> 1] = (uint8_t)((q0 << 4) | q1);
+    }
+    if (lane == 0) absmax[b] = mx;
+  }
+}
+
+__global__ __launch_bounds__(256) void nf4_dequant_kernel(const uint8_t* __restrict__ packed,
+                                                          const uint8_t* __restrict__ aq,
+                                                          const float* __restrict__ s2, float off,
+                                                          uint16_t* __restrict__ out, long long n, int block,
+                                                          int block2) {
+  // each thread: 16 codes (8 bytes) -> 16 bf16 (32 bytes)
+  const long long n16 = n >> 4;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long long)gridDim.x * 256) {
+    const uint2 p = reinterpret_cast<const uint2*>(packed)[i];
+    const long long e0 = i << 4;
+    const long long bi = e0 / block;  // block >= 16 and a multiple of 16: one absmax per thread
+    const float a = off + ((float)aq[bi] - 128.0f) * (1.0f / 127.0f) * s2[bi / block2];
+    float f[16];
+    uint32_t words[2] = {p.x, p.y};
+#pragma unroll
+    for (int wd = 0; wd < 2; ++wd) {
+#pragma unroll
+      for (int bt = 0; bt < 4; ++bt) {
+        const uint32_t byte = (words[wd] >> (8 * bt)) & 0xffu;
+        f[wd * 8 + bt * 2] = kNF4[byte >> 4] * a;
+        f[wd * 8 + bt * 2 + 1] = kNF4[byte & 0xf] * a;
+      }
+    }
+    uint4* o = reinterpret_cast<uint4*>(out + e0);
+    o[0] = pack8(f);
+    o[1] = pack8(f + 8);
+  }
+}
+
+extern "C" int ftc_nf4_quant(const void* w, uint8_t* packed, float* absmax, long long n, int block,
+                             hipStream_t stream) {
+  if (block % 2 != 0 || n % block != 0) return -1;
+  const long long nb = n / block;
+  const int grid = ftc::stream_grid(nb, 4);
+  hipLaunchKernelGGL(nf4_quant_kernel, dim3(grid), dim3(256), 0, stream, (const uint16_t*)w, packed, absmax, nb, block);
+  return (int)hipGetLastError();
+}
+
+extern "C" int ftc_nf4_dequant(const uint8_t* packed, const uint8_t* absmax_q, const float* absmax_scale,
+                               float absmax_offset, void* out, long long n, int block, int block2,
+                               hipStream_t stream) {
+  if (n % 16 != 0 || block % 16 != 0) return -1;
+  const int grid = ftc::stream_grid(n / 16, 256);
+  hipLaunchKernelGGL(nf4_dequant_kernel, dim3(grid), dim3(256), 0, stream, packed, absmax_q, absmax_scale,
+                     absmax_offset, (uint16_t*)out, n, block, block2);
+  return (int)hipGetLastError();
+}

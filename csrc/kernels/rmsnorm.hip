@@ -1,0 +1,228 @@
+// K3: RMSNorm forward / backward with the residual add fused in.
+//
+//   fwd:  h = x (+ res)            (bf16, written back when res is given: the residual stream)
+//         rstd = rsqrt(mean(h^2) + eps)   (fp32, saved for backward)
+//         y = bf16(h * rstd * w)
+//   bwd:  xhat = h*rstd, g = dy*w
+//         dx = rstd*(g - xhat*mean(g*xhat)) (+ dres: gradient arriving along the residual stream)
+//         dw = sum_rows dy*xhat   (optional: frozen in LoRA runs)
+//
+// Layout: one wave64 per row, the row held in registers (NV x 16-byte vectors per lane) so the
+// reduction is a pure wave shuffle -- no LDS, no barrier on the row path.  4 waves per 256-thread
+// block, grid-stride over rows with the grid capped at 2048 blocks (8 per CU).  The dw partials
+// are reduced across the 4 waves of a block in LDS and across blocks by a second tiny kernel
+// (deterministic: no float atomics).
+#include "common.h"
+
+using namespace ftc;
+
+template <int NV, bool RES>
+__global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ res, const uint16_t* __restrict__ w,
+    uint16_t* __restrict__ h_out, uint16_t* __restrict__ y, float* __restrict__ rstd, int rows, int d,
+    float eps) {
+  const int lane = threadIdx.x & 63;
+  const int nvec = d >> 3;
+  const float inv_d = 1.0f / (float)d;
+  for (long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows;
+       row += (long long)gridDim.x * 4) {
+    const uint4* xr = reinterpret_cast<const uint4*>(x + row * d);
+    float v[NV][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int idx = lane + i * 64;
+      if (idx < nvec) {
+        uint4 a = xr[idx];
+        unpack8(a, v[i]);
+        if constexpr (RES) {
+          float r8[8];
+          unpack8(reinterpret_cast<const uint4*>(res + row * d)[idx], r8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[i][j] += r8[j];
+          uint4 hv = pack8(v[i]);
+          reinterpret_cast<uint4*>(h_out + row * d)[idx] = hv;
+          unpack8(hv, v[i]);  // statistics on the stored (rounded) residual stream
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+      }
+    }
+    ss = wave_sum(ss);
+    const float r = rsqrtf(ss * inv_d + eps);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int idx = lane + i * 64;
+      if (idx < nvec) {
+        float w8[8], o[8];
+        unpack8(reinterpret_cast<const uint4*>(w)[idx], w8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = v[i][j] * r * w8[j];
+        reinterpret_cast<uint4*>(y + row * d)[idx] = pack8(o);
+      }
+    }
+    if (lane == 0) rstd[row] = r;
+  }
+}
+
+template <int NV, bool DW, bool DRES>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ h, const uint16_t* __restrict__ w,
+    const float* __restrict__ rstd, const uint16_t* __restrict__ dres, uint16_t* __restrict__ dx,
+    float* __restrict__ dw_part, int rows, int d) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nvec = d >> 3;
+  const float inv_d = 1.0f / (float)d;
+  float acc[DW ? NV : 1][8];
+  if constexpr (DW) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
+  }
+  for (long long row = (long long)blockIdx.x * 4 + wid; row < rows; row += (long long)gridDim.x * 4) {
+    const float r = rstd[row];
+    float xh[NV][8], g[NV][8];
+    float dot = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int idx = lane + i * 64;
+      if (idx < nvec) {
+        float dy8[8], w8[8];
+        unpack8(reinterpret_cast<const uint4*>(dy + row * d)[idx], dy8);
+        unpack8(reinterpret_cast<const uint4*>(h + row * d)[idx], xh[i]);
+        unpack8(reinterpret_cast<const uint4*>(w)[idx], w8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[i][j] *= r;
+          g[i][j] = dy8[j] * w8[j];
+          dot += g[i][j] * xh[i][j];
+          if constexpr (DW) acc[i][j] += dy8[j] * xh[i][j];
+        }
+      }
+    }
+    dot = wave_sum(dot) * inv_d;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int idx = lane + i * 64;
+      if (idx < nvec) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = r * (g[i][j] - xh[i][j] * dot);
+        if constexpr (DRES) {
+          float d8[8];
+          unpack8(reinterpret_cast<const uint4*>(dres + row * d)[idx], d8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += d8[j];
+        }
+        reinterpret_cast<uint4*>(dx + row * d)[idx] = pack8(o);
+      }
+    }
+  }
+  if constexpr (DW) {
+    // reduce the 4 waves' partial dw rows in LDS: lds[4][d]
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int idx = lane + i * 64;
+      if (idx < nvec) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) lds[wid * d + idx * 8 + j] = acc[i][j];
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < d; c += 256) {
+      float s = lds[c] + lds[d + c] + lds[2 * d + c] + lds[3 * d + c];
+      dw_part[(long long)blockIdx.x * d + c] = s;
+    }
+  }
+}
+
+// dw[c] = sum_b part[b][c]; one thread per column, coalesced across the row of partials.
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                     int nrows, int d) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= d) return;
+  float s = 0.f;
+  for (int b = 0; b < nrows; ++b) s += part[(long long)b * d + c];
+  out[c] = s;
+}
+
+static int pick_nv(int d) {
+  const int per_lane = (d / 8 + 63) / 64;
+  int nv = 1;
+  while (nv < per_lane) nv <<= 1;
+  return nv;
+}
+
+extern "C" int ftc_rmsnorm_fwd(const void* x, const void* res, const void* w, void* h_out, void* y, float* rstd,
+                               int rows, int d, float eps, hipStream_t stream) {
+  if (d % 8 != 0 || d > 16 * 512) return -1;
+  const int nv = pick_nv(d);
+  const int grid = ftc::stream_grid(rows, 4);
+  auto X = (const uint16_t*)x;
+  auto R = (const uint16_t*)res;
+  auto W = (const uint16_t*)w;
+  auto H = (uint16_t*)h_out;
+  auto Y = (uint16_t*)y;
+#define FTC_LAUNCH_FWD(NV)                                                                                    \
+  if (res)                                                                                                    \
+    hipLaunchKernelGGL((rmsnorm_fwd_kernel<NV, true>), dim3(grid), dim3(256), 0, stream, X, R, W, H, Y, rstd, \
+                       rows, d, eps);                                                                         \
+  else                                                                                                        \
+    hipLaunchKernelGGL((rmsnorm_fwd_kernel<NV, false>), dim3(grid), dim3(256), 0, stream, X, R, W, H, Y,     \
+                       rstd, rows, d, eps);
+  switch (nv) {
+    case 1: FTC_LAUNCH_FWD(1); break;
+    case 2: FTC_LAUNCH_FWD(2); break;
+    case 4: FTC_LAUNCH_FWD(4); break;
+    case 8: FTC_LAUNCH_FWD(8); break;
+    case 16: FTC_LAUNCH_FWD(16); break;
+    default: return -1;
+  }
+#undef FTC_LAUNCH_FWD
+  return (int)hipGetLastError();
+}
+
+// dw_part must hold grid*d floats where grid = ftc_rmsnorm_bwd_grid(rows); dw (fp32, d) may be null.
+extern "C" int ftc_rmsnorm_bwd_grid(int rows) { return ftc::stream_grid(rows, 4) > 512 ? 512 : ftc::stream_grid(rows, 4); }
+
+extern "C" int ftc_rmsnorm_bwd(const void* dy, const void* h, const void* w, const float* rstd, const void* dres,
+                               void* dx, float* dw_part, float* dw, int rows, int d, hipStream_t stream) {
+  if (d % 8 != 0 || d > 16 * 512) return -1;
+  const int nv = pick_nv(d);
+  const bool need_dw = dw != nullptr;
+  // the dw path keeps per-wave accumulators: fewer, longer-lived blocks
+  const int grid = need_dw ? ftc_rmsnorm_bwd_grid(rows) : ftc::stream_grid(rows, 4);
+  const size_t lds = need_dw ? (size_t)4 * d * sizeof(float) : 0;
+  auto DY = (const uint16_t*)dy;
+  auto Hh = (const uint16_t*)h;
+  auto W = (const uint16_t*)w;
+  auto DR = (const uint16_t*)dres;
+  auto DX = (uint16_t*)dx;
+#define FTC_LAUNCH_BWD(NV, DWB, DRB)                                                                       \
+  hipLaunchKernelGGL((rmsnorm_bwd_kernel<NV, DWB, DRB>), dim3(grid), dim3(256), lds, stream, DY, Hh, W, rstd, \
+                     DR, DX, dw_part, rows, d)
+#define FTC_LAUNCH_BWD_NV(NV)                     \
+  if (need_dw) {                                  \
+    if (dres) FTC_LAUNCH_BWD(NV, true, true);     \
+    else FTC_LAUNCH_BWD(NV, true, false);         \
+  } else {                                        \
+    if (dres) FTC_LAUNCH_BWD(NV, false, true);    \
+    else FTC_LAUNCH_BWD(NV, false, false);        \
+  }
+  switch (nv) {
+    case 1: FTC_LAUNCH_BWD_NV(1); break;
+    case 2: FTC_LAUNCH_BWD_NV(2); break;
+    case 4: FTC_LAUNCH_BWD_NV(4); break;
+    case 8: FTC_LAUNCH_BWD_NV(8); break;
+    case 16: FTC_LAUNCH_BWD_NV(16); break;
+    default: return -1;
+  }
+#undef FTC_LAUNCH_BWD_NV
+#undef FTC_LAUNCH_BWD
+  if (need_dw) {
+    hipLaunchKernelGGL(colsum_kernel, dim3((d + 255) / 256), dim3(256), 0, stream, dw_part, dw, grid, d);
+  }
+  return (int)hipGetLastError();
+}

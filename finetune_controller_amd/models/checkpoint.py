@@ -1,0 +1,230 @@
+"""Checkpoint I/O in the formats the controller's artifact contract expects.
+
+The reference treats artifacts as opaque flat files synced from ``/data/artifacts`` by patterns
+(``/root/reference/app/models/base/finetuning.py:94-97``: ``*.json *.yaml *.csv *.pt *.ckpt``) and
+flattens sub-directories to basenames when zipping/presigning
+(``/root/reference/app/utils/S3Handler.py:193,317``).  So everything here is written FLAT, with
+unique names:
+
+* LoRA / QLoRA: ``adapter_config.json`` (PEFT) + ``adapter_model.safetensors`` + ``adapter_model.pt``
+  (same tensors; ``.pt`` is matched by the reference's default patterns, safetensors by ours);
+* full fine-tune: ``config.json`` + ``model-0000i-of-0000n.safetensors`` shards +
+  ``model.safetensors.index.json`` in Hugging Face naming (+ nothing pickled);
+* resume: ``checkpoint_step{N}.pt`` (trainable tensors + optimizer flat state + data cursor),
+  loaded with ``weights_only=True``.
+"""
+from __future__ import annotations
+
+import glob
+import json
+import os
+import re
+
+import torch
+from safetensors.torch import load_file, save_file
+
+from .lora import LoRAConfig
+
+PEFT_PREFIX = "base_model.model."
+
+_LLAMA_SEG_MODULE = {"q_proj": "self_attn", "k_proj": "self_attn", "v_proj": "self_attn", "o_proj": "self_attn",
+                     "gate_proj": "mlp", "up_proj": "mlp", "down_proj": "mlp"}
+_GPT2_SEG_MODULE = {"q_proj": "attn.c_attn", "k_proj": "attn.c_attn", "v_proj": "attn.c_attn", "o_proj": "attn.c_proj",
+                    "up_proj": "mlp.c_fc", "down_proj": "mlp.c_proj"}
+
+
+def _layers(model):
+    return model.layers if hasattr(model, "layers") else model.blocks
+
+
+def adapter_state_dict(model) -> dict[str, torch.Tensor]:
+    """PEFT-named LoRA tensors: ``...layers.{i}.self_attn.q_proj.lora_A.weight`` [r, in] / ``lora_B`` [out, r]."""
+    sd = {}
+    gpt2 = model.cfg.family == "gpt2"
+    for i, layer in enumerate(_layers(model)):
+        for pair in layer.lora.values():
+            for seg, A_s, B_s in pair.segment_tensors():
+                if gpt2:
+                    base = f"{PEFT_PREFIX}transformer.h.{i}.{_GPT2_SEG_MODULE[seg]}.{seg}"
+                else:
+                    base = f"{PEFT_PREFIX}model.layers.{i}.{_LLAMA_SEG_MODULE[seg]}.{seg}"
+                sd[f"{base}.lora_A.weight"] = A_s.detach().to(torch.bfloat16).contiguous().cpu()
+                sd[f"{base}.lora_B.weight"] = B_s.detach().to(torch.bfloat16).contiguous().cpu()
+    return sd
+
+
+def save_adapter(model, out_dir: str, base_model_name: str, lora: LoRAConfig, write_pt: bool = True) -> list[str]:
+    os.makedirs(out_dir, exist_ok=True)
+    sd = adapter_state_dict(model)
+    files = []
+    p = os.path.join(out_dir, "adapter_model.safetensors")
+    save_file(sd, p, metadata={"format": "pt"})
+    files.append(p)
+    if write_pt:
+        p = os.path.join(out_dir, "adapter_model.pt")
+        torch.save(sd, p)
+        files.append(p)
+    p = os.path.join(out_dir, "adapter_config.json")
+    with open(p, "w") as f:
+        json.dump(lora.to_peft(base_model_name), f, indent=2)
+    files.append(p)
+    return files
+
+
+@torch.no_grad()
+def load_adapter(model, path: str):
+    """Load PEFT-named adapter tensors (safetensors or weights-only .pt) into the model's pairs."""
+    if os.path.isdir(path):
+        st = os.path.join(path, "adapter_model.safetensors")
+        path = st if os.path.exists(st) else os.path.join(path, "adapter_model.pt")
+    sd = load_file(path) if path.endswith(".safetensors") else torch.load(path, map_location="cpu", weights_only=True)
+    pat = re.compile(r"\.(?:layers|h)\.(\d+)\..*?\.(\w+_proj)\.lora_A\.weight$")
+    layers = _layers(model)
+    n = 0
+    for k, A in sd.items():
+        m = pat.search(k)
+        if not m:
+            continue
+        i, seg = int(m.group(1)), m.group(2)
+        B = sd[k.replace("lora_A", "lora_B")]
+        for pair in layers[i].lora.values():
+            if seg in pair.names:
+                pair.load_segment(seg, A.to(pair.A.device, pair.A.dtype), B.to(pair.B.device, pair.B.dtype))
+                n += 1
+    return n
+
+
+# ---------------- full model (HF naming) ----------------
+
+def _llama_hf_tensors(model):
+    cfg = model.cfg
+    H, KV, D, Fd = cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, cfg.ffn_dim
+    yield "model.embed_tokens.weight", model.embed
+    for i, l in enumerate(model.layers):
+        p = f"model.layers.{i}."
+        yield p + "input_layernorm.weight", l.attn_norm
+        w = l.wqkv
+        yield p + "self_attn.q_proj.weight", w[: H * D]
+        yield p + "self_attn.k_proj.weight", w[H * D:(H + KV) * D]
+        yield p + "self_attn.v_proj.weight", w[(H + KV) * D:]
+        yield p + "self_attn.o_proj.weight", l.wo
+        yield p + "post_attention_layernorm.weight", l.mlp_norm
+        yield p + "mlp.gate_proj.weight", l.wgu[:Fd]
+        yield p + "mlp.up_proj.weight", l.wgu[Fd:]
+        yield p + "mlp.down_proj.weight", l.wdown
+    yield "model.norm.weight", model.final_norm
+    if not cfg.tie_embeddings:
+        yield "lm_head.weight", model.lm_head
+
+
+def _gpt2_hf_tensors(model):
+    yield "transformer.wte.weight", model.wte
+    yield "transformer.wpe.weight", model.wpe
+    for i, b in enumerate(model.blocks):
+        p = f"transformer.h.{i}."
+        yield p + "ln_1.weight", b.ln1_w
+        yield p + "ln_1.bias", b.ln1_b
+        yield p + "attn.c_attn.weight", b.attn_w.t()  # HF Conv1D stores [in, out]
+        yield p + "attn.c_attn.bias", b.attn_b
+        yield p + "attn.c_proj.weight", b.proj_w.t()
+        yield p + "attn.c_proj.bias", b.proj_b
+        yield p + "ln_2.weight", b.ln2_w
+        yield p + "ln_2.bias", b.ln2_b
+        yield p + "mlp.c_fc.weight", b.fc_w.t()
+        yield p + "mlp.c_fc.bias", b.fc_b
+        yield p + "mlp.c_proj.weight", b.out_w.t()
+        yield p + "mlp.c_proj.bias", b.out_b
+    yield "transformer.ln_f.weight", model.lnf_w
+    yield "transformer.ln_f.bias", model.lnf_b
+
+
+def hf_tensors(model):
+    return _gpt2_hf_tensors(model) if model.cfg.family == "gpt2" else _llama_hf_tensors(model)
+
+
+def save_full(model, out_dir: str, shard_bytes: int = 5 * 1024**3, merge_lora: bool = True) -> list[str]:
+    """HF-layout safetensors shards + index + config.json (LoRA merged in if present)."""
+    os.makedirs(out_dir, exist_ok=True)
+    from .lora import merge_pair_into
+
+    merged = []
+    if merge_lora and model.lora_cfg is not None and model.cfg.family != "gpt2":
+        for l in model.layers:
+            for name, pair in l.lora.items():
+                if name in l.qweights:
+                    continue
+                merge_pair_into(l.base_weight(name).data, pair, +1.0)
+                merged.append((l, name, pair))
+    try:
+        shards, cur, size = [], {}, 0
+        for name, t in hf_tensors(model):
+            t = t.detach().contiguous().cpu()
+            nb = t.numel() * t.element_size()
+            if cur and size + nb > shard_bytes:
+                shards.append(cur)
+                cur, size = {}, 0
+            cur[name] = t
+            size += nb
+        if cur:
+            shards.append(cur)
+        files, weight_map = [], {}
+        for i, sh in enumerate(shards):
+            fn = f"model-{i + 1:05d}-of-{len(shards):05d}.safetensors"
+            save_file(sh, os.path.join(out_dir, fn), metadata={"format": "pt"})
+            files.append(os.path.join(out_dir, fn))
+            for k in sh:
+                weight_map[k] = fn
+        idx = os.path.join(out_dir, "model.safetensors.index.json")
+        with open(idx, "w") as f:
+            json.dump({"metadata": {}, "weight_map": weight_map}, f)
+        cfgp = os.path.join(out_dir, "config.json")
+        with open(cfgp, "w") as f:
+            json.dump(model.cfg.to_hf_config(), f, indent=2)
+        return files + [idx, cfgp]
+    finally:
+        for l, name, pair in merged:  # keep training state unmerged
+            merge_pair_into(l.base_weight(name).data, pair, -1.0)
+
+
+@torch.no_grad()
+def load_hf_checkpoint(model, path: str) -> int:
+    """Load HF safetensors (sharded or single) into the packed layout; returns tensors loaded."""
+    files = sorted(glob.glob(os.path.join(path, "*.safetensors"))) if os.path.isdir(path) else [path]
+    files = [f for f in files if "adapter" not in os.path.basename(f)]
+    targets = dict(hf_tensors(model))
+    n = 0
+    for fp in files:
+        sd = load_file(fp)
+        for k, v in sd.items():
+            if k not in targets:
+                continue
+            dst = targets[k]
+            dst.copy_(v.to(dst.dtype))
+            n += 1
+    return n
+
+
+# ---------------- resume checkpoints ----------------
+
+def save_resume(path: str, step: int, opt, data_state: dict, extra: dict | None = None):
+    st = {"step": step, "param_flat": opt.param_flat.detach().cpu(), "opt": {k: (v.detach().cpu() if torch.is_tensor(v) else v)
+                                                                            for k, v in opt.state_dict().items()},
+          "data": data_state, "extra": extra or {}}
+    tmp = path + ".tmp"
+    torch.save(st, tmp)
+    os.replace(tmp, path)
+
+
+def latest_resume(ckpt_dir: str) -> str | None:
+    c = glob.glob(os.path.join(ckpt_dir, "checkpoint_step*.pt"))
+    if not c:
+        return None
+    return max(c, key=lambda p: int(re.search(r"checkpoint_step(\d+)\.pt$", p).group(1)))
+
+
+@torch.no_grad()
+def load_resume(path: str, opt) -> dict:
+    st = torch.load(path, map_location="cpu", weights_only=True)
+    opt.param_flat.copy_(st["param_flat"])
+    opt.load_state_dict({k: (v.to(opt.device) if torch.is_tensor(v) else v) for k, v in st["opt"].items()})
+    return st

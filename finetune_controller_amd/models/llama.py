@@ -1,0 +1,137 @@
+"""Llama-3 / Mistral decoder (one trunk; Mistral = sliding-window attention + its own vocab/RoPE).
+
+MI355X-first layout decisions (not a port of any reference module -- the reference has no model
+code):
+
+* **Packed frozen weights.** q/k/v live in one ``Wqkv [(H+2KV)*D, d]`` and gate/up in one
+  ``Wgu [2F, d]``: two GEMMs per layer fewer, each larger (better MFMA occupancy on 256 CUs), and
+  the RoPE / attention / SwiGLU kernels read the packed outputs in place.
+* **Residual add fused into every norm** (``add_rms_norm``): the residual stream ``h`` and the
+  sub-block output are combined by the norm kernel itself.
+* **No activation checkpointing by default**: with 288 GB of HBM a frozen-base LoRA step keeps all
+  activations of 16k tokens of Llama-3-8B resident (≈4.2 MB/token), saving the 33 % recompute.
+  ``checkpoint_layers`` is available for longer sequences / full FT.
+* **Loss through the chunked fused linear+CE** (never [tokens, vocab] fp32 logits).
+
+Weight names map 1:1 onto Hugging Face ``LlamaForCausalLM`` / ``MistralForCausalLM`` (see
+``checkpoint.py``), so random-init benchmarks and real checkpoints use the same module.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch.utils.checkpoint import checkpoint
+
+from .. import ops
+from .config import ModelConfig
+from .lora import LoRAConfig, make_pairs
+
+
+class LlamaLayer(nn.Module):
+    def __init__(self, cfg: ModelConfig, lora: LoRAConfig | None, device=None, dtype=torch.bfloat16):
+        super().__init__()
+        d, D, H, KV, Fd = cfg.dim, cfg.head_dim, cfg.n_heads, cfg.n_kv_heads, cfg.ffn_dim
+        self.cfg = cfg
+        kw = dict(device=device, dtype=dtype)
+        self.attn_norm = nn.Parameter(torch.ones(d, **kw))
+        self.wqkv = nn.Parameter(torch.empty((H + 2 * KV) * D, d, **kw))
+        self.wo = nn.Parameter(torch.empty(d, H * D, **kw))
+        self.mlp_norm = nn.Parameter(torch.ones(d, **kw))
+        self.wgu = nn.Parameter(torch.empty(2 * Fd, d, **kw))
+        self.wdown = nn.Parameter(torch.empty(d, Fd, **kw))
+        self.shapes = {
+            "qkv": (d, [("q_proj", H * D), ("k_proj", KV * D), ("v_proj", KV * D)]),
+            "o": (H * D, [("o_proj", d)]),
+            "gu": (d, [("gate_proj", Fd), ("up_proj", Fd)]),
+            "down": (Fd, [("down_proj", d)]),
+        }
+        self.lora = make_pairs(self.shapes, lora, device=device, dtype=dtype) if lora else nn.ModuleDict()
+        self.qweights: dict[str, object] = {}  # QLoRA: proj -> NF4Weight (replaces the bf16 Parameter)
+
+    def base_weight(self, proj: str):
+        return {"qkv": self.wqkv, "o": self.wo, "gu": self.wgu, "down": self.wdown}[proj]
+
+    def proj(self, name: str, x: torch.Tensor) -> torch.Tensor:
+        pair = self.lora[name] if name in self.lora else None
+        qw = self.qweights.get(name)
+        if qw is not None:
+            from ..ops.nf4 import qlora_linear
+
+            return qlora_linear(x, qw, pair.A if pair else None, pair.B if pair else None,
+                                pair.scale if pair else 1.0, pair.blocks if pair else None)
+        W = self.base_weight(name)
+        if pair is None:
+            return ops.lora_linear(x, W)
+        return ops.lora_linear(x, W, pair.A, pair.B, pair.scale, blocks=pair.blocks)
+
+    def forward(self, h, delta, rope: ops.RotaryTable, B: int, S: int, positions=None):
+        cfg = self.cfg
+        h, x = ops.add_rms_norm(h, delta, self.attn_norm, cfg.norm_eps)
+        qkv = self.proj("qkv", x)
+        qkv = ops.apply_rope_packed(qkv, rope, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, S, positions)
+        a = ops.attention_packed(qkv, B, S, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, True, cfg.sliding_window)
+        o = self.proj("o", a)
+        h, x = ops.add_rms_norm(h, o, self.mlp_norm, cfg.norm_eps)
+        gu = self.proj("gu", x)
+        act = ops.swiglu(gu)
+        return h, self.proj("down", act)
+
+
+class LlamaForCausalLM(nn.Module):
+    def __init__(self, cfg: ModelConfig, lora: LoRAConfig | None = None, device=None, dtype=torch.bfloat16,
+                 checkpoint_layers: bool = False):
+        super().__init__()
+        self.cfg, self.lora_cfg = cfg, lora
+        kw = dict(device=device, dtype=dtype)
+        self.embed = nn.Parameter(torch.empty(cfg.vocab_size, cfg.dim, **kw))
+        self.layers = nn.ModuleList([LlamaLayer(cfg, lora, device, dtype) for _ in range(cfg.n_layers)])
+        self.final_norm = nn.Parameter(torch.ones(cfg.dim, **kw))
+        self.lm_head = self.embed if cfg.tie_embeddings else nn.Parameter(torch.empty(cfg.vocab_size, cfg.dim, **kw))
+        self.rope = ops.RotaryTable(cfg.head_dim, cfg.max_seq_len, cfg.rope_theta, cfg.rope_scaling)
+        self.checkpoint_layers = checkpoint_layers
+        self.ce_chunk_rows = 4096
+
+    @torch.no_grad()
+    def init_weights(self, seed: int = 0, std: float = 0.02):
+        """Random init (synthetic benchmarks). Generated on the parameters' own device."""
+        g = torch.Generator(device=self.embed.device).manual_seed(seed)
+        out_std = std / math.sqrt(2 * self.cfg.n_layers)
+        for name, p in self.named_parameters():
+            if ".lora." in name:
+                continue
+            if p.dim() == 1:
+                p.fill_(1.0)
+            elif name.endswith("wo") or name.endswith("wdown"):
+                p.normal_(0.0, out_std, generator=g)
+            else:
+                p.normal_(0.0, std, generator=g)
+        for layer in self.layers:
+            for pair in layer.lora.values():
+                pair.reset_parameters()
+
+    def freeze_base(self):
+        """LoRA/QLoRA: only adapter parameters train."""
+        for name, p in self.named_parameters():
+            p.requires_grad_(".lora." in name)
+
+    def hidden(self, input_ids: torch.Tensor, positions=None) -> torch.Tensor:
+        B, S = input_ids.shape
+        h = F.embedding(input_ids.reshape(-1), self.embed)
+        delta = None
+        for layer in self.layers:
+            if self.checkpoint_layers and self.training and torch.is_grad_enabled():
+                h, delta = checkpoint(layer, h, delta, self.rope, B, S, positions, use_reentrant=False)
+            else:
+                h, delta = layer(h, delta, self.rope, B, S, positions)
+        _, x = ops.add_rms_norm(h, delta, self.final_norm, self.cfg.norm_eps)
+        return x
+
+    def forward(self, input_ids: torch.Tensor, labels: torch.Tensor | None = None, positions=None,
+                n_valid: int | None = None):
+        x = self.hidden(input_ids, positions)
+        if labels is None:
+            return x @ self.lm_head.t()
+        return ops.fused_linear_cross_entropy(x, self.lm_head, labels, self.ce_chunk_rows, -100, n_valid)

@@ -1,0 +1,105 @@
+"""Causal (optionally sliding-window) GQA attention over a packed qkv projection (K1/K2).
+
+``attention_packed(qkv, B, S, H, KV, D)`` takes the ``[B*S, (H+2KV)*D]`` projection output
+(q heads, then k heads, then v heads -- the layout the packed Wqkv GEMM writes) and returns the
+``[B*S, H*D]`` attention output that feeds the o-projection GEMM directly.  q/k/v are consumed as
+strided views: nothing is transposed or copied.
+
+GPU: the gfx950 flash-attention kernels (``csrc/kernels/flash_attn.hip``: MFMA bf16, LDS-tiled K/V,
+online softmax, LSE saved for the backward, GQA handled by mapping q heads onto their kv head).
+The backward writes dq/dk/dv straight into ONE packed ``dqkv`` buffer, which is the gradient of the
+packed projection output -- again no concatenation.
+
+CPU / ``FTC_KERNELS=torch``: ``torch.nn.functional.scaled_dot_product_attention``.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from ._backend import ext, use_hip
+
+
+# flipped to True once csrc/kernels/flash_attn.hip replaces the stub launcher
+FLASH_READY = False
+
+
+def flash_supported(D: int, S: int) -> bool:
+    return FLASH_READY and D in (64, 128) and S % 64 == 0
+
+
+def _split(qkv, B, S, H, KV, D):
+    q = qkv[:, : H * D]
+    k = qkv[:, H * D : (H + KV) * D]
+    v = qkv[:, (H + KV) * D : (H + 2 * KV) * D]
+    return q, k, v
+
+
+def _sdpa_packed(qkv, B, S, H, KV, D, causal, window, scale):
+    q, k, v = _split(qkv, B, S, H, KV, D)
+    q = q.reshape(B, S, H, D).transpose(1, 2)
+    k = k.reshape(B, S, KV, D).transpose(1, 2)
+    v = v.reshape(B, S, KV, D).transpose(1, 2)
+    if KV != H:
+        rep = H // KV
+        k = k.repeat_interleave(rep, dim=1)
+        v = v.repeat_interleave(rep, dim=1)
+    mask = None
+    if window and window > 0 and window < S:
+        i = torch.arange(S, device=qkv.device)
+        allowed = (i[None, :] <= i[:, None]) & (i[:, None] - i[None, :] < window)
+        mask = allowed
+        o = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, scale=scale)
+    else:
+        o = F.scaled_dot_product_attention(q, k, v, is_causal=causal, scale=scale)
+    return o.transpose(1, 2).reshape(B * S, H * D)
+
+
+class _FlashPacked(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, B, S, H, KV, D, causal, window, scale):
+        q, k, v = _split(qkv, B, S, H, KV, D)
+        o, lse = ext().flash_fwd(q, k, v, B, S, H, KV, D, scale, causal, window)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.cfg = (B, S, H, KV, D, causal, window, scale)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        B, S, H, KV, D, causal, window, scale = ctx.cfg
+        do = do.contiguous()
+        q, k, v = _split(qkv, B, S, H, KV, D)
+        dqkv = torch.empty_like(qkv)
+        dq, dk, dv = _split(dqkv, B, S, H, KV, D)
+        ext().flash_bwd(q, k, v, o, do, lse, dq, dk, dv, B, S, H, KV, D, scale, causal, window)
+        return dqkv, None, None, None, None, None, None, None, None
+
+
+def attention_packed(qkv: torch.Tensor, B: int, S: int, H: int, KV: int, D: int, causal: bool = True,
+                     window: int = 0, scale: float | None = None) -> torch.Tensor:
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if use_hip(qkv) and qkv.dtype == torch.bfloat16 and flash_supported(D, S):
+        return _FlashPacked.apply(qkv, B, S, H, KV, D, causal, int(window or 0), scale)
+    return _sdpa_packed(qkv, B, S, H, KV, D, causal, window, scale)
+
+
+def attention_reference(qkv, B, S, H, KV, D, causal=True, window=0, scale=None):
+    """fp32 math reference used by the kernel numerics tests."""
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    q, k, v = (t.float() for t in _split(qkv, B, S, H, KV, D))
+    q = q.reshape(B, S, H, D).transpose(1, 2)
+    k = k.reshape(B, S, KV, D).transpose(1, 2).repeat_interleave(H // KV, dim=1)
+    v = v.reshape(B, S, KV, D).transpose(1, 2).repeat_interleave(H // KV, dim=1)
+    s = (q @ k.transpose(-1, -2)) * scale
+    i = torch.arange(S, device=qkv.device)
+    allowed = torch.ones(S, S, dtype=torch.bool, device=qkv.device)
+    if causal:
+        allowed &= i[None, :] <= i[:, None]
+    if window and window > 0:
+        allowed &= (i[:, None] - i[None, :]) < window
+    s = s.masked_fill(~allowed, float("-inf"))
+    p = s.softmax(-1)
+    return (p @ v).transpose(1, 2).reshape(B * S, H * D)

@@ -1,0 +1,166 @@
+"""QLoRA: NF4 base weights (K8) and the LoRA linear over them.
+
+``NF4Weight`` stores a frozen ``[out, in]`` weight as 4-bit NormalFloat codes (blocks of 64, one
+absmax per block) with double quantisation of the absmax vector (uint8 codes + one fp32 scale per
+256 absmaxes + a global offset): 0.5 + 1/64 + 4/16384 bytes per parameter, i.e. Mistral-7B's
+7.2 B projection parameters take ≈3.7 GB instead of 14.5 GB.
+
+Two GEMM paths, picked per call by shape:
+
+* **fused** -- ``nf4_linear`` (``csrc/kernels/nf4_gemm.hip``): the NF4 decode happens in the MFMA
+  kernel's B-operand staging (packed nibbles -> codebook -> x absmax -> bf16 LDS tile), so the bf16
+  weight never exists in HBM.  Best when the weight stream dominates (few rows: decode, small
+  micro-batches);
+* **dequant + hipBLASLt** -- decode the whole weight into a transient bf16 buffer (one streaming
+  kernel, ≈4.5 B/param of traffic) and run the library GEMM; best at training-sized M where the
+  GEMM is compute bound and the decode is a few % of it.
+
+The backward needs ``W`` again for ``dx = dy W`` and re-decodes it (nothing weight-sized is saved).
+"""
+from __future__ import annotations
+
+import torch
+
+from ._backend import ext, use_hip
+from .linear import _mask_blocks
+
+NF4_CODE = torch.tensor([-1.0, -0.6961928009986877, -0.5250730514526367, -0.39491748809814453, -0.28444138169288635,
+                         -0.18477343022823334, -0.09105003625154495, 0.0, 0.07958029955625534, 0.16093020141124725,
+                         0.24611230194568634, 0.33791524171829224, 0.44070982933044434, 0.5626170039176941,
+                         0.7229568362236023, 1.0])
+
+FUSED_MAX_ROWS = 512  # below this many activation rows the fused NF4 GEMM wins (weight-stream bound)
+
+
+class NF4Weight:
+    def __init__(self, packed, absmax_q, absmax_scale, absmax_offset: float, shape, block=64, block2=256):
+        self.packed, self.absmax_q, self.absmax_scale = packed, absmax_q, absmax_scale
+        self.absmax_offset = float(absmax_offset)
+        self.shape = tuple(shape)
+        self.block, self.block2 = block, block2
+
+    @property
+    def device(self):
+        return self.packed.device
+
+    def nbytes(self) -> int:
+        return self.packed.numel() + self.absmax_q.numel() + 4 * self.absmax_scale.numel()
+
+    @classmethod
+    @torch.no_grad()
+    def quantize(cls, w: torch.Tensor, block: int = 64, block2: int = 256) -> "NF4Weight":
+        rows, cols = w.shape
+        flat = w.reshape(-1)
+        if use_hip(w) and w.dtype == torch.bfloat16:
+            packed, absmax = ext().nf4_quantize(flat.contiguous(), block)
+        else:
+            packed, absmax = _quantize_ref(flat, block)
+        offset = float(absmax.mean().item())
+        centered = absmax - offset
+        nb2 = (absmax.numel() + block2 - 1) // block2
+        pad = nb2 * block2 - absmax.numel()
+        c2 = torch.nn.functional.pad(centered, (0, pad)).view(nb2, block2)
+        scale2 = c2.abs().amax(1).clamp_min(1e-12)
+        q2 = torch.round(c2 / scale2[:, None] * 127.0 + 128.0).clamp(0, 255).to(torch.uint8).reshape(-1)[: absmax.numel()]
+        return cls(packed, q2.contiguous(), scale2.float().contiguous(), offset, (rows, cols), block, block2)
+
+    def absmax(self) -> torch.Tensor:
+        idx = torch.arange(self.absmax_q.numel(), device=self.absmax_q.device) // self.block2
+        return self.absmax_offset + (self.absmax_q.float() - 128.0) / 127.0 * self.absmax_scale[idx]
+
+    def dequantize(self, dtype=torch.bfloat16) -> torch.Tensor:
+        if use_hip(self.packed):
+            return ext().nf4_dequantize(self.packed, self.absmax_q, self.absmax_scale, self.absmax_offset,
+                                        self.shape[0], self.shape[1], self.block, self.block2)
+        return dequantize_reference(self).to(dtype)
+
+
+def _quantize_ref(flat: torch.Tensor, block: int):
+    x = flat.float().view(-1, block)
+    absmax = x.abs().amax(1)
+    xn = x / absmax.clamp_min(1e-30)[:, None]
+    code = NF4_CODE.to(flat.device)
+    q = (xn[..., None] - code).abs().argmin(-1).to(torch.uint8).reshape(-1)
+    packed = (q[0::2] << 4) | q[1::2]
+    return packed.contiguous(), absmax
+
+
+def dequantize_reference(q: NF4Weight) -> torch.Tensor:
+    code = NF4_CODE.to(q.packed.device)
+    hi = (q.packed >> 4).long()
+    lo = (q.packed & 0xF).long()
+    vals = torch.stack([code[hi], code[lo]], dim=1).reshape(-1)
+    am = q.absmax().repeat_interleave(q.block)
+    return (vals * am).view(q.shape)
+
+
+def nf4_matmul(x2: torch.Tensor, qw: NF4Weight) -> torch.Tensor:
+    """x2 [M, K] @ W^T with W stored NF4 -> [M, N] (bf16)."""
+    M = x2.shape[0]
+    N, K = qw.shape
+    if (use_hip(x2) and M <= FUSED_MAX_ROWS and K % 64 == 0 and N % 64 == 0 and qw.block == 64
+            and getattr(ext(), "nf4_gemm_ready", lambda: False)()):
+        return ext().nf4_linear(x2.contiguous(), qw.packed, qw.absmax_q, qw.absmax_scale, qw.absmax_offset, N,
+                                qw.block, qw.block2)
+    W = qw.dequantize(x2.dtype)
+    return x2 @ W.t()
+
+
+class _QLoRALinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, A, B, qw, scale, blocks):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1])
+        y = nf4_matmul(x2, qw)
+        xa = None
+        if A is not None:
+            xa = x2 @ A.t()
+            y.addmm_(xa, B.t(), alpha=scale)
+        ctx.save_for_backward(x2, A, B, xa)
+        ctx.qw, ctx.scale, ctx.blocks, ctx.shp = qw, scale, blocks, shp
+        return y.view(*shp[:-1], qw.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, A, B, xa = ctx.saved_tensors
+        s = ctx.scale
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dx = dA = dB = None
+        dyb = dy2 @ B if A is not None else None
+        if ctx.needs_input_grad[0]:
+            W = ctx.qw.dequantize(dy2.dtype)
+            dx = dy2 @ W
+            del W
+            if dyb is not None:
+                dx.addmm_(dyb, A, alpha=s)
+            dx = dx.view(ctx.shp)
+        if A is not None:
+            if ctx.needs_input_grad[2]:
+                dB = _mask_blocks(torch.mm(dy2.t(), xa) * s, ctx.blocks)
+            if ctx.needs_input_grad[1]:
+                dA = torch.mm(dyb.t(), x2) * s
+        return dx, dA, dB, None, None, None
+
+
+def qlora_linear(x, qw: NF4Weight, A=None, B=None, scale=1.0, blocks=None):
+    return _QLoRALinearFn.apply(x, A, B, qw, scale, blocks)
+
+
+@torch.no_grad()
+def quantize_model_(model) -> int:
+    """Replace every frozen projection weight of a Llama/Mistral model by an NF4Weight (in place).
+
+    Returns bytes saved.  Embeddings, norms and lm_head stay bf16 (QLoRA convention)."""
+    if model.cfg.family != "llama":
+        raise ValueError("QLoRA quantisation is implemented for the Llama/Mistral trunk")
+    saved = 0
+    for layer in model.layers:
+        for name, attr in (("qkv", "wqkv"), ("o", "wo"), ("gu", "wgu"), ("down", "wdown")):
+            W = getattr(layer, attr)
+            qw = NF4Weight.quantize(W.data)
+            layer.qweights[name] = qw
+            saved += W.numel() * W.element_size() - qw.nbytes()
+            setattr(layer, attr, torch.nn.Parameter(torch.empty(0, device=W.device, dtype=W.dtype), requires_grad=False))
+    if torch.cuda.is_available():
+        torch.cuda.empty_cache()
+    return saved

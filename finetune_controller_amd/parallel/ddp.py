@@ -1,0 +1,132 @@
+"""Bucketed, backward-overlapped gradient all-reduce over the flat grad buffer (N1).
+
+The optimizer (``train.optim.FlatAdamW``) lays every trainable parameter's gradient out in ONE
+flat buffer in the order backward produces them.  This module cuts that buffer into contiguous
+buckets of ``bucket_mb`` and launches an asynchronous SUM all-reduce of a bucket the moment the
+last gradient inside it has been written -- while backward keeps computing earlier layers.  No
+gradient is ever copied into or out of a staging buffer.
+
+Readiness signals:
+* parameters whose grads flow through autograd's ``AccumulateGrad`` (LoRA A/B, norms, embeddings)
+  -> ``register_post_accumulate_grad_hook``;
+* frozen-shape base weights in full fine-tuning, whose GEMM backward adds straight into
+  ``main_grad`` -> the ``ops.linear`` grad-ready hook.
+
+Parameters used more than once per step (tied embeddings) are deferred to ``finish()``.
+
+Transport: ``torch.distributed`` (ProcessGroupNCCL == RCCL over xGMI on MI355X; gloo on CPU), or the
+native engine in ``parallel.comm`` (own RCCL communicator + dedicated high-priority HIP stream)
+with ``engine="native"``.  Averaging is NOT done here: the optimizer folds 1/world into its
+device-side grad scale, saving a full pass over the buffer.
+
+Bucket sizing for MI355X: each GPU has 7 xGMI links of ≈153 GB/s; a ring
+all-reduce is per-link bound, so buckets must be large enough for RCCL to spread over several
+channels (default 64 MB) but small enough that the last bucket -- which cannot overlap -- stays
+short.  LoRA grads (27-84 MB) fit 1-2 buckets; full FT (16 GB bf16) ~250 buckets.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from ..ops import linear as _linear
+
+
+class GradBucketer:
+    def __init__(self, optimizer, bucket_mb: float = 64.0, group=None, engine: str = "torch",
+                 multi_use_params=()):
+        self.opt = optimizer
+        self.group = group
+        self.engine = engine
+        self.enabled = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        self.world = dist.get_world_size(group) if self.enabled else 1
+        esize = optimizer.grad_flat.element_size()
+        cap = max(1, int(bucket_mb * 1024 * 1024 / esize))
+        self.buckets: list[tuple[int, int]] = []  # (start, end) element ranges of grad_flat
+        self.param_bucket: dict[int, int] = {}
+        self.pending: list[int] = []
+        multi = {id(p) for p in multi_use_params}
+        self.deferred = []
+        start = 0
+        cur_end = 0
+        members: list[list[int]] = [[]]
+        for p, (o, n) in zip(optimizer.params, optimizer.offsets):
+            if id(p) in multi:
+                self.deferred.append((o, n))
+                continue
+            if cur_end - start >= cap and members[-1]:
+                self.buckets.append((start, cur_end))
+                members.append([])
+                start = cur_end
+            members[-1].append(id(p))
+            cur_end = o + n
+        if members[-1]:
+            self.buckets.append((start, cur_end))
+        self.members = members
+        for b, ids in enumerate(members):
+            for pid in ids:
+                self.param_bucket[pid] = b
+        self._native = None
+        if self.enabled and engine == "native":
+            from .comm import NativeAllReduce
+
+            self._native = NativeAllReduce(group)
+        self.armed = True  # False on non-final micro-batches of gradient accumulation
+        self._hooks = []
+        if self.enabled:
+            for p in optimizer.params:
+                if id(p) in self.param_bucket:
+                    self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+            _linear.set_grad_ready_hook(self._on_grad)
+        self.reset()
+
+    def reset(self):
+        self.remaining = [len(m) for m in self.members]
+        self.seen: set[int] = set()
+        self.works = []
+        self.launched = [False] * len(self.buckets)
+
+    def _on_grad(self, p):
+        if not self.armed:
+            return
+        pid = id(p)
+        b = self.param_bucket.get(pid)
+        if b is None or pid in self.seen:
+            return
+        self.seen.add(pid)
+        self.remaining[b] -= 1
+        if self.remaining[b] == 0:
+            self._launch(b)
+
+    def _launch(self, b: int):
+        if self.launched[b]:
+            return
+        self.launched[b] = True
+        s, e = self.buckets[b]
+        view = self.opt.grad_flat[s:e]
+        if self._native is not None:
+            self.works.append(self._native.all_reduce_async(view))
+        else:
+            self.works.append(dist.all_reduce(view, group=self.group, async_op=True))
+
+    def finish(self):
+        """Launch anything not yet launched (unused params, deferred tied weights) and wait."""
+        if not self.enabled:
+            return
+        for b in range(len(self.buckets)):
+            if not self.launched[b]:
+                self._launch(b)
+        for o, n in self.deferred:
+            view = self.opt.grad_flat[o:o + n]
+            if self._native is not None:
+                self.works.append(self._native.all_reduce_async(view))
+            else:
+                self.works.append(dist.all_reduce(view, group=self.group, async_op=True))
+        for w in self.works:
+            w.wait()
+        self.reset()
+
+    def close(self):
+        for h in self._hooks:
+            h.remove()
+        _linear.set_grad_ready_hook(None)

@@ -1,0 +1,96 @@
+"""Process-group bootstrap: one process per GPU, rendezvous from the env the training operator
+(or torchrun) injects -- ``MASTER_ADDR/MASTER_PORT/WORLD_SIZE/RANK/LOCAL_RANK``
+(reference injects only ``NCCL_DEBUG`` at
+``/root/reference/app/jobs/kubeflow/PyTorchJobDeployer.py:115``).
+
+On ROCm the ``nccl`` backend of torch.distributed IS RCCL; collectives run over xGMI inside a node.
+CPU runs (tests, the CPU plumbing job) use ``gloo``.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1
+
+
+def init_distributed(device_type: str = "auto", timeout_s: int = 1800) -> DistInfo:
+    """Initialise torch.distributed when WORLD_SIZE > 1; bind this rank to its GPU."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if device_type == "auto":
+        # device_count() does not initialise the HIP runtime on this image; is_available() does
+        device_type = "cuda" if torch.cuda.device_count() > 0 and torch.cuda.is_available() else "cpu"
+    if device_type == "cuda":
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    backend = "none"
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        backend = "nccl" if device.type == "cuda" else "gloo"
+        if not dist.is_initialized():
+            kw = {}
+            if backend == "nccl":
+                kw["device_id"] = device
+            dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                    timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return DistInfo(rank, world, local, backend, device)
+
+
+def barrier(info: DistInfo):
+    if info.distributed:
+        if info.backend == "nccl":
+            dist.barrier(device_ids=[info.local_rank])
+        else:
+            dist.barrier()
+
+
+def all_reduce_max(x: float, info: DistInfo) -> float:
+    if not info.distributed:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=info.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def all_reduce_mean_(t: torch.Tensor, info: DistInfo) -> torch.Tensor:
+    if info.distributed:
+        dist.all_reduce(t)
+        t /= info.world_size
+    return t
+
+
+def broadcast_params_(params, info: DistInfo, src: int = 0):
+    """Make every rank start from rank 0's weights (N2 in SURVEY.md §2.3)."""
+    if not info.distributed:
+        return
+    for p in params:
+        dist.broadcast(p.data, src=src)
+
+
+def destroy(info: DistInfo):
+    if info.distributed and dist.is_initialized():
+        dist.destroy_process_group()

@@ -1,0 +1,207 @@
+"""Token data for the worker: synthetic streams (benchmarks) and the dataset the controller's
+init container drops into ``/data/dataset`` (``/root/reference/app/jobs/kubeflow/PyTorchJobDeployer.py:70-91``).
+
+Dataset formats accepted in ``--dataset_path`` (a file, or a directory holding one):
+
+* ``*.bin`` / ``*.tokens``  -- raw little-endian uint16 (vocab <= 65536) or uint32 token ids
+  (``.u32.bin``), memory-mapped and packed by the native loader (``csrc/runtime/token_loader.cpp``);
+* ``*.npy``                 -- 1-D integer token array (``allow_pickle=False``);
+* ``*.jsonl`` / ``*.json``  -- records with a ``text`` field (or ``prompt``/``completion``);
+* ``*.txt`` / ``*.csv``     -- text, one sample per line (CSV: first text-like column).
+
+Text is tokenised with a ``tokenizer.json`` found next to the data (HF ``tokenizers``) or, failing
+that, a byte-level fallback (ids = bytes + 3, so the vocab must be >= 259).  Samples are packed into
+fixed ``[batch, seq_len]`` blocks with next-token labels.
+"""
+from __future__ import annotations
+
+import csv
+import glob
+import json
+import os
+from pathlib import Path
+
+import numpy as np
+import torch
+
+
+class SyntheticTokens:
+    """Uniform random token ids of the configured shape (the benchmark contract's synthetic data)."""
+
+    def __init__(self, vocab: int, batch: int, seq_len: int, device, seed: int = 0):
+        self.vocab, self.batch, self.seq_len, self.device = vocab, batch, seq_len, device
+        self.gen = torch.Generator(device="cpu").manual_seed(seed)
+        # a small pool of pre-generated batches on device: no host->device copy in the timed loop
+        self.pool = [torch.randint(0, vocab, (batch, seq_len + 1), generator=self.gen).to(device) for _ in range(4)]
+        self.i = 0
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        t = self.pool[self.i % len(self.pool)]
+        self.i += 1
+        return t[:, :-1], t[:, 1:]
+
+    def state(self):
+        return {"i": self.i}
+
+    def load_state(self, st):
+        self.i = int(st.get("i", 0))
+
+
+def _find_data_file(path: str) -> str | None:
+    if not path or not os.path.exists(path):
+        return None
+    if os.path.isfile(path):
+        return path
+    cands = []
+    for pat in ("*.bin", "*.tokens", "*.npy", "*.jsonl", "*.json", "*.txt", "*.csv"):
+        cands += sorted(glob.glob(os.path.join(path, "**", pat), recursive=True))
+    cands = [c for c in cands if not os.path.basename(c).startswith("tokenizer")]
+    return cands[0] if cands else None
+
+
+def _texts(path: str):
+    ext = Path(path).suffix.lower()
+    if ext in (".jsonl", ".json"):
+        with open(path, encoding="utf-8") as f:
+            head = f.read(1)
+            f.seek(0)
+            rows = json.load(f) if (ext == ".json" and head == "[") else (json.loads(l) for l in f if l.strip())
+            for r in rows:
+                if isinstance(r, str):
+                    yield r
+                elif "text" in r:
+                    yield str(r["text"])
+                else:
+                    yield str(r.get("prompt", "")) + str(r.get("completion", r.get("response", "")))
+    elif ext == ".csv":
+        with open(path, encoding="utf-8", newline="") as f:
+            rd = csv.reader(f)
+            header = next(rd, None)
+            col = 0
+            if header:
+                for i, h in enumerate(header):
+                    if h.lower() in ("text", "smiles", "sequence", "prompt", "content"):
+                        col = i
+                        break
+            for row in rd:
+                if row:
+                    yield row[col]
+    else:
+        with open(path, encoding="utf-8", errors="replace") as f:
+            for line in f:
+                if line.strip():
+                    yield line.rstrip("\n")
+
+
+class Tokenizer:
+    def __init__(self, data_path: str | None, vocab: int):
+        self.vocab = vocab
+        self.tk = None
+        self.eos = 2
+        cand = None
+        if data_path:
+            d = data_path if os.path.isdir(data_path) else os.path.dirname(data_path)
+            p = os.path.join(d, "tokenizer.json")
+            cand = p if os.path.exists(p) else None
+        if cand:
+            from tokenizers import Tokenizer as HFTok
+
+            self.tk = HFTok.from_file(cand)
+        elif vocab < 259:
+            raise ValueError("byte-level fallback tokenizer needs vocab >= 259")
+
+    def encode(self, text: str) -> list[int]:
+        if self.tk is not None:
+            return self.tk.encode(text).ids
+        return [b + 3 for b in text.encode("utf-8")]
+
+
+def load_token_array(path: str, vocab: int) -> np.ndarray:
+    """Return a 1-D int array of token ids for a dataset path (memory-mapped when binary)."""
+    f = _find_data_file(path)
+    if f is None:
+        raise FileNotFoundError(f"no dataset file under {path!r}")
+    ext = Path(f).suffix.lower()
+    if ext in (".bin", ".tokens"):
+        dt = np.uint32 if f.endswith(".u32.bin") or vocab > 65536 else np.uint16
+        return np.memmap(f, dtype=dt, mode="r")
+    if ext == ".npy":
+        return np.load(f, mmap_mode="r", allow_pickle=False)
+    tok = Tokenizer(path, vocab)
+    ids: list[int] = []
+    for t in _texts(f):
+        ids.extend(tok.encode(t))
+        ids.append(tok.eos)
+    arr = np.asarray(ids, dtype=np.int64)
+    if arr.size and int(arr.max()) >= vocab:
+        arr = arr % vocab
+    return arr
+
+
+class PackedTokenDataset:
+    """Fixed [batch, seq_len+1] windows over a token array, sharded by rank, epoch-shuffled.
+
+    Uses the native loader (C++ thread pool, prefetching pinned batches) when ``_rt.so`` is built,
+    otherwise numpy indexing.
+    """
+
+    def __init__(self, path: str, vocab: int, batch: int, seq_len: int, device, rank: int = 0, world: int = 1,
+                 seed: int = 0):
+        self.tokens = load_token_array(path, vocab)
+        self.vocab, self.batch, self.seq_len, self.device = vocab, batch, seq_len, device
+        self.rank, self.world, self.seed = rank, world, seed
+        n_windows = (len(self.tokens) - 1) // seq_len
+        if n_windows < 1:
+            raise ValueError(f"dataset has {len(self.tokens)} tokens; need > seq_len={seq_len}")
+        self.n_windows = n_windows
+        self.steps_per_epoch = max(1, n_windows // (batch * world))
+        self.epoch = 0
+        self.pos = 0
+        self._native = None
+        try:
+            from ..utils.native import NativeTokenLoader
+
+            if isinstance(self.tokens, np.memmap):
+                self._native = NativeTokenLoader(self.tokens.filename, self.tokens.dtype.itemsize, seq_len, batch,
+                                                 rank, world, seed)
+        except Exception:
+            self._native = None
+        self._perm()
+
+    def _perm(self):
+        rng = np.random.default_rng(self.seed + self.epoch)
+        self.order = rng.permutation(self.n_windows)
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        if self._native is not None:
+            arr = self._native.next_batch()  # [batch, seq_len+1] int64 (pinned)
+            self.pos += 1
+            if self.pos >= self.steps_per_epoch:
+                self.pos, self.epoch = 0, self.epoch + 1
+        else:
+            if self.pos >= self.steps_per_epoch:
+                self.pos, self.epoch = 0, self.epoch + 1
+                self._perm()
+            base = (self.pos * self.world + self.rank) * self.batch
+            idx = [self.order[(base + i) % self.n_windows] for i in range(self.batch)]
+            S = self.seq_len
+            arr = np.stack([np.asarray(self.tokens[j * S: j * S + S + 1], dtype=np.int64) for j in idx])
+            arr = torch.from_numpy(arr)
+            self.pos += 1
+        t = arr.to(self.device, non_blocking=True)
+        return t[:, :-1], t[:, 1:]
+
+    def state(self):
+        return {"epoch": self.epoch, "pos": self.pos}
+
+    def load_state(self, st):
+        self.epoch, self.pos = int(st.get("epoch", 0)), int(st.get("pos", 0))
+        self._perm()
+        if self._native is not None:
+            self._native.seek(self.epoch, self.pos)

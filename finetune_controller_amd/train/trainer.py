@@ -1,0 +1,245 @@
+"""The worker-side training loop: full fine-tune, LoRA and QLoRA for GPT-2 / Llama-3 / Mistral.
+
+This is the piece the reference delegates to an opaque container image.  It
+honours that image's contract with the controller:
+
+* flags ``--dataset_path`` / ``--checkpoint_path`` (mounts ``/data/dataset`` and ``/data/artifacts``,
+  ``/root/reference/app/models/examples/mnist.py:95-96``);
+* ``metrics.csv`` appended every log interval (ingested by the monitor);
+* log lines that contain ``Epoch`` (the UI log stream suppresses everything before the first one,
+  ``/root/reference/app/utils/stream_logger.py:404-418``);
+* flat, uniquely named artifacts matching the model's ``store_asset_patterns``;
+* restart-safe: resumes from the newest ``checkpoint_step*.pt`` (backoffLimit restarts,
+  ``/root/reference/app/jobs/kubeflow/PyTorchJobDeployer.py:183``).
+
+Distributed: one process per GPU; gradients of the flat buffer are all-reduced in buckets
+overlapped with backward (``parallel.ddp``); the optimizer averages via its device-side scale.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import math
+import os
+import time
+from dataclasses import asdict, dataclass, field
+
+import torch
+
+from ..models import LoRAConfig, build_model, get_config
+from ..models import checkpoint as ckpt
+from ..parallel import dist as pdist
+from ..parallel.ddp import GradBucketer
+from ..utils.metrics import MetricsCSV
+from .data import PackedTokenDataset, SyntheticTokens
+from .optim import FlatAdamW, lr_at
+
+log = logging.getLogger("ftc.train")
+
+
+@dataclass
+class TrainConfig:
+    model: str = "llama3-8b"
+    method: str = "lora"  # lora | qlora | full
+    lora_r: int = 16
+    lora_alpha: float = 32.0
+    lora_targets: list[str] = field(default_factory=lambda: ["q_proj", "k_proj", "v_proj", "o_proj", "gate_proj",
+                                                              "up_proj", "down_proj"])
+    batch_size: int = 4  # micro-batch per GPU
+    seq_len: int = 4096
+    grad_accum: int = 1
+    epochs: int = 1
+    max_steps: int = 0  # 0 = epochs x steps_per_epoch (synthetic data: 100)
+    lr: float = 2e-4
+    warmup_steps: int = 10
+    schedule: str = "cosine"
+    weight_decay: float = 0.0
+    max_grad_norm: float = 1.0
+    seed: int = 1
+    dataset_path: str = ""
+    checkpoint_path: str = "./artifacts"
+    log_interval: int = 10
+    save_every: int = 0
+    resume: bool = True
+    synthetic: bool = False
+    bucket_mb: float = 64.0
+    comm_engine: str = "torch"  # torch | native
+    checkpoint_layers: bool = False
+    init_from: str = ""
+    dtype: str = "auto"  # auto: bf16 on GPU, fp32 on CPU
+    device: str = "auto"
+    ce_chunk_rows: int = 4096
+    save_model: bool = True
+
+    def lora_config(self) -> LoRAConfig | None:
+        if self.method not in ("lora", "qlora"):
+            return None
+        return LoRAConfig(r=self.lora_r, alpha=self.lora_alpha, target_modules=list(self.lora_targets))
+
+
+class Trainer:
+    def __init__(self, tc: TrainConfig):
+        self.tc = tc
+        self.info = pdist.init_distributed(tc.device)
+        self.device = self.info.device
+        torch.manual_seed(tc.seed)
+        if tc.dtype == "auto":
+            self.dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
+        else:
+            self.dtype = {"bf16": torch.bfloat16, "fp32": torch.float32, "bfloat16": torch.bfloat16,
+                          "float32": torch.float32}[tc.dtype]
+        self.cfg = get_config(tc.model)
+        if tc.seq_len > self.cfg.max_seq_len:
+            self.cfg.max_seq_len = tc.seq_len
+        self.lora = tc.lora_config()
+        self.model = build_model(self.cfg, self.lora, device=self.device, dtype=self.dtype,
+                                 checkpoint_layers=tc.checkpoint_layers)
+        self.model.ce_chunk_rows = tc.ce_chunk_rows
+        self.model.init_weights(seed=tc.seed)
+        if tc.init_from:
+            n = ckpt.load_hf_checkpoint(self.model, tc.init_from)
+            log.info("loaded %d tensors from %s", n, tc.init_from)
+        if tc.method in ("lora", "qlora"):
+            self.model.freeze_base()
+        if tc.method == "qlora":
+            from ..ops.nf4 import quantize_model_
+
+            quantize_model_(self.model)
+        self.model.train()
+        self.opt = FlatAdamW([p for p in self.model.parameters() if p.requires_grad], lr=tc.lr,
+                             weight_decay=tc.weight_decay, max_grad_norm=tc.max_grad_norm,
+                             grad_scale=1.0 / (self.info.world_size * tc.grad_accum))
+        # the loss is a per-micro-batch mean; summing grads over accum x world and scaling once
+        # in the optimizer gives the global mean
+        if self.info.distributed:
+            torch.distributed.broadcast(self.opt.param_flat, src=0)
+            if tc.method == "full":
+                pdist.broadcast_params_([p for p in self.model.parameters() if not p.requires_grad], self.info)
+        tied = [self.model.lm_head] if self.cfg.tie_embeddings and tc.method == "full" else []
+        self.ddp = GradBucketer(self.opt, tc.bucket_mb, engine=tc.comm_engine, multi_use_params=tied)
+        self._data = None
+        self.step = 0
+        self.is_main = self.info.is_main
+
+    # ------------------------------------------------------------------ data
+    def data(self):
+        if self._data is None:
+            tc = self.tc
+            if tc.synthetic or not tc.dataset_path or not os.path.exists(tc.dataset_path) or not os.listdir(
+                    tc.dataset_path if os.path.isdir(tc.dataset_path) else os.path.dirname(tc.dataset_path)):
+                self._data = SyntheticTokens(self.cfg.vocab_size, tc.batch_size, tc.seq_len, self.device,
+                                             seed=tc.seed + self.info.rank)
+                self.steps_per_epoch = 100
+            else:
+                self._data = PackedTokenDataset(tc.dataset_path, self.cfg.vocab_size, tc.batch_size, tc.seq_len,
+                                                self.device, self.info.rank, self.info.world_size, tc.seed)
+                self.steps_per_epoch = max(1, self._data.steps_per_epoch // tc.grad_accum)
+        return self._data
+
+    def total_steps(self) -> int:
+        self.data()
+        return self.tc.max_steps or self.tc.epochs * self.steps_per_epoch
+
+    # ------------------------------------------------------------------ one step
+    def train_step(self, lr: float) -> torch.Tensor:
+        """fwd + bwd (+accum) + overlapped all-reduce + optimizer. Returns the loss (device tensor)."""
+        tc = self.tc
+        data = self.data()
+        self.opt.zero_grad()
+        total = None
+        n_valid = tc.batch_size * tc.seq_len
+        for micro in range(tc.grad_accum):
+            x, y = next(data)
+            self.ddp.armed = micro == tc.grad_accum - 1
+            loss = self.model(x, y, n_valid=n_valid)
+            loss.backward()
+            total = loss.detach() if total is None else total + loss.detach()
+        self.ddp.finish()
+        self.opt.step(lr)
+        return total / tc.grad_accum
+
+    # ------------------------------------------------------------------ loop
+    def run(self) -> dict:
+        tc = self.tc
+        os.makedirs(tc.checkpoint_path, exist_ok=True)
+        total = self.total_steps()
+        start = 0
+        if tc.resume and (rp := ckpt.latest_resume(tc.checkpoint_path)):
+            st = ckpt.load_resume(rp, self.opt)
+            start = int(st["step"])
+            self.data().load_state(st.get("data", {}))
+            if self.is_main:
+                log.info("resumed from %s at step %d", os.path.basename(rp), start)
+        metrics = MetricsCSV(os.path.join(tc.checkpoint_path, "metrics.csv"), enabled=self.is_main,
+                             resume=start > 0)
+        tok_per_step = tc.batch_size * tc.seq_len * tc.grad_accum * self.info.world_size
+        flops_tok = self.cfg.flops_per_token(tc.seq_len, lora=tc.method != "full")
+        if self.is_main:
+            n_train = self.opt.num_params()
+            log.info("model=%s method=%s params=%.3fB trainable=%.2fM world=%d micro_batch=%d seq=%d accum=%d steps=%d",
+                     self.cfg.name, tc.method, self.cfg.num_params() / 1e9, n_train / 1e6, self.info.world_size,
+                     tc.batch_size, tc.seq_len, tc.grad_accum, total)
+        last = {}
+        sync = torch.cuda.synchronize if self.device.type == "cuda" else (lambda: None)
+        sync()
+        t0 = time.perf_counter()
+        losses = []
+        for step in range(start, total):
+            lr = lr_at(step, tc.lr, tc.warmup_steps, total, tc.schedule)
+            losses.append(self.train_step(lr))
+            self.step = step + 1
+            if self.step % tc.log_interval == 0 or self.step == total:
+                sync()
+                dt = time.perf_counter() - t0
+                n = len(losses)
+                loss_v = float(torch.stack(losses).float().mean().item())
+                step_ms = dt / n * 1000
+                tps = tok_per_step * n / dt
+                mem = torch.cuda.max_memory_allocated(self.device) / 1e9 if self.device.type == "cuda" else 0.0
+                epoch = step // max(1, self.steps_per_epoch)
+                last = {"epoch": epoch, "step": self.step, "loss": round(loss_v, 6), "lr": lr,
+                        "tokens_per_sec": round(tps, 1), "step_time_ms": round(step_ms, 2),
+                        "grad_norm": round(self.opt.grad_norm(), 6), "world_size": self.info.world_size,
+                        "mem_gb": round(mem, 2),
+                        "tflops_per_gpu": round(tps * flops_tok / self.info.world_size / 1e12, 1)}
+                if self.is_main:
+                    metrics.write(last)
+                    # "Epoch" marks the start of the UI-visible log (LOG_STREAM_SEARCH_STRING)
+                    print(f"Epoch {epoch} | step {self.step}/{total} | loss {loss_v:.4f} | lr {lr:.3e} | "
+                          f"{tps:,.0f} tok/s | {step_ms:.1f} ms/step | grad_norm {last['grad_norm']:.4f} | "
+                          f"mem {mem:.1f} GB", flush=True)
+                losses = []
+                t0 = time.perf_counter()
+            if tc.save_every and self.step % tc.save_every == 0 and self.step < total:
+                self.save_resume()
+        metrics.close()
+        if tc.save_model:
+            self.save_artifacts()
+        pdist.barrier(self.info)
+        return last
+
+    def save_resume(self):
+        if not self.is_main:
+            return
+        p = os.path.join(self.tc.checkpoint_path, f"checkpoint_step{self.step}.pt")
+        ckpt.save_resume(p, self.step, self.opt, self.data().state(), {"config": asdict(self.tc)})
+        # keep only the newest resume point
+        for old in os.listdir(self.tc.checkpoint_path):
+            if old.startswith("checkpoint_step") and old.endswith(".pt") and old != os.path.basename(p):
+                os.remove(os.path.join(self.tc.checkpoint_path, old))
+
+    def save_artifacts(self) -> list[str]:
+        if not self.is_main:
+            return []
+        out = self.tc.checkpoint_path
+        if self.lora is not None:
+            files = ckpt.save_adapter(self.model, out, self.cfg.name, self.lora)
+        else:
+            files = ckpt.save_full(self.model, out)
+        with open(os.path.join(out, "training_config.json"), "w") as f:
+            json.dump({"train": asdict(self.tc), "model": self.cfg.to_dict()}, f, indent=2, default=str)
+        return files
+
+    def close(self):
+        self.ddp.close()
+        pdist.destroy(self.info)

@@ -1,0 +1,151 @@
+"""Numerics of every gfx950 HIP kernel against a plain PyTorch fp32 reference of the same op.
+
+Run on an MI355X: ``python -m pytest tests -m gpu``.  These tests import the in-tree extension
+directly (``finetune_controller_amd._C``) and fail -- not skip -- when it is missing on a GPU box.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def C():
+    import finetune_controller_amd._C as C  # must load: native code is the point of these tests
+
+    return C
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("rows,d", [(257, 4096), (64, 768), (33, 128), (8, 8192)])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_rmsnorm_fwd_bwd(C, rows, d, with_res):
+    torch.manual_seed(0)
+    x = bf(torch.randn(rows, d, device=DEV))
+    r = bf(torch.randn(rows, d, device=DEV)) if with_res else None
+    w = bf(torch.rand(d, device=DEV) + 0.5)
+    y, rstd, h = C.rmsnorm_fwd(x, r, w, 1e-5)
+    href = (x.float() + r.float()) if with_res else x.float()
+    href_b = bf(href).float()
+    ref = href_b * torch.rsqrt(href_b.pow(2).mean(-1, keepdim=True) + 1e-5) * w.float()
+    torch.testing.assert_close(y.float(), ref, atol=2e-2, rtol=2e-2)
+    if with_res:
+        torch.testing.assert_close(h.float(), href_b, atol=0, rtol=0)
+    # backward vs autograd in fp32
+    dy = bf(torch.randn(rows, d, device=DEV))
+    dres = bf(torch.randn(rows, d, device=DEV))
+    hv = href_b.clone().requires_grad_(True)
+    wv = w.float().clone().requires_grad_(True)
+    out = hv * torch.rsqrt(hv.pow(2).mean(-1, keepdim=True) + 1e-5) * wv
+    out.backward(dy.float())
+    dx, dw = C.rmsnorm_bwd(dy, h if with_res else x, w, rstd, dres, True)
+    torch.testing.assert_close(dx.float(), hv.grad + dres.float(), atol=3e-2, rtol=3e-2)
+    torch.testing.assert_close(dw, wv.grad, atol=5e-2 * math.sqrt(rows), rtol=2e-2)
+
+
+def test_rope_roundtrip_and_reference(C):
+    from finetune_controller_amd.ops.rope import RotaryTable, _rope_ref
+
+    torch.manual_seed(0)
+    H, KV, D, B, S = 8, 2, 128, 2, 64
+    tab = RotaryTable(D, 256, 500000.0)
+    cos, sin = tab.get(DEV)
+    qkv = bf(torch.randn(B * S, (H + 2 * KV) * D, device=DEV))
+    ref = _rope_ref(qkv, cos, sin, H + KV, D, S, None, False)
+    out = qkv.clone()
+    C.rope_(out, cos, sin, None, H + KV, D, S, False)
+    torch.testing.assert_close(out.float(), ref.float(), atol=2e-2, rtol=2e-2)
+    # v untouched, inverse restores
+    assert torch.equal(out[:, (H + KV) * D:], qkv[:, (H + KV) * D:])
+    C.rope_(out, cos, sin, None, H + KV, D, S, True)
+    torch.testing.assert_close(out.float(), qkv.float(), atol=3e-2, rtol=3e-2)
+
+
+def test_swiglu(C):
+    torch.manual_seed(0)
+    gu = bf(torch.randn(300, 2 * 1024, device=DEV))
+    a = C.swiglu_fwd(gu)
+    g, u = gu.float().chunk(2, -1)
+    torch.testing.assert_close(a.float(), torch.nn.functional.silu(g) * u, atol=2e-2, rtol=2e-2)
+    da = bf(torch.randn(300, 1024, device=DEV))
+    gv = gu.float().clone().requires_grad_(True)
+    gg, uu = gv.chunk(2, -1)
+    (torch.nn.functional.silu(gg) * uu).backward(da.float())
+    dgu = C.swiglu_bwd(da, gu)
+    torch.testing.assert_close(dgu.float(), gv.grad, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("V", [128256, 32000, 50257])
+def test_cross_entropy_inplace(C, V):
+    torch.manual_seed(0)
+    n = 37
+    logits = bf(torch.randn(n, V, device=DEV) * 3)
+    labels = torch.randint(0, V, (n,), device=DEV)
+    labels[3] = -100
+    ref_logits = logits.float().clone().requires_grad_(True)
+    nval = int((labels != -100).sum())
+    loss_ref = torch.nn.functional.cross_entropy(ref_logits, labels, ignore_index=-100, reduction="sum") / nval
+    loss_ref.backward()
+    buf = logits.clone()
+    loss_rows = C.ce_fwd_bwd_(buf, labels, 1.0 / nval, -100)
+    torch.testing.assert_close(loss_rows.sum() / nval, loss_ref.detach(), atol=1e-3, rtol=1e-3)
+    assert loss_rows[3].item() == 0.0
+    torch.testing.assert_close(buf.float(), ref_logits.grad, atol=2e-3, rtol=5e-2)
+
+
+@pytest.mark.parametrize("gdtype", [torch.bfloat16, torch.float32])
+def test_adamw_flat(C, gdtype):
+    torch.manual_seed(0)
+    n = 10_003
+    master = torch.randn(n, device=DEV)
+    param = bf(master)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    ref = master.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([ref], lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    for step in range(1, 4):
+        g = torch.randn(n, device=DEV).to(gdtype)
+        ref.grad = g.float() * 0.5
+        opt.step()
+        stats = C.grad_sumsq(g, 0.0, 0.5)  # no clip, scale 0.5
+        C.adamw_(param, master, m, v, g, 1e-2, 0.9, 0.95, 1e-8, 0.1, step, stats[1:2])
+        torch.testing.assert_close(stats[0], (g.float() ** 2).sum(), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(master, ref.detach(), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(param.float(), bf(ref.detach()).float(), atol=1e-2, rtol=1e-2)
+
+
+def test_grad_clip_coef(C):
+    g = torch.full((4096,), 0.5, device=DEV)
+    stats = C.grad_sumsq(g, 1.0, 1.0)
+    norm = math.sqrt(4096 * 0.25)
+    assert abs(stats[1].item() - 1.0 / norm) < 1e-4
+
+
+def test_nf4_roundtrip(C):
+    from finetune_controller_amd.ops import nf4
+
+    torch.manual_seed(0)
+    w = bf(torch.randn(256, 512, device=DEV) * 0.02)
+    q = nf4.NF4Weight.quantize(w)
+    deq = q.dequantize()
+    ref = nf4.dequantize_reference(q)
+    torch.testing.assert_close(deq.float(), ref.float(), atol=1e-3, rtol=1e-2)
+    # NF4 error bound: half the widest code gap times absmax
+    assert (deq.float() - w.float()).abs().max().item() < 0.2 * w.abs().max().item()
+
+
+def test_lora_merge(C):
+    torch.manual_seed(0)
+    W = bf(torch.randn(384, 256, device=DEV))
+    A = bf(torch.randn(16, 256, device=DEV) * 0.1)
+    B = bf(torch.randn(384, 16, device=DEV) * 0.1)
+    ref = W.float() + 2.0 * (B.float() @ A.float())
+    C.lora_merge_(W, A, B, 2.0, 0)
+    torch.testing.assert_close(W.float(), ref, atol=3e-2, rtol=1e-2)

@@ -1,0 +1,52 @@
+#!/bin/bash
+# One gpurun session: GPU tests -> smoke -> short benches -> rocprofv3 kernel stats.
+# Every GPU step has its own timeout; a crash/abort/timeout (rc >= 124 or signal) ends the session.
+# Usage (from the repo root, on the GPU box): bash tools/gpu_session.sh [steps...]
+#   steps: tests smoke bench1l bench bench_torch prof  (default: all)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+mkdir -p gpurun_out
+STEPS=("$@")
+[ ${#STEPS[@]} -eq 0 ] && STEPS=(tests smoke bench1l bench bench_torch prof)
+
+fatal() {  # rc -> 0 if the session may continue
+  local rc=$1 name=$2
+  echo "[session] $name rc=$rc"
+  if [ "$rc" -ge 124 ] || [ "$rc" -eq 134 ] || [ "$rc" -eq 139 ]; then
+    echo "[session] $name crashed or timed out: stopping the session"
+    exit "$rc"
+  fi
+  return 0
+}
+
+for s in "${STEPS[@]}"; do
+  case "$s" in
+    tests)
+      timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
+      fatal $? tests; tail -5 gpurun_out/pytest_gpu.log ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+      fatal $? smoke; tail -3 gpurun_out/smoke.log ;;
+    bench1l)
+      timeout -k 10 300 python bench.py --model llama3-8b-1l --steps 5 --warmup 2 > gpurun_out/bench1l.log 2>&1
+      fatal $? bench1l; tail -2 gpurun_out/bench1l.log ;;
+    bench)
+      timeout -k 10 600 python bench.py --steps 10 --warmup 3 > gpurun_out/bench.log 2>&1
+      fatal $? bench; tail -2 gpurun_out/bench.log ;;
+    bench_b8)
+      timeout -k 10 600 python bench.py --steps 8 --warmup 3 --batch-size 8 > gpurun_out/bench_b8.log 2>&1
+      fatal $? bench_b8; tail -2 gpurun_out/bench_b8.log ;;
+    bench_torch)
+      timeout -k 10 600 python bench.py --steps 10 --warmup 3 --kernels torch > gpurun_out/bench_torch.log 2>&1
+      fatal $? bench_torch; tail -2 gpurun_out/bench_torch.log ;;
+    prof)
+      (cd /tmp && export TMPDIR=/tmp)
+      export TMPDIR=/tmp
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench \
+        -- python3 bench.py --steps 3 --warmup 2 > gpurun_out/prof.log 2>&1
+      fatal $? prof; ls -R gpurun_out/prof | head -20 ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
+echo "[session] done"
