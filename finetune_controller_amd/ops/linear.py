@@ -43,14 +43,21 @@ class _LoRALinearFn(torch.autograd.Function):
     def forward(ctx, x, W, bias, A, B, scale, blocks):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
-        y = x2 @ W.t() if bias is None else torch.addmm(bias, x2, W.t())
+        # allocate the output in its final shape: the returned tensor must not be a view (RoPE
+        # rotates it in place downstream)
+        out = torch.empty(*shp[:-1], W.shape[0], dtype=x.dtype, device=x.device)
+        y = out.view(-1, W.shape[0])
+        if bias is None:
+            torch.mm(x2, W.t(), out=y)
+        else:
+            torch.addmm(bias, x2, W.t(), out=y)
         xa = None
         if A is not None:
             xa = x2 @ A.t()
             y.addmm_(xa, B.t(), alpha=scale)
         ctx.save_for_backward(x2, W, A, B, xa)
         ctx.scale, ctx.blocks, ctx.shp, ctx.has_bias = scale, blocks, shp, bias is not None
-        return y.view(*shp[:-1], W.shape[0])
+        return out
 
     @staticmethod
     def backward(ctx, dy):

@@ -118,7 +118,7 @@ class _QLoRALinearFn(torch.autograd.Function):
             y.addmm_(xa, B.t(), alpha=scale)
         ctx.save_for_backward(x2, A, B, xa)
         ctx.qw, ctx.scale, ctx.blocks, ctx.shp = qw, scale, blocks, shp
-        return y.view(*shp[:-1], qw.shape[0])
+        return y if x.dim() == 2 else y.reshape(*shp[:-1], qw.shape[0]).clone()
 
     @staticmethod
     def backward(ctx, dy):
