@@ -1,0 +1,444 @@
+// K2: flash-attention backward for gfx950 (causal / sliding window, GQA, bf16, recompute P from LSE).
+//
+// Three launches, no float atomics anywhere (bitwise reproducible):
+//   1. delta[b,h,q] = sum_d dO*O                                   (streaming, one wave per row)
+//   2. dK/dV: one workgroup = 128 keys of one (batch, kv head); it sweeps ALL G = H/KV query heads
+//      of the group and every 32-row query slice that can see its keys, so dK and dV are complete
+//      when the workgroup ends (GQA summation inside the kernel, no cross-workgroup reduction).
+//         S  [q][k] = Q K^T    - LSE/scale   (accumulator pre-loaded with the row constant)
+//         dP'[q][k] = dO V^T   - delta
+//         P = exp2(c S), dS = P * dP'
+//         dV^T[d][k] += dO^T P        dK^T[d][k] += Q^T dS
+//      "key on the lane": S and dP' accumulators have the key on the MFMA lane, so they ARE the
+//      B operands of the two accumulating products (permuted-k order, guide §3), and the dO^T / Q^T
+//      A operands come from one LDS image each through ds_read_b64_tr_b16.
+//   3. dQ: one workgroup = 128 query rows of one (batch, q head); K/V tiles stream through LDS like the
+//      forward:  S^T = K Q^T, dP^T = V dO^T (query on the lane: LSE/delta are per-lane scalars),
+//      dQ^T[d][q] += K^T dS^T with K^T read by tr_b16 from the same K image.
+// The dQ pass recomputes S and dP (7 MFMA products per tile pair instead of 5) -- on MI355X the
+// alternative, summing dQ over key blocks with fp32 atomics, is bound by the ≈1.3 TB/s atomic rate
+// (≈4.3 GB of adds per Llama-3-8B layer at 16k tokens), slower than the extra MFMAs.
+#include "common.h"
+
+using namespace ftc;
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr float LOG2E = 1.4426950408889634f;
+
+FTC_DEV int swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+template <int D>
+FTC_DEV int lds_off(int r, int chunk) {
+  constexpr int NCH = D / 8;
+  return r * (D * 2) + 16 * ((chunk ^ swz(r)) & (NCH - 1));
+}
+FTC_DEV bf16x8 as_bf8(const uint4& v) { return __builtin_bit_cast(bf16x8, v); }
+FTC_DEV bf16x8 pack8_bf(const f32x16& p, int base) {
+  uint4 u;
+  u.x = pack_bf2(p[base + 0], p[base + 1]);
+  u.y = pack_bf2(p[base + 2], p[base + 3]);
+  u.z = pack_bf2(p[base + 4], p[base + 5]);
+  u.w = pack_bf2(p[base + 6], p[base + 7]);
+  return as_bf8(u);
+}
+// A operand (32 rows x 16 k, permuted k) via two transposed reads of an LDS image whose rows are k
+// and columns are the A rows: elements 0..3 <- image rows kb+4h+0..3, elements 4..7 <- +8.
+template <int D>
+FTC_DEV bf16x8 tr_operand(const char* img, int kb, int colbase, int hh, int lane) {
+  const int gi = lane >> 4, li = lane & 15;
+  const int trq = li >> 2, trp = li & 3;
+  const int col = colbase + 16 * (gi & 1) + 4 * trp;
+  const int chunk = col >> 3, half8 = (col & 7) ? 8 : 0;
+  const int r1 = kb + 4 * hh + trq;
+  s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + lds_off<D>(r1, chunk) + half8));
+  s16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + lds_off<D>(r1 + 8, chunk) + half8));
+  s16x8 va = {v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
+  return __builtin_bit_cast(bf16x8, va);
+}
+
+struct BwdArgs {
+  const uint16_t *q, *k, *v, *o, *dout;
+  const float* lse;
+  float* delta;
+  uint16_t *dq, *dk, *dv;
+  long long q_rs, kv_rs, o_rs, dq_rs, dkv_rs;
+  int B, S, H, KV;
+  float scale, c;  // c = scale * log2(e)
+  int causal, window;
+};
+
+// ---------------------------------------------------------------- 1. delta
+template <int D>
+__global__ __launch_bounds__(256) void bwd_delta_kernel(BwdArgs a) {
+  constexpr int CPH = D / 8;  // 16-byte chunks per head
+  const int lane = threadIdx.x & 63;
+  const long long rows = (long long)a.B * a.S;
+  const int nch = a.H * CPH;
+  for (long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += (long long)gridDim.x * 4) {
+    const uint16_t* orow = a.o + row * a.o_rs;
+    const uint16_t* drow = a.dout + row * a.o_rs;
+    const int b = (int)(row / a.S), s = (int)(row % a.S);
+    for (int c0 = 0; c0 < nch; c0 += 64) {
+      const int c = c0 + lane;
+      float acc = 0.f;
+      if (c < nch) {
+        float x[8], y[8];
+        unpack8(reinterpret_cast<const uint4*>(orow)[c], x);
+        unpack8(reinterpret_cast<const uint4*>(drow)[c], y);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc += x[j] * y[j];
+      }
+#pragma unroll
+      for (int off = CPH / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+      if (c < nch && (c % CPH) == 0) {
+        const int h = c / CPH;
+        a.delta[((long long)b * a.H + h) * a.S + s] = acc;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- 2. dK / dV
+template <int D>
+__global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(BwdArgs a) {
+  constexpr int NCH = D / 8, DSTEPS = D / 16, DT = D / 32;
+  constexpr int BKV = 128, BQ2 = 32;
+  constexpr int KBYTES = BKV * D * 2, QBYTES = BQ2 * D * 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Ks = smem;                      // [128 keys][D]
+  char* Qs = smem + KBYTES;             // [32 q][D]
+  char* Ds = Qs + QBYTES;               // [32 q][D]  (dO)
+  float* lse_s = reinterpret_cast<float*>(Ds + QBYTES);   // [32] (-lse/scale)
+  float* dlt_s = lse_s + BQ2;                            // [32] (-delta)
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hh = lane >> 5, lr = lane & 31;
+  const int S = a.S, G = a.H / a.KV;
+  const int nkb = S / BKV;
+  // heavy-first: early key blocks see the most (causal) query rows
+  const int kb = blockIdx.x % nkb;
+  const int bk = blockIdx.x / nkb;
+  const int kvh = bk % a.KV, b = bk / a.KV;
+  const int kv0 = kb * BKV;
+  const int key = kv0 + wave * 32 + lr;  // this lane's key
+
+  // stage the key block's K rows into LDS; V^T fragments for dP go to registers
+  const uint16_t* kbase = a.k + ((long long)b * S) * a.kv_rs + (long long)kvh * D;
+  {
+    constexpr int RPP = 256 / NCH;
+    const int lrow = tid / NCH, lch = tid % NCH;
+#pragma unroll
+    for (int p = 0; p < BKV / RPP; ++p) {
+      const int r = p * RPP + lrow;
+      *reinterpret_cast<uint4*>(Ks + lds_off<D>(r, lch)) =
+          *reinterpret_cast<const uint4*>(kbase + (long long)(kv0 + r) * a.kv_rs + lch * 8);
+    }
+  }
+  bf16x8 vf[DSTEPS];
+  {
+    const uint16_t* vp = a.v + ((long long)b * S + key) * a.kv_rs + (long long)kvh * D + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < DSTEPS; ++s) vf[s] = as_bf8(*reinterpret_cast<const uint4*>(vp + 16 * s));
+  }
+
+  f32x16 dv[DT], dk[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { dv[t][i] = 0.f; dk[t][i] = 0.f; }
+
+  // query range that can see this key block
+  int qbeg = a.causal ? kv0 : 0;
+  int qend = S;
+  if (a.window > 0) qend = min(S, kv0 + BKV - 1 + a.window);
+  qbeg = (qbeg / BQ2) * BQ2;
+  const int nqt = (qend - qbeg + BQ2 - 1) / BQ2;
+  const float inv_scale = 1.0f / a.scale;
+
+  // staging: 32 rows x D of Q and of dO per tile; 256 threads x 16 B = 4 KB per pass
+  constexpr int RPP2 = 256 / NCH, NP2 = BQ2 / RPP2;
+  const int lrow = tid / NCH, lch = tid % NCH;
+  uint4 qreg[NP2], dreg[NP2];
+  float lreg = 0.f, dlreg = 0.f;
+  auto gload = [&](int hq, int qt) {
+    const uint16_t* qp = a.q + ((long long)b * S + qt) * a.q_rs + (long long)hq * D;
+    const uint16_t* dp = a.dout + ((long long)b * S + qt) * a.o_rs + (long long)hq * D;
+#pragma unroll
+    for (int p = 0; p < NP2; ++p) {
+      const int r = p * RPP2 + lrow;
+      qreg[p] = *reinterpret_cast<const uint4*>(qp + (long long)r * a.q_rs + lch * 8);
+      dreg[p] = *reinterpret_cast<const uint4*>(dp + (long long)r * a.o_rs + lch * 8);
+    }
+    if (tid < BQ2) {
+      const long long idx = ((long long)b * a.H + hq) * S + qt + tid;
+      lreg = -a.lse[idx] * inv_scale;
+      dlreg = -a.delta[idx];
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int p = 0; p < NP2; ++p) {
+      const int r = p * RPP2 + lrow;
+      *reinterpret_cast<uint4*>(Qs + lds_off<D>(r, lch)) = qreg[p];
+      *reinterpret_cast<uint4*>(Ds + lds_off<D>(r, lch)) = dreg[p];
+    }
+    if (tid < BQ2) {
+      lse_s[tid] = lreg;
+      dlt_s[tid] = dlreg;
+    }
+  };
+
+  const int total = G * nqt;
+  if (total > 0) {
+    gload(kvh * G, qbeg);
+  }
+  __syncthreads();  // K staged
+  for (int it = 0; it < total; ++it) {
+    const int g = it / nqt, qi = it % nqt;
+    const int qt = qbeg + qi * BQ2;
+    lstore();
+    __syncthreads();
+    if (it + 1 < total) {
+      const int g2 = (it + 1) / nqt, q2 = qbeg + ((it + 1) % nqt) * BQ2;
+      gload(kvh * G + g2, q2);
+    }
+    (void)g;
+    // ---- S[q][k] and dP'[q][k]: rows q (registers), key on the lane
+    f32x16 s, dp;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const float4 lv = *reinterpret_cast<const float4*>(lse_s + 8 * g4 + 4 * hh);
+      const float4 dv4 = *reinterpret_cast<const float4*>(dlt_s + 8 * g4 + 4 * hh);
+      s[4 * g4 + 0] = lv.x; s[4 * g4 + 1] = lv.y; s[4 * g4 + 2] = lv.z; s[4 * g4 + 3] = lv.w;
+      dp[4 * g4 + 0] = dv4.x; dp[4 * g4 + 1] = dv4.y; dp[4 * g4 + 2] = dv4.z; dp[4 * g4 + 3] = dv4.w;
+    }
+    const int krow = wave * 32 + lr;
+#pragma unroll
+    for (int st = 0; st < DSTEPS; ++st) {
+      const uint4 qa = *reinterpret_cast<const uint4*>(Qs + lds_off<D>(lr, 2 * st + hh));
+      const uint4 kbv = *reinterpret_cast<const uint4*>(Ks + lds_off<D>(krow, 2 * st + hh));
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(qa), as_bf8(kbv), s, 0, 0, 0);
+      const uint4 da = *reinterpret_cast<const uint4*>(Ds + lds_off<D>(lr, 2 * st + hh));
+      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(da), vf[st], dp, 0, 0, 0);
+    }
+    // ---- P, dS (masked)
+    const bool need_mask = (a.causal && qt < kv0 + wave * 32 + 31) ||
+                           (a.window > 0 && qt + BQ2 - 1 - (kv0 + wave * 32) >= a.window);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float p = __builtin_amdgcn_exp2f(a.c * s[i]);
+      if (need_mask) {
+        const int q = qt + (i & 3) + 8 * (i >> 2) + 4 * hh;
+        const bool bad = (a.causal && key > q) || (a.window > 0 && q - key >= a.window);
+        p = bad ? 0.f : p;
+      }
+      s[i] = p;
+      dp[i] = p * dp[i];
+    }
+    const bf16x8 pb0 = pack8_bf(s, 0), pb1 = pack8_bf(s, 8);
+    const bf16x8 sb0 = pack8_bf(dp, 0), sb1 = pack8_bf(dp, 8);
+    // ---- dV^T += dO^T P ; dK^T += Q^T dS   (k of these MFMAs = the 32 query rows)
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const bf16x8 a0 = tr_operand<D>(Ds, 0, dt * 32, hh, lane);
+      const bf16x8 a1 = tr_operand<D>(Ds, 16, dt * 32, hh, lane);
+      dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, pb0, dv[dt], 0, 0, 0);
+      dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, pb1, dv[dt], 0, 0, 0);
+      const bf16x8 q0v = tr_operand<D>(Qs, 0, dt * 32, hh, lane);
+      const bf16x8 q1v = tr_operand<D>(Qs, 16, dt * 32, hh, lane);
+      dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q0v, sb0, dk[dt], 0, 0, 0);
+      dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q1v, sb1, dk[dt], 0, 0, 0);
+    }
+    __syncthreads();  // Qs/Ds/lse_s are overwritten by the next iteration's lstore
+  }
+
+  // ---- epilogue: dK = scale * dK^T^T, dV; lane owns one key row
+  uint16_t* dkp = a.dk + ((long long)b * S + key) * a.dkv_rs + (long long)kvh * D;
+  uint16_t* dvp = a.dv + ((long long)b * S + key) * a.dkv_rs + (long long)kvh * D;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = dt * 32 + 8 * g4 + 4 * hh;
+      uint2 wk, wv;
+      wk.x = pack_bf2(dk[dt][4 * g4 + 0] * a.scale, dk[dt][4 * g4 + 1] * a.scale);
+      wk.y = pack_bf2(dk[dt][4 * g4 + 2] * a.scale, dk[dt][4 * g4 + 3] * a.scale);
+      wv.x = pack_bf2(dv[dt][4 * g4 + 0], dv[dt][4 * g4 + 1]);
+      wv.y = pack_bf2(dv[dt][4 * g4 + 2], dv[dt][4 * g4 + 3]);
+      *reinterpret_cast<uint2*>(dkp + d) = wk;
+      *reinterpret_cast<uint2*>(dvp + d) = wv;
+    }
+}
+
+// ---------------------------------------------------------------- 3. dQ
+template <int D>
+__global__ __launch_bounds__(256, 2) void bwd_dq_kernel(BwdArgs a) {
+  constexpr int NCH = D / 8, DSTEPS = D / 16, DT = D / 32;
+  constexpr int BQ = 128, BK = 64;
+  constexpr int TILE = BK * D * 2;
+  constexpr int RPP = 256 / NCH, NPASS = BK / RPP;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Kb = smem;             // [2][64][D]
+  char* Vb = smem + 2 * TILE;  // [2][64][D]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hh = lane >> 5, lr = lane & 31;
+  const int S = a.S, G = a.H / a.KV;
+  const int nqb = S / BQ;
+  // heaviest (latest) query blocks first; q heads of one kv group adjacent
+  const int qr = blockIdx.x / (a.B * a.H);
+  const int rem = blockIdx.x % (a.B * a.H);
+  const int b = rem / a.H, hq = rem % a.H;
+  const int kvh = hq / G;
+  const int qb = nqb - 1 - qr;
+  const int q0 = qb * BQ;
+  const int qrow = q0 + wave * 32 + lr;
+
+  bf16x8 qf[DSTEPS], df[DSTEPS];
+  {
+    const uint16_t* qp = a.q + ((long long)b * S + qrow) * a.q_rs + (long long)hq * D + 8 * hh;
+    const uint16_t* dp = a.dout + ((long long)b * S + qrow) * a.o_rs + (long long)hq * D + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < DSTEPS; ++s) {
+      qf[s] = as_bf8(*reinterpret_cast<const uint4*>(qp + 16 * s));
+      df[s] = as_bf8(*reinterpret_cast<const uint4*>(dp + 16 * s));
+    }
+  }
+  const long long sidx = ((long long)b * a.H + hq) * S + qrow;
+  const float lse2 = a.lse[sidx] * LOG2E;
+  const float dlt = a.delta[sidx];
+
+  int kv_end = a.causal ? q0 + BQ : S;
+  int kv_begin = 0;
+  if (a.window > 0) kv_begin = (max(0, q0 - a.window + 1) / BK) * BK;
+  const int ntiles = (kv_end - kv_begin + BK - 1) / BK;
+  const uint16_t* kbase = a.k + (long long)b * S * a.kv_rs + (long long)kvh * D;
+  const uint16_t* vbase = a.v + (long long)b * S * a.kv_rs + (long long)kvh * D;
+  const int lrow = tid / NCH, lch = tid % NCH;
+  uint4 kreg[NPASS], vreg[NPASS];
+  auto gload = [&](int kv0) {
+#pragma unroll
+    for (int p = 0; p < NPASS; ++p) {
+      const long long kk = kv0 + p * RPP + lrow;
+      kreg[p] = *reinterpret_cast<const uint4*>(kbase + kk * a.kv_rs + lch * 8);
+      vreg[p] = *reinterpret_cast<const uint4*>(vbase + kk * a.kv_rs + lch * 8);
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int p = 0; p < NPASS; ++p) {
+      const int r = p * RPP + lrow;
+      *reinterpret_cast<uint4*>(Kb + buf * TILE + lds_off<D>(r, lch)) = kreg[p];
+      *reinterpret_cast<uint4*>(Vb + buf * TILE + lds_off<D>(r, lch)) = vreg[p];
+    }
+  };
+
+  f32x16 dq[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dq[t][i] = 0.f;
+
+  if (ntiles > 0) {
+    gload(kv_begin);
+    lstore(0);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int t = 0; t < ntiles; ++t) {
+    const int kv0 = kv_begin + t * BK;
+    const bool more = t + 1 < ntiles;
+    if (more) gload(kv0 + BK);
+    const char* Kc = Kb + cur * TILE;
+    const char* Vc = Vb + cur * TILE;
+    f32x16 s[2], dp[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { s[kt][i] = 0.f; dp[kt][i] = 0.f; }
+      const int r = kt * 32 + lr;
+#pragma unroll
+      for (int st = 0; st < DSTEPS; ++st) {
+        const uint4 kv = *reinterpret_cast<const uint4*>(Kc + lds_off<D>(r, 2 * st + hh));
+        s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(kv), qf[st], s[kt], 0, 0, 0);
+        const uint4 vv = *reinterpret_cast<const uint4*>(Vc + lds_off<D>(r, 2 * st + hh));
+        dp[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(vv), df[st], dp[kt], 0, 0, 0);
+      }
+    }
+    const int qmin_w = q0 + wave * 32;
+    const bool need_mask = (a.causal && kv0 + BK - 1 > qmin_w) || (a.window > 0 && qmin_w + 31 - kv0 >= a.window);
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float p = __builtin_amdgcn_exp2f(a.c * s[kt][i] - lse2);
+        if (need_mask) {
+          const int key = kv0 + kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          const bool bad = (a.causal && key > qrow) || (a.window > 0 && qrow - key >= a.window);
+          p = bad ? 0.f : p;
+        }
+        dp[kt][i] = p * (dp[kt][i] - dlt);  // dS^T
+      }
+    bf16x8 sb[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) sb[ks] = pack8_bf(dp[ks >> 1], 8 * (ks & 1));
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8 ka = tr_operand<D>(Kc, 16 * ks, dt * 32, hh, lane);
+        dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, sb[ks], dq[dt], 0, 0, 0);
+      }
+    if (more) lstore(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+  uint16_t* op = a.dq + ((long long)b * S + qrow) * a.dq_rs + (long long)hq * D;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = dt * 32 + 8 * g4 + 4 * hh;
+      uint2 w;
+      w.x = pack_bf2(dq[dt][4 * g4 + 0] * a.scale, dq[dt][4 * g4 + 1] * a.scale);
+      w.y = pack_bf2(dq[dt][4 * g4 + 2] * a.scale, dq[dt][4 * g4 + 3] * a.scale);
+      *reinterpret_cast<uint2*>(op + d) = w;
+    }
+}
+
+}  // namespace
+
+extern "C" int ftc_flash_bwd_workspace(int B, int S, int H, int D, long long* bytes) {
+  (void)D;
+  *bytes = (long long)B * H * S * sizeof(float);  // delta
+  return 0;
+}
+
+extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                             const float* lse, void* dq, void* dk, void* dv, void* workspace, int B, int S, int H,
+                             int KV, int D, long long q_rs, long long kv_rs, long long o_rs, long long dq_rs,
+                             long long dkv_rs, float scale, int causal, int window, hipStream_t stream) {
+  if (S % 128 != 0 || H % KV != 0 || (D != 128 && D != 64)) return -1;
+  BwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)o, (const uint16_t*)dout,
+            lse, (float*)workspace, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, q_rs, kv_rs, o_rs, dq_rs, dkv_rs,
+            B, S, H, KV, scale, scale * LOG2E, causal, window};
+  const int grid_d = ftc::stream_grid((long long)B * S, 4);
+  const size_t lds_kv = (size_t)128 * D * 2 + 2 * 32 * D * 2 + 2 * 32 * sizeof(float);
+  const size_t lds_q = (size_t)4 * 64 * D * 2;
+  const int g_kv = B * KV * (S / 128);
+  const int g_q = B * H * (S / 128);
+  if (D == 128) {
+    hipLaunchKernelGGL(bwd_delta_kernel<128>, dim3(grid_d), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(bwd_dkdv_kernel<128>, dim3(g_kv), dim3(256), lds_kv, stream, a);
+    hipLaunchKernelGGL(bwd_dq_kernel<128>, dim3(g_q), dim3(256), lds_q, stream, a);
+  } else {
+    hipLaunchKernelGGL(bwd_delta_kernel<64>, dim3(grid_d), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(bwd_dkdv_kernel<64>, dim3(g_kv), dim3(256), lds_kv, stream, a);
+    hipLaunchKernelGGL(bwd_dq_kernel<64>, dim3(g_q), dim3(256), lds_q, stream, a);
+  }
+  return (int)hipGetLastError();
+}

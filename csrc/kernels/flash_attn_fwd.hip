@@ -1,0 +1,297 @@
+// K1: flash-attention forward for gfx950 -- causal / sliding-window, GQA, bf16 in/out, fp32 LSE.
+//
+// Geometry: one 256-thread workgroup (4 waves) = 128 query rows of one (batch, q-head); each wave
+// owns 32 rows.  K/V stream through LDS in 64-key tiles, double buffered; the next tile's global
+// loads are issued before the current tile's MFMAs and written to LDS after them (register
+// staging, guide T14), one barrier per tile.
+//
+// MFMA orientation (v_mfma_f32_32x32x16_bf16, wave64):
+//   S^T[key][q] = K . Q^T      A = K rows from LDS (ds_read_b128), B = Q^T kept in registers.
+//                             The accumulator has the query on the lane and 16 keys per lane half
+//                             in registers, so softmax row statistics are lane-local (+1 xor-32
+//                             exchange) -- no LDS traffic for softmax.
+//   O^T[d][q]  += V^T . P^T    B = P^T straight from the S^T accumulator (bf16-packed): the
+//                             accumulator's permuted row order is used as the k order of this
+//                             MFMA, and the V^T A-operand is read in that same order with
+//                             ds_read_b64_tr_b16 (hardware transpose), two 4-key reads per step.
+//                             O^T keeps the query on the lane, so the online-softmax rescale is a
+//                             per-lane scalar multiply.
+// LDS image (K and V, [64 keys][D] bf16, 256-byte rows for D=128): 16-byte chunk c of row r lives
+// at chunk c ^ (((r&3)<<2) | ((r>>2)&3)) -- conflict-free for both the b128 row reads of K and the
+// tr_b16 column reads of V (guide T10 "one image for row reads and transposed reads").
+// Block order: heaviest causal q-blocks first; the G = H/KV query heads that share a kv head are
+// placed on the same XCD (blockIdx % 8 group) so their K/V tiles are L2 hits.
+#include "common.h"
+
+using namespace ftc;
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int BQ = 128;  // query rows per workgroup
+constexpr int BK = 64;   // keys per tile
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+FTC_DEV int swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+
+template <int D>
+FTC_DEV int lds_off(int r, int chunk) {  // byte offset of 16-byte chunk `chunk` of row r
+  constexpr int NCH = D / 8;
+  return r * (D * 2) + 16 * ((chunk ^ swz(r)) & (NCH - 1));
+}
+
+FTC_DEV bf16x8 as_bf8(const uint4& v) { return __builtin_bit_cast(bf16x8, v); }
+
+FTC_DEV bf16x8 pack_p(const f32x16& p, int base) {
+  f32x4 lo = {p[base + 0], p[base + 1], p[base + 2], p[base + 3]};
+  f32x4 hi = {p[base + 4], p[base + 5], p[base + 6], p[base + 7]};
+  uint4 u;
+  u.x = pack_bf2(lo[0], lo[1]);
+  u.y = pack_bf2(lo[2], lo[3]);
+  u.z = pack_bf2(hi[0], hi[1]);
+  u.w = pack_bf2(hi[2], hi[3]);
+  return as_bf8(u);
+}
+
+struct FwdArgs {
+  const uint16_t* q;
+  const uint16_t* k;
+  const uint16_t* v;
+  uint16_t* o;
+  float* lse;
+  long long q_rs, kv_rs, o_rs;
+  int B, S, H, KV, nqb;
+  float scale_log2;
+  int causal, window;
+};
+
+// logical block -> (qb, b, kvh, g) with heavy-first order and GQA groups co-located on one XCD
+FTC_DEV void decode_block(const FwdArgs& a, int& qb, int& b, int& hq, int& kvh) {
+  const int G = a.H / a.KV;
+  const int bid = blockIdx.x;
+  const int ngroups = a.nqb * a.B * a.KV;
+  int j, g;
+  if ((ngroups & 7) == 0) {
+    const int xcd = bid & 7, slot = bid >> 3;
+    g = slot % G;
+    j = (slot / G) * 8 + xcd;
+  } else {
+    g = bid % G;
+    j = bid / G;
+  }
+  kvh = j % a.KV;
+  const int t = j / a.KV;
+  b = t % a.B;
+  const int qr = t / a.B;
+  qb = a.nqb - 1 - qr;  // heaviest (latest) query blocks first
+  hq = kvh * G + g;
+}
+
+template <int D>
+__global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
+  constexpr int NCH = D / 8;           // 16-byte chunks per row
+  constexpr int DSTEPS = D / 16;       // k-steps of the S MFMA
+  constexpr int DT = D / 32;           // 32-wide d tiles of O
+  constexpr int RPP = 256 / NCH;       // rows loaded per pass
+  constexpr int NPASS = BK / RPP;      // passes per tile
+  constexpr int TILE_BYTES = BK * D * 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Kb = smem;                     // [2][TILE_BYTES]
+  char* Vb = smem + 2 * TILE_BYTES;    // [2][TILE_BYTES]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hh = lane >> 5, lr = lane & 31;
+  int qb, b, hq, kvh;
+  decode_block(a, qb, b, hq, kvh);
+  const int S = a.S;
+  const int q0 = qb * BQ;
+  const int qrow = q0 + wave * 32 + lr;
+  const bool qvalid = qrow < S;
+
+  // ---- Q^T fragments (B operand of S^T = K Q^T): lane holds Q[qrow][16s + 8hh .. +8)
+  bf16x8 qf[DSTEPS];
+  {
+    const uint16_t* qp = a.q + ((long long)b * S + (qvalid ? qrow : 0)) * a.q_rs + (long long)hq * D + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < DSTEPS; ++s) {
+      uint4 v = qvalid ? *reinterpret_cast<const uint4*>(qp + 16 * s) : make_uint4(0, 0, 0, 0);
+      qf[s] = as_bf8(v);
+    }
+  }
+
+  // ---- key range
+  const int q_last = min(S, q0 + BQ) - 1;
+  int kv_end = a.causal ? q_last + 1 : S;
+  int kv_begin = 0;
+  if (a.window > 0) {
+    kv_begin = max(0, q0 - a.window + 1);
+    kv_begin = (kv_begin / BK) * BK;
+  }
+  const int ntiles = (kv_end - kv_begin + BK - 1) / BK;
+
+  const uint16_t* kbase = a.k + (long long)b * S * a.kv_rs + (long long)kvh * D;
+  const uint16_t* vbase = a.v + (long long)b * S * a.kv_rs + (long long)kvh * D;
+  const int lrow = tid / NCH, lch = tid % NCH;
+
+  uint4 kreg[NPASS], vreg[NPASS];
+  auto gload = [&](int kv0) {
+#pragma unroll
+    for (int p = 0; p < NPASS; ++p) {
+      const long long key = kv0 + p * RPP + lrow;
+      kreg[p] = *reinterpret_cast<const uint4*>(kbase + key * a.kv_rs + lch * 8);
+      vreg[p] = *reinterpret_cast<const uint4*>(vbase + key * a.kv_rs + lch * 8);
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int p = 0; p < NPASS; ++p) {
+      const int r = p * RPP + lrow;
+      *reinterpret_cast<uint4*>(Kb + buf * TILE_BYTES + lds_off<D>(r, lch)) = kreg[p];
+      *reinterpret_cast<uint4*>(Vb + buf * TILE_BYTES + lds_off<D>(r, lch)) = vreg[p];
+    }
+  };
+
+  f32x16 o[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[t][i] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  const float c = a.scale_log2;
+
+  if (ntiles > 0) {
+    gload(kv_begin);
+    lstore(0);
+  }
+  __syncthreads();
+
+  // tr-read addressing (V^T A operand): 16-lane group gi = lane>>4 covers d cols [16*(gi&1), +16)
+  // of the 32-wide d tile and key rows [16ks + 4*hh (+8), +4)
+  const int gi = lane >> 4, li = lane & 15;
+  const int trq = li >> 2, trp = li & 3;
+
+  int cur = 0;
+  for (int t = 0; t < ntiles; ++t) {
+    const int kv0 = kv_begin + t * BK;
+    const bool more = t + 1 < ntiles;
+    if (more) gload(kv0 + BK);
+    const char* Kc = Kb + cur * TILE_BYTES;
+    const char* Vc = Vb + cur * TILE_BYTES;
+
+    // ---- S^T = K Q^T : two 32-key blocks
+    f32x16 s[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[kt][i] = 0.f;
+      const int r = kt * 32 + lr;
+#pragma unroll
+      for (int st = 0; st < DSTEPS; ++st) {
+        const uint4 kv = *reinterpret_cast<const uint4*>(Kc + lds_off<D>(r, 2 * st + hh));
+        s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(kv), qf[st], s[kt], 0, 0, 0);
+      }
+    }
+
+    // ---- mask + online softmax (log2 domain), query = qrow (lane), keys in registers
+    const int qmin_w = q0 + wave * 32;
+    const bool need_mask = (a.causal && kv0 + BK - 1 > qmin_w) || (a.window > 0 && qmin_w + 31 - kv0 >= a.window);
+    float mt = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float x = s[kt][i] * c;
+        if (need_mask) {
+          const int key = kv0 + kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          bool bad = (a.causal && key > qrow) || (a.window > 0 && qrow - key >= a.window);
+          x = bad ? -INFINITY : x;
+        }
+        s[kt][i] = x;
+        mt = fmaxf(mt, x);
+      }
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(m, mt);
+    const float mref = (mn == -INFINITY) ? 0.f : mn;
+    const float alpha = __builtin_amdgcn_exp2f(m - mref);
+    m = mn;
+    float rs = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = __builtin_amdgcn_exp2f(s[kt][i] - mref);
+        s[kt][i] = p;
+        rs += p;
+      }
+    l = l * alpha + rs;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+
+    // ---- O^T += V^T P^T : 4 k-steps of 16 keys
+    bf16x8 pf[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) pf[ks] = pack_p(s[ks >> 1], 8 * (ks & 1));
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int col = dt * 32 + 16 * (gi & 1) + 4 * trp;
+      const int chunk = col >> 3, half8 = (col & 7) ? 8 : 0;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int r1 = 16 * ks + 4 * hh + trq;
+        const int r2 = r1 + 8;
+        s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vc + lds_off<D>(r1, chunk) + half8));
+        s16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vc + lds_off<D>(r2, chunk) + half8));
+        s16x8 va = {v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
+        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, va), pf[ks], o[dt], 0, 0, 0);
+      }
+    }
+    if (more) lstore(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // ---- epilogue: normalise, store O (bf16) and LSE (natural log)
+  const float ltot = l + __shfl_xor(l, 32, 64);
+  const float inv = ltot > 0.f ? 1.0f / ltot : 0.f;
+  if (qvalid) {
+    uint16_t* op = a.o + ((long long)b * S + qrow) * a.o_rs + (long long)hq * D;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = dt * 32 + 8 * g4 + 4 * hh;
+        uint2 w;
+        w.x = pack_bf2(o[dt][4 * g4 + 0] * inv, o[dt][4 * g4 + 1] * inv);
+        w.y = pack_bf2(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
+        *reinterpret_cast<uint2*>(op + d) = w;
+      }
+    if (hh == 0) {
+      const float lse2 = (m == -INFINITY) ? -INFINITY : m + __log2f(ltot);
+      a.lse[((long long)b * a.H + hq) * S + qrow] = lse2 * LN2;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int ftc_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H,
+                             int KV, int D, long long q_rs, long long kv_rs, long long o_rs, float scale, int causal,
+                             int window, hipStream_t stream) {
+  if (S % BK != 0 || H % KV != 0 || (D != 128 && D != 64)) return -1;
+  FwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, q_rs, kv_rs, o_rs,
+            B, S, H, KV, (S + BQ - 1) / BQ, scale * LOG2E, causal, window};
+  const int nblocks = a.nqb * B * H;
+  const size_t lds = (size_t)4 * BK * D * 2;
+  if (D == 128)
+    hipLaunchKernelGGL(flash_fwd_kernel<128>, dim3(nblocks), dim3(256), lds, stream, a);
+  else
+    hipLaunchKernelGGL(flash_fwd_kernel<64>, dim3(nblocks), dim3(256), lds, stream, a);
+  return (int)hipGetLastError();
+}

@@ -2,19 +2,6 @@
 // side only calls them once ops/_backend reports the capability (see ops/attention.py, ops/nf4.py).
 #include "common.h"
 
-extern "C" int ftc_flash_fwd(const void*, const void*, const void*, void*, float*, int, int, int, int, int, long long,
-                             long long, long long, float, int, int, hipStream_t) {
-  return -2;
-}
-extern "C" int ftc_flash_bwd_workspace(int, int, int, int, long long* bytes) {
-  *bytes = 16;
-  return 0;
-}
-extern "C" int ftc_flash_bwd(const void*, const void*, const void*, const void*, const void*, const float*, void*,
-                             void*, void*, void*, int, int, int, int, int, long long, long long, long long, long long,
-                             long long, float, int, int, hipStream_t) {
-  return -2;
-}
 extern "C" int ftc_nf4_gemm(const void*, const uint8_t*, const uint8_t*, const float*, float, void*, int, int, int,
                             int, int, hipStream_t) {
   return -2;

@@ -23,11 +23,11 @@ from ._backend import ext, use_hip
 
 
 # flipped to True once csrc/kernels/flash_attn.hip replaces the stub launcher
-FLASH_READY = False
+FLASH_READY = True
 
 
 def flash_supported(D: int, S: int) -> bool:
-    return FLASH_READY and D in (64, 128) and S % 64 == 0
+    return FLASH_READY and D in (64, 128) and S % 128 == 0
 
 
 def _split(qkv, B, S, H, KV, D):

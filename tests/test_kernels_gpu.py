@@ -149,3 +149,45 @@ def test_lora_merge(C):
     ref = W.float() + 2.0 * (B.float() @ A.float())
     C.lora_merge_(W, A, B, 2.0, 0)
     torch.testing.assert_close(W.float(), ref, atol=3e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("B,S,H,KV,D,causal,window", [
+    (2, 256, 8, 2, 128, True, 0),
+    (1, 384, 4, 4, 128, False, 0),
+    (1, 512, 8, 2, 128, True, 192),
+    (2, 256, 4, 4, 64, True, 0),
+])
+def test_flash_attention_fwd_bwd(C, B, S, H, KV, D, causal, window):
+    from finetune_controller_amd.ops.attention import _FlashPacked, attention_reference
+
+    torch.manual_seed(0)
+    W = (H + 2 * KV) * D
+    qkv = bf(torch.randn(B * S, W, device=DEV))
+    scale = 1.0 / math.sqrt(D)
+    ref_in = qkv.float().clone().requires_grad_(True)
+    ref = attention_reference(ref_in, B, S, H, KV, D, causal, window, scale)
+    x = qkv.clone().requires_grad_(True)
+    out = _FlashPacked.apply(x, B, S, H, KV, D, causal, window, scale)
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+    dout = bf(torch.randn(B * S, H * D, device=DEV))
+    ref.backward(dout.float())
+    out.backward(dout)
+    g, gr = x.grad.float(), ref_in.grad
+    # per-part relative error (dq | dk | dv)
+    for lo, hi in ((0, H * D), (H * D, (H + KV) * D), ((H + KV) * D, W)):
+        err = (g[:, lo:hi] - gr[:, lo:hi]).abs().max().item()
+        mag = gr[:, lo:hi].abs().max().item()
+        assert err <= 2e-2 * mag + 2e-2, (lo, err, mag)
+
+
+def test_flash_lse(C):
+    torch.manual_seed(1)
+    B, S, H, KV, D = 1, 256, 4, 2, 128
+    qkv = bf(torch.randn(B * S, (H + 2 * KV) * D, device=DEV))
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:(H + KV) * D], qkv[:, (H + KV) * D:]
+    o, lse = C.flash_fwd(q, k, v, B, S, H, KV, D, 1 / math.sqrt(D), True, 0)
+    qf = q.float().view(S, H, D).transpose(0, 1)
+    kf = k.float().view(S, KV, D).transpose(0, 1).repeat_interleave(H // KV, 0)
+    s = qf @ kf.transpose(-1, -2) / math.sqrt(D)
+    s = s.masked_fill(torch.triu(torch.ones(S, S, dtype=torch.bool, device=DEV), 1), float("-inf"))
+    torch.testing.assert_close(lse.view(H, S), torch.logsumexp(s, -1), atol=2e-3, rtol=1e-3)
