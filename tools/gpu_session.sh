@@ -34,6 +34,9 @@ for s in "${STEPS[@]}"; do
     bench)
       timeout -k 10 600 python bench.py --steps 10 --warmup 3 > gpurun_out/bench.log 2>&1
       fatal $? bench; tail -2 gpurun_out/bench.log ;;
+    attn)
+      timeout -k 10 300 python tools/bench_attention.py > gpurun_out/bench_attn.log 2>&1
+      fatal $? attn; tail -2 gpurun_out/bench_attn.log ;;
     bench_b8)
       timeout -k 10 600 python bench.py --steps 8 --warmup 3 --batch-size 8 > gpurun_out/bench_b8.log 2>&1
       fatal $? bench_b8; tail -2 gpurun_out/bench_b8.log ;;
