@@ -1,0 +1,137 @@
+"""Streaming ``multipart/form-data`` / urlencoded form parsing.
+
+FastAPI's ``Form``/``File`` parameters need the python-multipart package; this control plane parses
+the job-submission form itself: text fields are collected in memory (bounded), file parts are
+streamed to a temp file in ``/tmp/ftjobs`` (the reference spools uploads there too,
+``/root/reference/app/utils/dataset_helpers.py:27``) so a multi-GB dataset upload never sits in RAM.
+"""
+from __future__ import annotations
+
+import os
+import tempfile
+from urllib.parse import parse_qs
+
+from ..schemas.jobs import UploadedFile
+
+MAX_FIELD_BYTES = 1 << 20
+UPLOAD_DIR = "/tmp/ftjobs"
+
+
+class FormError(ValueError):
+    pass
+
+
+def _boundary(ctype: str) -> bytes:
+    for part in ctype.split(";"):
+        part = part.strip()
+        if part.lower().startswith("boundary="):
+            b = part.split("=", 1)[1].strip().strip('"')
+            return b.encode()
+    raise FormError("multipart boundary missing")
+
+
+def _parse_disposition(value: str) -> dict:
+    out = {}
+    for item in value.split(";")[1:]:
+        if "=" in item:
+            k, v = item.strip().split("=", 1)
+            out[k.lower()] = v.strip().strip('"')
+    return out
+
+
+async def parse_form(request) -> tuple[dict[str, str], dict[str, UploadedFile]]:
+    ctype = request.headers.get("content-type", "")
+    if ctype.startswith("application/x-www-form-urlencoded"):
+        body = await request.body()
+        q = parse_qs(body.decode("utf-8"), keep_blank_values=True)
+        return {k: v[-1] for k, v in q.items()}, {}
+    if not ctype.startswith("multipart/form-data"):
+        raise FormError("expected multipart/form-data or application/x-www-form-urlencoded")
+    delim = b"--" + _boundary(ctype)
+    fields: dict[str, str] = {}
+    files: dict[str, UploadedFile] = {}
+    buf = b""
+    state = "preamble"
+    headers: dict[str, str] = {}
+    cur_name = None
+    cur_file = None
+    cur_fh = None
+    cur_val = bytearray()
+    os.makedirs(UPLOAD_DIR, exist_ok=True)
+
+    def finish_part():
+        nonlocal cur_fh, cur_file, cur_val
+        if cur_file is not None:
+            cur_fh.close()
+            cur_file.size = os.path.getsize(cur_file.path)
+            if cur_file.filename:
+                files[cur_name] = cur_file
+            else:
+                os.remove(cur_file.path)
+        elif cur_name is not None:
+            fields[cur_name] = cur_val.decode("utf-8", errors="replace")
+        cur_fh = cur_file = None
+        cur_val = bytearray()
+
+    async for chunk in request.stream():
+        buf += chunk
+        while True:
+            if state == "preamble":
+                i = buf.find(delim)
+                if i < 0:
+                    buf = buf[-len(delim):]
+                    break
+                buf = buf[i + len(delim):]
+                state = "after_delim"
+            if state == "after_delim":
+                if len(buf) < 2:
+                    break
+                if buf.startswith(b"--"):
+                    return fields, files
+                if buf.startswith(b"\r\n"):
+                    buf = buf[2:]
+                state = "headers"
+                headers = {}
+            if state == "headers":
+                j = buf.find(b"\r\n\r\n")
+                if j < 0:
+                    if len(buf) > 64 * 1024:
+                        raise FormError("part headers too large")
+                    break
+                for line in buf[:j].decode("utf-8", errors="replace").split("\r\n"):
+                    if ":" in line:
+                        k, v = line.split(":", 1)
+                        headers[k.strip().lower()] = v.strip()
+                buf = buf[j + 4:]
+                disp = _parse_disposition(headers.get("content-disposition", ""))
+                cur_name = disp.get("name")
+                if "filename" in disp:
+                    fname = os.path.basename(disp["filename"])
+                    fd, path = tempfile.mkstemp(prefix="upload-", dir=UPLOAD_DIR)
+                    cur_fh = os.fdopen(fd, "wb")
+                    cur_file = UploadedFile(filename=fname, path=path,
+                                            content_type=headers.get("content-type", "application/octet-stream"))
+                state = "body"
+            if state == "body":
+                k = buf.find(b"\r\n" + delim)
+                if k < 0:
+                    keep = len(delim) + 2
+                    if len(buf) > keep:
+                        data, buf = buf[:-keep], buf[-keep:]
+                        if cur_fh is not None:
+                            cur_fh.write(data)
+                        else:
+                            cur_val.extend(data)
+                            if len(cur_val) > MAX_FIELD_BYTES:
+                                raise FormError("form field too large")
+                    break
+                data, buf = buf[:k], buf[k + 2 + len(delim):]
+                if cur_fh is not None:
+                    cur_fh.write(data)
+                else:
+                    cur_val.extend(data)
+                finish_part()
+                state = "after_delim"
+    if state not in ("after_delim", "preamble"):
+        finish_part()
+    return fields, files

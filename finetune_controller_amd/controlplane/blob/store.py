@@ -1,0 +1,325 @@
+"""Object storage behind one protocol (C10 transport layer).
+
+The reference binds S3 through aioboto3 (``/root/reference/app/utils/S3Handler.py:22-44``).  Neither
+boto nor aioboto3 is required here:
+
+* ``S3ObjectStore`` -- S3 REST with AWS Signature V4 written against ``httpx`` (ListObjectsV2 with
+  continuation, Get/Put/Head/Copy/DeleteObjects, multipart upload for large files, presigned GETs);
+  works with AWS, MinIO, Ceph RGW (``S3_ENDPOINT_URL``);
+* ``LocalObjectStore`` -- ``s3://bucket/key`` mapped onto ``<root>/bucket/key`` (tests, single-node
+  deployments, the FakeCluster's dataset init container and sync sidecar).
+
+All methods are synchronous and thread-safe; the async ``S3Handler`` runs them in worker threads.
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import hashlib
+import hmac
+import os
+import shutil
+import threading
+import urllib.parse
+import xml.etree.ElementTree as ET
+from dataclasses import dataclass
+
+import httpx
+
+
+def split_s3_uri(uri: str) -> tuple[str, str]:
+    if not uri.startswith("s3://"):
+        raise ValueError(f"not an s3 uri: {uri!r}")
+    rest = uri[5:]
+    bucket, _, key = rest.partition("/")
+    return bucket, key
+
+
+@dataclass
+class ObjectInfo:
+    Key: str
+    Size: int
+    LastModified: _dt.datetime
+
+    def as_dict(self):
+        return {"Key": self.Key, "Size": self.Size, "LastModified": self.LastModified}
+
+
+class ObjectNotFound(Exception):
+    pass
+
+
+class ObjectStore:
+    def put_bytes(self, bucket: str, key: str, data: bytes) -> None: raise NotImplementedError
+    def put_file(self, bucket: str, key: str, path: str) -> None: raise NotImplementedError
+    def put_stream(self, bucket: str, key: str, chunks) -> None: raise NotImplementedError
+    def get_bytes(self, bucket: str, key: str) -> bytes: raise NotImplementedError
+    def get_file(self, bucket: str, key: str, path: str) -> None: raise NotImplementedError
+    def head(self, bucket: str, key: str) -> ObjectInfo | None: raise NotImplementedError
+    def list(self, bucket: str, prefix: str) -> list[ObjectInfo]: raise NotImplementedError
+    def delete(self, bucket: str, keys: list[str]) -> None: raise NotImplementedError
+    def copy(self, src_bucket: str, src_key: str, dst_bucket: str, dst_key: str) -> None: raise NotImplementedError
+    def presign(self, bucket: str, key: str, expires: int = 3600) -> str: raise NotImplementedError
+
+
+# ---------------------------------------------------------------- local directory store
+class LocalObjectStore(ObjectStore):
+    def __init__(self, root: str, url_base: str | None = None):
+        self.root = os.path.abspath(root)
+        os.makedirs(self.root, exist_ok=True)
+        self.url_base = url_base  # e.g. "http://host:8000/files" when served; default file://
+        self._lock = threading.Lock()
+
+    def _p(self, bucket, key):
+        p = os.path.abspath(os.path.join(self.root, bucket, key))
+        if not p.startswith(os.path.join(self.root, bucket)):
+            raise ValueError("key escapes bucket")
+        return p
+
+    def put_bytes(self, bucket, key, data):
+        p = self._p(bucket, key)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        tmp = p + ".part"
+        with open(tmp, "wb") as f:
+            f.write(data)
+        os.replace(tmp, p)
+
+    def put_file(self, bucket, key, path):
+        p = self._p(bucket, key)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        shutil.copyfile(path, p + ".part")
+        os.replace(p + ".part", p)
+
+    def put_stream(self, bucket, key, chunks):
+        p = self._p(bucket, key)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        with open(p + ".part", "wb") as f:
+            for c in chunks:
+                f.write(c)
+        os.replace(p + ".part", p)
+
+    def get_bytes(self, bucket, key):
+        p = self._p(bucket, key)
+        if not os.path.isfile(p):
+            raise ObjectNotFound(f"s3://{bucket}/{key}")
+        with open(p, "rb") as f:
+            return f.read()
+
+    def get_file(self, bucket, key, path):
+        p = self._p(bucket, key)
+        if not os.path.isfile(p):
+            raise ObjectNotFound(f"s3://{bucket}/{key}")
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        shutil.copyfile(p, path)
+
+    def head(self, bucket, key):
+        p = self._p(bucket, key)
+        if not os.path.isfile(p):
+            return None
+        st = os.stat(p)
+        return ObjectInfo(key, st.st_size, _dt.datetime.fromtimestamp(st.st_mtime, _dt.timezone.utc))
+
+    def list(self, bucket, prefix):
+        base = os.path.join(self.root, bucket)
+        out = []
+        if not os.path.isdir(base):
+            return out
+        for dp, _, files in os.walk(base):
+            for fn in files:
+                if fn.endswith(".part"):
+                    continue
+                full = os.path.join(dp, fn)
+                key = os.path.relpath(full, base).replace(os.sep, "/")
+                if key.startswith(prefix):
+                    st = os.stat(full)
+                    out.append(ObjectInfo(key, st.st_size, _dt.datetime.fromtimestamp(st.st_mtime, _dt.timezone.utc)))
+        return sorted(out, key=lambda o: o.Key)
+
+    def delete(self, bucket, keys):
+        for k in keys:
+            p = self._p(bucket, k)
+            if os.path.isfile(p):
+                os.remove(p)
+
+    def copy(self, src_bucket, src_key, dst_bucket, dst_key):
+        self.put_file(dst_bucket, dst_key, self._p(src_bucket, src_key))
+
+    def presign(self, bucket, key, expires=3600):
+        if self.url_base:
+            return f"{self.url_base.rstrip('/')}/{bucket}/{urllib.parse.quote(key)}"
+        return "file://" + self._p(bucket, key)
+
+
+# ---------------------------------------------------------------- S3 (SigV4) store
+def _sha256(b: bytes) -> str:
+    return hashlib.sha256(b).hexdigest()
+
+
+def _sign(key: bytes, msg: str) -> bytes:
+    return hmac.new(key, msg.encode(), hashlib.sha256).digest()
+
+
+class S3ObjectStore(ObjectStore):
+    """Minimal S3 client: AWS Signature Version 4, path-style addressing."""
+
+    MULTIPART_THRESHOLD = 64 * 1024 * 1024
+    PART_SIZE = 32 * 1024 * 1024
+
+    def __init__(self, access_key: str | None, secret_key: str | None, region: str = "us-east-1",
+                 endpoint: str | None = None, session_token: str | None = None, timeout: float = 120.0):
+        self.ak, self.sk, self.region, self.token = access_key, secret_key, region, session_token
+        self.endpoint = (endpoint or f"https://s3.{region}.amazonaws.com").rstrip("/")
+        self.host = urllib.parse.urlparse(self.endpoint).netloc
+        self.http = httpx.Client(timeout=timeout)
+
+    # ---- signing ----
+    def _headers(self, method, path, query: dict, payload_hash: str, extra: dict | None = None):
+        now = _dt.datetime.now(_dt.timezone.utc)
+        amz = now.strftime("%Y%m%dT%H%M%SZ")
+        date = now.strftime("%Y%m%d")
+        h = {"host": self.host, "x-amz-date": amz, "x-amz-content-sha256": payload_hash}
+        if self.token:
+            h["x-amz-security-token"] = self.token
+        if extra:
+            h.update({k.lower(): v for k, v in extra.items()})
+        if not (self.ak and self.sk):
+            return h
+        canon_q = "&".join(f"{urllib.parse.quote(k, safe='-_.~')}={urllib.parse.quote(str(v), safe='-_.~')}"
+                           for k, v in sorted(query.items()))
+        signed = ";".join(sorted(h))
+        canon_h = "".join(f"{k}:{str(h[k]).strip()}\n" for k in sorted(h))
+        creq = "\n".join([method, urllib.parse.quote(path, safe="/-_.~"), canon_q, canon_h, signed, payload_hash])
+        scope = f"{date}/{self.region}/s3/aws4_request"
+        sts = "\n".join(["AWS4-HMAC-SHA256", amz, scope, _sha256(creq.encode())])
+        k = _sign(_sign(_sign(_sign(("AWS4" + self.sk).encode(), date), self.region), "s3"), "aws4_request")
+        sig = hmac.new(k, sts.encode(), hashlib.sha256).hexdigest()
+        h["authorization"] = f"AWS4-HMAC-SHA256 Credential={self.ak}/{scope}, SignedHeaders={signed}, Signature={sig}"
+        return h
+
+    def _req(self, method, bucket, key="", query=None, body: bytes = b"", extra=None, ok=(200, 204, 206)):
+        path = f"/{bucket}" + (f"/{key}" if key else "")
+        query = query or {}
+        h = self._headers(method, path, query, _sha256(body), extra)
+        url = self.endpoint + urllib.parse.quote(path, safe="/-_.~")
+        r = self.http.request(method, url, params=query or None, content=body or None, headers=h)
+        if r.status_code == 404:
+            raise ObjectNotFound(f"s3://{bucket}/{key}")
+        if r.status_code not in ok:
+            raise RuntimeError(f"S3 {method} {path} failed: {r.status_code} {r.text[:300]}")
+        return r
+
+    # ---- operations ----
+    def put_bytes(self, bucket, key, data):
+        self._req("PUT", bucket, key, body=data)
+
+    def put_file(self, bucket, key, path):
+        size = os.path.getsize(path)
+        if size <= self.MULTIPART_THRESHOLD:
+            with open(path, "rb") as f:
+                self.put_bytes(bucket, key, f.read())
+            return
+        with open(path, "rb") as f:
+            self.put_stream(bucket, key, iter(lambda: f.read(self.PART_SIZE), b""))
+
+    def put_stream(self, bucket, key, chunks):
+        r = self._req("POST", bucket, key, query={"uploads": ""})
+        upload_id = ET.fromstring(r.text).find("{*}UploadId").text
+        parts, buf, n = [], b"", 1
+        try:
+            for c in chunks:
+                buf += c
+                while len(buf) >= self.PART_SIZE:
+                    part, buf = buf[: self.PART_SIZE], buf[self.PART_SIZE:]
+                    rr = self._req("PUT", bucket, key, query={"partNumber": n, "uploadId": upload_id}, body=part)
+                    parts.append((n, rr.headers["ETag"]))
+                    n += 1
+            if buf or not parts:
+                rr = self._req("PUT", bucket, key, query={"partNumber": n, "uploadId": upload_id}, body=buf)
+                parts.append((n, rr.headers["ETag"]))
+            xml = "<CompleteMultipartUpload>" + "".join(
+                f"<Part><PartNumber>{i}</PartNumber><ETag>{e}</ETag></Part>" for i, e in parts) + \
+                "</CompleteMultipartUpload>"
+            self._req("POST", bucket, key, query={"uploadId": upload_id}, body=xml.encode())
+        except Exception:
+            self._req("DELETE", bucket, key, query={"uploadId": upload_id}, ok=(200, 204, 404))
+            raise
+
+    def get_bytes(self, bucket, key):
+        return self._req("GET", bucket, key).content
+
+    def get_file(self, bucket, key, path):
+        with open(path, "wb") as f:
+            f.write(self.get_bytes(bucket, key))
+
+    def head(self, bucket, key):
+        try:
+            r = self._req("HEAD", bucket, key)
+        except ObjectNotFound:
+            return None
+        lm = r.headers.get("Last-Modified")
+        ts = _dt.datetime.strptime(lm, "%a, %d %b %Y %H:%M:%S %Z").replace(tzinfo=_dt.timezone.utc) if lm else None
+        return ObjectInfo(key, int(r.headers.get("Content-Length", 0)), ts)
+
+    def list(self, bucket, prefix):
+        out, token = [], None
+        while True:
+            q = {"list-type": "2", "prefix": prefix}
+            if token:
+                q["continuation-token"] = token
+            root = ET.fromstring(self._req("GET", bucket, query=q).text)
+            for c in root.findall("{*}Contents"):
+                lm = c.find("{*}LastModified").text
+                out.append(ObjectInfo(c.find("{*}Key").text, int(c.find("{*}Size").text),
+                                      _dt.datetime.fromisoformat(lm.replace("Z", "+00:00"))))
+            trunc = root.find("{*}IsTruncated")
+            if trunc is not None and trunc.text == "true":
+                token = root.find("{*}NextContinuationToken").text
+            else:
+                return out
+
+    def delete(self, bucket, keys):
+        for i in range(0, len(keys), 1000):
+            xml = "<Delete><Quiet>true</Quiet>" + "".join(
+                f"<Object><Key>{_xml_escape(k)}</Key></Object>" for k in keys[i:i + 1000]) + "</Delete>"
+            body = xml.encode()
+            md5 = __import__("base64").b64encode(hashlib.md5(body).digest()).decode()
+            self._req("POST", bucket, query={"delete": ""}, body=body, extra={"Content-MD5": md5})
+
+    def copy(self, src_bucket, src_key, dst_bucket, dst_key):
+        self._req("PUT", dst_bucket, dst_key,
+                  extra={"x-amz-copy-source": urllib.parse.quote(f"/{src_bucket}/{src_key}", safe="/-_.~")})
+
+    def presign(self, bucket, key, expires=3600):
+        now = _dt.datetime.now(_dt.timezone.utc)
+        amz = now.strftime("%Y%m%dT%H%M%SZ")
+        date = now.strftime("%Y%m%d")
+        scope = f"{date}/{self.region}/s3/aws4_request"
+        path = f"/{bucket}/{key}"
+        q = {"X-Amz-Algorithm": "AWS4-HMAC-SHA256", "X-Amz-Credential": f"{self.ak}/{scope}", "X-Amz-Date": amz,
+             "X-Amz-Expires": str(int(expires)), "X-Amz-SignedHeaders": "host"}
+        if self.token:
+            q["X-Amz-Security-Token"] = self.token
+        canon_q = "&".join(f"{urllib.parse.quote(k, safe='-_.~')}={urllib.parse.quote(v, safe='-_.~')}"
+                           for k, v in sorted(q.items()))
+        creq = "\n".join(["GET", urllib.parse.quote(path, safe="/-_.~"), canon_q, f"host:{self.host}\n", "host",
+                          "UNSIGNED-PAYLOAD"])
+        sts = "\n".join(["AWS4-HMAC-SHA256", amz, scope, _sha256(creq.encode())])
+        k = _sign(_sign(_sign(_sign(("AWS4" + (self.sk or "")).encode(), date), self.region), "s3"), "aws4_request")
+        sig = hmac.new(k, sts.encode(), hashlib.sha256).hexdigest()
+        return f"{self.endpoint}{urllib.parse.quote(path, safe='/-_.~')}?{canon_q}&X-Amz-Signature={sig}"
+
+
+def _xml_escape(s: str) -> str:
+    return s.replace("&", "&amp;").replace("<", "&lt;").replace(">", "&gt;")
+
+
+def make_object_store(spec: str, settings=None) -> ObjectStore:
+    """``"s3"`` -> S3ObjectStore from settings; ``"local:<dir>"`` -> LocalObjectStore."""
+    if spec.startswith("local:"):
+        return LocalObjectStore(spec[len("local:"):])
+    if spec == "s3":
+        ak = settings.aws_access_key.get_secret_value() if settings and settings.aws_access_key else None
+        sk = settings.aws_secret_key.get_secret_value() if settings and settings.aws_secret_key else None
+        return S3ObjectStore(ak, sk, settings.AWS_REGION if settings else "us-east-1",
+                             getattr(settings, "S3_ENDPOINT_URL", None) if settings else None,
+                             os.environ.get("AWS_SESSION_TOKEN"))
+    raise ValueError(f"unknown object store {spec!r}")

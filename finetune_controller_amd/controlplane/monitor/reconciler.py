@@ -1,0 +1,180 @@
+"""Job monitor / reconciler (C12) and its standalone service entry point (C13).
+
+Every ``JOB_MONITOR_INTERVAL`` seconds: list PyTorchJobs, get the Kueue pending order, map each job's
+latest condition to a DB status (a suspended job that already has a ``startTime`` counts as
+``Created``), write status + lifecycle metadata + ``queue_pos``, ingest the newest metrics CSV for
+running and finished jobs, store ``training_duration`` on completion and delete succeeded PyTorchJobs
+(``/root/reference/app/core/monitor.py:124-197``).
+
+Fixes:
+* "already stopped" is decided by comparing the DB status with the MAPPED Kubeflow status (the
+  reference compares ``completed`` with ``Succeeded`` and re-processes every finished job forever);
+* jobs the user canceled are never moved back to another state;
+* Kubernetes calls run in worker threads (the reference blocks the event loop);
+* a Mongo lease (``locks`` collection) keeps ONE active monitor even when several API workers run
+  with ``DEV_LOCAL_JOB_MONITOR`` or several monitor replicas are deployed.
+"""
+from __future__ import annotations
+
+import asyncio
+import datetime as _dt
+import logging
+import os
+import signal
+import socket
+import uuid
+
+from ..context import AppContext
+from ..k8s.queue import queue_positions
+from ..schemas.db import DatabaseStatusEnum
+from ..schemas.kubeflow import KubeflowStatusEnum, TrainingJobStatus
+
+logger = logging.getLogger("ftc.monitor")
+
+LEASE = "job-monitor"
+
+
+def _ts(s):
+    if not s:
+        return None
+    if isinstance(s, _dt.datetime):
+        return s
+    return _dt.datetime.fromisoformat(str(s).replace("Z", "+00:00"))
+
+
+class JobMonitor:
+    def __init__(self, ctx: AppContext, interval: float | None = None, lease_ttl: float | None = None):
+        self.ctx = ctx
+        self.interval = interval if interval is not None else ctx.settings.JOB_MONITOR_INTERVAL
+        self.lease_ttl = lease_ttl or max(10.0, 5 * self.interval)
+        self.owner = f"{socket.gethostname()}-{os.getpid()}-{uuid.uuid4().hex[:6]}"
+        self.stop_monitoring = False
+        self.monitoring_task: asyncio.Task | None = None
+        self.is_leader = False
+
+    # ---------------------------------------------------------------- one reconcile pass
+    async def reconcile_once(self) -> int:
+        ctx = self.ctx
+        ns = ctx.namespace
+        jobs = await asyncio.to_thread(ctx.kube.list_pytorchjobs, ns)
+        queue = await asyncio.to_thread(queue_positions, ctx.kube, ns)
+        n = 0
+        for job in jobs:
+            job_id = job["metadata"]["name"]
+            st = job.get("status") or {}
+            conds = st.get("conditions") or []
+            if not conds:
+                continue
+            cond = conds[-1]
+            status = cond.get("type")
+            if status == KubeflowStatusEnum.suspended.value and st.get("startTime") and \
+                    not any(c.get("type") == "Running" for c in conds):
+                status = KubeflowStatusEnum.created.value
+            mapped = TrainingJobStatus.map_status(status)
+            prev = await ctx.store.get_job(job_id)
+            if prev is None:
+                continue  # not ours (another controller / DB)
+            if prev.status == DatabaseStatusEnum.canceled:
+                continue
+            if TrainingJobStatus.is_stopped(prev.status) and prev.status == mapped:
+                continue  # already reconciled
+            if prev.status != mapped:
+                logger.info("job %s status %s -> %s", job_id, prev.status.value, mapped.value)
+            info = await ctx.store.update_job_status(job_id, mapped, metadata={
+                "last_transition_time": _ts(cond.get("lastTransitionTime")),
+                "last_update_time": _ts(cond.get("lastUpdateTime")),
+                "start_time": _ts(st.get("startTime")),
+                "completion_time": _ts(st.get("completionTime")),
+                "message": cond.get("message"),
+                "reason": cond.get("reason"),
+                "queue_pos": queue.get(job_id),
+            })
+            n += 1
+            if info is None:
+                continue
+            done = TrainingJobStatus.is_stopped(mapped)
+            await self._process_metrics(job_id, info, st, done)
+            if status == KubeflowStatusEnum.succeeded.value:
+                logger.info("job %s completed successfully, cleaning up", job_id)
+                await self.delete_job(job_id)
+            elif status == KubeflowStatusEnum.failed.value:
+                logger.error("job %s failed: %s", job_id, cond.get("message"))
+        return n
+
+    async def _process_metrics(self, job_id, info, st, completed: bool):
+        try:
+            metrics = await self.ctx.s3.get_metrics(info.user_id, job_id)
+        except Exception:
+            metrics = None
+        tasks = []
+        if completed and st.get("startTime") and st.get("completionTime"):
+            dur = (_ts(st["completionTime"]) - _ts(st["startTime"])).total_seconds()
+            tasks.append(self.ctx.store.update_job_status(job_id, info.status, {"training_duration": dur}))
+        if metrics:
+            tasks.append(self.ctx.store.upsert_job_metrics(info.user_id, job_id, info.job_name, metrics))
+        if tasks:
+            await asyncio.gather(*tasks)
+
+    async def delete_job(self, job_id: str):
+        try:
+            await asyncio.to_thread(self.ctx.kube.delete_pytorchjob, self.ctx.namespace, job_id)
+        except Exception as e:
+            logger.error("failed to delete job %s: %s", job_id, e)
+
+    # ---------------------------------------------------------------- loop
+    async def monitor_jobs(self):
+        logger.info("starting job monitoring in namespace %s as %s", self.ctx.namespace, self.owner)
+        while not self.stop_monitoring:
+            try:
+                self.is_leader = await self.ctx.store.acquire_lock(LEASE, self.owner, self.lease_ttl)
+                if self.is_leader:
+                    await self.reconcile_once()
+            except asyncio.CancelledError:
+                raise
+            except Exception as e:
+                logger.error("error in job monitoring loop: %s", e, exc_info=True)
+                await asyncio.sleep(5)
+                continue
+            await asyncio.sleep(self.interval)
+
+    async def start(self):
+        self.stop_monitoring = False
+        self.monitoring_task = asyncio.create_task(self.monitor_jobs())
+
+    async def stop(self):
+        self.stop_monitoring = True
+        if self.monitoring_task:
+            self.monitoring_task.cancel()
+            try:
+                await self.monitoring_task
+            except (asyncio.CancelledError, Exception):
+                pass
+            self.monitoring_task = None
+        try:
+            await self.ctx.store.release_lock(LEASE, self.owner)
+        except Exception:
+            pass
+
+
+async def run_service(ctx: AppContext) -> None:
+    """Standalone monitor process (``python -m finetune_controller_amd.controlplane.monitor``):
+    signal-driven graceful shutdown (HUP/TERM/INT), DB connect, monitor loop
+    (``/root/reference/app/monitor_main.py:43-77``)."""
+    loop = asyncio.get_running_loop()
+    stop = asyncio.Event()
+    for s in (signal.SIGHUP, signal.SIGTERM, signal.SIGINT):
+        try:
+            loop.add_signal_handler(s, stop.set)
+        except (NotImplementedError, RuntimeError):
+            pass
+    loop.set_exception_handler(lambda lp, c: (logger.error("caught exception: %s", c.get("exception", c["message"])),
+                                              stop.set()))
+    await ctx.store.connect()
+    mon = JobMonitor(ctx)
+    await mon.start()
+    try:
+        await stop.wait()
+        logger.info("received exit signal, shutting down")
+    finally:
+        await mon.stop()
+        await ctx.store.close()

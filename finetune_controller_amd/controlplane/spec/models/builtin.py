@@ -1,0 +1,218 @@
+"""Built-in fine-tune job specs.
+
+* ``MNIST`` -- the reference's example (``/root/reference/app/models/examples/mnist.py:13-99``), kept so
+  existing clients/frontends keep working; it still points at the external example image.
+* MI355X specs for the BASELINE.json configs, all running this repository's worker runtime
+  (``python -m finetune_controller_amd.train.cli``, see ``train/cli.py``) in the ROCm worker image:
+
+  ==================  ===================================  =====================
+  name                config                               resources
+  ==================  ===================================  =====================
+  GPT2-small-FT       GPT-2-small full fine-tune           1 CPU worker (plumbing)
+  Llama3-8B-LoRA      Llama-3-8B LoRA bf16 (r16, all-lin)  amd.com/gpu x N
+  Llama3-8B-Full      Llama-3-8B full FT, DDP over RCCL    amd.com/gpu x 8
+  Mistral-7B-QLoRA    Mistral-7B QLoRA NF4                 amd.com/gpu x 1
+  ==================  ===================================  =====================
+
+Multi-GPU specs launch one process per GPU with torchrun inside the pod; with ``cluster_nodes > 1``
+the Kubeflow operator's ``PET_*`` rendezvous variables are forwarded (one pod per node, one process
+per GPU, RCCL over xGMI inside each node).
+"""
+from __future__ import annotations
+
+from typing import ClassVar
+
+from pydantic import Field
+
+from ..finetuning import (BaseFineTuneModel, TrainingArguments, TrainingDataset, TrainingFramework,
+                          TrainingResources, TrainingTask)
+
+WORKER_IMAGE = "ghcr.io/finetune-controller-amd/worker-rocm:latest"
+
+
+# ------------------------------------------------------------------ reference example (compat)
+class MNISTConfig(TrainingArguments):
+    """Model Params for MNIST Finetune Job"""
+
+    batch_size: int = Field(default=64, description="Size of each batch during training")
+    test_batch_size: int = Field(default=1000, description="Size of each batch during testing")
+    epochs: int = Field(default=1, description="Number of epochs for training")
+    lr: float = Field(default=1.0, description="Learning rate for the optimizer")
+    gamma: float = Field(default=0.7, description="Learning rate step gamma for scheduler")
+    no_cuda: bool = Field(default=False, description="Disable the GPU (use CPU instead)")
+    seed: int = Field(default=1, description="Random seed for reproducibility")
+    log_interval: int = Field(default=10, description="How many batches to wait before logging training status")
+    save_model: bool = Field(default=False, description="Whether to save the trained model")
+
+
+class MNIST(BaseFineTuneModel):
+    """Finetune Job Spec for MNIST (external example image)"""
+
+    name: str = "MNIST"
+    inference_name: str | None = "MNIST"
+    description: str = "Example MNIST model for fine-tuning"
+    project_url: str = "https://github.com/acceleratedscience/model-foobar"
+    image: str = "quay.io/brian_duenas/mnist:latest"
+    command: list[str] = ["/bin/bash", "-c", "python mnist_training_script.py"]
+    framework: TrainingFramework = TrainingFramework.PYTORCH
+    task: TrainingTask = TrainingTask.CLASSIFICATION
+    dataset_info: TrainingDataset = TrainingDataset(description="MNIST model does not expect a dataset",
+                                                    dataset_required=False)
+    resources: TrainingResources = TrainingResources(requests={"cpu": 4, "memory": "1Gi"},
+                                                     limits={"cpu": 8, "memory": "2Gi"})
+    # the reference's default of 0 (below ge=1, defaults are not validated) means "request no GPU"
+    accelerator_count: int = Field(default=0, ge=1, description="Number of gpu devices to use for training per worker")
+    promotion_path: str = Field(default="molecules/mnist/mnist_test", description="s3 promotion prefix")
+    training_arguments: MNISTConfig = MNISTConfig()
+
+    def run_cmd(self) -> list[str]:
+        t = self.training_arguments
+        args = []
+        if t.no_cuda:
+            args.append("--no-cuda")
+        if t.save_model:
+            args.append("--save-model")
+        args += [f"--batch-size={t.batch_size}", f"--test-batch-size={t.test_batch_size}", f"--epochs={t.epochs}",
+                 f"--lr={t.lr}", f"--seed={t.seed}", f"--log-interval={t.log_interval}", f"--gamma={t.gamma}"]
+        return self.append_args(args)
+
+
+# ------------------------------------------------------------------ MI355X worker-runtime specs
+class LMTrainingArguments(TrainingArguments):
+    """Flags of ``finetune_controller_amd.train.cli`` exposed to the UI form."""
+
+    batch_size: int = Field(default=4, ge=1, description="Micro-batch (sequences) per GPU")
+    seq_len: int = Field(default=4096, ge=16, description="Tokens per sequence")
+    grad_accum: int = Field(default=1, ge=1, description="Gradient accumulation steps")
+    epochs: int = Field(default=1, ge=1, description="Passes over the dataset")
+    max_steps: int = Field(default=0, ge=0, description="Stop after this many optimizer steps (0 = epochs)")
+    lr: float = Field(default=2e-4, gt=0, description="Peak learning rate")
+    warmup_steps: int = Field(default=10, ge=0, description="Linear warmup steps")
+    schedule: str = Field(default="cosine", description="cosine | linear | constant")
+    weight_decay: float = Field(default=0.0, ge=0, description="AdamW decoupled weight decay")
+    max_grad_norm: float = Field(default=1.0, ge=0, description="Global grad-norm clip (0 = off)")
+    seed: int = Field(default=1, description="Random seed")
+    log_interval: int = Field(default=10, ge=1, description="Steps between metrics.csv rows / Epoch log lines")
+    save_every: int = Field(default=0, ge=0, description="Resume checkpoint every N steps (0 = only at the end)")
+    checkpoint_layers: bool = Field(default=False, description="Activation checkpointing per decoder layer")
+
+
+class LoRAArguments(LMTrainingArguments):
+    lora_r: int = Field(default=16, ge=1, le=256, description="LoRA rank")
+    lora_alpha: float = Field(default=32.0, gt=0, description="LoRA alpha (scale = alpha / r)")
+    lora_targets: str = Field(default="q_proj,k_proj,v_proj,o_proj,gate_proj,up_proj,down_proj",
+                              description="Comma-separated target modules")
+    lr: float = Field(default=2e-4, gt=0, description="Peak learning rate")
+
+
+class _WorkerSpec(BaseFineTuneModel):
+    """Common run_cmd for specs that run this repository's trainer."""
+
+    image: str = WORKER_IMAGE
+    command: list[str] = ["/bin/bash", "-c", ""]
+    framework: TrainingFramework = TrainingFramework.PYTORCH
+    task: TrainingTask = TrainingTask.CAUSAL_LM
+    store_asset_patterns: list[str] = Field(default=["*.json", "*.yaml", "*.csv", "*.pt", "*.ckpt", "*.safetensors"],
+                                            description="Pattern match a list of files to store.")
+    dataset_info: TrainingDataset = TrainingDataset(
+        description="Optional: tokens (.bin uint16/uint32, .npy) or text (.jsonl with 'text', .txt, .csv). "
+                    "Without a dataset the worker trains on synthetic tokens.", dataset_required=False)
+
+    # subclass knobs (class-level, not form fields)
+    model_preset: ClassVar[str] = "llama3-8b"
+    method: ClassVar[str] = "lora"
+
+    def _launcher(self) -> str:
+        n = max(1, int(self.accelerator_count))
+        if n == 1 and self.cluster_nodes == 1:
+            return "python -m finetune_controller_amd.train.cli"
+        rdzv = ("--nnodes=${PET_NNODES:-1} --node-rank=${PET_NODE_RANK:-0} "
+                "--master-addr=${PET_MASTER_ADDR:-127.0.0.1} --master-port=${PET_MASTER_PORT:-29500}"
+                if self.cluster_nodes > 1 else "--standalone")
+        return f"torchrun {rdzv} --nproc-per-node={n} -m finetune_controller_amd.train.cli"
+
+    def run_cmd(self) -> list[str]:
+        t = self.training_arguments
+        args = [f"--model={self.model_preset}", f"--method={self.method}"]
+        for k, v in t.model_dump().items():
+            if isinstance(v, bool):
+                if v:
+                    args.append(f"--{k.replace('_', '-')}")
+            else:
+                args.append(f"--{k.replace('_', '-')}={v}")
+        cmd = list(self.command)
+        cmd[-1] = self._launcher()
+        self_cmd = self.model_copy(update={"command": cmd})
+        return BaseFineTuneModel.append_args(self_cmd, args)
+
+
+class GPT2SmallFT(_WorkerSpec):
+    """GPT-2-small full fine-tune on one CPU worker (BASELINE.json plumbing config)."""
+
+    name: str = "GPT2-small-FT"
+    inference_name: str | None = "GPT2-small"
+    description: str = "GPT-2 small (124M) full fine-tune; CPU worker -- end-to-end plumbing of the controller"
+    project_url: str = "https://huggingface.co/openai-community/gpt2"
+    resources: TrainingResources = TrainingResources(requests={"cpu": 4, "memory": "8Gi"},
+                                                     limits={"cpu": 8, "memory": "16Gi"})
+    accelerator_count: int = Field(default=0, ge=1, description="CPU job: no GPU requested")
+    promotion_path: str = Field(default="language/gpt2/finetune", description="s3 promotion prefix")
+    model_preset: ClassVar[str] = "gpt2-small"
+    method: ClassVar[str] = "full"
+    training_arguments: LMTrainingArguments = LMTrainingArguments(batch_size=2, seq_len=256, lr=5e-5, max_steps=20)
+
+    def run_cmd(self) -> list[str]:
+        cmd = super().run_cmd()
+        cmd[-1] += " --device=cpu"
+        return cmd
+
+
+class Llama3_8B_LoRA(_WorkerSpec):
+    """Llama-3-8B LoRA (bf16) on MI355X -- the north-star config."""
+
+    name: str = "Llama3-8B-LoRA"
+    inference_name: str | None = "Llama3-8B"
+    description: str = "Llama-3-8B LoRA fine-tune on AMD Instinct MI355X (HIP/CDNA4 kernels, RCCL data parallel)"
+    project_url: str = "https://huggingface.co/meta-llama/Meta-Llama-3-8B"
+    resources: TrainingResources = TrainingResources(requests={"cpu": 16, "memory": "128Gi"},
+                                                     limits={"cpu": 32, "memory": "256Gi"})
+    accelerator_count: int = Field(default=1, ge=1, description="MI355X GPUs per worker")
+    promotion_path: str = Field(default="language/llama3-8b/lora", description="s3 promotion prefix")
+    model_preset: ClassVar[str] = "llama3-8b"
+    method: ClassVar[str] = "lora"
+    training_arguments: LoRAArguments = LoRAArguments()
+
+
+class Llama3_8B_Full(_WorkerSpec):
+    """Llama-3-8B full fine-tune, DDP over 8 x MI355X (RCCL all-reduce over xGMI)."""
+
+    name: str = "Llama3-8B-Full"
+    inference_name: str | None = "Llama3-8B"
+    description: str = "Llama-3-8B full fine-tune, 8 x MI355X data parallel (bf16 weights, fp32 master/Adam)"
+    project_url: str = "https://huggingface.co/meta-llama/Meta-Llama-3-8B"
+    resources: TrainingResources = TrainingResources(requests={"cpu": 64, "memory": "512Gi"},
+                                                     limits={"cpu": 128, "memory": "1024Gi"})
+    accelerator_count: int = Field(default=8, ge=1, description="MI355X GPUs per worker")
+    promotion_path: str = Field(default="language/llama3-8b/full", description="s3 promotion prefix")
+    model_preset: ClassVar[str] = "llama3-8b"
+    method: ClassVar[str] = "full"
+    training_arguments: LMTrainingArguments = LMTrainingArguments(batch_size=2, lr=2e-5, checkpoint_layers=False)
+
+
+class Mistral7B_QLoRA(_WorkerSpec):
+    """Mistral-7B QLoRA (NF4 base, bf16 adapters) on one MI355X."""
+
+    name: str = "Mistral-7B-QLoRA"
+    inference_name: str | None = "Mistral-7B"
+    description: str = "Mistral-7B QLoRA: NF4 base weights decoded on the fly for bf16 MFMA GEMMs"
+    project_url: str = "https://huggingface.co/mistralai/Mistral-7B-v0.1"
+    resources: TrainingResources = TrainingResources(requests={"cpu": 16, "memory": "64Gi"},
+                                                     limits={"cpu": 32, "memory": "128Gi"})
+    accelerator_count: int = Field(default=1, ge=1, description="MI355X GPUs per worker")
+    promotion_path: str = Field(default="language/mistral-7b/qlora", description="s3 promotion prefix")
+    model_preset: ClassVar[str] = "mistral-7b"
+    method: ClassVar[str] = "qlora"
+    training_arguments: LoRAArguments = LoRAArguments()
+
+
+BUILTIN_MODELS = [MNIST, GPT2SmallFT, Llama3_8B_LoRA, Llama3_8B_Full, Mistral7B_QLoRA]

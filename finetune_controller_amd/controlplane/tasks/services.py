@@ -1,0 +1,127 @@
+"""Orchestration services (C5 task builder, C14 dataset ingest, C15 promotion).
+
+* ``task_builder`` -- resolve the dataset (reuse by id / stream from URL / uploaded file), compute the
+  artifacts URI, render and submit the PyTorchJob, insert the job document
+  (``/root/reference/app/jobs/task_builder.py:19-81``);
+* ``upload_dataset_file`` / ``stream_dataset_url`` -- into ``finetune_jobs/{user}/{job}/dataset/`` plus
+  a dataset document (``/root/reference/app/utils/dataset_helpers.py:20-145``); the URL path streams
+  chunks straight to object storage (never buffered whole);
+* ``PromotionTask`` -- IN_PROGRESS -> copy -> COMPLETED / FAILED, and DELETING -> cleanup ->
+  NOT_PROMOTED (revert to COMPLETED on error) (``/root/reference/app/tasks/promotion.py:11-62``).
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import os
+from urllib.parse import urlparse
+
+import httpx
+
+from ..context import AppContext
+from ..core.naming import generate_short_uuid
+from ..k8s.manifest import build_pytorchjob_manifest
+from ..schemas.db import DatasetModel, DatasetTypes, PromotionStatus
+from ..schemas.jobs import DatasetInput, JobInput
+
+logger = logging.getLogger("ftc.tasks")
+
+
+class NotFound(Exception):
+    pass
+
+
+async def upload_dataset_file(ctx: AppContext, job: JobInput, upload, description: str) -> DatasetModel:
+    try:
+        s3_uri = await ctx.s3.upload_dataset(upload.path, job.user_id, job.job_id, name=upload.filename)
+        doc = await ctx.store.insert_dataset(job.user_id, job.job_id, DatasetTypes(s3_uri=s3_uri), upload.filename,
+                                             description)
+        job.s3_uri = doc.dataset.s3_uri
+        job.model.dataset_info.dataset_name = doc.dataset_name
+        return doc
+    finally:
+        if os.path.exists(upload.path):
+            os.remove(upload.path)
+
+
+def filename_from_response(headers, url: str) -> str:
+    cd = headers.get("Content-Disposition") or headers.get("content-disposition")
+    if cd and "filename=" in cd:
+        return cd.split("filename=")[-1].strip().strip('"')
+    return os.path.basename(urlparse(url).path) or "default_filename-" + generate_short_uuid()
+
+
+async def stream_dataset_url(ctx: AppContext, job: JobInput, url: str, description: str,
+                             http_client: httpx.Client | None = None) -> DatasetModel:
+    def run():
+        client = http_client or httpx.Client(timeout=None, follow_redirects=True)
+        try:
+            with client.stream("GET", url) as r:
+                r.raise_for_status()
+                name = filename_from_response(r.headers, url)
+                key = f"{ctx.s3.get_dataset_uri_string(ctx.s3.bucket, job.user_id, job.job_id, True)}/{os.path.basename(name)}"
+                ctx.objects.put_stream(ctx.s3.bucket, key, r.iter_bytes(1 << 20))
+                return name, f"s3://{ctx.s3.bucket}/{key}"
+        finally:
+            if http_client is None:
+                client.close()
+
+    name, s3_uri = await asyncio.to_thread(run)
+    doc = await ctx.store.insert_dataset(job.user_id, job.job_id, DatasetTypes(s3_uri=s3_uri, http_url=url), name,
+                                         description)
+    job.s3_uri = doc.dataset.s3_uri
+    job.model.dataset_info.dataset_name = doc.dataset_name
+    return doc
+
+
+async def task_builder(ctx: AppContext, job: JobInput, dataset_input: DatasetInput, http_client=None) -> dict:
+    dataset_doc = None
+    if dataset_input.dataset_id:
+        dataset_doc = await ctx.store.update_dataset(job.user_id, dataset_input.dataset_id, job.job_id)
+        if dataset_doc is None:
+            raise NotFound("Selected dataset not available")
+        job.s3_uri = dataset_doc.dataset.s3_uri
+        job.model.dataset_info.dataset_name = dataset_doc.dataset_name
+    elif dataset_input.dataset_url:
+        dataset_doc = await stream_dataset_url(ctx, job, str(dataset_input.dataset_url),
+                                               dataset_input.dataset_description, http_client)
+    elif dataset_input.dataset_file:
+        dataset_doc = await upload_dataset_file(ctx, job, dataset_input.dataset_file, dataset_input.dataset_description)
+
+    job.s3_artifacts_uri = ctx.s3.get_artifacts_uri_string(ctx.settings.S3_BUCKET_NAME, job.user_id, job.job_id)
+    worker = ctx.devices.get_worker(job.device)
+    if worker is None:
+        raise ValueError(f"Invalid device '{job.device}'. Must be one of {ctx.devices.list_workers()}.")
+    manifest = build_pytorchjob_manifest(job, worker, ctx.settings, ctx.namespace)
+    result = await asyncio.to_thread(ctx.kube.create_pytorchjob, ctx.namespace, manifest)
+    await ctx.store.create_job(
+        user_id=job.user_id, job_id=job.job_id, job_name=job.job_name, model_name=job.model_name, device=job.device,
+        task=job.model.task.value, framework=job.model.framework.value, arguments=job.arguments,
+        dataset_id=dataset_doc.id if dataset_doc else None, atrifacts_uri=job.s3_artifacts_uri,
+        dataset_name=job.model.dataset_info.dataset_name or None,
+        metadata={"kubernetes_job_name": (result.get("metadata") or {}).get("name")})
+    return result
+
+
+class PromotionTask:
+    @staticmethod
+    async def promote_job_task(ctx: AppContext, job_id: str, atrifacts_uri: str, destination_uri: str) -> None:
+        try:
+            await ctx.store.update_job_promotion(job_id, PromotionStatus.IN_PROGRESS, destination_uri)
+            await ctx.s3.copy_s3_object(atrifacts_uri, destination_uri)
+            await ctx.store.update_job_promotion(job_id, PromotionStatus.COMPLETED, destination_uri)
+            logger.info("promotion complete for job %s", job_id)
+        except Exception as e:
+            logger.error("promotion failed for job %s: %s", job_id, e)
+            await ctx.store.update_job_promotion(job_id, PromotionStatus.FAILED, destination_uri)
+
+    @staticmethod
+    async def unpromote_job_task(ctx: AppContext, job_id: str, destination_uri: str) -> None:
+        try:
+            await ctx.store.update_job_promotion(job_id, PromotionStatus.DELETING, destination_uri)
+            await ctx.s3.cleanup_uri_items(destination_uri)
+            await ctx.store.update_job_promotion(job_id, PromotionStatus.NOT_PROMOTED, None)
+            logger.info("unpromotion complete for job %s", job_id)
+        except Exception as e:
+            logger.error("unpromotion failed for job %s: %s", job_id, e)
+            await ctx.store.update_job_promotion(job_id, PromotionStatus.COMPLETED, destination_uri)
