@@ -310,7 +310,11 @@ def create_app(ctx: AppContext, run_monitor: bool | None = None, validator_facto
             cls = ctx.registry.get(model)
             if not cls:
                 raise HTTPException(status_code=404, detail=f"Model '{model}' not found")
-            inst = cls.model_validate(cls(training_arguments=model_arguments))
+            # user arguments override the SPEC's default arguments (the reference rebuilds the arguments
+            # class from its field defaults, silently dropping per-spec defaults such as GPT-2's seq_len)
+            base = cls.model_fields["training_arguments"].get_default()
+            merged = {**(base.model_dump() if base is not None else {}), **model_arguments}
+            inst = cls.model_validate(cls(training_arguments=merged))
             model_arguments = inst.training_arguments.model_dump()
             if task != inst.task:
                 raise HTTPException(status_code=400, detail=f"Invalid task ({task.name}) for model ({inst.task.name})")

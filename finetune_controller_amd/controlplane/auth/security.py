@@ -230,7 +230,14 @@ class OpenBridgeAuthMiddleware:
             state = scope.setdefault("state", {})
             state["jwt_data"] = JWTExtraInfo(active=bool(info.get("active")), user_id=info.get("sub"),
                                              group_id=info.get("group_id"))
-            state["decoded_jwt"] = decode_jwt(token)
+            try:
+                state["decoded_jwt"] = decode_jwt(token)
+            except HTTPAuthError:
+                # opaque (non-JWT) access token validated by introspection: claims come from the IdP
+                scp = info.get("scp") or [x for x in str(info.get("scope", "")).split() if x]
+                state["decoded_jwt"] = UserJWT(user_id=str(info.get("sub") or info.get("username")),
+                                               audience=info.get("aud"), available_models=list(scp),
+                                               expires=info.get("exp"))
         except HTTPAuthError as e:
             return await self._deny(scope, receive, send, e.status_code, e.detail)
         except Exception as e:

@@ -115,6 +115,7 @@ class FakeCluster(KubeClient):
         self._stop = threading.Event()
         self._fail_next: set[str] = set()
         self.history: list[tuple[str, str]] = []  # (job, condition) transitions, for tests
+        self.deleted_pod_logs: dict[str, list[str]] = {}  # logs of pods removed with their job
 
     # ------------------------------------------------------------------ KubeClient API
     def create_custom(self, group, version, namespace, plural, body):
@@ -133,6 +134,8 @@ class FakeCluster(KubeClient):
             if plural == "pytorchjobs":
                 obj["status"] = {"conditions": []}
                 self._set_condition(obj, "Created", "PyTorchJobCreated", f"PyTorchJob {name} is created.")
+                if obj["spec"]["runPolicy"].get("suspend"):
+                    self._set_condition(obj, "Suspended", "PyTorchJobSuspended", f"PyTorchJob {name} is suspended.")
             self._event(namespace, name, "Normal", "Created", f"{plural}/{name} created")
             return copy.deepcopy(obj)
 
@@ -153,7 +156,9 @@ class FakeCluster(KubeClient):
                 self._release(namespace, name)
                 self.objects.pop(("kueue.x-k8s.io", "workloads", namespace, f"pytorchjob-{name}"), None)
                 for pkey in [k for k in self.pods if k[0] == namespace and self.pods[k].job == name]:
-                    self._kill(self.pods.pop(pkey))
+                    pod = self.pods.pop(pkey)
+                    self.deleted_pod_logs[pod.name] = list(pod.logs)
+                    self._kill(pod)
             return {"status": "Success", "metadata": obj["metadata"]}
 
     def list_custom(self, group, version, namespace, plural, label_selector=None):

@@ -31,6 +31,11 @@ class NotFound(Exception):
     pass
 
 
+def _http_client() -> httpx.Client:
+    """HTTP client used to stream dataset URLs (patched in tests)."""
+    return httpx.Client(timeout=None, follow_redirects=True)
+
+
 async def upload_dataset_file(ctx: AppContext, job: JobInput, upload, description: str) -> DatasetModel:
     try:
         s3_uri = await ctx.s3.upload_dataset(upload.path, job.user_id, job.job_id, name=upload.filename)
@@ -54,7 +59,7 @@ def filename_from_response(headers, url: str) -> str:
 async def stream_dataset_url(ctx: AppContext, job: JobInput, url: str, description: str,
                              http_client: httpx.Client | None = None) -> DatasetModel:
     def run():
-        client = http_client or httpx.Client(timeout=None, follow_redirects=True)
+        client = http_client or _http_client()
         try:
             with client.stream("GET", url) as r:
                 r.raise_for_status()

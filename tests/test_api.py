@@ -1,0 +1,238 @@
+"""Every route of the REST + WebSocket surface against in-process fakes: in-memory
+Mongo engine, local object store, FakeCluster (simulated pods) -- SURVEY.md §4 "[new] API integration"."""
+import asyncio
+import io
+import json
+import zipfile
+
+import httpx
+import pytest
+from fastapi.testclient import TestClient
+
+from finetune_controller_amd.controlplane.api.app import create_app
+from finetune_controller_amd.controlplane.context import AppContext
+from finetune_controller_amd.controlplane.monitor.reconciler import JobMonitor
+from finetune_controller_amd.controlplane.tasks import services
+
+FORM = {"job_name": "my run", "model": "Llama3-8B-LoRA", "device": "mi355x", "task": "causal_lm",
+        "arguments": json.dumps({"max_steps": 3, "lora_r": 8})}
+
+
+@pytest.fixture
+def env(tmp_path):
+    ctx = AppContext.local(workdir=str(tmp_path), run_processes=False)
+    ctx.kube.sim_ticks = 2
+    app = create_app(ctx, run_monitor=False, force_auth=False)
+    with TestClient(app) as c:
+        yield ctx, c
+
+
+def settle(ctx, rounds=12):
+    """Drive the FakeCluster and one monitor pass per round (sidecar threads get time to sync)."""
+    import time
+
+    mon = JobMonitor(ctx, interval=0)
+    ctx.kube.sync_interval = 0.02
+    for i in range(rounds * 10):
+        ctx.kube.reconcile()
+        asyncio.run(mon.reconcile_once())
+        time.sleep(0.03)
+        if i >= rounds and not ctx.kube.list_pytorchjobs(ctx.namespace):
+            break
+
+
+def submit(c, **over):
+    f = dict(FORM)
+    f.update(over)
+    r = c.post("/api/v1/jobs", data=f)
+    assert r.status_code == 200, r.text
+    return r.json()["job_id"]
+
+
+def test_health_models_details(env):
+    ctx, c = env
+    assert c.get("/health").json() == {"status": "ok"}
+    assert c.get("/api/v1/health").json() == {"status": "ok"}
+    models = c.get("/api/v1/models").json()
+    assert "Llama3-8B-LoRA" in models
+    m = models["Llama3-8B-LoRA"]
+    assert m["devices"] == ["cpu", "mi355x"] and "lora_r" in m["arguments"] and m["task"] == "causal_lm"
+    d = c.get("/api/v1/models/Llama3-8B-LoRA").json()
+    assert d["task"] == "causal_lm" and d["framework"] == "pytorch"
+    assert d["arguments"]["accelerator_count"] == 1 and "image" not in d["arguments"]
+    assert c.get("/api/v1/models/Nope").status_code == 404
+    assert c.get("/api/v1/sample-data.csv").text.startswith("Id,SMILES,esol")
+
+
+def test_submit_validation_errors(env):
+    ctx, c = env
+    assert c.post("/api/v1/jobs", data={"job_name": "x"}).status_code == 422
+    assert c.post("/api/v1/jobs", data=dict(FORM, device="tpu")).status_code == 422
+    assert c.post("/api/v1/jobs", data=dict(FORM, arguments="{bad")).json()["detail"] == "Invalid JSON for arguments"
+    r = c.post("/api/v1/jobs", data=dict(FORM, arguments=json.dumps({"lora_r": 0})))
+    assert r.status_code == 400 and "Invalid model parameters" in r.json()["detail"] and "lora_r" in r.json()["detail"]
+    r = c.post("/api/v1/jobs", data=dict(FORM, task="regression"))
+    assert r.status_code == 400 and "Invalid task" in r.json()["detail"]
+    assert c.post("/api/v1/jobs", data=dict(FORM, model="Nope")).status_code == 404
+    assert c.post("/api/v1/jobs", data=dict(FORM, user_id="a!")).status_code == 422
+
+
+def test_submit_lifecycle_metrics_logs_cancel(env):
+    ctx, c = env
+    jid = submit(c)
+    j = c.get(f"/api/v1/jobs/{jid}").json()
+    assert j["status"] == "queued" and j["arguments"]["lora_r"] == 8 and j["atrifacts_uri"].endswith(f"{jid}/artifacts")
+    assert c.get(f"/api/v1/jobs/{jid}/metrics").status_code == 202  # running, no metrics yet
+    settle(ctx)
+    j = c.get(f"/api/v1/jobs/{jid}").json()
+    assert j["status"] == "completed" and j["metadata"]["training_duration"] >= 0
+    assert j["metadata"]["completion_time"] and j["duration"] is not None
+    m = c.get(f"/api/v1/jobs/{jid}/metrics").json()
+    steps = [row["step"] for row in m["metrics"]]
+    assert steps == sorted(steps, reverse=True) and m["metrics_url"]
+    # succeeded PyTorchJobs are deleted by the monitor
+    assert c.get("/api/v1/admin/jobs/list").json() == {"jobs": []}
+    assert c.post(f"/api/v1/jobs/{jid}/cancel").status_code == 409
+    jid2 = submit(c)
+    r = c.post(f"/api/v1/jobs/{jid2}/cancel").json()
+    assert r["status"] == "canceled" and r["end_time"]
+    assert c.get(f"/api/v1/jobs/{jid2}").json()["metadata"]["message"] == "Job canceled by user"
+    page = c.get("/api/v1/jobs", params={"page": 1, "page_size": 10}).json()
+    assert page["total"] == 2 and {i["status"] for i in page["items"]} == {"completed", "canceled"}
+    item = [i for i in page["items"] if i["job_id"] == jid][0]
+    assert item["meta_"]["data"]["promotion_path"] == "language/llama3-8b/lora" and item["index_"] >= 1
+
+
+def test_dataset_upload_reuse_url_and_delete(env, monkeypatch):
+    ctx, c = env
+    files = {"dataset": ("train.jsonl", io.BytesIO(b'{"text": "hello"}\n' * 10), "application/json")}
+    r = c.post("/api/v1/jobs", data=dict(FORM, dataset_description="tiny"), files=files)
+    assert r.status_code == 200, r.text
+    jid = r.json()["job_id"]
+    job = ctx.kube.get_pytorchjob(ctx.namespace, jid)
+    init = job["spec"]["pytorchReplicaSpecs"]["Master"]["template"]["spec"]["initContainers"]
+    assert "dataset/train.jsonl" in init[0]["args"][0]
+    all_ds = c.get("/api/v1/datasets/all").json()
+    assert len(all_ds) == 1 and "s3_uri" not in all_ds[0]["dataset"] and all_ds[0]["dataset_name"] == "train.jsonl"
+    ds_id = all_ds[0]["id"]
+    jid2 = submit(c, dataset_id=ds_id)
+    assert c.get(f"/api/v1/jobs/{jid2}").json()["dataset_id"] == ds_id
+    assert c.post("/api/v1/jobs", data=dict(FORM, dataset_id="0" * 24)).status_code == 404
+
+    def handler(req):
+        return httpx.Response(200, content=b"a,b\n1,2\n", headers={"Content-Disposition": 'attachment; filename="x.csv"'})
+
+    monkeypatch.setattr(services, "_http_client", lambda: httpx.Client(transport=httpx.MockTransport(handler)))
+    jid3 = submit(c, dataset_url="https://example.org/data/x.csv")
+    page = c.get("/api/v1/datasets", params={"page_size": 10}).json()
+    assert page["total"] == 2
+    urls = [i for i in page["items"] if i["dataset_name"] == "x.csv"][0]
+    assert urls["meta_"]["data"]["Source"] == "https://example.org/data/x.csv"
+    first = [i for i in page["items"] if i["dataset_name"] == "train.jsonl"][0]
+    assert first["job_ref_names"] == ["my run", "my run"]
+    assert c.delete(f"/api/v1/datasets/{ds_id}").json() == {"message": "Dataset deleted successfully"}
+    assert c.delete(f"/api/v1/datasets/{ds_id}").status_code == 404
+    assert jid3
+
+
+def test_promote_unpromote_artifacts_delete(env):
+    ctx, c = env
+    jid = submit(c)
+    r = c.post(f"/api/v1/jobs/{jid}/promote")
+    assert r.status_code == 200 and r.json()["detail"] == "Cannot promote running job"  # reference quirk
+    settle(ctx)
+    r = c.post(f"/api/v1/jobs/{jid}/promote").json()
+    assert r["status"] == "promotion_initiated"
+    j = c.get(f"/api/v1/jobs/{jid}").json()
+    assert j["promoted"] == "completed" and j["destination_uri"] == f"s3://ftc-deploy/language/llama3-8b/lora/{jid}"
+    assert j["status_merged"] == "deployed"
+    promoted = ctx.objects.list("ftc-deploy", f"language/llama3-8b/lora/{jid}")
+    assert {o.Key.rsplit("/", 1)[1] for o in promoted} >= {"metrics.csv"}
+    urls = c.get(f"/api/v1/admin/artifacts/presigned_urls/{jid}").json()["artifacts"]
+    assert {u["key"] for u in urls} >= {"metrics.csv", "adapter_config.json"}
+    z = c.get(f"/api/v1/admin/artifacts/{jid}")
+    assert z.status_code == 200 and z.headers["content-type"] == "application/zip"
+    assert "metrics.csv" in zipfile.ZipFile(io.BytesIO(z.content)).namelist()
+    # rate limit: promote is 2/minute per client
+    assert c.post(f"/api/v1/jobs/{jid}/unpromote").json()["status"] == "unpromotion_initiated"
+    assert c.post(f"/api/v1/jobs/{jid}/promote").status_code == 429
+    j = c.get(f"/api/v1/jobs/{jid}").json()
+    assert j["promoted"] == "not_promoted" and not ctx.objects.list("ftc-deploy", "language/")
+    r = c.request("DELETE", "/api/v1/jobs/delete", json={"job_ids": [jid]})
+    assert r.json() == {"job_id": {"message": "Jobs deleted successfully"}}
+    assert c.get(f"/api/v1/jobs/{jid}").status_code == 404
+    assert not ctx.objects.list("ftc-bucket", f"finetune_jobs/default_user/{jid}")
+
+
+def test_admin_poll_and_clean(env):
+    ctx, c = env
+    jid = submit(c)
+    ctx.kube.reconcile()
+    ctx.kube.reconcile()
+    st = c.get(f"/api/v1/admin/job/poll/{jid}").json()["status"]
+    assert st["type"] in ("Created", "Running") and "events" in st and "restart_count" in st
+    assert c.get("/api/v1/admin/job/poll/nope").status_code == 404
+    settle(ctx)
+    jid2 = submit(c)  # still running -> skipped by clean
+    r = c.delete("/api/v1/admin/jobs/default_user").json()
+    assert r["jobs"] == [jid] and r["skipped"][0]["job_id"] == jid2
+
+
+def test_websocket_log_stream(env):
+    ctx, c = env
+    jid = submit(c)
+    settle(ctx, rounds=3)  # running, some log lines
+    # pods of the succeeded job are deleted; stream a running job instead
+    jid2 = submit(c)
+    ctx.kube.reconcile()
+    ctx.kube.reconcile()
+    asyncio.run(JobMonitor(ctx, interval=0).reconcile_once())
+    ctx.kube.reconcile()
+    with c.websocket_connect(f"/api/v1/logs/{jid2}?follow=false&full_log=true") as ws:
+        msgs = []
+        try:
+            while True:
+                msgs.append(ws.receive_text())
+        except Exception:
+            pass
+    text = "\n".join(msgs)
+    assert "Fetching all previous logs" in text and "Epoch 0" in text
+    assert "simulated training container" not in text  # suppressed until the first "Epoch" line
+    assert jid
+
+
+def test_dev_auth_routes(env):
+    ctx, c = env
+    tok = c.get("/auth/generate", params={"user": "erin"}).json()["token"]
+    assert c.get("/auth/verify", params={"token": tok}).json()["sub"] == "erin"
+    r = c.get("/auth/cookie", params={"user": "frank"})
+    assert r.status_code == 200 and "bridge-user" in r.cookies
+    schema = c.get("/openapi.json").json()
+    assert schema["components"]["securitySchemes"]["BearerAuth"]["scheme"] == "bearer"
+    assert schema["paths"]["/api/v1/jobs"]["post"]["security"] == [{"BearerAuth": []}]
+
+
+def test_auth_enforced_ownership_and_model_scopes(tmp_path):
+    ctx = AppContext.local(workdir=str(tmp_path), run_processes=False, ENVIRONMENT="local")
+    app = create_app(ctx, run_monitor=False, force_auth=True,
+                     validator_factory=lambda: type("V", (), {"validate_token": staticmethod(_reject)})())
+    with TestClient(app) as c:
+        from finetune_controller_amd.controlplane.auth.security import dev_generate_token
+
+        a = dev_generate_token("dev-secret", "HS256", "alice", ["Llama3-8B"])
+        b = dev_generate_token("dev-secret", "HS256", "bob", ["GPT2-small"])
+        assert c.get("/api/v1/models").status_code == 401
+        ha, hb = {"Authorization": f"Bearer {a}"}, {"Authorization": f"Bearer {b}"}
+        assert list(c.get("/api/v1/models", headers=hb).json()) == ["GPT2-small-FT"]
+        assert c.post("/api/v1/jobs", data=FORM, headers=hb).status_code == 404  # model not in bob's scopes
+        jid = c.post("/api/v1/jobs", data=dict(FORM, user_id="ignored"), headers=ha).json()["job_id"]
+        assert c.get(f"/api/v1/jobs/{jid}", headers=ha).json()["user_id"] == "alice"
+        assert c.get(f"/api/v1/jobs/{jid}", headers=hb).status_code == 400
+        assert c.get("/api/v1/jobs", headers=hb).json()["total"] == 0
+        with pytest.raises(Exception):
+            with c.websocket_connect(f"/api/v1/logs/{jid}") as ws:  # no credentials
+                ws.receive_text()
+
+
+async def _reject(token):
+    raise RuntimeError("IdP unavailable")
