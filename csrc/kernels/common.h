@@ -22,8 +22,18 @@ constexpr int kWave = 64;
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+// Raw buffer resource over a wave-uniform base pointer (guide T8): loads then take one 32-bit VGPR
+// offset + an SGPR offset instead of a 64-bit VGPR address per row.
+FTC_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+FTC_DEV u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, int voff_bytes, int soff_bytes) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, voff_bytes, soff_bytes, 0);
+}
 
 FTC_DEV float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
 FTC_DEV float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }

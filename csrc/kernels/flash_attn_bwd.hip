@@ -20,6 +20,8 @@
 // (≈4.3 GB of adds per Llama-3-8B layer at 16k tokens), slower than the extra MFMAs.
 #include "common.h"
 
+#include <cstdlib>
+
 using namespace ftc;
 
 namespace {
@@ -47,15 +49,21 @@ FTC_DEV bf16x8 pack8_bf(const f32x16& p, int base) {
 }
 // A operand (32 rows x 16 k, permuted k) via two transposed reads of an LDS image whose rows are k
 // and columns are the A rows: elements 0..3 <- image rows kb+4h+0..3, elements 4..7 <- +8.
+// tr_offsets() gives the lane's two byte offsets for kb = 0; since the swizzle depends on r & 15 only,
+// kb (a multiple of 16) is a plain immediate on top (few live address VGPRs).
 template <int D>
-FTC_DEV bf16x8 tr_operand(const char* img, int kb, int colbase, int hh, int lane) {
-  const int gi = lane >> 4, li = lane & 15;
+FTC_DEV int2 tr_offsets(int colbase, int lane) {
+  const int hh = lane >> 5, gi = (lane >> 4) & 3, li = lane & 15;
   const int trq = li >> 2, trp = li & 3;
   const int col = colbase + 16 * (gi & 1) + 4 * trp;
   const int chunk = col >> 3, half8 = (col & 7) ? 8 : 0;
-  const int r1 = kb + 4 * hh + trq;
-  s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + lds_off<D>(r1, chunk) + half8));
-  s16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + lds_off<D>(r1 + 8, chunk) + half8));
+  const int r1 = 4 * hh + trq;
+  return make_int2(lds_off<D>(r1, chunk) + half8, lds_off<D>(r1 + 8, chunk) + half8);
+}
+template <int D>
+FTC_DEV bf16x8 tr_read(const char* img, int kb, int2 off) {
+  s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + off.x + kb * D * 2));
+  s16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + off.y + kb * D * 2));
   s16x8 va = {v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
   return __builtin_bit_cast(bf16x8, va);
 }
@@ -103,19 +111,18 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(BwdArgs a) {
 }
 
 // ---------------------------------------------------------------- 2. dK / dV
-template <int D>
-__global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(BwdArgs a) {
+template <int D, int OCC>
+__global__ __launch_bounds__(256, OCC) void bwd_dkdv_kernel(BwdArgs a) {
   constexpr int NCH = D / 8, DSTEPS = D / 16, DT = D / 32;
   constexpr int BKV = 128, BQ2 = 32;
   constexpr int KBYTES = BKV * D * 2, QBYTES = BQ2 * D * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Ks = smem;                      // [128 keys][D]
-  char* Qs = smem + KBYTES;             // [32 q][D]
-  char* Ds = Qs + QBYTES;               // [32 q][D]  (dO)
-  float* lse_s = reinterpret_cast<float*>(Ds + QBYTES);   // [32] (-lse/scale)
-  float* dlt_s = lse_s + BQ2;                            // [32] (-delta)
+  // LDS: K [128 keys][D] | 2 x { Q [32][D] | dO [32][D] | -lse/scale [32] | -delta [32] }
+  constexpr int SLICE = 2 * QBYTES + 2 * BQ2 * 4;
+  char* Ks = smem;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform -> scalar branches
   const int hh = lane >> 5, lr = lane & 31;
   const int S = a.S, G = a.H / a.KV;
   const int nkb = S / BKV;
@@ -159,54 +166,59 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(BwdArgs a) {
   const int nqt = (qend - qbeg + BQ2 - 1) / BQ2;
   const float inv_scale = 1.0f / a.scale;
 
-  // staging: 32 rows x D of Q and of dO per tile; 256 threads x 16 B = 4 KB per pass
+  // staging: 32 rows x D of Q and of dO per slice; buffer loads (wave-uniform slice base in SGPRs)
   constexpr int RPP2 = 256 / NCH, NP2 = BQ2 / RPP2;
   const int lrow = tid / NCH, lch = tid % NCH;
-  uint4 qreg[NP2], dreg[NP2];
+  u32x4 qreg[NP2], dreg[NP2];
   float lreg = 0.f, dlreg = 0.f;
-  auto gload = [&](int hq, int qt) {
-    const uint16_t* qp = a.q + ((long long)b * S + qt) * a.q_rs + (long long)hq * D;
-    const uint16_t* dp = a.dout + ((long long)b * S + qt) * a.o_rs + (long long)hq * D;
-#pragma unroll
-    for (int p = 0; p < NP2; ++p) {
-      const int r = p * RPP2 + lrow;
-      qreg[p] = *reinterpret_cast<const uint4*>(qp + (long long)r * a.q_rs + lch * 8);
-      dreg[p] = *reinterpret_cast<const uint4*>(dp + (long long)r * a.o_rs + lch * 8);
-    }
-    if (tid < BQ2) {
-      const long long idx = ((long long)b * a.H + hq) * S + qt + tid;
-      lreg = -a.lse[idx] * inv_scale;
-      dlreg = -a.delta[idx];
-    }
-  };
-  auto lstore = [&]() {
-#pragma unroll
-    for (int p = 0; p < NP2; ++p) {
-      const int r = p * RPP2 + lrow;
-      *reinterpret_cast<uint4*>(Qs + lds_off<D>(r, lch)) = qreg[p];
-      *reinterpret_cast<uint4*>(Ds + lds_off<D>(r, lch)) = dreg[p];
-    }
-    if (tid < BQ2) {
-      lse_s[tid] = lreg;
-      dlt_s[tid] = dlreg;
-    }
-  };
+  const int qvoff = (lrow * (int)a.q_rs + lch * 8) * 2, dvoff = (lrow * (int)a.o_rs + lch * 8) * 2;
+#define FTC_GLOAD(HQ, QT)                                                                          \
+  {                                                                                                \
+    const auto qrs = make_rsrc(a.q + ((long long)b * S + (QT)) * a.q_rs + (long long)(HQ) * D);    \
+    const auto drs = make_rsrc(a.dout + ((long long)b * S + (QT)) * a.o_rs + (long long)(HQ) * D); \
+    _Pragma("unroll") for (int p = 0; p < NP2; ++p) {                                              \
+      qreg[p] = buf_load16(qrs, qvoff, p * RPP2 * (int)a.q_rs * 2);                                \
+      dreg[p] = buf_load16(drs, dvoff, p * RPP2 * (int)a.o_rs * 2);                                \
+    }                                                                                              \
+    if (tid < BQ2) {                                                                               \
+      const long long idx = ((long long)b * a.H + (HQ)) * S + (QT) + tid;                         \
+      lreg = -a.lse[idx] * inv_scale;                                                              \
+      dlreg = -a.delta[idx];                                                                       \
+    }                                                                                              \
+  }
+#define FTC_LSTORE(BUF)                                                                            \
+  {                                                                                                \
+    char* qs_ = Ks + KBYTES + (BUF) * SLICE;                                                       \
+    _Pragma("unroll") for (int p = 0; p < NP2; ++p) {                                              \
+      *reinterpret_cast<u32x4*>(qs_ + lds_off<D>(p * RPP2 + lrow, lch)) = qreg[p];                 \
+      *reinterpret_cast<u32x4*>(qs_ + QBYTES + lds_off<D>(p * RPP2 + lrow, lch)) = dreg[p];        \
+    }                                                                                              \
+    if (tid < BQ2) {                                                                               \
+      reinterpret_cast<float*>(qs_ + 2 * QBYTES)[tid] = lreg;                                      \
+      reinterpret_cast<float*>(qs_ + 2 * QBYTES)[BQ2 + tid] = dlreg;                               \
+    }                                                                                              \
+  }
 
+  // one barrier per slice: slice it+1 is loaded into registers during slice it's MFMAs and written
+  // to the other LDS buffer afterwards
   const int total = G * nqt;
   if (total > 0) {
-    gload(kvh * G, qbeg);
+    FTC_GLOAD(kvh * G, qbeg);
+    FTC_LSTORE(0);
   }
-  __syncthreads();  // K staged
+  __syncthreads();  // K and slice 0 staged
+  int cur = 0;
   for (int it = 0; it < total; ++it) {
-    const int g = it / nqt, qi = it % nqt;
-    const int qt = qbeg + qi * BQ2;
-    lstore();
-    __syncthreads();
-    if (it + 1 < total) {
+    const int qt = qbeg + (it % nqt) * BQ2;
+    const bool more = it + 1 < total;
+    const char* Qs = Ks + KBYTES + cur * SLICE;
+    const char* Ds = Qs + QBYTES;
+    const float* lse_s = reinterpret_cast<const float*>(Ds + QBYTES);
+    const float* dlt_s = lse_s + BQ2;
+    if (more) {
       const int g2 = (it + 1) / nqt, q2 = qbeg + ((it + 1) % nqt) * BQ2;
-      gload(kvh * G + g2, q2);
+      FTC_GLOAD(kvh * G + g2, q2);
     }
-    (void)g;
     // ---- S[q][k] and dP'[q][k]: rows q (registers), key on the lane
     f32x16 s, dp;
 #pragma unroll
@@ -219,42 +231,52 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(BwdArgs a) {
     const int krow = wave * 32 + lr;
 #pragma unroll
     for (int st = 0; st < DSTEPS; ++st) {
-      const uint4 qa = *reinterpret_cast<const uint4*>(Qs + lds_off<D>(lr, 2 * st + hh));
-      const uint4 kbv = *reinterpret_cast<const uint4*>(Ks + lds_off<D>(krow, 2 * st + hh));
-      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(qa), as_bf8(kbv), s, 0, 0, 0);
-      const uint4 da = *reinterpret_cast<const uint4*>(Ds + lds_off<D>(lr, 2 * st + hh));
-      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(da), vf[st], dp, 0, 0, 0);
+      const u32x4 qa = *reinterpret_cast<const u32x4*>(Qs + lds_off<D>(lr, 2 * st + hh));
+      const u32x4 kbv = *reinterpret_cast<const u32x4*>(Ks + lds_off<D>(krow, 2 * st + hh));
+      const u32x4 da = *reinterpret_cast<const u32x4*>(Ds + lds_off<D>(lr, 2 * st + hh));
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, qa), __builtin_bit_cast(bf16x8, kbv), s, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, da), vf[st], dp, 0, 0, 0);
     }
-    // ---- P, dS (masked)
+    // ---- P, dS (masked; wave-uniform branch, selects inside)
     const bool need_mask = (a.causal && qt < kv0 + wave * 32 + 31) ||
                            (a.window > 0 && qt + BQ2 - 1 - (kv0 + wave * 32) >= a.window);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      float p = __builtin_amdgcn_exp2f(a.c * s[i]);
-      if (need_mask) {
-        const int q = qt + (i & 3) + 8 * (i >> 2) + 4 * hh;
-        const bool bad = (a.causal && key > q) || (a.window > 0 && q - key >= a.window);
-        p = bad ? 0.f : p;
+    for (int i = 0; i < 16; ++i) s[i] = __builtin_amdgcn_exp2f(a.c * s[i]);
+    if (need_mask) {
+      // query q of element i = qt + (i&3) + 8(i>>2) + 4hh is valid iff key <= q (causal) and
+      // q - key < window
+      const int base = qt + 4 * hh;
+      const int lo = (a.causal ? key : -0x3fffffff) - base;
+      const int hi = (a.window > 0 ? key + a.window - 1 : 0x3fffffff) - base;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int off = (i & 3) + 8 * (i >> 2);
+        s[i] = (off >= lo && off <= hi) ? s[i] : 0.f;
       }
-      s[i] = p;
-      dp[i] = p * dp[i];
     }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dp[i] = s[i] * dp[i];
     const bf16x8 pb0 = pack8_bf(s, 0), pb1 = pack8_bf(s, 8);
     const bf16x8 sb0 = pack8_bf(dp, 0), sb1 = pack8_bf(dp, 8);
     // ---- dV^T += dO^T P ; dK^T += Q^T dS   (k of these MFMAs = the 32 query rows)
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
-      const bf16x8 a0 = tr_operand<D>(Ds, 0, dt * 32, hh, lane);
-      const bf16x8 a1 = tr_operand<D>(Ds, 16, dt * 32, hh, lane);
+      const int2 to = tr_offsets<D>(dt * 32, lane);
+      const bf16x8 a0 = tr_read<D>(Ds, 0, to);
+      const bf16x8 a1 = tr_read<D>(Ds, 16, to);
       dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, pb0, dv[dt], 0, 0, 0);
       dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, pb1, dv[dt], 0, 0, 0);
-      const bf16x8 q0v = tr_operand<D>(Qs, 0, dt * 32, hh, lane);
-      const bf16x8 q1v = tr_operand<D>(Qs, 16, dt * 32, hh, lane);
+      const bf16x8 q0v = tr_read<D>(Qs, 0, to);
+      const bf16x8 q1v = tr_read<D>(Qs, 16, to);
       dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q0v, sb0, dk[dt], 0, 0, 0);
       dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q1v, sb1, dk[dt], 0, 0, 0);
     }
-    __syncthreads();  // Qs/Ds/lse_s are overwritten by the next iteration's lstore
+    if (more) { FTC_LSTORE(cur ^ 1); }
+    __syncthreads();
+    cur ^= 1;
   }
+#undef FTC_GLOAD
+#undef FTC_LSTORE
 
   // ---- epilogue: dK = scale * dK^T^T, dV; lane owns one key row
   uint16_t* dkp = a.dk + ((long long)b * S + key) * a.dkv_rs + (long long)kvh * D;
@@ -275,8 +297,8 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(BwdArgs a) {
 }
 
 // ---------------------------------------------------------------- 3. dQ
-template <int D>
-__global__ __launch_bounds__(256, 2) void bwd_dq_kernel(BwdArgs a) {
+template <int D, int OCC>
+__global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
   constexpr int NCH = D / 8, DSTEPS = D / 16, DT = D / 32;
   constexpr int BQ = 128, BK = 64;
   constexpr int TILE = BK * D * 2;
@@ -285,7 +307,8 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(BwdArgs a) {
   char* Kb = smem;             // [2][64][D]
   char* Vb = smem + 2 * TILE;  // [2][64][D]
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform -> scalar branches
   const int hh = lane >> 5, lr = lane & 31;
   const int S = a.S, G = a.H / a.KV;
   const int nqb = S / BQ;
@@ -319,23 +342,21 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(BwdArgs a) {
   const uint16_t* kbase = a.k + (long long)b * S * a.kv_rs + (long long)kvh * D;
   const uint16_t* vbase = a.v + (long long)b * S * a.kv_rs + (long long)kvh * D;
   const int lrow = tid / NCH, lch = tid % NCH;
-  uint4 kreg[NPASS], vreg[NPASS];
-  auto gload = [&](int kv0) {
-#pragma unroll
-    for (int p = 0; p < NPASS; ++p) {
-      const long long kk = kv0 + p * RPP + lrow;
-      kreg[p] = *reinterpret_cast<const uint4*>(kbase + kk * a.kv_rs + lch * 8);
-      vreg[p] = *reinterpret_cast<const uint4*>(vbase + kk * a.kv_rs + lch * 8);
-    }
-  };
-  auto lstore = [&](int buf) {
-#pragma unroll
-    for (int p = 0; p < NPASS; ++p) {
-      const int r = p * RPP + lrow;
-      *reinterpret_cast<uint4*>(Kb + buf * TILE + lds_off<D>(r, lch)) = kreg[p];
-      *reinterpret_cast<uint4*>(Vb + buf * TILE + lds_off<D>(r, lch)) = vreg[p];
-    }
-  };
+  // register staging in native vectors via macros (HIP's uint4 struct / lambda captures left it in scratch)
+  u32x4 kreg[NPASS], vreg[NPASS];
+  const auto krs = make_rsrc(kbase), vrs = make_rsrc(vbase);
+  const int voff = (lrow * (int)a.kv_rs + lch * 8) * 2;
+  const int pass_bytes = RPP * (int)a.kv_rs * 2;
+  // K and V are staged in two halves (K under the softmax, V under the dQ MFMAs) so only 16 staging
+  // VGPRs are live at any point -- 32 spilled at D=128
+#define FTC_GLOAD(REG, RS, KV0)                                                           \
+  {                                                                                       \
+    const int toff = (KV0) * (int)a.kv_rs * 2;                                            \
+    _Pragma("unroll") for (int p = 0; p < NPASS; ++p) REG[p] = buf_load16(RS, voff, toff + p * pass_bytes); \
+  }
+#define FTC_LSTORE(REG, IMG)                                                              \
+  _Pragma("unroll") for (int p = 0; p < NPASS; ++p)                                       \
+    *reinterpret_cast<u32x4*>((IMG) + lds_off<D>(p * RPP + lrow, lch)) = REG[p];
 
   f32x16 dq[DT];
 #pragma unroll
@@ -344,15 +365,16 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(BwdArgs a) {
     for (int i = 0; i < 16; ++i) dq[t][i] = 0.f;
 
   if (ntiles > 0) {
-    gload(kv_begin);
-    lstore(0);
+    FTC_GLOAD(kreg, krs, kv_begin);
+    FTC_GLOAD(vreg, vrs, kv_begin);
+    FTC_LSTORE(kreg, Kb);
+    FTC_LSTORE(vreg, Vb);
   }
   __syncthreads();
   int cur = 0;
   for (int t = 0; t < ntiles; ++t) {
     const int kv0 = kv_begin + t * BK;
     const bool more = t + 1 < ntiles;
-    if (more) gload(kv0 + BK);
     const char* Kc = Kb + cur * TILE;
     const char* Vc = Vb + cur * TILE;
     f32x16 s[2], dp[2];
@@ -363,40 +385,68 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(BwdArgs a) {
       const int r = kt * 32 + lr;
 #pragma unroll
       for (int st = 0; st < DSTEPS; ++st) {
-        const uint4 kv = *reinterpret_cast<const uint4*>(Kc + lds_off<D>(r, 2 * st + hh));
-        s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(kv), qf[st], s[kt], 0, 0, 0);
-        const uint4 vv = *reinterpret_cast<const uint4*>(Vc + lds_off<D>(r, 2 * st + hh));
-        dp[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(vv), df[st], dp[kt], 0, 0, 0);
+        const u32x4 kv = *reinterpret_cast<const u32x4*>(Kc + lds_off<D>(r, 2 * st + hh));
+        const u32x4 vv = *reinterpret_cast<const u32x4*>(Vc + lds_off<D>(r, 2 * st + hh));
+        s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kv), qf[st], s[kt], 0, 0, 0);
+        dp[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, vv), df[st], dp[kt], 0, 0, 0);
       }
     }
-    const int qmin_w = q0 + wave * 32;
-    const bool need_mask = (a.causal && kv0 + BK - 1 > qmin_w) || (a.window > 0 && qmin_w + 31 - kv0 >= a.window);
+    // keep 2 K/V fragment reads in flight against the MFMA chain (deeper ones spill at D=128)
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+    for (int i = 0; i < 4 * DSTEPS - 2; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float p = __builtin_amdgcn_exp2f(a.c * s[kt][i] - lse2);
-        if (need_mask) {
-          const int key = kv0 + kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          const bool bad = (a.causal && key > qrow) || (a.window > 0 && qrow - key >= a.window);
-          p = bad ? 0.f : p;
+      for (int i = 0; i < 16; ++i) s[kt][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(a.c, s[kt][i], -lse2));
+    const int qmin_w = q0 + wave * 32;
+    const bool need_mask = (a.causal && kv0 + BK - 1 > qmin_w) || (a.window > 0 && qmin_w + 31 - kv0 >= a.window);
+    if (need_mask) {  // wave-uniform; selects inside
+      const int base = kv0 + 4 * hh;
+      const int hi = (a.causal ? qrow : 0x3fffffff) - base;
+      const int lo = (a.window > 0 ? qrow - a.window + 1 : -0x3fffffff) - base;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int off = kt * 32 + (i & 3) + 8 * (i >> 2);
+          s[kt][i] = (off >= lo && off <= hi) ? s[kt][i] : 0.f;
         }
-        dp[kt][i] = p * (dp[kt][i] - dlt);  // dS^T
-      }
+    }
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dp[kt][i] = s[kt][i] * (dp[kt][i] - dlt);  // dS^T
     bf16x8 sb[4];
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) sb[ks] = pack8_bf(dp[ks >> 1], 8 * (ks & 1));
+    // next tile's K/V loads fly under the dQ MFMAs (the S/dP accumulators are dead by now)
+    if (more) {
+      FTC_GLOAD(kreg, krs, kv0 + BK);
+      FTC_GLOAD(vreg, vrs, kv0 + BK);
+    }
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
+    for (int dt = 0; dt < DT; ++dt) {
+      bf16x8 ka[4];
+      const int2 to = tr_offsets<D>(dt * 32, lane);
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8 ka = tr_operand<D>(Kc, 16 * ks, dt * 32, hh, lane);
-        dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, sb[ks], dq[dt], 0, 0, 0);
-      }
-    if (more) lstore(cur ^ 1);
+      for (int ks = 0; ks < 4; ++ks) ka[ks] = tr_read<D>(Kc, 16 * ks, to);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[ks], sb[ks], dq[dt], 0, 0, 0);
+    }
+    if (more) {
+      FTC_LSTORE(kreg, Kb + (cur ^ 1) * TILE);
+      FTC_LSTORE(vreg, Vb + (cur ^ 1) * TILE);
+    }
     __syncthreads();
     cur ^= 1;
   }
+#undef FTC_GLOAD
+#undef FTC_LSTORE
   uint16_t* op = a.dq + ((long long)b * S + qrow) * a.dq_rs + (long long)hq * D;
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt)
@@ -427,18 +477,29 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
             lse, (float*)workspace, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, q_rs, kv_rs, o_rs, dq_rs, dkv_rs,
             B, S, H, KV, scale, scale * LOG2E, causal, window};
   const int grid_d = ftc::stream_grid((long long)B * S, 4);
-  const size_t lds_kv = (size_t)128 * D * 2 + 2 * 32 * D * 2 + 2 * 32 * sizeof(float);
+  const size_t lds_kv = (size_t)128 * D * 2 + 2 * (2 * 32 * D * 2 + 2 * 32 * sizeof(float));
   const size_t lds_q = (size_t)4 * 64 * D * 2;
   const int g_kv = B * KV * (S / 128);
   const int g_q = B * H * (S / 128);
+  // occupancy variant of the two main kernels: 2 waves/SIMD (256-VGPR budget, spills a few staging
+  // registers at D=128) or 1 wave/SIMD (512 VGPR+AGPR, no spills); FTC_FLASH_BWD_OCC=1|2
+  static const int occ = [] {
+    const char* e = getenv("FTC_FLASH_BWD_OCC");
+    return (e && e[0] == '1') ? 1 : 2;
+  }();
   if (D == 128) {
     hipLaunchKernelGGL(bwd_delta_kernel<128>, dim3(grid_d), dim3(256), 0, stream, a);
-    hipLaunchKernelGGL(bwd_dkdv_kernel<128>, dim3(g_kv), dim3(256), lds_kv, stream, a);
-    hipLaunchKernelGGL(bwd_dq_kernel<128>, dim3(g_q), dim3(256), lds_q, stream, a);
+    if (occ == 1) {
+      hipLaunchKernelGGL((bwd_dkdv_kernel<128, 1>), dim3(g_kv), dim3(256), lds_kv, stream, a);
+      hipLaunchKernelGGL((bwd_dq_kernel<128, 1>), dim3(g_q), dim3(256), lds_q, stream, a);
+    } else {
+      hipLaunchKernelGGL((bwd_dkdv_kernel<128, 2>), dim3(g_kv), dim3(256), lds_kv, stream, a);
+      hipLaunchKernelGGL((bwd_dq_kernel<128, 2>), dim3(g_q), dim3(256), lds_q, stream, a);
+    }
   } else {
     hipLaunchKernelGGL(bwd_delta_kernel<64>, dim3(grid_d), dim3(256), 0, stream, a);
-    hipLaunchKernelGGL(bwd_dkdv_kernel<64>, dim3(g_kv), dim3(256), lds_kv, stream, a);
-    hipLaunchKernelGGL(bwd_dq_kernel<64>, dim3(g_q), dim3(256), lds_q, stream, a);
+    hipLaunchKernelGGL((bwd_dkdv_kernel<64, 2>), dim3(g_kv), dim3(256), lds_kv, stream, a);
+    hipLaunchKernelGGL((bwd_dq_kernel<64, 2>), dim3(g_q), dim3(256), lds_q, stream, a);
   }
   return (int)hipGetLastError();
 }

@@ -103,7 +103,8 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
   char* Kb = smem;                     // [2][TILE_BYTES]
   char* Vb = smem + 2 * TILE_BYTES;    // [2][TILE_BYTES]
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform -> scalar branches
   const int hh = lane >> 5, lr = lane & 31;
   int qb, b, hq, kvh;
   decode_block(a, qb, b, hq, kvh);
@@ -137,23 +138,29 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
   const uint16_t* vbase = a.v + (long long)b * S * a.kv_rs + (long long)kvh * D;
   const int lrow = tid / NCH, lch = tid % NCH;
 
-  uint4 kreg[NPASS], vreg[NPASS];
-  auto gload = [&](int kv0) {
-#pragma unroll
-    for (int p = 0; p < NPASS; ++p) {
-      const long long key = kv0 + p * RPP + lrow;
-      kreg[p] = *reinterpret_cast<const uint4*>(kbase + key * a.kv_rs + lch * 8);
-      vreg[p] = *reinterpret_cast<const uint4*>(vbase + key * a.kv_rs + lch * 8);
-    }
-  };
-  auto lstore = [&](int buf) {
-#pragma unroll
-    for (int p = 0; p < NPASS; ++p) {
-      const int r = p * RPP + lrow;
-      *reinterpret_cast<uint4*>(Kb + buf * TILE_BYTES + lds_off<D>(r, lch)) = kreg[p];
-      *reinterpret_cast<uint4*>(Vb + buf * TILE_BYTES + lds_off<D>(r, lch)) = vreg[p];
-    }
-  };
+  // register-staged K/V prefetch (plain macros: lambdas capturing the staging arrays by reference left
+  // them in scratch memory)
+  u32x4 kreg[NPASS], vreg[NPASS];
+  // per-thread row pointers (64-bit math hoisted out of the loop; a tile advances by BK rows)
+  // buffer loads: one VGPR row offset per thread, tile/pass offsets in SGPRs (rows of one (b, kv head)
+  // span < 2 GiB: S * kv_rs * 2 bytes)
+  const auto krs = make_rsrc(kbase), vrs = make_rsrc(vbase);
+  const int voff = (lrow * (int)a.kv_rs + lch * 8) * 2;
+  const int pass_bytes = RPP * (int)a.kv_rs * 2;
+#define FTC_GLOAD(KV0)                                                                  \
+  {                                                                                     \
+    const int toff = (KV0) * (int)a.kv_rs * 2;                                          \
+    _Pragma("unroll") for (int p = 0; p < NPASS; ++p) {                                 \
+      kreg[p] = buf_load16(krs, voff, toff + p * pass_bytes);                           \
+      vreg[p] = buf_load16(vrs, voff, toff + p * pass_bytes);                           \
+    }                                                                                   \
+  }
+#define FTC_LSTORE(BUF)                                                                 \
+  _Pragma("unroll") for (int p = 0; p < NPASS; ++p) {                                   \
+    const int r = p * RPP + lrow;                                                       \
+    *reinterpret_cast<u32x4*>(Kb + (BUF) * TILE_BYTES + lds_off<D>(r, lch)) = kreg[p];  \
+    *reinterpret_cast<u32x4*>(Vb + (BUF) * TILE_BYTES + lds_off<D>(r, lch)) = vreg[p];  \
+  }
 
   f32x16 o[DT];
 #pragma unroll
@@ -164,8 +171,8 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
   const float c = a.scale_log2;
 
   if (ntiles > 0) {
-    gload(kv_begin);
-    lstore(0);
+    FTC_GLOAD(kv_begin);
+    FTC_LSTORE(0);
   }
   __syncthreads();
 
@@ -178,7 +185,6 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
   for (int t = 0; t < ntiles; ++t) {
     const int kv0 = kv_begin + t * BK;
     const bool more = t + 1 < ntiles;
-    if (more) gload(kv0 + BK);
     const char* Kc = Kb + cur * TILE_BYTES;
     const char* Vc = Vb + cur * TILE_BYTES;
 
@@ -186,35 +192,51 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
     f32x16 s[2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) s[kt][i] = 0.f;
+      // issue all LDS reads of this 32-key block before its MFMA chain (no read->wait->mfma serialisation)
       const int r = kt * 32 + lr;
+      uint4 kf[DSTEPS];
 #pragma unroll
-      for (int st = 0; st < DSTEPS; ++st) {
-        const uint4 kv = *reinterpret_cast<const uint4*>(Kc + lds_off<D>(r, 2 * st + hh));
-        s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(kv), qf[st], s[kt], 0, 0, 0);
-      }
+      for (int st = 0; st < DSTEPS; ++st) kf[st] = *reinterpret_cast<const uint4*>(Kc + lds_off<D>(r, 2 * st + hh));
+      f32x16 acc;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+      for (int st = 0; st < DSTEPS; ++st) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(kf[st]), qf[st], acc, 0, 0, 0);
+      s[kt] = acc;
     }
+    // software pipeline of the 2*DSTEPS K-fragment reads against the MFMA chain, 4 reads in flight
+    // (the default scheduler serialises read -> wait -> mfma to save registers)
+    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+    for (int i = 0; i < 2 * DSTEPS - 4; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
 
-    // ---- mask + online softmax (log2 domain), query = qrow (lane), keys in registers
+    if (more) { FTC_GLOAD(kv0 + BK); }
+    // ---- mask (wave-uniform branch, branch-free selects inside) + online softmax in the log2 domain
     const int qmin_w = q0 + wave * 32;
     const bool need_mask = (a.causal && kv0 + BK - 1 > qmin_w) || (a.window > 0 && qmin_w + 31 - kv0 >= a.window);
+    if (need_mask) {
+      // key k of element (kt, i) = kv0 + kt*32 + (i&3) + 8*(i>>2) + 4*hh; valid iff lo <= k <= hi
+      const int base = kv0 + 4 * hh;
+      const int hi = (a.causal ? qrow : 0x3fffffff) - base;
+      const int lo = (a.window > 0 ? qrow - a.window + 1 : -0x3fffffff) - base;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int off = kt * 32 + (i & 3) + 8 * (i >> 2);
+          s[kt][i] = (off >= lo && off <= hi) ? s[kt][i] : -INFINITY;
+        }
+    }
     float mt = -INFINITY;
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
+    for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float x = s[kt][i] * c;
-        if (need_mask) {
-          const int key = kv0 + kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-          bool bad = (a.causal && key > qrow) || (a.window > 0 && qrow - key >= a.window);
-          x = bad ? -INFINITY : x;
-        }
-        s[kt][i] = x;
-        mt = fmaxf(mt, x);
-      }
-    }
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[kt][i]);
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * c;  // c > 0: max commutes with the scale
     const float mn = fmaxf(m, mt);
     const float mref = (mn == -INFINITY) ? 0.f : mn;
     const float alpha = __builtin_amdgcn_exp2f(m - mref);
@@ -224,7 +246,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(s[kt][i] - mref);
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kt][i], c, -mref));
         s[kt][i] = p;
         rs += p;
       }
@@ -242,21 +264,27 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
     for (int dt = 0; dt < DT; ++dt) {
       const int col = dt * 32 + 16 * (gi & 1) + 4 * trp;
       const int chunk = col >> 3, half8 = (col & 7) ? 8 : 0;
+      s16x4 vt[8];  // all 8 transposed reads of this 32-wide d tile in flight before the MFMA chain
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const int r1 = 16 * ks + 4 * hh + trq;
-        const int r2 = r1 + 8;
-        s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vc + lds_off<D>(r1, chunk) + half8));
-        s16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vc + lds_off<D>(r2, chunk) + half8));
+        vt[2 * ks] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vc + lds_off<D>(r1, chunk) + half8));
+        vt[2 * ks + 1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vc + lds_off<D>(r1 + 8, chunk) + half8));
+      }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const s16x4 v1 = vt[2 * ks], v2 = vt[2 * ks + 1];
         s16x8 va = {v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
         o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, va), pf[ks], o[dt], 0, 0, 0);
       }
     }
-    if (more) lstore(cur ^ 1);
+    if (more) { FTC_LSTORE(cur ^ 1); }
     __syncthreads();
     cur ^= 1;
   }
 
+#undef FTC_GLOAD
+#undef FTC_LSTORE
   // ---- epilogue: normalise, store O (bf16) and LSE (natural log)
   const float ltot = l + __shfl_xor(l, 32, 64);
   const float inv = ltot > 0.f ? 1.0f / ltot : 0.f;

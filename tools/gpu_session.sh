@@ -37,6 +37,12 @@ for s in "${STEPS[@]}"; do
     attn)
       timeout -k 10 300 python tools/bench_attention.py > gpurun_out/bench_attn.log 2>&1
       fatal $? attn; tail -2 gpurun_out/bench_attn.log ;;
+    attn_occ2)
+      FTC_FLASH_BWD_OCC=2 timeout -k 10 300 python tools/bench_attention.py > gpurun_out/bench_attn_occ2.log 2>&1
+      fatal $? attn_occ2; tail -2 gpurun_out/bench_attn_occ2.log ;;
+    flash)
+      timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py -m gpu -x -q -k flash > gpurun_out/pytest_flash.log 2>&1
+      fatal $? flash; tail -5 gpurun_out/pytest_flash.log ;;
     bench_b8)
       timeout -k 10 600 python bench.py --steps 8 --warmup 3 --batch-size 8 > gpurun_out/bench_b8.log 2>&1
       fatal $? bench_b8; tail -2 gpurun_out/bench_b8.log ;;
