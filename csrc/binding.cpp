@@ -263,7 +263,7 @@ void flash_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, co
   for (auto* t : {&q, &k, &v, &o, &dout}) need(*t, at::kBFloat16, "flash_bwd input");
   need(lse, at::kFloat, "lse");
   TORCH_CHECK(D == 128 || D == 64, "flash_bwd: head_dim");
-  TORCH_CHECK(S % 64 == 0 && H % KV == 0, "flash_bwd: shapes");
+  TORCH_CHECK(S % 256 == 0 && H % KV == 0, "flash_bwd: S must be a multiple of 256, H of KV");
   TORCH_CHECK(o.stride(0) == dout.stride(0), "flash_bwd: o/dout strides");
   TORCH_CHECK(dk.stride(0) == dv.stride(0) && k.stride(0) == v.stride(0), "flash_bwd: k/v strides");
   TORCH_CHECK(lse.numel() == B * H * S, "flash_bwd: lse size");

@@ -111,52 +111,71 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(BwdArgs a) {
 }
 
 // ---------------------------------------------------------------- 2. dK / dV
-template <int D, int OCC>
-__global__ __launch_bounds__(256, OCC) void bwd_dkdv_kernel(BwdArgs a) {
+// One workgroup = 4 waves = 256 keys of one (batch, kv head); each wave owns 64 keys as two 32-key
+// halves and keeps their dK^T / dV^T accumulators (2 x 2 x D/32 tiles = 256 VGPRs at D=128) for the
+// whole sweep over the G query heads x 32-row query slices, so the 512-register single-wave budget
+// (launch_bounds(256, 1)) is used.  Per slice and wave: 64 MFMAs between barriers, the Q/dO slice is
+// read from LDS once for both halves (dV/dK tr-operands shared), the next slice's global loads fly
+// under them (register staging into the other LDS slot, one barrier per slice).
+// Block order: heavy (early, causal) key blocks first; the key blocks of one (batch, kv head) pair
+// share an XCD so its Q/dO slices are L2 hits for the co-running blocks.
+template <int D>
+__global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(BwdArgs a) {
   constexpr int NCH = D / 8, DSTEPS = D / 16, DT = D / 32;
-  constexpr int BKV = 128, BQ2 = 32;
+  constexpr int BKV = 256, BQ2 = 32;
   constexpr int KBYTES = BKV * D * 2, QBYTES = BQ2 * D * 2;
+  constexpr int SLICE = 2 * QBYTES + 2 * BQ2 * 4;  // Q | dO | -lse/scale | -delta
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  // LDS: K [128 keys][D] | 2 x { Q [32][D] | dO [32][D] | -lse/scale [32] | -delta [32] }
-  constexpr int SLICE = 2 * QBYTES + 2 * BQ2 * 4;
   char* Ks = smem;
 
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform -> scalar branches
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hh = lane >> 5, lr = lane & 31;
   const int S = a.S, G = a.H / a.KV;
   const int nkb = S / BKV;
-  // heavy-first: early key blocks see the most (causal) query rows
-  const int kb = blockIdx.x % nkb;
-  const int bk = blockIdx.x / nkb;
-  const int kvh = bk % a.KV, b = bk / a.KV;
+  const int npairs = a.B * a.KV;
+  int kb, pair;
+  {
+    const int bid = blockIdx.x;
+    if ((npairs & 7) == 0) {
+      const int xcd = bid & 7, slot = bid >> 3, ppx = npairs >> 3;
+      kb = slot / ppx;
+      pair = (slot % ppx) * 8 + xcd;
+    } else {
+      kb = bid / npairs;
+      pair = bid % npairs;
+    }
+  }
+  const int kvh = pair % a.KV, b = pair / a.KV;
   const int kv0 = kb * BKV;
-  const int key = kv0 + wave * 32 + lr;  // this lane's key
+  const int wkey0 = kv0 + wave * 64;  // this wave's first key
 
-  // stage the key block's K rows into LDS; V^T fragments for dP go to registers
+  // stage the block's K rows into LDS; V^T fragments (B operand of dP) to registers
   const uint16_t* kbase = a.k + ((long long)b * S) * a.kv_rs + (long long)kvh * D;
   {
     constexpr int RPP = 256 / NCH;
     const int lrow = tid / NCH, lch = tid % NCH;
+    const auto krs = make_rsrc(kbase + (long long)kv0 * a.kv_rs);
+    const int voff = (lrow * (int)a.kv_rs + lch * 8) * 2;
 #pragma unroll
-    for (int p = 0; p < BKV / RPP; ++p) {
-      const int r = p * RPP + lrow;
-      *reinterpret_cast<uint4*>(Ks + lds_off<D>(r, lch)) =
-          *reinterpret_cast<const uint4*>(kbase + (long long)(kv0 + r) * a.kv_rs + lch * 8);
-    }
+    for (int p = 0; p < BKV / RPP; ++p)
+      *reinterpret_cast<u32x4*>(Ks + lds_off<D>(p * RPP + lrow, lch)) = buf_load16(krs, voff, p * RPP * (int)a.kv_rs * 2);
   }
-  bf16x8 vf[DSTEPS];
-  {
-    const uint16_t* vp = a.v + ((long long)b * S + key) * a.kv_rs + (long long)kvh * D + 8 * hh;
+  bf16x8 vf[2][DSTEPS];
 #pragma unroll
-    for (int s = 0; s < DSTEPS; ++s) vf[s] = as_bf8(*reinterpret_cast<const uint4*>(vp + 16 * s));
+  for (int j = 0; j < 2; ++j) {
+    const uint16_t* vp = a.v + ((long long)b * S + wkey0 + 32 * j + lr) * a.kv_rs + (long long)kvh * D + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < DSTEPS; ++s) vf[j][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(vp + 16 * s));
   }
 
-  f32x16 dv[DT], dk[DT];
+  f32x16 dv[2][DT], dk[2][DT];
 #pragma unroll
-  for (int t = 0; t < DT; ++t)
+  for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) { dv[t][i] = 0.f; dk[t][i] = 0.f; }
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { dv[j][t][i] = 0.f; dk[j][t][i] = 0.f; }
 
   // query range that can see this key block
   int qbeg = a.causal ? kv0 : 0;
@@ -199,8 +218,6 @@ __global__ __launch_bounds__(256, OCC) void bwd_dkdv_kernel(BwdArgs a) {
     }                                                                                              \
   }
 
-  // one barrier per slice: slice it+1 is loaded into registers during slice it's MFMAs and written
-  // to the other LDS buffer afterwards
   const int total = G * nqt;
   if (total > 0) {
     FTC_GLOAD(kvh * G, qbeg);
@@ -219,57 +236,65 @@ __global__ __launch_bounds__(256, OCC) void bwd_dkdv_kernel(BwdArgs a) {
       const int g2 = (it + 1) / nqt, q2 = qbeg + ((it + 1) % nqt) * BQ2;
       FTC_GLOAD(kvh * G + g2, q2);
     }
-    // ---- S[q][k] and dP'[q][k]: rows q (registers), key on the lane
-    f32x16 s, dp;
+    // ---- per half j: S[q][k], dP'[q][k] (rows q in registers, key on the lane) -> P, dS (bf16)
+    bf16x8 pb[2][2], sb[2][2];
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const float4 lv = *reinterpret_cast<const float4*>(lse_s + 8 * g4 + 4 * hh);
-      const float4 dv4 = *reinterpret_cast<const float4*>(dlt_s + 8 * g4 + 4 * hh);
-      s[4 * g4 + 0] = lv.x; s[4 * g4 + 1] = lv.y; s[4 * g4 + 2] = lv.z; s[4 * g4 + 3] = lv.w;
-      dp[4 * g4 + 0] = dv4.x; dp[4 * g4 + 1] = dv4.y; dp[4 * g4 + 2] = dv4.z; dp[4 * g4 + 3] = dv4.w;
-    }
-    const int krow = wave * 32 + lr;
+    for (int j = 0; j < 2; ++j) {
+      f32x16 s, dp;
 #pragma unroll
-    for (int st = 0; st < DSTEPS; ++st) {
-      const u32x4 qa = *reinterpret_cast<const u32x4*>(Qs + lds_off<D>(lr, 2 * st + hh));
-      const u32x4 kbv = *reinterpret_cast<const u32x4*>(Ks + lds_off<D>(krow, 2 * st + hh));
-      const u32x4 da = *reinterpret_cast<const u32x4*>(Ds + lds_off<D>(lr, 2 * st + hh));
-      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, qa), __builtin_bit_cast(bf16x8, kbv), s, 0, 0, 0);
-      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, da), vf[st], dp, 0, 0, 0);
-    }
-    // ---- P, dS (masked; wave-uniform branch, selects inside)
-    const bool need_mask = (a.causal && qt < kv0 + wave * 32 + 31) ||
-                           (a.window > 0 && qt + BQ2 - 1 - (kv0 + wave * 32) >= a.window);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) s[i] = __builtin_amdgcn_exp2f(a.c * s[i]);
-    if (need_mask) {
-      // query q of element i = qt + (i&3) + 8(i>>2) + 4hh is valid iff key <= q (causal) and
-      // q - key < window
-      const int base = qt + 4 * hh;
-      const int lo = (a.causal ? key : -0x3fffffff) - base;
-      const int hi = (a.window > 0 ? key + a.window - 1 : 0x3fffffff) - base;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int off = (i & 3) + 8 * (i >> 2);
-        s[i] = (off >= lo && off <= hi) ? s[i] : 0.f;
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 lv = *reinterpret_cast<const float4*>(lse_s + 8 * g4 + 4 * hh);
+        const float4 dv4 = *reinterpret_cast<const float4*>(dlt_s + 8 * g4 + 4 * hh);
+        s[4 * g4 + 0] = lv.x; s[4 * g4 + 1] = lv.y; s[4 * g4 + 2] = lv.z; s[4 * g4 + 3] = lv.w;
+        dp[4 * g4 + 0] = dv4.x; dp[4 * g4 + 1] = dv4.y; dp[4 * g4 + 2] = dv4.z; dp[4 * g4 + 3] = dv4.w;
       }
-    }
+      const int krow = wave * 64 + 32 * j + lr;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) dp[i] = s[i] * dp[i];
-    const bf16x8 pb0 = pack8_bf(s, 0), pb1 = pack8_bf(s, 8);
-    const bf16x8 sb0 = pack8_bf(dp, 0), sb1 = pack8_bf(dp, 8);
-    // ---- dV^T += dO^T P ; dK^T += Q^T dS   (k of these MFMAs = the 32 query rows)
+      for (int st = 0; st < DSTEPS; ++st) {
+        const u32x4 qa = *reinterpret_cast<const u32x4*>(Qs + lds_off<D>(lr, 2 * st + hh));
+        const u32x4 kbv = *reinterpret_cast<const u32x4*>(Ks + lds_off<D>(krow, 2 * st + hh));
+        const u32x4 da = *reinterpret_cast<const u32x4*>(Ds + lds_off<D>(lr, 2 * st + hh));
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, qa), __builtin_bit_cast(bf16x8, kbv), s, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, da), vf[j][st], dp, 0, 0, 0);
+      }
+      const int key = wkey0 + 32 * j + lr;
+      const int kmin = wkey0 + 32 * j;
+      const bool need_mask = (a.causal && qt < kmin + 31) || (a.window > 0 && qt + BQ2 - 1 - kmin >= a.window);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[i] = __builtin_amdgcn_exp2f(a.c * s[i]);
+      if (need_mask) {  // wave-uniform; query q = qt + (i&3) + 8(i>>2) + 4hh valid iff key <= q < key + window
+        const int base = qt + 4 * hh;
+        const int lo = (a.causal ? key : -0x3fffffff) - base;
+        const int hi = (a.window > 0 ? key + a.window - 1 : 0x3fffffff) - base;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int off = (i & 3) + 8 * (i >> 2);
+          s[i] = (off >= lo && off <= hi) ? s[i] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dp[i] = s[i] * dp[i];
+      pb[j][0] = pack8_bf(s, 0);
+      pb[j][1] = pack8_bf(s, 8);
+      sb[j][0] = pack8_bf(dp, 0);
+      sb[j][1] = pack8_bf(dp, 8);
+    }
+    // ---- dV^T += dO^T P ; dK^T += Q^T dS for both halves (k of these MFMAs = the 32 query rows);
+    // the dO^T / Q^T tr-operands are read once and used by both halves
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
       const int2 to = tr_offsets<D>(dt * 32, lane);
       const bf16x8 a0 = tr_read<D>(Ds, 0, to);
       const bf16x8 a1 = tr_read<D>(Ds, 16, to);
-      dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, pb0, dv[dt], 0, 0, 0);
-      dv[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, pb1, dv[dt], 0, 0, 0);
       const bf16x8 q0v = tr_read<D>(Qs, 0, to);
       const bf16x8 q1v = tr_read<D>(Qs, 16, to);
-      dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q0v, sb0, dk[dt], 0, 0, 0);
-      dk[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q1v, sb1, dk[dt], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        dv[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, pb[j][0], dv[j][dt], 0, 0, 0);
+        dv[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, pb[j][1], dv[j][dt], 0, 0, 0);
+        dk[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q0v, sb[j][0], dk[j][dt], 0, 0, 0);
+        dk[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q1v, sb[j][1], dk[j][dt], 0, 0, 0);
+      }
     }
     if (more) { FTC_LSTORE(cur ^ 1); }
     __syncthreads();
@@ -278,22 +303,26 @@ __global__ __launch_bounds__(256, OCC) void bwd_dkdv_kernel(BwdArgs a) {
 #undef FTC_GLOAD
 #undef FTC_LSTORE
 
-  // ---- epilogue: dK = scale * dK^T^T, dV; lane owns one key row
-  uint16_t* dkp = a.dk + ((long long)b * S + key) * a.dkv_rs + (long long)kvh * D;
-  uint16_t* dvp = a.dv + ((long long)b * S + key) * a.dkv_rs + (long long)kvh * D;
+  // ---- epilogue: dK = scale * dK^T^T, dV; lane owns one key row per half
 #pragma unroll
-  for (int dt = 0; dt < DT; ++dt)
+  for (int j = 0; j < 2; ++j) {
+    const int key = wkey0 + 32 * j + lr;
+    uint16_t* dkp = a.dk + ((long long)b * S + key) * a.dkv_rs + (long long)kvh * D;
+    uint16_t* dvp = a.dv + ((long long)b * S + key) * a.dkv_rs + (long long)kvh * D;
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int d = dt * 32 + 8 * g4 + 4 * hh;
-      uint2 wk, wv;
-      wk.x = pack_bf2(dk[dt][4 * g4 + 0] * a.scale, dk[dt][4 * g4 + 1] * a.scale);
-      wk.y = pack_bf2(dk[dt][4 * g4 + 2] * a.scale, dk[dt][4 * g4 + 3] * a.scale);
-      wv.x = pack_bf2(dv[dt][4 * g4 + 0], dv[dt][4 * g4 + 1]);
-      wv.y = pack_bf2(dv[dt][4 * g4 + 2], dv[dt][4 * g4 + 3]);
-      *reinterpret_cast<uint2*>(dkp + d) = wk;
-      *reinterpret_cast<uint2*>(dvp + d) = wv;
-    }
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = dt * 32 + 8 * g4 + 4 * hh;
+        uint2 wk, wv;
+        wk.x = pack_bf2(dk[j][dt][4 * g4 + 0] * a.scale, dk[j][dt][4 * g4 + 1] * a.scale);
+        wk.y = pack_bf2(dk[j][dt][4 * g4 + 2] * a.scale, dk[j][dt][4 * g4 + 3] * a.scale);
+        wv.x = pack_bf2(dv[j][dt][4 * g4 + 0], dv[j][dt][4 * g4 + 1]);
+        wv.y = pack_bf2(dv[j][dt][4 * g4 + 2], dv[j][dt][4 * g4 + 3]);
+        *reinterpret_cast<uint2*>(dkp + d) = wk;
+        *reinterpret_cast<uint2*>(dvp + d) = wv;
+      }
+  }
 }
 
 // ---------------------------------------------------------------- 3. dQ
@@ -472,14 +501,14 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
                              const float* lse, void* dq, void* dk, void* dv, void* workspace, int B, int S, int H,
                              int KV, int D, long long q_rs, long long kv_rs, long long o_rs, long long dq_rs,
                              long long dkv_rs, float scale, int causal, int window, hipStream_t stream) {
-  if (S % 128 != 0 || H % KV != 0 || (D != 128 && D != 64)) return -1;
+  if (S % 256 != 0 || H % KV != 0 || (D != 128 && D != 64)) return -1;
   BwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)o, (const uint16_t*)dout,
             lse, (float*)workspace, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, q_rs, kv_rs, o_rs, dq_rs, dkv_rs,
             B, S, H, KV, scale, scale * LOG2E, causal, window};
   const int grid_d = ftc::stream_grid((long long)B * S, 4);
-  const size_t lds_kv = (size_t)128 * D * 2 + 2 * (2 * 32 * D * 2 + 2 * 32 * sizeof(float));
+  const size_t lds_kv = (size_t)256 * D * 2 + 2 * (2 * 32 * D * 2 + 2 * 32 * sizeof(float));
   const size_t lds_q = (size_t)4 * 64 * D * 2;
-  const int g_kv = B * KV * (S / 128);
+  const int g_kv = B * KV * (S / 256);
   const int g_q = B * H * (S / 128);
   // occupancy variant of the two main kernels: 2 waves/SIMD (256-VGPR budget, spills a few staging
   // registers at D=128) or 1 wave/SIMD (512 VGPR+AGPR, no spills); FTC_FLASH_BWD_OCC=1|2
@@ -487,18 +516,25 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
     const char* e = getenv("FTC_FLASH_BWD_OCC");
     return (e && e[0] == '1') ? 1 : 2;
   }();
+  static bool attr_set = false;  // dK/dV uses 96.5 KiB of dynamic LDS (> the 64 KiB default)
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)bwd_dkdv_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        256 * 128 * 2 + 2 * (2 * 32 * 128 * 2 + 2 * 32 * 4));
+    hipFuncSetAttribute((const void*)bwd_dkdv_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        256 * 64 * 2 + 2 * (2 * 32 * 64 * 2 + 2 * 32 * 4));
+    attr_set = true;
+  }
   if (D == 128) {
     hipLaunchKernelGGL(bwd_delta_kernel<128>, dim3(grid_d), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(bwd_dkdv_kernel<128>, dim3(g_kv), dim3(256), lds_kv, stream, a);
     if (occ == 1) {
-      hipLaunchKernelGGL((bwd_dkdv_kernel<128, 1>), dim3(g_kv), dim3(256), lds_kv, stream, a);
       hipLaunchKernelGGL((bwd_dq_kernel<128, 1>), dim3(g_q), dim3(256), lds_q, stream, a);
     } else {
-      hipLaunchKernelGGL((bwd_dkdv_kernel<128, 2>), dim3(g_kv), dim3(256), lds_kv, stream, a);
       hipLaunchKernelGGL((bwd_dq_kernel<128, 2>), dim3(g_q), dim3(256), lds_q, stream, a);
     }
   } else {
     hipLaunchKernelGGL(bwd_delta_kernel<64>, dim3(grid_d), dim3(256), 0, stream, a);
-    hipLaunchKernelGGL((bwd_dkdv_kernel<64, 2>), dim3(g_kv), dim3(256), lds_kv, stream, a);
+    hipLaunchKernelGGL(bwd_dkdv_kernel<64>, dim3(g_kv), dim3(256), lds_kv, stream, a);
     hipLaunchKernelGGL((bwd_dq_kernel<64, 2>), dim3(g_q), dim3(256), lds_q, stream, a);
   }
   return (int)hipGetLastError();

@@ -27,7 +27,7 @@ FLASH_READY = True
 
 
 def flash_supported(D: int, S: int) -> bool:
-    return FLASH_READY and D in (64, 128) and S % 128 == 0
+    return FLASH_READY and D in (64, 128) and S % 256 == 0
 
 
 def _split(qkv, B, S, H, KV, D):

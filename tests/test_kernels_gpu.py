@@ -153,7 +153,8 @@ def test_lora_merge(C):
 
 @pytest.mark.parametrize("B,S,H,KV,D,causal,window", [
     (2, 256, 8, 2, 128, True, 0),
-    (1, 384, 4, 4, 128, False, 0),
+    (1, 768, 4, 4, 128, False, 0),
+    (1, 1024, 8, 2, 128, True, 0),
     (1, 512, 8, 2, 128, True, 192),
     (2, 256, 4, 4, 64, True, 0),
 ])
