@@ -10,14 +10,15 @@
 
 extern "C" {
 int ftc_rmsnorm_fwd(const void* x, const void* res, const void* w, void* h_out, void* y, float* rstd, int rows, int d,
-                    float eps, hipStream_t stream);
+                    float eps, long long y_rs, hipStream_t stream);
 int ftc_rmsnorm_bwd_grid(int rows);
 int ftc_rmsnorm_bwd(const void* dy, const void* h, const void* w, const float* rstd, const void* dres, void* dx,
                     float* dw_part, float* dw, int rows, int d, hipStream_t stream);
 int ftc_rope(void* qkv, const float* cosT, const float* sinT, const int* positions, long long rows, int ld,
              int n_rot_heads, int head_dim, int seq_len, int inverse, hipStream_t stream);
-int ftc_swiglu_fwd(const void* gu, void* a, long long rows, int F, hipStream_t stream);
-int ftc_swiglu_bwd(const void* da, const void* gu, void* dgu, long long rows, int F, hipStream_t stream);
+int ftc_swiglu_fwd(const void* gu, void* a, long long rows, int F, long long a_rs, hipStream_t stream);
+int ftc_swiglu_bwd(const void* da, const void* gu, void* dgu, long long rows, int F, long long dgu_rs,
+                   hipStream_t stream);
 int ftc_ce_fwd_bwd(void* logits, const long long* labels, float* loss, float* lse, long long rows, int V, long long ld,
                    float gscale, long long ignore_index, hipStream_t stream);
 int ftc_adamw(void* param_bf16, float* master, float* m, float* v, const void* grad, int grad_is_fp32, long long n,
@@ -32,7 +33,8 @@ int ftc_flash_fwd(const void* q, const void* k, const void* v, void* o, float* l
 int ftc_flash_bwd_workspace(int B, int S, int H, int D, long long* bytes);
 int ftc_flash_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
                   void* dq, void* dk, void* dv, void* workspace, int B, int S, int H, int KV, int D,
-                  long long q_row_stride, long long kv_row_stride, long long o_row_stride, long long dq_row_stride,
+                  long long q_row_stride, long long kv_row_stride, long long o_row_stride, long long do_row_stride,
+                  long long dq_row_stride,
                   long long dkv_row_stride, float scale, int causal, int window, hipStream_t stream);
 int ftc_nf4_dequant(const uint8_t* packed, const uint8_t* absmax_q, const float* absmax_scale, float absmax_offset,
                     void* out, long long n, int block, int block2, hipStream_t stream);
@@ -63,15 +65,18 @@ inline void need_rows(const at::Tensor& t, const char* name) {
 }
 
 // ---------------- RMSNorm ----------------
+// pad > 0: y is returned as the [rows, d] column view of a [rows, d + pad] buffer (LoRA "augmented" GEMM input)
 std::vector<at::Tensor> rmsnorm_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& res, const at::Tensor& w,
-                                    double eps) {
+                                    double eps, int64_t pad) {
   need(x, at::kBFloat16, "x");
   need(w, at::kBFloat16, "w");
   need_rows(x, "x");
   const int rows = (int)x.size(0), d = (int)x.size(1);
   TORCH_CHECK(w.numel() == d && w.is_contiguous(), "w must be [d] contiguous");
   TORCH_CHECK(d % 8 == 0 && d <= 8192, "rmsnorm: d must be a multiple of 8 and <= 8192");
-  auto y = at::empty_like(x);
+  TORCH_CHECK(pad >= 0 && pad % 8 == 0, "rmsnorm: pad must be a multiple of 8");
+  auto ybuf = at::empty({rows, d + pad}, x.options());
+  auto y = pad ? ybuf.narrow(1, 0, d) : ybuf;
   auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
   at::Tensor h;
   const void* rp = nullptr;
@@ -85,7 +90,7 @@ std::vector<at::Tensor> rmsnorm_fwd(const at::Tensor& x, const c10::optional<at:
     h = x;
   }
   check(ftc_rmsnorm_fwd(x.data_ptr(), rp, w.data_ptr(), rp ? h.data_ptr() : nullptr, y.data_ptr(),
-                        rstd.data_ptr<float>(), rows, d, (float)eps, cur_stream()),
+                        rstd.data_ptr<float>(), rows, d, (float)eps, (long long)(d + pad), cur_stream()),
         "rmsnorm_fwd");
   return {y, rstd, h};
 }
@@ -152,27 +157,30 @@ void rope_(at::Tensor& qkv, const at::Tensor& cos, const at::Tensor& sin, const 
 }
 
 // ---------------- SwiGLU ----------------
-at::Tensor swiglu_fwd(const at::Tensor& gu) {
+at::Tensor swiglu_fwd(const at::Tensor& gu, int64_t pad) {
   need(gu, at::kBFloat16, "gu");
   need_rows(gu, "gu");
   const long long rows = gu.size(0);
   const int F = (int)(gu.size(1) / 2);
   TORCH_CHECK(gu.size(1) % 16 == 0, "swiglu: 2F must be a multiple of 16");
-  auto a = at::empty({rows, F}, gu.options());
-  check(ftc_swiglu_fwd(gu.data_ptr(), a.data_ptr(), rows, F, cur_stream()), "swiglu_fwd");
-  return a;
+  TORCH_CHECK(pad >= 0 && pad % 8 == 0, "swiglu: pad must be a multiple of 8");
+  auto abuf = at::empty({rows, F + pad}, gu.options());
+  check(ftc_swiglu_fwd(gu.data_ptr(), abuf.data_ptr(), rows, F, F + pad, cur_stream()), "swiglu_fwd");
+  return pad ? abuf.narrow(1, 0, F) : abuf;
 }
 
-at::Tensor swiglu_bwd(const at::Tensor& da, const at::Tensor& gu) {
+at::Tensor swiglu_bwd(const at::Tensor& da, const at::Tensor& gu, int64_t pad) {
   need(da, at::kBFloat16, "da");
   need(gu, at::kBFloat16, "gu");
   need_rows(da, "da");
   need_rows(gu, "gu");
   TORCH_CHECK(da.size(0) == gu.size(0) && gu.size(1) == 2 * da.size(1), "swiglu_bwd shapes");
-  auto dgu = at::empty_like(gu);
-  check(ftc_swiglu_bwd(da.data_ptr(), gu.data_ptr(), dgu.data_ptr(), gu.size(0), (int)da.size(1), cur_stream()),
+  TORCH_CHECK(pad >= 0 && pad % 8 == 0, "swiglu_bwd: pad must be a multiple of 8");
+  auto dbuf = at::empty({gu.size(0), gu.size(1) + pad}, gu.options());
+  check(ftc_swiglu_bwd(da.data_ptr(), gu.data_ptr(), dbuf.data_ptr(), gu.size(0), (int)da.size(1), gu.size(1) + pad,
+                       cur_stream()),
         "swiglu_bwd");
-  return dgu;
+  return pad ? dbuf.narrow(1, 0, gu.size(1)) : dbuf;
 }
 
 // ---------------- cross entropy (in place on logits) ----------------
@@ -234,7 +242,8 @@ at::Tensor grad_sumsq(const at::Tensor& g, double max_norm, double scale) {
 // ---------------- flash attention ----------------
 // q: [B*S, >=H*D] view (row stride q_rs), k/v: [B*S, >=KV*D] views; all bf16 with unit column stride.
 std::vector<at::Tensor> flash_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, int64_t B, int64_t S,
-                                  int64_t H, int64_t KV, int64_t D, double scale, bool causal, int64_t window) {
+                                  int64_t H, int64_t KV, int64_t D, double scale, bool causal, int64_t window,
+                                  int64_t pad) {
   need(q, at::kBFloat16, "q");
   need(k, at::kBFloat16, "k");
   need(v, at::kBFloat16, "v");
@@ -247,7 +256,9 @@ std::vector<at::Tensor> flash_fwd(const at::Tensor& q, const at::Tensor& k, cons
   TORCH_CHECK(H % KV == 0, "flash_fwd: H % KV");
   TORCH_CHECK(S % 64 == 0, "flash_fwd: S must be a multiple of 64");
   TORCH_CHECK(q.stride(0) % 8 == 0 && k.stride(0) % 8 == 0, "flash_fwd: row strides must be 16B multiples");
-  auto o = at::empty({B * S, H * D}, q.options());
+  TORCH_CHECK(pad >= 0 && pad % 8 == 0, "flash_fwd: pad must be a multiple of 8");
+  auto obuf = at::empty({B * S, H * D + pad}, q.options());
+  auto o = pad ? obuf.narrow(1, 0, H * D) : obuf;
   auto lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
   check(ftc_flash_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), (int)B, (int)S,
                       (int)H, (int)KV, (int)D, q.stride(0), k.stride(0), o.stride(0), (float)scale, causal ? 1 : 0,
@@ -264,7 +275,8 @@ void flash_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, co
   need(lse, at::kFloat, "lse");
   TORCH_CHECK(D == 128 || D == 64, "flash_bwd: head_dim");
   TORCH_CHECK(S % 256 == 0 && H % KV == 0, "flash_bwd: S must be a multiple of 256, H of KV");
-  TORCH_CHECK(o.stride(0) == dout.stride(0), "flash_bwd: o/dout strides");
+  TORCH_CHECK(o.stride(1) == 1 && dout.stride(1) == 1 && o.stride(0) % 8 == 0 && dout.stride(0) % 8 == 0,
+              "flash_bwd: o/dout must be row views with 16-byte row strides");
   TORCH_CHECK(dk.stride(0) == dv.stride(0) && k.stride(0) == v.stride(0), "flash_bwd: k/v strides");
   TORCH_CHECK(lse.numel() == B * H * S, "flash_bwd: lse size");
   long long ws = 0;
@@ -272,7 +284,8 @@ void flash_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, co
   auto work = at::empty({ws}, q.options().dtype(at::kByte));
   check(ftc_flash_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
                       dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), work.data_ptr(), (int)B, (int)S, (int)H, (int)KV,
-                      (int)D, q.stride(0), k.stride(0), o.stride(0), dq.stride(0), dk.stride(0), (float)scale,
+                      (int)D, q.stride(0), k.stride(0), o.stride(0), dout.stride(0), dq.stride(0), dk.stride(0),
+                      (float)scale,
                       causal ? 1 : 0, (int)window, cur_stream()),
         "flash_bwd");
 }
@@ -342,15 +355,17 @@ void lora_merge_(at::Tensor& w, const at::Tensor& a, const at::Tensor& b, double
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "finetune_controller_amd gfx950 kernels";
-  m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  namespace py = pybind11;
+  m.def("rmsnorm_fwd", &rmsnorm_fwd, py::arg("x"), py::arg("res"), py::arg("w"), py::arg("eps"), py::arg("pad") = 0);
   m.def("rmsnorm_bwd", &rmsnorm_bwd);
   m.def("rope_", &rope_);
-  m.def("swiglu_fwd", &swiglu_fwd);
-  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("swiglu_fwd", &swiglu_fwd, py::arg("gu"), py::arg("pad") = 0);
+  m.def("swiglu_bwd", &swiglu_bwd, py::arg("da"), py::arg("gu"), py::arg("pad") = 0);
   m.def("ce_fwd_bwd_", &ce_fwd_bwd_);
   m.def("adamw_", &adamw_);
   m.def("grad_sumsq", &grad_sumsq);
-  m.def("flash_fwd", &flash_fwd);
+  m.def("flash_fwd", &flash_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("B"), py::arg("S"), py::arg("H"),
+        py::arg("KV"), py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("pad") = 0);
   m.def("flash_bwd", &flash_bwd);
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequantize", &nf4_dequantize);

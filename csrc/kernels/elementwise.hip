@@ -59,7 +59,7 @@ FTC_DEV float silu_f(float g) { return g / (1.0f + __expf(-g)); }
 
 // gu: [rows, 2F] (gate | up), a: [rows, F]
 __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ a,
-                                                         long long rows, int F) {
+                                                         long long rows, int F, long long a_rs) {
   const int fv = F >> 3;
   const long long total = rows * fv;
   for (long long it = (long long)blockIdx.x * 256 + threadIdx.x; it < total; it += (long long)gridDim.x * 256) {
@@ -71,13 +71,13 @@ __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const uint16_t* __restr
     unpack8(r[fv + c], u);
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = silu_f(g[j]) * u[j];
-    reinterpret_cast<uint4*>(a + row * F)[c] = pack8(o);
+    reinterpret_cast<uint4*>(a + row * a_rs)[c] = pack8(o);
   }
 }
 
 __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const uint16_t* __restrict__ da,
                                                          const uint16_t* __restrict__ gu, uint16_t* __restrict__ dgu,
-                                                         long long rows, int F) {
+                                                         long long rows, int F, long long dgu_rs) {
   const int fv = F >> 3;
   const long long total = rows * fv;
   for (long long it = (long long)blockIdx.x * 256 + threadIdx.x; it < total; it += (long long)gridDim.x * 256) {
@@ -95,23 +95,26 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const uint16_t* __restr
       du[j] = d[j] * sl;
       dg[j] = d[j] * u[j] * sg * (1.0f + g[j] * (1.0f - sg));
     }
-    uint4* o = reinterpret_cast<uint4*>(dgu + row * 2 * F);
+    uint4* o = reinterpret_cast<uint4*>(dgu + row * dgu_rs);
     o[c] = pack8(dg);
     o[fv + c] = pack8(du);
   }
 }
 
-extern "C" int ftc_swiglu_fwd(const void* gu, void* a, long long rows, int F, hipStream_t stream) {
-  if (F % 8 != 0) return -1;
+// a / dgu may be padded row views (row strides a_rs >= F, dgu_rs >= 2F; multiples of 8)
+extern "C" int ftc_swiglu_fwd(const void* gu, void* a, long long rows, int F, long long a_rs, hipStream_t stream) {
+  if (F % 8 != 0 || a_rs % 8 != 0) return -1;
   const int grid = ftc::stream_grid(rows * (F / 8), 256);
-  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(grid), dim3(256), 0, stream, (const uint16_t*)gu, (uint16_t*)a, rows, F);
+  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(grid), dim3(256), 0, stream, (const uint16_t*)gu, (uint16_t*)a, rows, F,
+                     a_rs);
   return (int)hipGetLastError();
 }
 
-extern "C" int ftc_swiglu_bwd(const void* da, const void* gu, void* dgu, long long rows, int F, hipStream_t stream) {
-  if (F % 8 != 0) return -1;
+extern "C" int ftc_swiglu_bwd(const void* da, const void* gu, void* dgu, long long rows, int F, long long dgu_rs,
+                              hipStream_t stream) {
+  if (F % 8 != 0 || dgu_rs % 8 != 0) return -1;
   const int grid = ftc::stream_grid(rows * (F / 8), 256);
   hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid), dim3(256), 0, stream, (const uint16_t*)da, (const uint16_t*)gu,
-                     (uint16_t*)dgu, rows, F);
+                     (uint16_t*)dgu, rows, F, dgu_rs);
   return (int)hipGetLastError();
 }

@@ -73,7 +73,7 @@ struct BwdArgs {
   const float* lse;
   float* delta;
   uint16_t *dq, *dk, *dv;
-  long long q_rs, kv_rs, o_rs, dq_rs, dkv_rs;
+  long long q_rs, kv_rs, o_rs, dq_rs, dkv_rs, do_rs;
   int B, S, H, KV;
   float scale, c;  // c = scale * log2(e)
   int causal, window;
@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(BwdArgs a) {
   const int nch = a.H * CPH;
   for (long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += (long long)gridDim.x * 4) {
     const uint16_t* orow = a.o + row * a.o_rs;
-    const uint16_t* drow = a.dout + row * a.o_rs;
+    const uint16_t* drow = a.dout + row * a.do_rs;
     const int b = (int)(row / a.S), s = (int)(row % a.S);
     for (int c0 = 0; c0 < nch; c0 += 64) {
       const int c = c0 + lane;
@@ -190,14 +190,14 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(BwdArgs a) {
   const int lrow = tid / NCH, lch = tid % NCH;
   u32x4 qreg[NP2], dreg[NP2];
   float lreg = 0.f, dlreg = 0.f;
-  const int qvoff = (lrow * (int)a.q_rs + lch * 8) * 2, dvoff = (lrow * (int)a.o_rs + lch * 8) * 2;
+  const int qvoff = (lrow * (int)a.q_rs + lch * 8) * 2, dvoff = (lrow * (int)a.do_rs + lch * 8) * 2;
 #define FTC_GLOAD(HQ, QT)                                                                          \
   {                                                                                                \
     const auto qrs = make_rsrc(a.q + ((long long)b * S + (QT)) * a.q_rs + (long long)(HQ) * D);    \
-    const auto drs = make_rsrc(a.dout + ((long long)b * S + (QT)) * a.o_rs + (long long)(HQ) * D); \
+    const auto drs = make_rsrc(a.dout + ((long long)b * S + (QT)) * a.do_rs + (long long)(HQ) * D); \
     _Pragma("unroll") for (int p = 0; p < NP2; ++p) {                                              \
       qreg[p] = buf_load16(qrs, qvoff, p * RPP2 * (int)a.q_rs * 2);                                \
-      dreg[p] = buf_load16(drs, dvoff, p * RPP2 * (int)a.o_rs * 2);                                \
+      dreg[p] = buf_load16(drs, dvoff, p * RPP2 * (int)a.do_rs * 2);                                \
     }                                                                                              \
     if (tid < BQ2) {                                                                               \
       const long long idx = ((long long)b * a.H + (HQ)) * S + (QT) + tid;                         \
@@ -353,7 +353,7 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
   bf16x8 qf[DSTEPS], df[DSTEPS];
   {
     const uint16_t* qp = a.q + ((long long)b * S + qrow) * a.q_rs + (long long)hq * D + 8 * hh;
-    const uint16_t* dp = a.dout + ((long long)b * S + qrow) * a.o_rs + (long long)hq * D + 8 * hh;
+    const uint16_t* dp = a.dout + ((long long)b * S + qrow) * a.do_rs + (long long)hq * D + 8 * hh;
 #pragma unroll
     for (int s = 0; s < DSTEPS; ++s) {
       qf[s] = as_bf8(*reinterpret_cast<const uint4*>(qp + 16 * s));
@@ -499,11 +499,12 @@ extern "C" int ftc_flash_bwd_workspace(int B, int S, int H, int D, long long* by
 
 extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
                              const float* lse, void* dq, void* dk, void* dv, void* workspace, int B, int S, int H,
-                             int KV, int D, long long q_rs, long long kv_rs, long long o_rs, long long dq_rs,
-                             long long dkv_rs, float scale, int causal, int window, hipStream_t stream) {
+                             int KV, int D, long long q_rs, long long kv_rs, long long o_rs, long long do_rs,
+                             long long dq_rs, long long dkv_rs, float scale, int causal, int window,
+                             hipStream_t stream) {
   if (S % 256 != 0 || H % KV != 0 || (D != 128 && D != 64)) return -1;
   BwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)o, (const uint16_t*)dout,
-            lse, (float*)workspace, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, q_rs, kv_rs, o_rs, dq_rs, dkv_rs,
+            lse, (float*)workspace, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, q_rs, kv_rs, o_rs, dq_rs, dkv_rs, do_rs,
             B, S, H, KV, scale, scale * LOG2E, causal, window};
   const int grid_d = ftc::stream_grid((long long)B * S, 4);
   const size_t lds_kv = (size_t)256 * D * 2 + 2 * (2 * 32 * D * 2 + 2 * 32 * sizeof(float));

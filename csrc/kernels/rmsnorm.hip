@@ -20,7 +20,7 @@ template <int NV, bool RES>
 __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ res, const uint16_t* __restrict__ w,
     uint16_t* __restrict__ h_out, uint16_t* __restrict__ y, float* __restrict__ rstd, int rows, int d,
-    float eps) {
+    float eps, long long y_rs) {
   const int lane = threadIdx.x & 63;
   const int nvec = d >> 3;
   const float inv_d = 1.0f / (float)d;
@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(
         unpack8(reinterpret_cast<const uint4*>(w)[idx], w8);
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = v[i][j] * r * w8[j];
-        reinterpret_cast<uint4*>(y + row * d)[idx] = pack8(o);
+        reinterpret_cast<uint4*>(y + row * y_rs)[idx] = pack8(o);
       }
     }
     if (lane == 0) rstd[row] = r;
@@ -155,8 +155,10 @@ static int pick_nv(int d) {
   return nv;
 }
 
+// y is written with row stride y_rs (>= d): a padded buffer lets the next projection append its LoRA
+// activations as extra GEMM columns (ops/linear.py "augmented" path)
 extern "C" int ftc_rmsnorm_fwd(const void* x, const void* res, const void* w, void* h_out, void* y, float* rstd,
-                               int rows, int d, float eps, hipStream_t stream) {
+                               int rows, int d, float eps, long long y_rs, hipStream_t stream) {
   if (d % 8 != 0 || d > 16 * 512) return -1;
   const int nv = pick_nv(d);
   const int grid = ftc::stream_grid(rows, 4);
@@ -168,10 +170,10 @@ extern "C" int ftc_rmsnorm_fwd(const void* x, const void* res, const void* w, vo
 #define FTC_LAUNCH_FWD(NV)                                                                                    \
   if (res)                                                                                                    \
     hipLaunchKernelGGL((rmsnorm_fwd_kernel<NV, true>), dim3(grid), dim3(256), 0, stream, X, R, W, H, Y, rstd, \
-                       rows, d, eps);                                                                         \
+                       rows, d, eps, y_rs);                                                                         \
   else                                                                                                        \
     hipLaunchKernelGGL((rmsnorm_fwd_kernel<NV, false>), dim3(grid), dim3(256), 0, stream, X, R, W, H, Y,     \
-                       rstd, rows, d, eps);
+                       rstd, rows, d, eps, y_rs);
   switch (nv) {
     case 1: FTC_LAUNCH_FWD(1); break;
     case 2: FTC_LAUNCH_FWD(2); break;

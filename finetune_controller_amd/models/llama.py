@@ -19,6 +19,7 @@ Weight names map 1:1 onto Hugging Face ``LlamaForCausalLM`` / ``MistralForCausal
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -27,6 +28,7 @@ from torch.utils.checkpoint import checkpoint
 
 from .. import ops
 from .config import ModelConfig
+from ..ops.linear import AugWeight
 from .lora import LoRAConfig, make_pairs
 
 
@@ -50,9 +52,29 @@ class LlamaLayer(nn.Module):
         }
         self.lora = make_pairs(self.shapes, lora, device=device, dtype=dtype) if lora else nn.ModuleDict()
         self.qweights: dict[str, object] = {}  # QLoRA: proj -> NF4Weight (replaces the bf16 Parameter)
+        # LoRA: the frozen base weight lives inside an augmented [N+R, K+R] buffer (ops.linear.AugWeight)
+        # so the rank-r update rides along in the big GEMMs; the Parameter is a view of it
+        self.aug: dict[str, AugWeight] = {}
+        attr = {"qkv": "wqkv", "o": "wo", "gu": "wgu", "down": "wdown"}
+        for name, pair in self.lora.items():
+            R = pair.A.shape[0]
+            if R > 0:
+                W = getattr(self, attr[name])
+                aw = AugWeight(W.shape[0], W.shape[1], R, device=device, dtype=dtype)
+                setattr(self, attr[name], nn.Parameter(aw.W, requires_grad=W.requires_grad))
+                self.aug[name] = aw
 
     def base_weight(self, proj: str):
         return {"qkv": self.wqkv, "o": self.wo, "gu": self.wgu, "down": self.wdown}[proj]
+
+    def pad(self, name: str) -> int:
+        """Spare columns the producer of this projection's input (and of its output gradient) adds."""
+        aw = self.aug.get(name)
+        if aw is None or name in self.qweights or not aw.owns(self.base_weight(name)):
+            return 0
+        if os.environ.get("FTC_LORA_AUG", "1") == "0":  # A/B switch: two-GEMM LoRA path
+            return 0
+        return aw.Rp
 
     def proj(self, name: str, x: torch.Tensor) -> torch.Tensor:
         pair = self.lora[name] if name in self.lora else None
@@ -60,23 +82,25 @@ class LlamaLayer(nn.Module):
         if qw is not None:
             from ..ops.nf4 import qlora_linear
 
-            return qlora_linear(x, qw, pair.A if pair else None, pair.B if pair else None,
+            return qlora_linear(x.contiguous(), qw, pair.A if pair else None, pair.B if pair else None,
                                 pair.scale if pair else 1.0, pair.blocks if pair else None)
         W = self.base_weight(name)
         if pair is None:
             return ops.lora_linear(x, W)
-        return ops.lora_linear(x, W, pair.A, pair.B, pair.scale, blocks=pair.blocks)
+        return ops.lora_linear(x, W, pair.A, pair.B, pair.scale, blocks=pair.blocks, aug=self.aug.get(name))
 
     def forward(self, h, delta, rope: ops.RotaryTable, B: int, S: int, positions=None):
         cfg = self.cfg
-        h, x = ops.add_rms_norm(h, delta, self.attn_norm, cfg.norm_eps)
+        p_qkv, p_o, p_gu, p_down = (self.pad(n) for n in ("qkv", "o", "gu", "down"))
+        h, x = ops.add_rms_norm(h, delta, self.attn_norm, cfg.norm_eps, pad=p_qkv)
         qkv = self.proj("qkv", x)
         qkv = ops.apply_rope_packed(qkv, rope, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, S, positions)
-        a = ops.attention_packed(qkv, B, S, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, True, cfg.sliding_window)
+        a = ops.attention_packed(qkv, B, S, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, True, cfg.sliding_window,
+                                 out_pad=p_o, grad_pad=p_qkv)
         o = self.proj("o", a)
-        h, x = ops.add_rms_norm(h, o, self.mlp_norm, cfg.norm_eps)
+        h, x = ops.add_rms_norm(h, o, self.mlp_norm, cfg.norm_eps, pad=p_gu)
         gu = self.proj("gu", x)
-        act = ops.swiglu(gu)
+        act = ops.swiglu(gu, out_pad=p_down, grad_pad=p_gu)
         return h, self.proj("down", act)
 
 

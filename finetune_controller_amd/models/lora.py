@@ -129,7 +129,12 @@ def merge_pair_into(W: torch.Tensor, pair: LoRAPair, sign: float = 1.0):
             B_s = pair.B[row:row + rows, i * pair.r:(i + 1) * pair.r].to(W.dtype).contiguous()
             Wv = W[row:row + rows]
             if use_hip(W) and W.dtype == torch.bfloat16:
-                ext().lora_merge_(Wv, A_s, B_s, sign * pair.scale, 0)
+                if Wv.is_contiguous():
+                    ext().lora_merge_(Wv, A_s, B_s, sign * pair.scale, 0)
+                else:  # column view of an augmented weight buffer (ops/linear.py)
+                    Wc = Wv.contiguous()
+                    ext().lora_merge_(Wc, A_s, B_s, sign * pair.scale, 0)
+                    Wv.copy_(Wc)
             else:
                 Wv.add_((B_s.float() @ A_s.float()).to(W.dtype), alpha=sign * pair.scale)
             i += 1

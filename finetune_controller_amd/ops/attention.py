@@ -59,30 +59,45 @@ def _sdpa_packed(qkv, B, S, H, KV, D, causal, window, scale):
 
 class _FlashPacked(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, B, S, H, KV, D, causal, window, scale):
+    def forward(ctx, qkv, B, S, H, KV, D, causal, window, scale, out_pad=0, grad_pad=0):
         q, k, v = _split(qkv, B, S, H, KV, D)
-        o, lse = ext().flash_fwd(q, k, v, B, S, H, KV, D, scale, causal, window)
-        ctx.save_for_backward(qkv, o, lse)
+        o, lse = ext().flash_fwd(q, k, v, B, S, H, KV, D, scale, causal, window, out_pad)
+        # o is kept outside save_for_backward: with out_pad the consumer writes its LoRA activations
+        # into the spare columns of o's buffer, which bumps the shared version counter (the [:, :H*D]
+        # values themselves never change)
+        ctx.save_for_backward(qkv, lse)
+        ctx.o = o.detach()
         ctx.cfg = (B, S, H, KV, D, causal, window, scale)
+        ctx.grad_pad = grad_pad
         return o
 
     @staticmethod
     def backward(ctx, do):
-        qkv, o, lse = ctx.saved_tensors
+        qkv, lse = ctx.saved_tensors
+        o = ctx.o
         B, S, H, KV, D, causal, window, scale = ctx.cfg
-        do = do.contiguous()
+        if do.stride(-1) != 1 or do.stride(0) % 8:
+            do = do.contiguous()
         q, k, v = _split(qkv, B, S, H, KV, D)
-        dqkv = torch.empty_like(qkv)
+        Wd = qkv.shape[1]
+        # grad_pad: dqkv is a column view of a row-padded buffer (spare columns for the augmented
+        # LoRA backward GEMM of the qkv projection)
+        dqkv = torch.empty(qkv.shape[0], Wd + ctx.grad_pad, dtype=qkv.dtype, device=qkv.device)[:, :Wd]
         dq, dk, dv = _split(dqkv, B, S, H, KV, D)
         ext().flash_bwd(q, k, v, o, do, lse, dq, dk, dv, B, S, H, KV, D, scale, causal, window)
-        return dqkv, None, None, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None, None, None, None
 
 
 def attention_packed(qkv: torch.Tensor, B: int, S: int, H: int, KV: int, D: int, causal: bool = True,
-                     window: int = 0, scale: float | None = None) -> torch.Tensor:
+                     window: int = 0, scale: float | None = None, out_pad: int = 0,
+                     grad_pad: int = 0) -> torch.Tensor:
+    """Causal / sliding-window GQA attention on a packed ``[B*S, (H+2KV)*D]`` projection.
+
+    ``out_pad`` / ``grad_pad``: the output / the gradient of ``qkv`` are column views of
+    row-padded buffers (spare columns for the augmented LoRA GEMMs, ``ops.linear``)."""
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if use_hip(qkv) and qkv.dtype == torch.bfloat16 and flash_supported(D, S):
-        return _FlashPacked.apply(qkv, B, S, H, KV, D, causal, int(window or 0), scale)
+        return _FlashPacked.apply(qkv, B, S, H, KV, D, causal, int(window or 0), scale, out_pad, grad_pad)
     return _sdpa_packed(qkv, B, S, H, KV, D, causal, window, scale)
 
 

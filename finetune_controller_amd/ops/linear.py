@@ -15,6 +15,21 @@ segment A's are stacked (``A = [A_q; A_k; A_v]``, one GEMM for all of them) and 
 a block-diagonal ``B`` so the LoRA update of the whole packed output is a single GEMM with
 K = segments * r.  Off-diagonal blocks of B are structural zeros: their gradient is dropped in the
 backward (``lora_blocks``), so they stay exactly zero under AdamW.
+
+**Augmented GEMMs** (MI355X path, ``AugWeight``).  The rank-r update folded into the big GEMMs
+instead of a read-modify-write of the [T, N] output (and of the [T, K] input gradient):
+
+* forward   ``y  = [x | s x A^T] . [W | B]^T``       -- one GEMM with K + Rp columns
+* backward  ``dx = [dy | dy B] . [W ; s A]``          -- one GEMM with N + Rp rows
+
+One buffer ``big [N+Rp, K+Rp]`` (Rp = R rounded up to the 64-wide GEMM K-tile: hipBLASLt's
+K-tail handling cost more than the rank update saved) holds W in ``big[:N, :K]`` (the frozen
+Parameter is a view of it), ``[B | 0]`` in ``big[:N, K:]`` and ``[s A ; 0]`` in ``big[N:, :K]``
+(refreshed from the trainable A/B each call).  The producers of ``x`` (RMSNorm, flash attention,
+SwiGLU) and of ``dy`` (flash backward, SwiGLU backward) write into row-padded buffers, so
+``s x A^T`` / ``dy B`` (and the zero pad columns) land in the spare columns and the augmented
+operands are plain strided views -- no concatenation copies.  When an operand has no spare
+columns the two-GEMM path runs instead.
 """
 from __future__ import annotations
 
@@ -38,42 +53,114 @@ def _mask_blocks(dB: torch.Tensor, blocks):
     return out
 
 
+def _spare_cols(t: torch.Tensor, width: int, extra: int) -> bool:
+    """True if the 2-D row view ``t[:, :width]`` has ``extra`` writable columns after it in every row."""
+    if t.dim() != 2 or t.stride(1) != 1 or t.stride(0) < width + extra or extra <= 0:
+        return False
+    need = t.storage_offset() + (t.shape[0] - 1) * t.stride(0) + width + extra
+    return t.untyped_storage().nbytes() >= need * t.element_size()
+
+
+def _tail(t: torch.Tensor, width: int, extra: int) -> torch.Tensor:
+    return t.as_strided((t.shape[0], extra), (t.stride(0), 1), t.storage_offset() + width)
+
+
+def _wide(t: torch.Tensor, width: int) -> torch.Tensor:
+    return t.as_strided((t.shape[0], width), (t.stride(0), 1), t.storage_offset())
+
+
+class AugWeight:
+    """``big [N+Rp, K+Rp]`` bf16 buffer whose ``[:N, :K]`` block is the frozen base weight."""
+
+    TILE = 64
+
+    def __init__(self, N: int, K: int, R: int, device=None, dtype=torch.bfloat16):
+        self.N, self.K, self.R = N, K, R
+        self.Rp = -(-R // self.TILE) * self.TILE
+        self.big = torch.zeros(N + self.Rp, K + self.Rp, device=device, dtype=dtype)
+
+    @property
+    def W(self) -> torch.Tensor:
+        return self.big[:self.N, :self.K]
+
+    def owns(self, W: torch.Tensor) -> bool:
+        return W.data_ptr() == self.big.data_ptr() and W.shape == (self.N, self.K) and W.stride(0) == self.K + self.Rp
+
+    def refresh(self, A: torch.Tensor, B: torch.Tensor, scale: float):
+        """big[:N, K:K+R] = B ; big[N:N+R, :K] = s A (pad rows / columns stay zero)."""
+        N, K, R = self.N, self.K, self.R
+        self.big[:N, K:K + R].copy_(B)
+        torch.mul(A, scale, out=self.big[N:N + R, :K])
+
+
 class _LoRALinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, W, bias, A, B, scale, blocks):
+    def forward(ctx, x, W, bias, A, B, scale, blocks, aug):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
+        N, K = W.shape
         # allocate the output in its final shape: the returned tensor must not be a view (RoPE
         # rotates it in place downstream)
-        out = torch.empty(*shp[:-1], W.shape[0], dtype=x.dtype, device=x.device)
-        y = out.view(-1, W.shape[0])
-        if bias is None:
-            torch.mm(x2, W.t(), out=y)
-        else:
-            torch.addmm(bias, x2, W.t(), out=y)
+        out = torch.empty(*shp[:-1], N, dtype=x.dtype, device=x.device)
+        y = out.view(-1, N)
         xa = None
-        if A is not None:
-            xa = x2 @ A.t()
-            y.addmm_(xa, B.t(), alpha=scale)
-        ctx.save_for_backward(x2, W, A, B, xa)
-        ctx.scale, ctx.blocks, ctx.shp, ctx.has_bias = scale, blocks, shp, bias is not None
+        use_aug = (aug is not None and A is not None and bias is None and aug.owns(W)
+                   and _spare_cols(x2, K, aug.Rp))
+        if use_aug:
+            Rp = aug.Rp
+            aug.refresh(A, B, scale)
+            # [s x A^T | 0] straight into the spare columns of the producer's buffer
+            torch.mm(x2, aug.big[N:, :K].t(), out=_tail(x2, K, Rp))
+            xa = _tail(x2, K, aug.R)  # = s * x A^T
+            torch.mm(_wide(x2, K + Rp), aug.big[:N].t(), out=y)
+        else:
+            if bias is None:
+                torch.mm(x2, W.t(), out=y)
+            else:
+                torch.addmm(bias, x2, W.t(), out=y)
+            if A is not None:
+                xa = x2 @ A.t()
+                y.addmm_(xa, B.t(), alpha=scale)
+        if use_aug:
+            # the frozen W shares big's version counter, which the s*B / s*A refreshes bump: keep it
+            # outside save_for_backward (it never changes while the graph lives)
+            ctx.save_for_backward(x2, None, A, B, xa)
+            ctx.W = W.detach()
+        else:
+            ctx.save_for_backward(x2, W, A, B, xa)
+            ctx.W = None
+        ctx.scale, ctx.blocks, ctx.shp, ctx.has_bias, ctx.aug = scale, blocks, shp, bias is not None, aug
+        ctx.aug_fwd = use_aug  # saved xa is s * x A^T
         return out
 
     @staticmethod
     def backward(ctx, dy):
         x2, W, A, B, xa = ctx.saved_tensors
+        if W is None:
+            W = ctx.W
         s = ctx.scale
+        aug = ctx.aug
+        N = W.shape[0]
         dy2 = dy.reshape(-1, dy.shape[-1])
         need_x, need_w, need_b, need_a, need_bb = ctx.needs_input_grad[:5]
         dx = dW = db = dA = dB = None
         dyb = None
-        if A is not None and (need_x or need_a):
-            dyb = dy2 @ B  # [T, R]
-        if need_x:
-            dx = dy2 @ W
-            if dyb is not None:
-                dx.addmm_(dyb, A, alpha=s)
-            dx = dx.view(ctx.shp)
+        xa_scaled = ctx.aug_fwd
+        if (need_x and aug is not None and A is not None and aug.owns(W) and _spare_cols(dy2, N, aug.Rp)):
+            # dx = [dy | dy B | 0] . [W ; s A ; 0]: dy B lands in the spare columns of the producer's buffer
+            Rp = aug.Rp
+            aug.refresh(A, B, s)
+            torch.mm(dy2, aug.big[:N, aug.K:], out=_tail(dy2, N, Rp))
+            dyb = _tail(dy2, N, aug.R)
+            dx = torch.mm(_wide(dy2, N + Rp), aug.big[:, :aug.K]).view(ctx.shp)
+        else:
+            if A is not None and (need_x or need_a):
+                dyb = dy2 @ B  # [T, R]
+            if need_x:
+                dx = dy2 @ W
+                if dyb is not None:
+                    dx.addmm_(dyb, A, alpha=s)
+                dx = dx.view(ctx.shp)
         if need_w:
             mg = getattr(W, "main_grad", None)
             if mg is not None:
@@ -86,12 +173,18 @@ class _LoRALinearFn(torch.autograd.Function):
             db = dy2.sum(0)
         if A is not None:
             if need_bb:
-                dB = _mask_blocks(torch.mm(dy2.t(), xa) * s, ctx.blocks)
+                dB = torch.mm(dy2.t(), xa)
+                if not xa_scaled:
+                    dB.mul_(s)
+                dB = _mask_blocks(dB, ctx.blocks)
             if need_a:
-                dA = torch.mm(dyb.t(), x2) * s
-        return dx, dW, db, dA, dB, None, None
+                if dyb is None:
+                    dyb = dy2 @ B
+                dA = torch.mm(dyb.t(), x2).mul_(s)
+        return dx, dW, db, dA, dB, None, None, None
 
 
 def lora_linear(x: torch.Tensor, W: torch.Tensor, A: torch.Tensor | None = None, B: torch.Tensor | None = None,
-                scale: float = 1.0, bias: torch.Tensor | None = None, blocks=None) -> torch.Tensor:
-    return _LoRALinearFn.apply(x, W, bias, A, B, scale, blocks)
+                scale: float = 1.0, bias: torch.Tensor | None = None, blocks=None,
+                aug: AugWeight | None = None) -> torch.Tensor:
+    return _LoRALinearFn.apply(x, W, bias, A, B, scale, blocks, aug)

@@ -157,10 +157,11 @@ def quantize_model_(model) -> int:
     for layer in model.layers:
         for name, attr in (("qkv", "wqkv"), ("o", "wo"), ("gu", "wgu"), ("down", "wdown")):
             W = getattr(layer, attr)
-            qw = NF4Weight.quantize(W.data)
+            qw = NF4Weight.quantize(W.data.contiguous())
             layer.qweights[name] = qw
             saved += W.numel() * W.element_size() - qw.nbytes()
             setattr(layer, attr, torch.nn.Parameter(torch.empty(0, device=W.device, dtype=W.dtype), requires_grad=False))
+            getattr(layer, "aug", {}).pop(name, None)  # drop the augmented bf16 buffer as well
     if torch.cuda.is_available():
         torch.cuda.empty_cache()
     return saved

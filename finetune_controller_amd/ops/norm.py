@@ -21,15 +21,15 @@ def _rms_ref(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
 
 class _AddRMSNormHip(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h, delta, w, eps):
+    def forward(ctx, h, delta, w, eps, pad):
         shp = h.shape
         h2 = h.reshape(-1, shp[-1])
         d2 = delta.reshape(-1, shp[-1]) if delta is not None else None
-        y, rstd, hn = ext().rmsnorm_fwd(h2, d2, w, eps)
+        y, rstd, hn = ext().rmsnorm_fwd(h2, d2, w, eps, pad)
         ctx.save_for_backward(hn, w, rstd)
         ctx.has_delta = delta is not None
         ctx.shp = shp
-        return hn.view(shp), y.view(shp)
+        return hn.view(shp), (y if pad else y.view(shp))
 
     @staticmethod
     def backward(ctx, dh_out, dy):
@@ -41,13 +41,16 @@ class _AddRMSNormHip(torch.autograd.Function):
         outs = ext().rmsnorm_bwd(dy2, hn, w, rstd, dres, need_dw)
         dx = outs[0].view(ctx.shp)
         dw = outs[1].to(w.dtype) if need_dw else None
-        return dx, (dx if ctx.has_delta else None), dw, None
+        return dx, (dx if ctx.has_delta else None), dw, None, None
 
 
-def add_rms_norm(h: torch.Tensor, delta: torch.Tensor | None, w: torch.Tensor, eps: float = 1e-5):
-    """Returns ``(h_new, y)`` with ``h_new = h + delta`` (or ``h``) and ``y = rmsnorm(h_new) * w``."""
+def add_rms_norm(h: torch.Tensor, delta: torch.Tensor | None, w: torch.Tensor, eps: float = 1e-5, pad: int = 0):
+    """Returns ``(h_new, y)`` with ``h_new = h + delta`` (or ``h``) and ``y = rmsnorm(h_new) * w``.
+
+    ``pad > 0`` (2-D ``h`` only): ``y`` is a column view of a ``[T, d + pad]`` buffer whose spare
+    columns the next LoRA projection uses (``ops.linear`` augmented GEMM)."""
     if use_hip(h) and h.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
-        return _AddRMSNormHip.apply(h, delta, w, eps)
+        return _AddRMSNormHip.apply(h, delta, w, eps, pad if h.dim() == 2 else 0)
     hn = h + delta if delta is not None else h
     return hn, _rms_ref(hn, w, eps)
 

@@ -76,7 +76,8 @@ class _RopeHip(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         cos, sin, n_rot, D, seq_len, positions = ctx.args
-        g = g.contiguous()
+        if g.dim() != 2 or g.stride(1) != 1 or g.stride(0) % 8:
+            g = g.contiguous()  # (a row-padded 2-D view is rotated in place, keeping its spare columns)
         ext().rope_(g, cos, sin, positions, n_rot, D, seq_len, True)
         return g, None, None, None, None, None, None
 

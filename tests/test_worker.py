@@ -45,6 +45,61 @@ def test_lora_linear_grads_match_autograd():
     assert (Bm.grad * (1 - mask)).abs().max() == 0  # off-diagonal blocks stay structural zeros
 
 
+class _PadIdentity(torch.autograd.Function):
+    """Hands ``x`` on as a column view of a row-padded buffer and the gradient likewise (what the
+    RMSNorm / SwiGLU / flash producers do on the GPU)."""
+
+    @staticmethod
+    def forward(ctx, x, pad):
+        ctx.pad = pad
+        buf = torch.full((x.shape[0], x.shape[1] + pad), float("nan"))
+        buf[:, :x.shape[1]] = x
+        return buf[:, :x.shape[1]]
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
+class _PadGrad(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, pad):
+        ctx.pad = pad
+        return y.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        buf = torch.full((g.shape[0], g.shape[1] + ctx.pad), float("nan"))
+        buf[:, :g.shape[1]] = g
+        return buf[:, :g.shape[1]], None
+
+
+def test_augmented_lora_gemms_match_two_gemm_path():
+    """ops.linear augmented path: y = [x | xA^T][W | sB]^T and dx = [dy | dyB][W ; sA] computed in
+    the producers' spare columns (NaN-filled here, so any read of an unwritten column fails)."""
+    from finetune_controller_amd.ops.linear import AugWeight
+
+    torch.manual_seed(0)
+    T, K, N, R = 10, 16, 24, 8
+    aw = AugWeight(N, K, R, dtype=torch.float32)
+    aw.W.copy_(torch.randn(N, K))
+    W = torch.nn.Parameter(aw.W, requires_grad=False)
+    assert aw.owns(W)
+    A = torch.randn(R, K, requires_grad=True)
+    B = torch.randn(N, R, requires_grad=True)
+    x = torch.randn(T, K, requires_grad=True)
+    y = _PadGrad.apply(ops.lora_linear(_PadIdentity.apply(x, aw.Rp), W, A, B, 0.5, aug=aw), aw.Rp)
+    x2, A2, B2 = (t.detach().clone().requires_grad_(True) for t in (x, A, B))
+    ref = x2 @ W.detach().clone().t() + 0.5 * (x2 @ A2.t()) @ B2.t()
+    torch.testing.assert_close(y, ref)
+    g = torch.randn_like(y)
+    y.backward(g)
+    ref.backward(g)
+    for a_, b_ in ((x.grad, x2.grad), (A.grad, A2.grad), (B.grad, B2.grad)):
+        assert torch.isfinite(a_).all()
+        torch.testing.assert_close(a_, b_)
+
+
 def test_fused_ce_matches_reference():
     torch.manual_seed(0)
     h = torch.randn(37, 16, requires_grad=True)
