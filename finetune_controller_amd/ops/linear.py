@@ -33,6 +33,8 @@ columns the two-GEMM path runs instead.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 _GRAD_READY_HOOK = None  # set by parallel.ddp to learn when a main_grad was written
@@ -63,6 +65,18 @@ def _spare_cols(t: torch.Tensor, width: int, extra: int) -> bool:
 
 def _tail(t: torch.Tensor, width: int, extra: int) -> torch.Tensor:
     return t.as_strided((t.shape[0], extra), (t.stride(0), 1), t.storage_offset() + width)
+
+
+# PyTorch TunableOp assumes ldc == n for GEMM outputs: under it the spare-column products go through
+# a contiguous temporary (two tiny copies per call) instead of being written in place
+_TUNABLEOP = os.environ.get("PYTORCH_TUNABLEOP_ENABLED", "0") == "1"
+
+
+def _mm_into(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor):
+    if _TUNABLEOP:
+        out.copy_(torch.mm(a, b))
+    else:
+        torch.mm(a, b, out=out)
 
 
 def _wide(t: torch.Tensor, width: int) -> torch.Tensor:
@@ -110,7 +124,7 @@ class _LoRALinearFn(torch.autograd.Function):
             Rp = aug.Rp
             aug.refresh(A, B, scale)
             # [s x A^T | 0] straight into the spare columns of the producer's buffer
-            torch.mm(x2, aug.big[N:, :K].t(), out=_tail(x2, K, Rp))
+            _mm_into(x2, aug.big[N:, :K].t(), _tail(x2, K, Rp))
             xa = _tail(x2, K, aug.R)  # = s * x A^T
             torch.mm(_wide(x2, K + Rp), aug.big[:N].t(), out=y)
         else:
@@ -150,7 +164,7 @@ class _LoRALinearFn(torch.autograd.Function):
             # dx = [dy | dy B | 0] . [W ; s A ; 0]: dy B lands in the spare columns of the producer's buffer
             Rp = aug.Rp
             aug.refresh(A, B, s)
-            torch.mm(dy2, aug.big[:N, aug.K:], out=_tail(dy2, N, Rp))
+            _mm_into(dy2, aug.big[:N, aug.K:], _tail(dy2, N, Rp))
             dyb = _tail(dy2, N, aug.R)
             dx = torch.mm(_wide(dy2, N + Rp), aug.big[:, :aug.K]).view(ctx.shp)
         else:

@@ -124,6 +124,8 @@ class GradBucketer:
                 self.works.append(dist.all_reduce(view, group=self.group, async_op=True))
         for w in self.works:
             w.wait()
+        if self._native is not None:
+            self._native.reset()
         self.reset()
 
     def close(self):

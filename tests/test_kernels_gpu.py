@@ -238,3 +238,41 @@ def test_llama_lora_step_hip_matches_torch_path(C, monkeypatch, window, aug):
         if err > 5e-2 * b.abs().max().item() + 1e-3:
             bad.append((n, round(err, 5), round(b.abs().max().item(), 5)))
     assert not bad, bad
+
+
+def test_native_rccl_engine_world1(C):
+    """csrc/comm engine on one rank: communicator bootstrap through c10d, every collective, event
+    ordering against the current stream (the multi-rank math is RCCL's; the 2-rank gradient
+    equivalence of the bucketer runs over gloo in test_worker.py)."""
+    import os
+
+    import torch.distributed as dist
+
+    from finetune_controller_amd.parallel.comm import NativeComm
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device(DEV, 0))
+    try:
+        comm = NativeComm()
+        for dt in (torch.float32, torch.bfloat16):
+            t = torch.randn(4099, device=DEV).to(dt)
+            ref = t.clone()
+            t.mul_(1.0)  # queued on the current stream before the collective
+            comm.all_reduce_async(t).wait()
+            t.add_(1)  # ordered after it on the device
+            torch.cuda.synchronize()
+            torch.testing.assert_close(t, ref + 1)
+        b = torch.arange(64, device=DEV, dtype=torch.float32)
+        comm.broadcast_async(b, 0).wait()
+        out = torch.empty(64, device=DEV)
+        comm.all_gather_async(out, b).wait()
+        rs = torch.empty(64, device=DEV)
+        comm.reduce_scatter_async(rs, b).wait()
+        torch.cuda.synchronize()
+        assert torch.equal(out, b) and torch.equal(rs, b)
+        assert comm.bench_all_reduce(torch.empty(1 << 20, device=DEV), 3) > 0
+        comm.reset()
+        comm.close()
+    finally:
+        dist.destroy_process_group()
