@@ -519,9 +519,9 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
   }();
   static bool attr_set = false;  // dK/dV uses 96.5 KiB of dynamic LDS (> the 64 KiB default)
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)bwd_dkdv_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)bwd_dkdv_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         256 * 128 * 2 + 2 * (2 * 32 * 128 * 2 + 2 * 32 * 4));
-    hipFuncSetAttribute((const void*)bwd_dkdv_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)bwd_dkdv_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         256 * 64 * 2 + 2 * (2 * 32 * 64 * 2 + 2 * 32 * 4));
     attr_set = true;
   }

@@ -29,7 +29,7 @@ NF4_CODE = torch.tensor([-1.0, -0.6961928009986877, -0.5250730514526367, -0.3949
                          0.24611230194568634, 0.33791524171829224, 0.44070982933044434, 0.5626170039176941,
                          0.7229568362236023, 1.0])
 
-FUSED_MAX_ROWS = 512  # below this many activation rows the fused NF4 GEMM wins (weight-stream bound)
+FUSED_MAX_ROWS = 128  # fused NF4 GEMM wins up to here (tools/bench_nf4.py, profiles/r1_bench_nf4.log)
 
 
 class NF4Weight:
