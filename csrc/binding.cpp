@@ -13,7 +13,8 @@ int ftc_rmsnorm_fwd(const void* x, const void* res, const void* w, void* h_out, 
                     float eps, long long y_rs, hipStream_t stream);
 int ftc_rmsnorm_bwd_grid(int rows);
 int ftc_rmsnorm_bwd(const void* dy, const void* h, const void* w, const float* rstd, const void* dres, void* dx,
-                    float* dw_part, float* dw, int rows, int d, hipStream_t stream);
+                    float* dw_part, float* dw, int rows, int d, long long dres_rs, long long dx_rs,
+                    hipStream_t stream);
 int ftc_rope(void* qkv, const float* cosT, const float* sinT, const int* positions, long long rows, int ld,
              int n_rot_heads, int head_dim, int seq_len, int inverse, hipStream_t stream);
 int ftc_swiglu_fwd(const void* gu, void* a, long long rows, int F, long long a_rs, hipStream_t stream);
@@ -95,8 +96,10 @@ std::vector<at::Tensor> rmsnorm_fwd(const at::Tensor& x, const c10::optional<at:
   return {y, rstd, h};
 }
 
+// dres may be a row-padded view; pad > 0 returns dx as the [rows, d] view of a [rows, d + pad] buffer
 std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, const at::Tensor& w,
-                                    const at::Tensor& rstd, const c10::optional<at::Tensor>& dres, bool need_dw) {
+                                    const at::Tensor& rstd, const c10::optional<at::Tensor>& dres, bool need_dw,
+                                    int64_t pad) {
   need(dy, at::kBFloat16, "dy");
   need(h, at::kBFloat16, "h");
   need(w, at::kBFloat16, "w");
@@ -110,11 +113,15 @@ std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, c
   const void* drp = nullptr;
   if (dres.has_value()) {
     need(*dres, at::kBFloat16, "dres");
-    need_rows(*dres, "dres");
+    TORCH_CHECK(dres->dim() == 2 && dres->stride(1) == 1 && dres->stride(0) % 8 == 0 &&
+                    reinterpret_cast<uintptr_t>(dres->data_ptr()) % 16 == 0,
+                "dres must be a 16-byte aligned row view");
     TORCH_CHECK(dres->sizes() == h.sizes(), "dres shape mismatch");
     drp = dres->data_ptr();
   }
-  auto dx = at::empty_like(h);
+  TORCH_CHECK(pad >= 0 && pad % 8 == 0, "rmsnorm_bwd: pad must be a multiple of 8");
+  auto dxbuf = at::empty({rows, d + pad}, h.options());
+  auto dx = pad ? dxbuf.narrow(1, 0, d) : dxbuf;
   at::Tensor dw, part;
   if (need_dw) {
     const int g = ftc_rmsnorm_bwd_grid(rows);
@@ -123,7 +130,7 @@ std::vector<at::Tensor> rmsnorm_bwd(const at::Tensor& dy, const at::Tensor& h, c
   }
   check(ftc_rmsnorm_bwd(dy.data_ptr(), h.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), drp, dx.data_ptr(),
                         need_dw ? part.data_ptr<float>() : nullptr, need_dw ? dw.data_ptr<float>() : nullptr, rows, d,
-                        cur_stream()),
+                        drp ? dres->stride(0) : d, d + pad, cur_stream()),
         "rmsnorm_bwd");
   if (need_dw) return {dx, dw};
   return {dx};
@@ -357,7 +364,8 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "finetune_controller_amd gfx950 kernels";
   namespace py = pybind11;
   m.def("rmsnorm_fwd", &rmsnorm_fwd, py::arg("x"), py::arg("res"), py::arg("w"), py::arg("eps"), py::arg("pad") = 0);
-  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd, py::arg("dy"), py::arg("h"), py::arg("w"), py::arg("rstd"), py::arg("dres"),
+        py::arg("need_dw"), py::arg("pad") = 0);
   m.def("rope_", &rope_);
   m.def("swiglu_fwd", &swiglu_fwd, py::arg("gu"), py::arg("pad") = 0);
   m.def("swiglu_bwd", &swiglu_bwd, py::arg("da"), py::arg("gu"), py::arg("pad") = 0);

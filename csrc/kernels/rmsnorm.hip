@@ -65,11 +65,16 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(
   }
 }
 
+// One wave per row.  dy / h rows stay in registers as packed bf16 (4 VGPRs per 8 elements) and are
+// re-expanded in the second pass, and w is loaded once per wave: ~100 VGPRs at d = 4096 instead of
+// ~180 for fp32 copies, i.e. twice the waves in flight for this HBM-bound kernel.
+// dres (gradient of the residual stream from the next layer) and dx may be row-padded views
+// (row strides dres_rs / dx_rs): dx's spare columns take the next projection's LoRA term (ops/linear.py).
 template <int NV, bool DW, bool DRES>
 __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ h, const uint16_t* __restrict__ w,
     const float* __restrict__ rstd, const uint16_t* __restrict__ dres, uint16_t* __restrict__ dx,
-    float* __restrict__ dw_part, int rows, int d) {
+    float* __restrict__ dw_part, int rows, int d, long long dres_rs, long long dx_rs) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nvec = d >> 3;
@@ -81,24 +86,31 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
   }
+  uint4 wv[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int idx = lane + i * 64;
+    wv[i] = idx < nvec ? reinterpret_cast<const uint4*>(w)[idx] : make_uint4(0, 0, 0, 0);
+  }
   for (long long row = (long long)blockIdx.x * 4 + wid; row < rows; row += (long long)gridDim.x * 4) {
     const float r = rstd[row];
-    float xh[NV][8], g[NV][8];
+    uint4 dyv[NV], hv[NV];
     float dot = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int idx = lane + i * 64;
       if (idx < nvec) {
-        float dy8[8], w8[8];
-        unpack8(reinterpret_cast<const uint4*>(dy + row * d)[idx], dy8);
-        unpack8(reinterpret_cast<const uint4*>(h + row * d)[idx], xh[i]);
-        unpack8(reinterpret_cast<const uint4*>(w)[idx], w8);
+        dyv[i] = reinterpret_cast<const uint4*>(dy + row * d)[idx];
+        hv[i] = reinterpret_cast<const uint4*>(h + row * d)[idx];
+        float dy8[8], h8[8], w8[8];
+        unpack8(dyv[i], dy8);
+        unpack8(hv[i], h8);
+        unpack8(wv[i], w8);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          xh[i][j] *= r;
-          g[i][j] = dy8[j] * w8[j];
-          dot += g[i][j] * xh[i][j];
-          if constexpr (DW) acc[i][j] += dy8[j] * xh[i][j];
+          const float xh = h8[j] * r;
+          dot += dy8[j] * w8[j] * xh;
+          if constexpr (DW) acc[i][j] += dy8[j] * xh;
         }
       }
     }
@@ -107,16 +119,19 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
     for (int i = 0; i < NV; ++i) {
       const int idx = lane + i * 64;
       if (idx < nvec) {
-        float o[8];
+        float dy8[8], h8[8], w8[8], o[8];
+        unpack8(dyv[i], dy8);
+        unpack8(hv[i], h8);
+        unpack8(wv[i], w8);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = r * (g[i][j] - xh[i][j] * dot);
+        for (int j = 0; j < 8; ++j) o[j] = r * (dy8[j] * w8[j] - h8[j] * r * dot);
         if constexpr (DRES) {
           float d8[8];
-          unpack8(reinterpret_cast<const uint4*>(dres + row * d)[idx], d8);
+          unpack8(reinterpret_cast<const uint4*>(dres + row * dres_rs)[idx], d8);
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] += d8[j];
         }
-        reinterpret_cast<uint4*>(dx + row * d)[idx] = pack8(o);
+        reinterpret_cast<uint4*>(dx + row * dx_rs)[idx] = pack8(o);
       }
     }
   }
@@ -190,7 +205,8 @@ extern "C" int ftc_rmsnorm_fwd(const void* x, const void* res, const void* w, vo
 extern "C" int ftc_rmsnorm_bwd_grid(int rows) { return ftc::stream_grid(rows, 4) > 512 ? 512 : ftc::stream_grid(rows, 4); }
 
 extern "C" int ftc_rmsnorm_bwd(const void* dy, const void* h, const void* w, const float* rstd, const void* dres,
-                               void* dx, float* dw_part, float* dw, int rows, int d, hipStream_t stream) {
+                               void* dx, float* dw_part, float* dw, int rows, int d, long long dres_rs,
+                               long long dx_rs, hipStream_t stream) {
   if (d % 8 != 0 || d > 16 * 512) return -1;
   const int nv = pick_nv(d);
   const bool need_dw = dw != nullptr;
@@ -204,7 +220,7 @@ extern "C" int ftc_rmsnorm_bwd(const void* dy, const void* h, const void* w, con
   auto DX = (uint16_t*)dx;
 #define FTC_LAUNCH_BWD(NV, DWB, DRB)                                                                       \
   hipLaunchKernelGGL((rmsnorm_bwd_kernel<NV, DWB, DRB>), dim3(grid), dim3(256), lds, stream, DY, Hh, W, rstd, \
-                     DR, DX, dw_part, rows, d)
+                     DR, DX, dw_part, rows, d, dres_rs, dx_rs)
 #define FTC_LAUNCH_BWD_NV(NV)                     \
   if (need_dw) {                                  \
     if (dres) FTC_LAUNCH_BWD(NV, true, true);     \

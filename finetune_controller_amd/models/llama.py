@@ -92,13 +92,15 @@ class LlamaLayer(nn.Module):
     def forward(self, h, delta, rope: ops.RotaryTable, B: int, S: int, positions=None):
         cfg = self.cfg
         p_qkv, p_o, p_gu, p_down = (self.pad(n) for n in ("qkv", "o", "gu", "down"))
-        h, x = ops.add_rms_norm(h, delta, self.attn_norm, cfg.norm_eps, pad=p_qkv)
+        # grad_pad: delta came from the previous layer's down projection (same LoRA shape in every layer;
+        # a pad that is too small just falls back to the two-GEMM backward)
+        h, x = ops.add_rms_norm(h, delta, self.attn_norm, cfg.norm_eps, pad=p_qkv, grad_pad=p_down)
         qkv = self.proj("qkv", x)
         qkv = ops.apply_rope_packed(qkv, rope, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, S, positions)
         a = ops.attention_packed(qkv, B, S, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, True, cfg.sliding_window,
                                  out_pad=p_o, grad_pad=p_qkv)
         o = self.proj("o", a)
-        h, x = ops.add_rms_norm(h, o, self.mlp_norm, cfg.norm_eps, pad=p_gu)
+        h, x = ops.add_rms_norm(h, o, self.mlp_norm, cfg.norm_eps, pad=p_gu, grad_pad=p_o)
         gu = self.proj("gu", x)
         act = ops.swiglu(gu, out_pad=p_down, grad_pad=p_gu)
         return h, self.proj("down", act)
@@ -150,7 +152,8 @@ class LlamaForCausalLM(nn.Module):
                 h, delta = checkpoint(layer, h, delta, self.rope, B, S, positions, use_reentrant=False)
             else:
                 h, delta = layer(h, delta, self.rope, B, S, positions)
-        _, x = ops.add_rms_norm(h, delta, self.final_norm, self.cfg.norm_eps)
+        gp = self.layers[-1].pad("down") if len(self.layers) else 0
+        _, x = ops.add_rms_norm(h, delta, self.final_norm, self.cfg.norm_eps, grad_pad=gp)
         return x
 
     def forward(self, input_ids: torch.Tensor, labels: torch.Tensor | None = None, positions=None,

@@ -21,7 +21,7 @@ def _rms_ref(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
 
 class _AddRMSNormHip(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h, delta, w, eps, pad):
+    def forward(ctx, h, delta, w, eps, pad, grad_pad):
         shp = h.shape
         h2 = h.reshape(-1, shp[-1])
         d2 = delta.reshape(-1, shp[-1]) if delta is not None else None
@@ -29,6 +29,7 @@ class _AddRMSNormHip(torch.autograd.Function):
         ctx.save_for_backward(hn, w, rstd)
         ctx.has_delta = delta is not None
         ctx.shp = shp
+        ctx.grad_pad = grad_pad if (delta is not None and h.dim() == 2) else 0
         return hn.view(shp), (y if pad else y.view(shp))
 
     @staticmethod
@@ -36,21 +37,28 @@ class _AddRMSNormHip(torch.autograd.Function):
         hn, w, rstd = ctx.saved_tensors
         d = ctx.shp[-1]
         dy2 = dy.reshape(-1, d).contiguous()
-        dres = None if dh_out is None else dh_out.reshape(-1, d).contiguous()
+        dres = None
+        if dh_out is not None:
+            dres = dh_out.reshape(-1, d)
+            if dres.stride(1) != 1 or dres.stride(0) % 8 or dres.data_ptr() % 16:
+                dres = dres.contiguous()  # (row-padded views from the next norm are read in place)
         need_dw = ctx.needs_input_grad[2]
-        outs = ext().rmsnorm_bwd(dy2, hn, w, rstd, dres, need_dw)
-        dx = outs[0].view(ctx.shp)
+        outs = ext().rmsnorm_bwd(dy2, hn, w, rstd, dres, need_dw, ctx.grad_pad)
+        dx = outs[0] if ctx.grad_pad else outs[0].view(ctx.shp)
         dw = outs[1].to(w.dtype) if need_dw else None
-        return dx, (dx if ctx.has_delta else None), dw, None, None
+        return dx, (dx if ctx.has_delta else None), dw, None, None, None
 
 
-def add_rms_norm(h: torch.Tensor, delta: torch.Tensor | None, w: torch.Tensor, eps: float = 1e-5, pad: int = 0):
+def add_rms_norm(h: torch.Tensor, delta: torch.Tensor | None, w: torch.Tensor, eps: float = 1e-5, pad: int = 0,
+                 grad_pad: int = 0):
     """Returns ``(h_new, y)`` with ``h_new = h + delta`` (or ``h``) and ``y = rmsnorm(h_new) * w``.
 
     ``pad > 0`` (2-D ``h`` only): ``y`` is a column view of a ``[T, d + pad]`` buffer whose spare
-    columns the next LoRA projection uses (``ops.linear`` augmented GEMM)."""
+    columns the next LoRA projection uses (``ops.linear`` augmented GEMM).  ``grad_pad``: the
+    gradient of ``h``/``delta`` is likewise padded, for the augmented backward of the projection
+    that produced ``delta``."""
     if use_hip(h) and h.dtype == torch.bfloat16 and w.dtype == torch.bfloat16:
-        return _AddRMSNormHip.apply(h, delta, w, eps, pad if h.dim() == 2 else 0)
+        return _AddRMSNormHip.apply(h, delta, w, eps, pad if h.dim() == 2 else 0, grad_pad)
     hn = h + delta if delta is not None else h
     return hn, _rms_ref(hn, w, eps)
 
