@@ -46,6 +46,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--dtype", default="auto")
     ap.add_argument("--dataset_path", "--dataset-path", dest="dataset_path", default="/data/dataset")
     ap.add_argument("--checkpoint_path", "--checkpoint-path", dest="checkpoint_path", default="/data/artifacts")
+    ap.add_argument("--timers", action="store_true", help="per-phase device timers (fwd/bwd/comm/optim) in metrics.csv")
+    ap.add_argument("--profile-steps", type=int, default=0, help="torch.profiler chrome trace of N steps")
     return ap
 
 
@@ -58,7 +60,7 @@ def config_from_args(a) -> TrainConfig:
                        dataset_path=a.dataset_path, checkpoint_path=a.checkpoint_path, log_interval=a.log_interval,
                        save_every=a.save_every, resume=not a.no_resume, synthetic=a.synthetic, bucket_mb=a.bucket_mb,
                        comm_engine=a.comm_engine, checkpoint_layers=a.checkpoint_layers, init_from=a.init_from,
-                       dtype=a.dtype, device=a.device)
+                       dtype=a.dtype, device=a.device, timers=a.timers, profile_steps=a.profile_steps)
 
 
 def main(argv=None) -> int:

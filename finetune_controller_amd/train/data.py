@@ -164,10 +164,10 @@ class PackedTokenDataset:
         try:
             from ..utils.native import NativeTokenLoader
 
-            if isinstance(self.tokens, np.memmap):
+            if isinstance(self.tokens, np.memmap) and os.environ.get("FTC_NATIVE_LOADER", "1") != "0":
                 self._native = NativeTokenLoader(self.tokens.filename, self.tokens.dtype.itemsize, seq_len, batch,
                                                  rank, world, seed)
-        except Exception:
+        except ImportError:  # _rt.so not built: numpy path
             self._native = None
         self._perm()
 
@@ -194,7 +194,14 @@ class PackedTokenDataset:
             arr = np.stack([np.asarray(self.tokens[j * S: j * S + S + 1], dtype=np.int64) for j in idx])
             arr = torch.from_numpy(arr)
             self.pos += 1
-        t = arr.to(self.device, non_blocking=True)
+        if self._native is not None:
+            if torch.device(self.device).type == "cpu":
+                t = arr.clone()  # the ring buffer is refilled after the next call
+            else:
+                t = arr.to(self.device, non_blocking=True)
+                self._native.copied()
+        else:
+            t = arr.to(self.device, non_blocking=True)
         return t[:, :-1], t[:, 1:]
 
     def state(self):

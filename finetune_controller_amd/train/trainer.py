@@ -70,6 +70,8 @@ class TrainConfig:
     device: str = "auto"
     ce_chunk_rows: int = 4096
     save_model: bool = True
+    timers: bool = False  # per-phase device timers (fwd/bwd/comm/optim) -> metrics.csv
+    profile_steps: int = 0  # >0: torch.profiler chrome trace of that many steps -> trace_rank<r>.json
 
     def lora_config(self) -> LoRAConfig | None:
         if self.method not in ("lora", "qlora"):
@@ -120,6 +122,7 @@ class Trainer:
         self._data = None
         self.step = 0
         self.is_main = self.info.is_main
+        self._timing: list[tuple] = []  # per-step (start, fwd, bwd, comm, optim) device events
 
     # ------------------------------------------------------------------ data
     def data(self):
@@ -145,6 +148,10 @@ class Trainer:
         """fwd + bwd (+accum) + overlapped all-reduce + optimizer. Returns the loss (device tensor)."""
         tc = self.tc
         data = self.data()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if (tc.timers and self.device.type == "cuda") \
+            else None
+        if ev:
+            ev[0].record()
         self.opt.zero_grad()
         total = None
         n_valid = tc.batch_size * tc.seq_len
@@ -152,11 +159,32 @@ class Trainer:
             x, y = next(data)
             self.ddp.armed = micro == tc.grad_accum - 1
             loss = self.model(x, y, n_valid=n_valid)
+            if ev:
+                ev[1].record()  # (last micro-batch's forward end)
             loss.backward()
             total = loss.detach() if total is None else total + loss.detach()
-        self.ddp.finish()
+        if ev:
+            ev[2].record()
+        self.ddp.finish()  # device-side waits on the bucket all-reduces: the non-overlapped comm tail
+        if ev:
+            ev[3].record()
         self.opt.step(lr)
+        if ev:
+            ev[4].record()
+            self._timing.append(tuple(ev))
         return total / tc.grad_accum
+
+    def _phase_ms(self) -> dict:
+        """Mean fwd/bwd/comm/optim milliseconds of the steps since the last call (after a sync)."""
+        if not self._timing:
+            return {}
+        acc = [0.0, 0.0, 0.0, 0.0]
+        for ev in self._timing:
+            for i in range(4):
+                acc[i] += ev[i].elapsed_time(ev[i + 1])
+        n = len(self._timing)
+        self._timing = []
+        return {k: round(v / n, 2) for k, v in zip(("fwd_ms", "bwd_ms", "comm_ms", "optim_ms"), acc)}
 
     # ------------------------------------------------------------------ loop
     def run(self) -> dict:
@@ -184,9 +212,22 @@ class Trainer:
         sync()
         t0 = time.perf_counter()
         losses = []
+        prof = None
         for step in range(start, total):
             lr = lr_at(step, tc.lr, tc.warmup_steps, total, tc.schedule)
+            if tc.profile_steps and step == start + 2 and prof is None:
+                from torch.profiler import ProfilerActivity, profile
+
+                acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if self.device.type == "cuda" else [])
+                prof = profile(activities=acts)
+                prof.__enter__()
+                prof_end = step + tc.profile_steps
             losses.append(self.train_step(lr))
+            if prof is not None and step + 1 == prof_end:
+                sync()
+                prof.__exit__(None, None, None)
+                prof.export_chrome_trace(os.path.join(tc.checkpoint_path, f"trace_rank{self.info.rank}.json"))
+                prof = False
             self.step = step + 1
             if self.step % tc.log_interval == 0 or self.step == total:
                 sync()
@@ -201,7 +242,8 @@ class Trainer:
                         "tokens_per_sec": round(tps, 1), "step_time_ms": round(step_ms, 2),
                         "grad_norm": round(self.opt.grad_norm(), 6), "world_size": self.info.world_size,
                         "mem_gb": round(mem, 2),
-                        "tflops_per_gpu": round(tps * flops_tok / self.info.world_size / 1e12, 1)}
+                        "tflops_per_gpu": round(tps * flops_tok / self.info.world_size / 1e12, 1),
+                        **self._phase_ms()}
                 if self.is_main:
                     metrics.write(last)
                     # "Epoch" marks the start of the UI-visible log (LOG_STREAM_SEARCH_STRING)

@@ -275,6 +275,34 @@ def test_dataset_formats(tmp_path):
     assert len(load_token_array(str(tmp_path / "c.csv"), vocab=512)) > 4
 
 
+@pytest.mark.parametrize("dtype,vocab", [(np.uint16, 512), (np.uint32, 100000)])
+def test_native_token_loader_matches_numpy_path(tmp_path, monkeypatch, dtype, vocab):
+    """csrc/runtime token loader (mmap + prefetch threads) yields exactly the numpy path's batches,
+    across epoch boundaries, per rank, and after a resume seek."""
+    pytest.importorskip("finetune_controller_amd._rt")
+    toks = (np.arange(5000, dtype=np.int64) * 7919 % vocab).astype(dtype)
+    name = "t.u32.bin" if dtype == np.uint32 else "t.bin"
+    toks.tofile(tmp_path / name)
+    for rank in (0, 1):
+        monkeypatch.setenv("FTC_NATIVE_LOADER", "1")
+        nat = PackedTokenDataset(str(tmp_path / name), vocab=vocab, batch=3, seq_len=32, device="cpu", rank=rank,
+                                 world=2, seed=4)
+        assert nat._native is not None
+        monkeypatch.setenv("FTC_NATIVE_LOADER", "0")
+        ref = PackedTokenDataset(str(tmp_path / name), vocab=vocab, batch=3, seq_len=32, device="cpu", rank=rank,
+                                 world=2, seed=4)
+        assert ref._native is None
+        for _ in range(2 * nat.steps_per_epoch + 3):  # crosses two epoch boundaries
+            (xa, ya), (xb, yb) = next(nat), next(ref)
+            assert torch.equal(xa, xb) and torch.equal(ya, yb)
+        st = ref.state()
+        nat.load_state(st)
+        ref.load_state(st)
+        for _ in range(3):
+            assert torch.equal(next(nat)[0], next(ref)[0])
+        nat._native.close()
+
+
 def _ddp_worker(rank, world, port, tmp, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
