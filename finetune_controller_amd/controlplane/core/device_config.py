@@ -32,9 +32,13 @@ class ResourceDefaults(BaseModel):
 
 
 class Toleration(BaseModel):
+    """k8s toleration; the reference's {key, value, effect} (``device_config.py:21-24``) plus the
+    optional ``operator`` (``Exists`` tolerations -- e.g. the AMD GPU operator's taint -- have no value)."""
+
     key: str
-    value: str
+    value: str | None = None
     effect: str
+    operator: str | None = None
 
 
 class Defaults(BaseModel):
@@ -55,7 +59,7 @@ class Worker(BaseModel):
     tolerations: list[Toleration] | None = None
 
     def get_tolerations(self) -> list[dict]:
-        return [t.model_dump() for t in self.tolerations] if self.tolerations else []
+        return [t.model_dump(exclude_none=True) for t in self.tolerations] if self.tolerations else []
 
 
 class WorkersConfig(BaseModel):

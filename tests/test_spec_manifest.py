@@ -221,3 +221,38 @@ def test_local_context_builds():
     ctx = AppContext.local()
     assert ctx.devices.list_workers() == ["cpu", "mi355x"]
     assert ctx.s3.get_artifacts_uri_string("ftc-bucket", "u", "j") == "s3://ftc-bucket/finetune_jobs/u/j/artifacts"
+
+
+def test_deploy_example_config_parses_and_builds_amd_gpu_manifests():
+    """deploy/config.example.json (JSON with // comments) loads with the device-config parser; its
+    MI355X workers request amd.com/gpu and carry an Exists toleration without a value."""
+    import pathlib
+
+    from finetune_controller_amd.controlplane.core.device_config import load_config
+
+    root = pathlib.Path(__file__).resolve().parents[1]
+    cfg = load_config(str(root / "deploy" / "config.example.json"))
+    names = [w.name for w in cfg.workers.workers]
+    assert names == ["cpu", "mi355x", "mi355x-node"]
+    node = cfg.workers.get_worker("mi355x-node")
+    assert node.defaults.get_accelerators() == {"amd.com/gpu": 8}
+    assert node.get_tolerations() == [{"key": "amd.com/gpu", "effect": "NoSchedule", "operator": "Exists"}]
+
+
+def test_deploy_manifests_are_valid_yaml_with_amd_gpu_quota():
+    import pathlib
+
+    import yaml
+
+    root = pathlib.Path(__file__).resolve().parents[1] / "deploy"
+    docs = {}
+    for f in sorted(root.rglob("*.yaml")):
+        for d in yaml.safe_load_all(f.read_text()):
+            if d:
+                docs[(d["kind"], d["metadata"]["name"])] = d
+    cq = docs[("ClusterQueue", "cluster-queue")]
+    gpu = [r for g in cq["spec"]["resourceGroups"] for fl in g["flavors"] for r in fl["resources"]
+           if r["name"] == "amd.com/gpu"]
+    assert gpu and gpu[0]["nominalQuota"] == 8
+    assert ("LocalQueue", "finetune-queue") in docs and ("Role", "ftc-controlplane") in docs
+    assert not any(d["kind"] == "ClusterRoleBinding" for d in docs.values())  # no cluster-admin
