@@ -104,7 +104,10 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(BwdArgs a) {
       for (int off = CPH / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
       if (c < nch && (c % CPH) == 0) {
         const int h = c / CPH;
-        a.delta[((long long)b * a.H + h) * a.S + s] = acc;
+        // workspace rows: [-delta | -lse/scale] -- the dK/dV kernel's accumulator start values, DMA'd as is
+        const long long ri = ((long long)b * a.H + h) * a.S + s;
+        a.delta[ri] = -acc;
+        a.delta[rows * a.H + ri] = -a.lse[ri] / a.scale;
       }
     }
   }
@@ -125,8 +128,13 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(BwdArgs a) {
   constexpr int BKV = 256, BQ2 = 32;
   constexpr int KBYTES = BKV * D * 2, QBYTES = BQ2 * D * 2;
   constexpr int SLICE = 2 * QBYTES + 2 * BQ2 * 4;  // Q | dO | -lse/scale | -delta
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Ks = smem;
+  // K and the three ring slots are DISTINCT __shared__ objects: the compiler then knows (LDS alias
+  // scopes) that reading one slot does not depend on the DMA still writing the others, instead of
+  // draining every DMA (vmcnt(0)) before the first ds_read of each slice
+  __shared__ __attribute__((aligned(16))) char Ks[KBYTES];
+  __shared__ __attribute__((aligned(16))) char slot0[SLICE];
+  __shared__ __attribute__((aligned(16))) char slot1[SLICE];
+  __shared__ __attribute__((aligned(16))) char slot2[SLICE];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -183,85 +191,101 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(BwdArgs a) {
   if (a.window > 0) qend = min(S, kv0 + BKV - 1 + a.window);
   qbeg = (qbeg / BQ2) * BQ2;
   const int nqt = (qend - qbeg + BQ2 - 1) / BQ2;
-  const float inv_scale = 1.0f / a.scale;
-
-  // staging: 32 rows x D of Q and of dO per slice; buffer loads (wave-uniform slice base in SGPRs)
-  constexpr int RPP2 = 256 / NCH, NP2 = BQ2 / RPP2;
-  const int lrow = tid / NCH, lch = tid % NCH;
-  u32x4 qreg[NP2], dreg[NP2];
-  float lreg = 0.f, dlreg = 0.f;
-  const int qvoff = (lrow * (int)a.q_rs + lch * 8) * 2, dvoff = (lrow * (int)a.do_rs + lch * 8) * 2;
-#define FTC_GLOAD(HQ, QT)                                                                          \
-  {                                                                                                \
-    const auto qrs = make_rsrc(a.q + ((long long)b * S + (QT)) * a.q_rs + (long long)(HQ) * D);    \
-    const auto drs = make_rsrc(a.dout + ((long long)b * S + (QT)) * a.do_rs + (long long)(HQ) * D); \
-    _Pragma("unroll") for (int p = 0; p < NP2; ++p) {                                              \
-      qreg[p] = buf_load16(qrs, qvoff, p * RPP2 * (int)a.q_rs * 2);                                \
-      dreg[p] = buf_load16(drs, dvoff, p * RPP2 * (int)a.do_rs * 2);                                \
-    }                                                                                              \
-    if (tid < BQ2) {                                                                               \
-      const long long idx = ((long long)b * a.H + (HQ)) * S + (QT) + tid;                         \
-      lreg = -a.lse[idx] * inv_scale;                                                              \
-      dlreg = -a.delta[idx];                                                                       \
-    }                                                                                              \
-  }
-#define FTC_LSTORE(BUF)                                                                            \
-  {                                                                                                \
-    char* qs_ = Ks + KBYTES + (BUF) * SLICE;                                                       \
-    _Pragma("unroll") for (int p = 0; p < NP2; ++p) {                                              \
-      *reinterpret_cast<u32x4*>(qs_ + lds_off<D>(p * RPP2 + lrow, lch)) = qreg[p];                 \
-      *reinterpret_cast<u32x4*>(qs_ + QBYTES + lds_off<D>(p * RPP2 + lrow, lch)) = dreg[p];        \
-    }                                                                                              \
-    if (tid < BQ2) {                                                                               \
-      reinterpret_cast<float*>(qs_ + 2 * QBYTES)[tid] = lreg;                                      \
-      reinterpret_cast<float*>(qs_ + 2 * QBYTES)[BQ2 + tid] = dlreg;                               \
-    }                                                                                              \
-  }
+  // Q / dO / row-constant slices arrive by LDS-DMA (global_load_lds_dwordx4: no staging VGPRs) into a
+  // 3-slot ring, two slices ahead of the compute; one raw barrier per slice with a COUNTED vmcnt so the
+  // next slice's DMA stays in flight across it (guide §5 "Pipelining across barriers").  The swizzled
+  // LDS image is produced by pre-swizzling the per-lane global source (the DMA writes lane-linearly).
+  constexpr int NG = BQ2 * D * 2 / 1024 / 4;  // 1 KiB DMA pieces per wave per matrix (D=128: 2)
+  constexpr int PER_SLICE = 2 * NG + 1;       // DMA instructions per wave per slice (+1: row constants)
+  constexpr int RPG = 1024 / (D * 2);         // rows per 1 KiB piece
+  const float* ls_all = a.delta + (long long)a.B * a.H * S;  // workspace: [-delta | -lse/scale]
+  auto issue = [&](int it_, char* base_) {
+    const int g_ = it_ / nqt, qt_ = qbeg + (it_ % nqt) * BQ2;
+    const int hq_ = kvh * G + g_;
+    const long long row0 = (long long)b * S + qt_;
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {
+      const int r0 = (wave * NG + i) * RPG;
+      const int row = r0 + lane / NCH, pc = lane % NCH;
+      const int lc = (pc ^ swz(row)) & (NCH - 1);
+      const uint16_t* qsrc = a.q + (row0 + row) * a.q_rs + (long long)hq_ * D + lc * 8;
+      const uint16_t* dsrc = a.dout + (row0 + row) * a.do_rs + (long long)hq_ * D + lc * 8;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)qsrc,
+                                       (__attribute__((address_space(3))) void*)(base_ + r0 * D * 2), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)dsrc,
+                                       (__attribute__((address_space(3))) void*)(base_ + QBYTES + r0 * D * 2), 16,
+                                       0, 0);
+    }
+    // lanes 0..31: -lse/scale of the 32 rows, lanes 32..63: -delta (every wave issues the same piece)
+    const long long ridx = ((long long)b * a.H + hq_) * S + qt_ + lr;
+    const float* csrc = hh ? a.delta + ridx : ls_all + ridx;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)csrc,
+                                     (__attribute__((address_space(3))) void*)(base_ + 2 * QBYTES), 4, 0, 0);
+  };
+  constexpr int VM_ONE = 0x0F70 | (PER_SLICE & 15) | ((PER_SLICE >> 4) << 14);  // vmcnt(PER_SLICE)
+  constexpr int VM_ZERO = 0x0F70;                                               // vmcnt(0)
+  constexpr int LGKM_ZERO = 0xC07F;                                             // lgkmcnt(0)
 
   const int total = G * nqt;
-  if (total > 0) {
-    FTC_GLOAD(kvh * G, qbeg);
-    FTC_LSTORE(0);
-  }
-  __syncthreads();  // K and slice 0 staged
-  int cur = 0;
-  for (int it = 0; it < total; ++it) {
+  // K staging and the V fragments are ordinary loads: retire them before the first DMA so no
+  // compiler-inserted wait inside the loop has to count them
+  __builtin_amdgcn_s_waitcnt(VM_ZERO);
+  __syncthreads();  // K staged (no DMA in flight yet: a plain barrier is fine here)
+  if (total > 0) issue(0, slot0);
+  if (total > 1) issue(1, slot1);
+  // slice it computes from slot it % 3 and DMAs slice it + 2 into slot (it + 2) % 3, which held
+  // slice it - 1 (finished by every wave before this slice's barrier)
+  auto body = [&](const int it, const char* Qs, char* dma_slot) __attribute__((always_inline)) {
     const int qt = qbeg + (it % nqt) * BQ2;
-    const bool more = it + 1 < total;
-    const char* Qs = Ks + KBYTES + cur * SLICE;
+    if (it + 1 < total) __builtin_amdgcn_s_waitcnt(VM_ONE);  // slice it landed, it+1 may fly on
+    else __builtin_amdgcn_s_waitcnt(VM_ZERO);
+    __builtin_amdgcn_s_waitcnt(LGKM_ZERO);
+    __builtin_amdgcn_s_barrier();  // every wave's pieces of slice it are in
+    if (it + 2 < total) issue(it + 2, dma_slot);
     const char* Ds = Qs + QBYTES;
     const float* lse_s = reinterpret_cast<const float*>(Ds + QBYTES);
     const float* dlt_s = lse_s + BQ2;
-    if (more) {
-      const int g2 = (it + 1) / nqt, q2 = qbeg + ((it + 1) % nqt) * BQ2;
-      FTC_GLOAD(kvh * G + g2, q2);
+    // ---- S[q][k], dP'[q][k] for both 32-key halves in one k-loop (rows q in registers, key on the
+    // lane): the Q / dO A-fragments are read once for both halves, four independent MFMA chains
+    f32x16 s[2], dp[2];
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const float4 lv = *reinterpret_cast<const float4*>(lse_s + 8 * g4 + 4 * hh);
+      const float4 dv4 = *reinterpret_cast<const float4*>(dlt_s + 8 * g4 + 4 * hh);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        s[j][4 * g4 + 0] = lv.x; s[j][4 * g4 + 1] = lv.y; s[j][4 * g4 + 2] = lv.z; s[j][4 * g4 + 3] = lv.w;
+        dp[j][4 * g4 + 0] = dv4.x; dp[j][4 * g4 + 1] = dv4.y; dp[j][4 * g4 + 2] = dv4.z; dp[j][4 * g4 + 3] = dv4.w;
+      }
     }
-    // ---- per half j: S[q][k], dP'[q][k] (rows q in registers, key on the lane) -> P, dS (bf16)
+#pragma unroll
+    for (int st = 0; st < DSTEPS; ++st) {
+      const u32x4 qa = *reinterpret_cast<const u32x4*>(Qs + lds_off<D>(lr, 2 * st + hh));
+      const u32x4 da = *reinterpret_cast<const u32x4*>(Ds + lds_off<D>(lr, 2 * st + hh));
+      const u32x4 k0 = *reinterpret_cast<const u32x4*>(Ks + lds_off<D>(wave * 64 + lr, 2 * st + hh));
+      const u32x4 k1 = *reinterpret_cast<const u32x4*>(Ks + lds_off<D>(wave * 64 + 32 + lr, 2 * st + hh));
+      s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, qa), __builtin_bit_cast(bf16x8, k0), s[0], 0, 0, 0);
+      s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, qa), __builtin_bit_cast(bf16x8, k1), s[1], 0, 0, 0);
+      dp[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, da), vf[0][st], dp[0], 0, 0, 0);
+      dp[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, da), vf[1][st], dp[1], 0, 0, 0);
+    }
+    // 8 fragment reads (two k-steps) in flight ahead of the MFMA chain
+    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+    for (int i = 0; i < 4 * DSTEPS - 8; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    // ---- P, dS (bf16 B operands of the accumulating products)
     bf16x8 pb[2][2], sb[2][2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      f32x16 s, dp;
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const float4 lv = *reinterpret_cast<const float4*>(lse_s + 8 * g4 + 4 * hh);
-        const float4 dv4 = *reinterpret_cast<const float4*>(dlt_s + 8 * g4 + 4 * hh);
-        s[4 * g4 + 0] = lv.x; s[4 * g4 + 1] = lv.y; s[4 * g4 + 2] = lv.z; s[4 * g4 + 3] = lv.w;
-        dp[4 * g4 + 0] = dv4.x; dp[4 * g4 + 1] = dv4.y; dp[4 * g4 + 2] = dv4.z; dp[4 * g4 + 3] = dv4.w;
-      }
-      const int krow = wave * 64 + 32 * j + lr;
-#pragma unroll
-      for (int st = 0; st < DSTEPS; ++st) {
-        const u32x4 qa = *reinterpret_cast<const u32x4*>(Qs + lds_off<D>(lr, 2 * st + hh));
-        const u32x4 kbv = *reinterpret_cast<const u32x4*>(Ks + lds_off<D>(krow, 2 * st + hh));
-        const u32x4 da = *reinterpret_cast<const u32x4*>(Ds + lds_off<D>(lr, 2 * st + hh));
-        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, qa), __builtin_bit_cast(bf16x8, kbv), s, 0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, da), vf[j][st], dp, 0, 0, 0);
-      }
       const int key = wkey0 + 32 * j + lr;
       const int kmin = wkey0 + 32 * j;
       const bool need_mask = (a.causal && qt < kmin + 31) || (a.window > 0 && qt + BQ2 - 1 - kmin >= a.window);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) s[i] = __builtin_amdgcn_exp2f(a.c * s[i]);
+      for (int i = 0; i < 16; ++i) s[j][i] = __builtin_amdgcn_exp2f(a.c * s[j][i]);
       if (need_mask) {  // wave-uniform; query q = qt + (i&3) + 8(i>>2) + 4hh valid iff key <= q < key + window
         const int base = qt + 4 * hh;
         const int lo = (a.causal ? key : -0x3fffffff) - base;
@@ -269,15 +293,15 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(BwdArgs a) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int off = (i & 3) + 8 * (i >> 2);
-          s[i] = (off >= lo && off <= hi) ? s[i] : 0.f;
+          s[j][i] = (off >= lo && off <= hi) ? s[j][i] : 0.f;
         }
       }
 #pragma unroll
-      for (int i = 0; i < 16; ++i) dp[i] = s[i] * dp[i];
-      pb[j][0] = pack8_bf(s, 0);
-      pb[j][1] = pack8_bf(s, 8);
-      sb[j][0] = pack8_bf(dp, 0);
-      sb[j][1] = pack8_bf(dp, 8);
+      for (int i = 0; i < 16; ++i) dp[j][i] = s[j][i] * dp[j][i];
+      pb[j][0] = pack8_bf(s[j], 0);
+      pb[j][1] = pack8_bf(s[j], 8);
+      sb[j][0] = pack8_bf(dp[j], 0);
+      sb[j][1] = pack8_bf(dp[j], 8);
     }
     // ---- dV^T += dO^T P ; dK^T += Q^T dS for both halves (k of these MFMAs = the 32 query rows);
     // the dO^T / Q^T tr-operands are read once and used by both halves
@@ -296,12 +320,12 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(BwdArgs a) {
         dk[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q1v, sb[j][1], dk[j][dt], 0, 0, 0);
       }
     }
-    if (more) { FTC_LSTORE(cur ^ 1); }
-    __syncthreads();
-    cur ^= 1;
+  };
+  for (int it = 0; it < total; it += 3) {
+    body(it, slot0, slot2);
+    if (it + 1 < total) body(it + 1, slot1, slot0);
+    if (it + 2 < total) body(it + 2, slot2, slot1);
   }
-#undef FTC_GLOAD
-#undef FTC_LSTORE
 
   // ---- epilogue: dK = scale * dK^T^T, dV; lane owns one key row per half
 #pragma unroll
@@ -362,7 +386,7 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
   }
   const long long sidx = ((long long)b * a.H + hq) * S + qrow;
   const float lse2 = a.lse[sidx] * LOG2E;
-  const float dlt = a.delta[sidx];
+  const float ndlt = a.delta[sidx];  // -delta
 
   int kv_end = a.causal ? q0 + BQ : S;
   int kv_begin = 0;
@@ -449,7 +473,7 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) dp[kt][i] = s[kt][i] * (dp[kt][i] - dlt);  // dS^T
+      for (int i = 0; i < 16; ++i) dp[kt][i] = s[kt][i] * (dp[kt][i] + ndlt);  // dS^T
     bf16x8 sb[4];
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) sb[ks] = pack8_bf(dp[ks >> 1], 8 * (ks & 1));
@@ -493,7 +517,7 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
 
 extern "C" int ftc_flash_bwd_workspace(int B, int S, int H, int D, long long* bytes) {
   (void)D;
-  *bytes = (long long)B * H * S * sizeof(float);  // delta
+  *bytes = 2LL * B * H * S * sizeof(float);  // -delta, -lse/scale
   return 0;
 }
 
@@ -507,7 +531,6 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
             lse, (float*)workspace, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, q_rs, kv_rs, o_rs, dq_rs, dkv_rs, do_rs,
             B, S, H, KV, scale, scale * LOG2E, causal, window};
   const int grid_d = ftc::stream_grid((long long)B * S, 4);
-  const size_t lds_kv = (size_t)256 * D * 2 + 2 * (2 * 32 * D * 2 + 2 * 32 * sizeof(float));
   const size_t lds_q = (size_t)4 * 64 * D * 2;
   const int g_kv = B * KV * (S / 256);
   const int g_q = B * H * (S / 128);
@@ -517,17 +540,9 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
     const char* e = getenv("FTC_FLASH_BWD_OCC");
     return (e && e[0] == '1') ? 1 : 2;
   }();
-  static bool attr_set = false;  // dK/dV uses 96.5 KiB of dynamic LDS (> the 64 KiB default)
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)bwd_dkdv_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        256 * 128 * 2 + 2 * (2 * 32 * 128 * 2 + 2 * 32 * 4));
-    (void)hipFuncSetAttribute((const void*)bwd_dkdv_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        256 * 64 * 2 + 2 * (2 * 32 * 64 * 2 + 2 * 32 * 4));
-    attr_set = true;
-  }
   if (D == 128) {
     hipLaunchKernelGGL(bwd_delta_kernel<128>, dim3(grid_d), dim3(256), 0, stream, a);
-    hipLaunchKernelGGL(bwd_dkdv_kernel<128>, dim3(g_kv), dim3(256), lds_kv, stream, a);
+    hipLaunchKernelGGL(bwd_dkdv_kernel<128>, dim3(g_kv), dim3(256), 0, stream, a);
     if (occ == 1) {
       hipLaunchKernelGGL((bwd_dq_kernel<128, 1>), dim3(g_q), dim3(256), lds_q, stream, a);
     } else {
@@ -535,7 +550,7 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
     }
   } else {
     hipLaunchKernelGGL(bwd_delta_kernel<64>, dim3(grid_d), dim3(256), 0, stream, a);
-    hipLaunchKernelGGL(bwd_dkdv_kernel<64>, dim3(g_kv), dim3(256), lds_kv, stream, a);
+    hipLaunchKernelGGL(bwd_dkdv_kernel<64>, dim3(g_kv), dim3(256), 0, stream, a);
     hipLaunchKernelGGL((bwd_dq_kernel<64, 2>), dim3(g_q), dim3(256), lds_q, stream, a);
   }
   return (int)hipGetLastError();
