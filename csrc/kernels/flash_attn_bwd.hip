@@ -355,10 +355,12 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
   constexpr int NCH = D / 8, DSTEPS = D / 16, DT = D / 32;
   constexpr int BQ = 128, BK = 64;
   constexpr int TILE = BK * D * 2;
-  constexpr int RPP = 256 / NCH, NPASS = BK / RPP;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Kb = smem;             // [2][64][D]
-  char* Vb = smem + 2 * TILE;  // [2][64][D]
+  // K/V tiles arrive by LDS-DMA (global_load_lds_dwordx4) into two distinct buffer pairs: no staging
+  // registers (the register-staged version spilled at D=128) and no ds_write pass
+  __shared__ __attribute__((aligned(16))) char Kt0[TILE];
+  __shared__ __attribute__((aligned(16))) char Vt0[TILE];
+  __shared__ __attribute__((aligned(16))) char Kt1[TILE];
+  __shared__ __attribute__((aligned(16))) char Vt1[TILE];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform -> scalar branches
@@ -394,22 +396,21 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
   const int ntiles = (kv_end - kv_begin + BK - 1) / BK;
   const uint16_t* kbase = a.k + (long long)b * S * a.kv_rs + (long long)kvh * D;
   const uint16_t* vbase = a.v + (long long)b * S * a.kv_rs + (long long)kvh * D;
-  const int lrow = tid / NCH, lch = tid % NCH;
-  // register staging in native vectors via macros (HIP's uint4 struct / lambda captures left it in scratch)
-  u32x4 kreg[NPASS], vreg[NPASS];
-  const auto krs = make_rsrc(kbase), vrs = make_rsrc(vbase);
-  const int voff = (lrow * (int)a.kv_rs + lch * 8) * 2;
-  const int pass_bytes = RPP * (int)a.kv_rs * 2;
-  // K and V are staged in two halves (K under the softmax, V under the dQ MFMAs) so only 16 staging
-  // VGPRs are live at any point -- 32 spilled at D=128
-#define FTC_GLOAD(REG, RS, KV0)                                                           \
-  {                                                                                       \
-    const int toff = (KV0) * (int)a.kv_rs * 2;                                            \
-    _Pragma("unroll") for (int p = 0; p < NPASS; ++p) REG[p] = buf_load16(RS, voff, toff + p * pass_bytes); \
-  }
-#define FTC_LSTORE(REG, IMG)                                                              \
-  _Pragma("unroll") for (int p = 0; p < NPASS; ++p)                                       \
-    *reinterpret_cast<u32x4*>((IMG) + lds_off<D>(p * RPP + lrow, lch)) = REG[p];
+  constexpr int NGT = TILE / 1024 / 4;  // 1 KiB DMA pieces per wave per matrix
+  constexpr int RPG = 1024 / (D * 2);  // rows per piece
+  auto issue = [&](int kv0_, char* kdst, char* vdst) {
+#pragma unroll
+    for (int i = 0; i < NGT; ++i) {
+      const int r0 = (wave * NGT + i) * RPG;
+      const int row = r0 + lane / NCH, pc = lane % NCH;
+      const int lc = (pc ^ swz(row)) & (NCH - 1);  // pre-swizzled source, lane-linear destination
+      const long long go = (long long)(kv0_ + row) * a.kv_rs + lc * 8;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(kbase + go),
+                                       (__attribute__((address_space(3))) void*)(kdst + r0 * D * 2), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(vbase + go),
+                                       (__attribute__((address_space(3))) void*)(vdst + r0 * D * 2), 16, 0, 0);
+    }
+  };
 
   f32x16 dq[DT];
 #pragma unroll
@@ -417,19 +418,14 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) dq[t][i] = 0.f;
 
-  if (ntiles > 0) {
-    FTC_GLOAD(kreg, krs, kv_begin);
-    FTC_GLOAD(vreg, vrs, kv_begin);
-    FTC_LSTORE(kreg, Kb);
-    FTC_LSTORE(vreg, Vb);
-  }
-  __syncthreads();
-  int cur = 0;
-  for (int t = 0; t < ntiles; ++t) {
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // retire the Q/dO/lse loads before any DMA (vmcnt(0))
+  if (ntiles > 0) issue(kv_begin, Kt0, Vt0);
+  auto tile = [&](const int t, const char* Kc, const char* Vc, char* Kn, char* Vn) __attribute__((always_inline)) {
     const int kv0 = kv_begin + t * BK;
-    const bool more = t + 1 < ntiles;
-    const char* Kc = Kb + cur * TILE;
-    const char* Vc = Vb + cur * TILE;
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's pieces of tile t landed (vmcnt(0))
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();        // ... everyone's; and tile t-1's buffers are free
+    if (t + 1 < ntiles) issue(kv0 + BK, Kn, Vn);  // flies under this tile's compute
     f32x16 s[2], dp[2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
@@ -477,11 +473,6 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
     bf16x8 sb[4];
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) sb[ks] = pack8_bf(dp[ks >> 1], 8 * (ks & 1));
-    // next tile's K/V loads fly under the dQ MFMAs (the S/dP accumulators are dead by now)
-    if (more) {
-      FTC_GLOAD(kreg, krs, kv0 + BK);
-      FTC_GLOAD(vreg, vrs, kv0 + BK);
-    }
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
       bf16x8 ka[4];
@@ -491,15 +482,11 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[ks], sb[ks], dq[dt], 0, 0, 0);
     }
-    if (more) {
-      FTC_LSTORE(kreg, Kb + (cur ^ 1) * TILE);
-      FTC_LSTORE(vreg, Vb + (cur ^ 1) * TILE);
-    }
-    __syncthreads();
-    cur ^= 1;
+  };
+  for (int t = 0; t < ntiles; t += 2) {
+    tile(t, Kt0, Vt0, Kt1, Vt1);
+    if (t + 1 < ntiles) tile(t + 1, Kt1, Vt1, Kt0, Vt0);
   }
-#undef FTC_GLOAD
-#undef FTC_LSTORE
   uint16_t* op = a.dq + ((long long)b * S + qrow) * a.dq_rs + (long long)hq * D;
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt)
@@ -531,7 +518,6 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
             lse, (float*)workspace, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, q_rs, kv_rs, o_rs, dq_rs, dkv_rs, do_rs,
             B, S, H, KV, scale, scale * LOG2E, causal, window};
   const int grid_d = ftc::stream_grid((long long)B * S, 4);
-  const size_t lds_q = (size_t)4 * 64 * D * 2;
   const int g_kv = B * KV * (S / 256);
   const int g_q = B * H * (S / 128);
   // occupancy variant of the two main kernels: 2 waves/SIMD (256-VGPR budget, spills a few staging
@@ -544,14 +530,14 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
     hipLaunchKernelGGL(bwd_delta_kernel<128>, dim3(grid_d), dim3(256), 0, stream, a);
     hipLaunchKernelGGL(bwd_dkdv_kernel<128>, dim3(g_kv), dim3(256), 0, stream, a);
     if (occ == 1) {
-      hipLaunchKernelGGL((bwd_dq_kernel<128, 1>), dim3(g_q), dim3(256), lds_q, stream, a);
+      hipLaunchKernelGGL((bwd_dq_kernel<128, 1>), dim3(g_q), dim3(256), 0, stream, a);
     } else {
-      hipLaunchKernelGGL((bwd_dq_kernel<128, 2>), dim3(g_q), dim3(256), lds_q, stream, a);
+      hipLaunchKernelGGL((bwd_dq_kernel<128, 2>), dim3(g_q), dim3(256), 0, stream, a);
     }
   } else {
     hipLaunchKernelGGL(bwd_delta_kernel<64>, dim3(grid_d), dim3(256), 0, stream, a);
     hipLaunchKernelGGL(bwd_dkdv_kernel<64>, dim3(g_kv), dim3(256), 0, stream, a);
-    hipLaunchKernelGGL((bwd_dq_kernel<64, 2>), dim3(g_q), dim3(256), lds_q, stream, a);
+    hipLaunchKernelGGL((bwd_dq_kernel<64, 2>), dim3(g_q), dim3(256), 0, stream, a);
   }
   return (int)hipGetLastError();
 }
