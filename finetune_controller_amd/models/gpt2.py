@@ -42,7 +42,8 @@ class GPT2Block(nn.Module):
         p = self.lora[name] if name in self.lora else None
         if p is None:
             return ops.lora_linear(x, W, bias=b)
-        return ops.lora_linear(x, W, p.A, p.B, p.scale, bias=b, blocks=p.blocks)
+        return ops.lora_linear(x, W, p.A, p.B, p.scale, bias=b, blocks=p.blocks,
+                               dropout=p.dropout if self.training else 0.0)
 
     def forward(self, h, B, S):
         cfg = self.cfg

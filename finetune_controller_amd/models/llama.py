@@ -87,7 +87,8 @@ class LlamaLayer(nn.Module):
         W = self.base_weight(name)
         if pair is None:
             return ops.lora_linear(x, W)
-        return ops.lora_linear(x, W, pair.A, pair.B, pair.scale, blocks=pair.blocks, aug=self.aug.get(name))
+        return ops.lora_linear(x, W, pair.A, pair.B, pair.scale, blocks=pair.blocks, aug=self.aug.get(name),
+                               dropout=pair.dropout if self.training else 0.0)
 
     def forward(self, h, delta, rope: ops.RotaryTable, B: int, S: int, positions=None):
         cfg = self.cfg

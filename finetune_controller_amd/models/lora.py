@@ -55,6 +55,7 @@ class LoRAPair(nn.Module):
                  device=None, dtype=torch.bfloat16):
         super().__init__()
         self.r, self.scale = cfg.r, cfg.scale
+        self.dropout = float(cfg.dropout)
         self.in_features = in_features
         self.names: list[str] = []
         blocks, row = [], 0

@@ -109,9 +109,15 @@ class AugWeight:
 
 class _LoRALinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, W, bias, A, B, scale, blocks, aug):
+    def forward(ctx, x, W, bias, A, B, scale, blocks, aug, p_drop=0.0):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
+        mask = None
+        if A is not None and p_drop > 0.0:
+            # LoRA dropout (PEFT semantics: on the adapter input only); the two-GEMM path keeps the
+            # base GEMM on the clean x.  The bool mask is saved; the dropped x is recomputed in backward.
+            mask = torch.rand(x2.shape, device=x2.device, dtype=torch.float32) >= p_drop
+            aug = None
         N, K = W.shape
         # allocate the output in its final shape: the returned tensor must not be a view (RoPE
         # rotates it in place downstream)
@@ -133,7 +139,8 @@ class _LoRALinearFn(torch.autograd.Function):
             else:
                 torch.addmm(bias, x2, W.t(), out=y)
             if A is not None:
-                xa = x2 @ A.t()
+                xin = x2 if mask is None else x2 * mask / (1.0 - p_drop)
+                xa = xin @ A.t()
                 y.addmm_(xa, B.t(), alpha=scale)
         if use_aug:
             # the frozen W shares big's version counter, which the s*B / s*A refreshes bump: keep it
@@ -145,6 +152,7 @@ class _LoRALinearFn(torch.autograd.Function):
             ctx.W = None
         ctx.scale, ctx.blocks, ctx.shp, ctx.has_bias, ctx.aug = scale, blocks, shp, bias is not None, aug
         ctx.aug_fwd = use_aug  # saved xa is s * x A^T
+        ctx.mask, ctx.p_drop = mask, p_drop
         return out
 
     @staticmethod
@@ -173,7 +181,10 @@ class _LoRALinearFn(torch.autograd.Function):
             if need_x:
                 dx = dy2 @ W
                 if dyb is not None:
-                    dx.addmm_(dyb, A, alpha=s)
+                    if ctx.mask is None:
+                        dx.addmm_(dyb, A, alpha=s)
+                    else:
+                        dx.add_((dyb @ A) * ctx.mask, alpha=s / (1.0 - ctx.p_drop))
                 dx = dx.view(ctx.shp)
         if need_w:
             mg = getattr(W, "main_grad", None)
@@ -194,11 +205,12 @@ class _LoRALinearFn(torch.autograd.Function):
             if need_a:
                 if dyb is None:
                     dyb = dy2 @ B
-                dA = torch.mm(dyb.t(), x2).mul_(s)
-        return dx, dW, db, dA, dB, None, None, None
+                xin = x2 if ctx.mask is None else x2 * ctx.mask / (1.0 - ctx.p_drop)
+                dA = torch.mm(dyb.t(), xin).mul_(s)
+        return dx, dW, db, dA, dB, None, None, None, None
 
 
 def lora_linear(x: torch.Tensor, W: torch.Tensor, A: torch.Tensor | None = None, B: torch.Tensor | None = None,
                 scale: float = 1.0, bias: torch.Tensor | None = None, blocks=None,
-                aug: AugWeight | None = None) -> torch.Tensor:
-    return _LoRALinearFn.apply(x, W, bias, A, B, scale, blocks, aug)
+                aug: AugWeight | None = None, dropout: float = 0.0) -> torch.Tensor:
+    return _LoRALinearFn.apply(x, W, bias, A, B, scale, blocks, aug, float(dropout))

@@ -22,6 +22,7 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--method", default="lora", choices=["lora", "qlora", "full"])
     ap.add_argument("--lora-r", type=int, default=16)
     ap.add_argument("--lora-alpha", type=float, default=32.0)
+    ap.add_argument("--lora-dropout", type=float, default=0.0)
     ap.add_argument("--lora-targets", default="q_proj,k_proj,v_proj,o_proj,gate_proj,up_proj,down_proj")
     ap.add_argument("--batch-size", type=int, default=4)
     ap.add_argument("--seq-len", type=int, default=4096)
@@ -53,6 +54,7 @@ def build_parser() -> argparse.ArgumentParser:
 
 def config_from_args(a) -> TrainConfig:
     return TrainConfig(model=a.model, method=a.method, lora_r=a.lora_r, lora_alpha=a.lora_alpha,
+                       lora_dropout=a.lora_dropout,
                        lora_targets=[t.strip() for t in a.lora_targets.split(",") if t.strip()],
                        batch_size=a.batch_size, seq_len=a.seq_len, grad_accum=a.grad_accum, epochs=a.epochs,
                        max_steps=a.max_steps, lr=a.lr, warmup_steps=a.warmup_steps, schedule=a.schedule,

@@ -43,6 +43,7 @@ class TrainConfig:
     method: str = "lora"  # lora | qlora | full
     lora_r: int = 16
     lora_alpha: float = 32.0
+    lora_dropout: float = 0.0
     lora_targets: list[str] = field(default_factory=lambda: ["q_proj", "k_proj", "v_proj", "o_proj", "gate_proj",
                                                               "up_proj", "down_proj"])
     batch_size: int = 4  # micro-batch per GPU
@@ -76,7 +77,8 @@ class TrainConfig:
     def lora_config(self) -> LoRAConfig | None:
         if self.method not in ("lora", "qlora"):
             return None
-        return LoRAConfig(r=self.lora_r, alpha=self.lora_alpha, target_modules=list(self.lora_targets))
+        return LoRAConfig(r=self.lora_r, alpha=self.lora_alpha, dropout=self.lora_dropout,
+                          target_modules=list(self.lora_targets))
 
 
 class Trainer:

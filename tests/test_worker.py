@@ -351,3 +351,26 @@ def test_ddp_gloo_two_ranks_matches_single_process(tmp_path):
         grads.append(tr.opt.grad_flat.detach().clone())
         tr.close()
     torch.testing.assert_close(g0, grads[0] + grads[1], atol=1e-5, rtol=1e-4)
+
+
+def test_lora_dropout_matches_autograd_reference():
+    """PEFT-style LoRA dropout (adapter input only): output and all grads against autograd on the same
+    mask (same RNG draw)."""
+    torch.manual_seed(0)
+    x = torch.randn(7, 16, requires_grad=True)
+    W = torch.randn(12, 16)
+    A = torch.randn(4, 16, requires_grad=True)
+    B = torch.randn(12, 4, requires_grad=True)
+    p = 0.3
+    torch.manual_seed(123)
+    y = ops.lora_linear(x, W, A, B, 0.5, dropout=p)
+    torch.manual_seed(123)
+    mask = torch.rand(7, 16) >= p
+    x2, A2, B2 = (t.detach().clone().requires_grad_(True) for t in (x, A, B))
+    ref = x2 @ W.t() + 0.5 * ((x2 * mask / (1 - p)) @ A2.t()) @ B2.t()
+    torch.testing.assert_close(y, ref)
+    g = torch.randn_like(y)
+    y.backward(g)
+    ref.backward(g)
+    for a_, b_ in ((x.grad, x2.grad), (A.grad, A2.grad), (B.grad, B2.grad)):
+        torch.testing.assert_close(a_, b_)
