@@ -237,10 +237,20 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[kt][i]);
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * c;  // c > 0: max commutes with the scale
-    const float mn = fmaxf(m, mt);
-    const float mref = (mn == -INFINITY) ? 0.f : mn;
-    const float alpha = __builtin_amdgcn_exp2f(m - mref);
-    m = mn;
+    // deferred rescale (guide T13): the running reference m moves -- and O, l are rescaled -- only
+    // when some row's max grew by more than 2^8; otherwise P <= 256 (exact in bf16's exponent range,
+    // fp32 accumulation) and the 64 multiplies of O are skipped.  Wave-uniform branch.
+    if (__builtin_amdgcn_ballot_w64(mt > m + 8.0f) != 0) {
+      const float mn = fmaxf(m, mt);
+      const float alpha = __builtin_amdgcn_exp2f(m - ((mn == -INFINITY) ? 0.f : mn));
+      m = mn;
+      l *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+    }
+    const float mref = (m == -INFINITY) ? 0.f : m;
     float rs = 0.f;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
@@ -250,11 +260,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
         s[kt][i] = p;
         rs += p;
       }
-    l = l * alpha + rs;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+    l += rs;
 
     // ---- O^T += V^T P^T : 4 k-steps of 16 keys
     bf16x8 pf[4];
