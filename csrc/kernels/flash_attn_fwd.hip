@@ -23,6 +23,8 @@
 // placed on the same XCD (blockIdx % 8 group) so their K/V tiles are L2 hits.
 #include "common.h"
 
+#include <cstdlib>
+
 using namespace ftc;
 
 namespace {
@@ -31,7 +33,8 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-constexpr int BQ = 128;  // query rows per workgroup
+// query rows per workgroup = 32 x waves (WAVES = 4: 256 threads, two workgroups per CU; WAVES = 8: 512
+// threads, one workgroup per CU sharing every K/V tile between twice the query rows)
 constexpr int BK = 64;   // keys per tile
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
@@ -91,12 +94,14 @@ FTC_DEV void decode_block(const FwdArgs& a, int& qb, int& b, int& hq, int& kvh) 
   hq = kvh * G + g;
 }
 
-template <int D>
-__global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
+template <int D, int WAVES>
+__global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArgs a) {
+  constexpr int BQ = 32 * WAVES;
+  constexpr int NT = 64 * WAVES;       // threads
   constexpr int NCH = D / 8;           // 16-byte chunks per row
   constexpr int DSTEPS = D / 16;       // k-steps of the S MFMA
   constexpr int DT = D / 32;           // 32-wide d tiles of O
-  constexpr int RPP = 256 / NCH;       // rows loaded per pass
+  constexpr int RPP = NT / NCH;        // rows loaded per pass
   constexpr int NPASS = BK / RPP;      // passes per tile
   constexpr int TILE_BYTES = BK * D * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -112,6 +117,7 @@ __global__ __launch_bounds__(256, 2) void flash_fwd_kernel(FwdArgs a) {
   const int q0 = qb * BQ;
   const int qrow = q0 + wave * 32 + lr;
   const bool qvalid = qrow < S;
+  static_assert(BQ == 32 * WAVES, "geometry");
 
   // ---- Q^T fragments (B operand of S^T = K Q^T): lane holds Q[qrow][16s + 8hh .. +8)
   bf16x8 qf[DSTEPS];
@@ -319,13 +325,25 @@ extern "C" int ftc_flash_fwd(const void* q, const void* k, const void* v, void* 
                              int KV, int D, long long q_rs, long long kv_rs, long long o_rs, float scale, int causal,
                              int window, hipStream_t stream) {
   if (S % BK != 0 || H % KV != 0 || (D != 128 && D != 64)) return -1;
+  static const int waves = [] {
+    const char* e = getenv("FTC_FLASH_FWD_WAVES");
+    return (e && e[0] == '8') ? 8 : 4;
+  }();
+  const int BQ = 32 * waves;
   FwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, q_rs, kv_rs, o_rs,
             B, S, H, KV, (S + BQ - 1) / BQ, scale * LOG2E, causal, window};
   const int nblocks = a.nqb * B * H;
   const size_t lds = (size_t)4 * BK * D * 2;
-  if (D == 128)
-    hipLaunchKernelGGL(flash_fwd_kernel<128>, dim3(nblocks), dim3(256), lds, stream, a);
-  else
-    hipLaunchKernelGGL(flash_fwd_kernel<64>, dim3(nblocks), dim3(256), lds, stream, a);
+  if (waves == 8) {
+    if (D == 128)
+      hipLaunchKernelGGL((flash_fwd_kernel<128, 8>), dim3(nblocks), dim3(512), lds, stream, a);
+    else
+      hipLaunchKernelGGL((flash_fwd_kernel<64, 8>), dim3(nblocks), dim3(512), lds, stream, a);
+  } else {
+    if (D == 128)
+      hipLaunchKernelGGL((flash_fwd_kernel<128, 4>), dim3(nblocks), dim3(256), lds, stream, a);
+    else
+      hipLaunchKernelGGL((flash_fwd_kernel<64, 4>), dim3(nblocks), dim3(256), lds, stream, a);
+  }
   return (int)hipGetLastError();
 }

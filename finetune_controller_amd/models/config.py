@@ -112,6 +112,8 @@ PRESETS: dict[str, ModelConfig] = {
     "llama-tiny": ModelConfig("llama", 512, 128, 2, 4, 2, 256, 512, 500000.0, name="llama-tiny"),
     "mistral-tiny": ModelConfig("llama", 384, 128, 2, 4, 2, 256, 512, 10000.0, sliding_window=64, name="mistral-tiny"),
     "gpt2-tiny": ModelConfig("gpt2", 515, 128, 2, 4, 4, 512, 256, tie_embeddings=True, name="gpt2-tiny"),
+    # Llama-3 attention geometry (head_dim 128, GQA 2:1) at toy width: exercises every HIP kernel in smoke()
+    "llama-smoke": ModelConfig("llama", 1024, 512, 2, 4, 2, 1024, 1024, 500000.0, name="llama-smoke"),
     # a 1-layer member of the exact Llama-3-8B width, for kernel/GEMM-shape smoke tests on the GPU
     "llama3-8b-1l": ModelConfig("llama", 128256, 4096, 1, 32, 8, 14336, 8192, 500000.0, name="llama3-8b-1l"),
 }

@@ -37,6 +37,12 @@ for s in "${STEPS[@]}"; do
     attn)
       timeout -k 10 300 python tools/bench_attention.py > gpurun_out/bench_attn.log 2>&1
       fatal $? attn; tail -2 gpurun_out/bench_attn.log ;;
+    attn_w8)
+      FTC_FLASH_FWD_WAVES=8 timeout -k 10 300 python tools/bench_attention.py > gpurun_out/bench_attn_w8.log 2>&1
+      fatal $? attn_w8; tail -2 gpurun_out/bench_attn_w8.log ;;
+    flash_w8)
+      FTC_FLASH_FWD_WAVES=8 timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py -m gpu -x -q -k "flash or llama_lora" > gpurun_out/pytest_flash_w8.log 2>&1
+      fatal $? flash_w8; tail -3 gpurun_out/pytest_flash_w8.log ;;
     attn_occ2)
       FTC_FLASH_BWD_OCC=2 timeout -k 10 300 python tools/bench_attention.py > gpurun_out/bench_attn_occ2.log 2>&1
       fatal $? attn_occ2; tail -2 gpurun_out/bench_attn_occ2.log ;;
