@@ -184,6 +184,8 @@ def save_full(model, out_dir: str, shard_bytes: int = 5 * 1024**3, merge_lora: b
     finally:
         for l, name, pair in merged:  # keep training state unmerged
             merge_pair_into(l.base_weight(name).data, pair, -1.0)
+        if merged and hasattr(model, "invalidate_transposed"):
+            model.invalidate_transposed()  # merge/unmerge round-trips W through bf16
 
 
 @torch.no_grad()
@@ -201,6 +203,8 @@ def load_hf_checkpoint(model, path: str) -> int:
             dst = targets[k]
             dst.copy_(v.to(dst.dtype))
             n += 1
+    if hasattr(model, "invalidate_transposed"):
+        model.invalidate_transposed()
     return n
 
 

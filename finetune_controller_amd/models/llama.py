@@ -138,6 +138,16 @@ class LlamaForCausalLM(nn.Module):
         for layer in self.layers:
             for pair in layer.lora.values():
                 pair.reset_parameters()
+        self.invalidate_transposed()
+
+    def invalidate_transposed(self):
+        """Base weights were rewritten: drop the transposed backward copies (ops.linear TN layout)."""
+        from ..ops.linear import frozen_t
+
+        for layer in self.layers:
+            for aw in layer.aug.values():
+                aw.invalidate()
+        frozen_t.clear()
 
     def freeze_base(self):
         """LoRA/QLoRA: only adapter parameters train."""

@@ -53,6 +53,12 @@ class _FusedLinearCE(torch.autograd.Function):
             dW = torch.zeros(W.shape, dtype=torch.float32, device=W.device)
         losses = torch.empty(T, dtype=torch.float32, device=h2.device)
         buf = None
+        # frozen head (LoRA / QLoRA): dh = dlogits . W through a cached W^T (TN GEMM layout, ~15 % faster)
+        WT = None
+        if need_dh and hip and not W.requires_grad:
+            from .linear import _TN_BWD, frozen_t
+
+            WT = frozen_t.get(W) if _TN_BWD else None
         for r0 in range(0, T, chunk_rows):
             r1 = min(T, r0 + chunk_rows)
             hc = h2[r0:r1]
@@ -69,7 +75,7 @@ class _FusedLinearCE(torch.autograd.Function):
                 l, dlog = _ce_chunk_ref(logits, labc, gscale, ignore_index)
                 losses[r0:r1] = l
             if need_dh:
-                torch.mm(dlog, W, out=dh[r0:r1])
+                torch.mm(dlog, W if WT is None else WT.t(), out=dh[r0:r1])
             if need_dw:
                 if mg is not None:
                     mg.addmm_(dlog.t(), hc)

@@ -70,6 +70,31 @@ def _tail(t: torch.Tensor, width: int, extra: int) -> torch.Tensor:
 # PyTorch TunableOp assumes ldc == n for GEMM outputs: under it the spare-column products go through
 # a contiguous temporary (two tiny copies per call) instead of being written in place
 _TUNABLEOP = os.environ.get("PYTORCH_TUNABLEOP_ENABLED", "0") == "1"
+_TN_BWD = os.environ.get("FTC_TN_BWD", "1") != "0"  # transposed frozen-weight copies for backward GEMMs
+
+
+class FrozenTransposed:
+    """Cache of ``W^T`` (contiguous) for frozen 2-D weights used as the right operand of ``x @ W`` in a
+    backward pass (TN layout, see AugWeight.bwd_operand).  Keyed by the parameter; rebuilt when the
+    parameter's version counter moves (in-place loads / init)."""
+
+    def __init__(self):
+        self._c: dict[int, tuple] = {}
+
+    def get(self, W: torch.Tensor) -> torch.Tensor:
+        key = id(W)
+        hit = self._c.get(key)
+        if hit is not None and hit[0] == W.data_ptr() and hit[1] == W._version:
+            return hit[2]
+        WT = W.detach().t().contiguous()
+        self._c[key] = (W.data_ptr(), W._version, WT)
+        return WT
+
+    def clear(self):
+        self._c.clear()
+
+
+frozen_t = FrozenTransposed()
 
 
 def _mm_into(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor):
@@ -105,6 +130,25 @@ class AugWeight:
         N, K, R = self.N, self.K, self.R
         self.big[:N, K:K + R].copy_(B)
         torch.mul(A, scale, out=self.big[N:N + R, :K])
+
+    # ---- backward operand in the "TN" layout.  hipBLASLt runs dx = [dy | dyB] . [W ; sA] 14-16 %
+    # faster when the right operand is stored K-contiguous (tools/bench_gemm_layouts.py), so a
+    # transposed copy bigT [K, N+Rp] of the frozen weight is kept (HBM is plentiful: +2 B/param).
+    # It is rebuilt lazily after invalidate() -- called wherever the base weight is rewritten
+    # (init_weights, HF checkpoint load, LoRA merge/unmerge).
+    bigT: torch.Tensor | None = None
+
+    def invalidate(self):
+        self.bigT = None
+
+    def bwd_operand(self, A: torch.Tensor, scale: float) -> torch.Tensor:
+        """[N+Rp, K] view of [W ; s A ; 0] with unit stride along N+Rp (column-major for the GEMM)."""
+        N, K, R = self.N, self.K, self.R
+        if self.bigT is None:
+            self.bigT = torch.zeros(K, N + self.Rp, device=self.big.device, dtype=self.big.dtype)
+            self.bigT[:, :N].copy_(self.big[:N, :K].t())
+        self.bigT[:, N:N + R].copy_((A * scale).t())
+        return self.bigT.t()
 
 
 class _LoRALinearFn(torch.autograd.Function):
@@ -174,7 +218,8 @@ class _LoRALinearFn(torch.autograd.Function):
             aug.refresh(A, B, s)
             _mm_into(dy2, aug.big[:N, aug.K:], _tail(dy2, N, Rp))
             dyb = _tail(dy2, N, aug.R)
-            dx = torch.mm(_wide(dy2, N + Rp), aug.big[:, :aug.K]).view(ctx.shp)
+            rhs = aug.bwd_operand(A, s) if _TN_BWD else aug.big[:, :aug.K]
+            dx = torch.mm(_wide(dy2, N + Rp), rhs).view(ctx.shp)
         else:
             if A is not None and (need_x or need_a):
                 dyb = dy2 @ B  # [T, R]
