@@ -40,6 +40,9 @@ int ftc_flash_bwd(const void* q, const void* k, const void* v, const void* o, co
 int ftc_nf4_dequant(const uint8_t* packed, const uint8_t* absmax_q, const float* absmax_scale, float absmax_offset,
                     void* out, long long n, int block, int block2, hipStream_t stream);
 int ftc_nf4_quant(const void* w, uint8_t* packed, float* absmax, long long n, int block, hipStream_t stream);
+int ftc_nf4_dequant_into(const uint8_t* packed, const uint8_t* absmax_q, const float* absmax_scale,
+                         float absmax_offset, void* out, int rows, int cols, long long ldo, int block, int block2,
+                         int transpose, hipStream_t stream);
 int ftc_nf4_gemm(const void* x, const uint8_t* packed, const uint8_t* absmax_q, const float* absmax_scale,
                  float absmax_offset, void* y, int M, int N, int K, int block, int block2, hipStream_t stream);
 int ftc_lora_merge(void* w, const void* a, const void* b, int out_f, int in_f, int r, int seg_rows, float scale,
@@ -325,6 +328,25 @@ at::Tensor nf4_dequantize(const at::Tensor& packed, const at::Tensor& absmax_q, 
   return out;
 }
 
+// dequantise W [rows, cols] into a row view `out` (row stride out.stride(0)); transpose=True writes W^T
+// into a [cols, >= rows] view (the TN backward operand)
+void nf4_dequantize_into(const at::Tensor& packed, const at::Tensor& absmax_q, const at::Tensor& absmax_scale,
+                         double absmax_offset, at::Tensor& out, int64_t rows, int64_t cols, int64_t block,
+                         int64_t block2, bool transpose) {
+  need(packed, at::kByte, "packed");
+  need(absmax_q, at::kByte, "absmax_q");
+  need(absmax_scale, at::kFloat, "absmax_scale");
+  need(out, at::kBFloat16, "out");
+  TORCH_CHECK(packed.numel() * 2 == rows * cols && absmax_q.numel() * block == rows * cols, "nf4_dequantize_into: sizes");
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.stride(0) % 8 == 0, "nf4_dequantize_into: out row view");
+  TORCH_CHECK(transpose ? (out.size(0) == cols && out.size(1) >= rows) : (out.size(0) == rows && out.size(1) >= cols),
+              "nf4_dequantize_into: out shape");
+  check(ftc_nf4_dequant_into(packed.data_ptr<uint8_t>(), absmax_q.data_ptr<uint8_t>(), absmax_scale.data_ptr<float>(),
+                             (float)absmax_offset, out.data_ptr(), (int)rows, (int)cols, out.stride(0), (int)block,
+                             (int)block2, transpose ? 1 : 0, cur_stream()),
+        "nf4_dequant_into");
+}
+
 // y[M,N] = x[M,K] @ dequant(W)[N,K]^T  with the NF4 decode fused into the MFMA operand load
 at::Tensor nf4_linear(const at::Tensor& x, const at::Tensor& packed, const at::Tensor& absmax_q,
                       const at::Tensor& absmax_scale, double absmax_offset, int64_t N, int64_t block, int64_t block2) {
@@ -380,4 +402,5 @@ PYBIND11_MODULE(_C, m) {
   m.def("nf4_linear", &nf4_linear);
   m.def("lora_merge_", &lora_merge_);
   m.def("nf4_gemm_ready", [] { return true; });
+  m.def("nf4_dequantize_into", &nf4_dequantize_into);
 }

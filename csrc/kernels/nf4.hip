@@ -86,6 +86,94 @@ __global__ __launch_bounds__(256) void nf4_dequant_kernel(const uint8_t* __restr
   }
 }
 
+// dequantise into a row view: out[n * ldo + k] (a column block of an augmented GEMM operand)
+__global__ __launch_bounds__(256) void nf4_dequant_rows_kernel(const uint8_t* __restrict__ packed,
+                                                               const uint8_t* __restrict__ aq,
+                                                               const float* __restrict__ s2, float off,
+                                                               uint16_t* __restrict__ out, long long n, int cols,
+                                                               long long ldo, int block, int block2) {
+  const long long n16 = n >> 4;
+  const int c16 = cols >> 4;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long long)gridDim.x * 256) {
+    const uint2 p = reinterpret_cast<const uint2*>(packed)[i];
+    const long long e0 = i << 4;
+    const long long bi = e0 / block;
+    const float a = off + ((float)aq[bi] - 128.0f) * (1.0f / 127.0f) * s2[bi / block2];
+    float f[16];
+    const uint32_t words[2] = {p.x, p.y};
+#pragma unroll
+    for (int wd = 0; wd < 2; ++wd)
+#pragma unroll
+      for (int bt = 0; bt < 4; ++bt) {
+        const uint32_t byte = (words[wd] >> (8 * bt)) & 0xffu;
+        f[wd * 8 + bt * 2] = kNF4[byte >> 4] * a;
+        f[wd * 8 + bt * 2 + 1] = kNF4[byte & 0xf] * a;
+      }
+    const long long row = i / c16;
+    const int c = (int)(i - row * c16) * 16;
+    uint4* o = reinterpret_cast<uint4*>(out + row * ldo + c);
+    o[0] = pack8(f);
+    o[1] = pack8(f + 8);
+  }
+}
+
+// dequantise TRANSPOSED: outT[k * ldo + n] = W[n][k] -- the K-contiguous right operand of the backward
+// GEMM dx = dy . W (TN layout).  A 64 x 64 tile per workgroup, transposed through LDS; one NF4 block
+// (64 along k) per row of the tile, so one absmax per thread.
+__global__ __launch_bounds__(256) void nf4_dequant_t_kernel(const uint8_t* __restrict__ packed,
+                                                            const uint8_t* __restrict__ aq,
+                                                            const float* __restrict__ s2, float off,
+                                                            uint16_t* __restrict__ outT, int N, int K, long long ldo,
+                                                            int block2) {
+  __shared__ uint16_t tile[64][64 + 2];
+  const int n0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
+  const int t = threadIdx.x;
+  {
+    const int nl = t >> 2, kq = (t & 3) * 16;
+    const long long e0 = (long long)(n0 + nl) * K + k0 + kq;
+    const uint2 p = *reinterpret_cast<const uint2*>(packed + (e0 >> 1));
+    const long long bi = e0 >> 6;  // block 64
+    const float a = off + ((float)aq[bi] - 128.0f) * (1.0f / 127.0f) * s2[bi / block2];
+    const uint32_t words[2] = {p.x, p.y};
+#pragma unroll
+    for (int wd = 0; wd < 2; ++wd)
+#pragma unroll
+      for (int bt = 0; bt < 4; ++bt) {
+        const uint32_t byte = (words[wd] >> (8 * bt)) & 0xffu;
+        const int kk = kq + wd * 8 + bt * 2;
+        tile[kk][nl] = f2bf(kNF4[byte >> 4] * a);
+        tile[kk + 1][nl] = f2bf(kNF4[byte & 0xf] * a);
+      }
+  }
+  __syncthreads();
+  {
+    const int kl = t >> 2, np = (t & 3) * 16;
+    uint32_t w[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = (uint32_t)tile[kl][np + 2 * j] | ((uint32_t)tile[kl][np + 2 * j + 1] << 16);
+    uint4* o = reinterpret_cast<uint4*>(outT + (long long)(k0 + kl) * ldo + n0 + np);
+    o[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    o[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  }
+}
+
+extern "C" int ftc_nf4_dequant_into(const uint8_t* packed, const uint8_t* absmax_q, const float* absmax_scale,
+                                    float absmax_offset, void* out, int rows, int cols, long long ldo, int block,
+                                    int block2, int transpose, hipStream_t stream) {
+  if (cols % 64 != 0 || block != 64 || ldo % 8 != 0) return -1;
+  if (transpose) {
+    if (rows % 64 != 0) return -1;
+    hipLaunchKernelGGL(nf4_dequant_t_kernel, dim3(rows / 64, cols / 64), dim3(256), 0, stream, packed, absmax_q,
+                       absmax_scale, absmax_offset, (uint16_t*)out, rows, cols, ldo, block2);
+  } else {
+    const long long n = (long long)rows * cols;
+    const int grid = ftc::stream_grid(n / 16, 256);
+    hipLaunchKernelGGL(nf4_dequant_rows_kernel, dim3(grid), dim3(256), 0, stream, packed, absmax_q, absmax_scale,
+                       absmax_offset, (uint16_t*)out, n, cols, ldo, block, block2);
+  }
+  return (int)hipGetLastError();
+}
+
 extern "C" int ftc_nf4_quant(const void* w, uint8_t* packed, float* absmax, long long n, int block,
                              hipStream_t stream) {
   if (block % 2 != 0 || n % block != 0) return -1;

@@ -69,10 +69,13 @@ class LlamaLayer(nn.Module):
 
     def pad(self, name: str) -> int:
         """Spare columns the producer of this projection's input (and of its output gradient) adds."""
-        aw = self.aug.get(name)
-        if aw is None or name in self.qweights or not aw.owns(self.base_weight(name)):
-            return 0
         if os.environ.get("FTC_LORA_AUG", "1") == "0":  # A/B switch: two-GEMM LoRA path
+            return 0
+        if name in self.qweights:  # QLoRA: the NF4 path augments its dequantised operand the same way
+            pair = self.lora[name] if name in self.lora else None
+            return -(-pair.A.shape[0] // AugWeight.TILE) * AugWeight.TILE if pair is not None else 0
+        aw = self.aug.get(name)
+        if aw is None or not aw.owns(self.base_weight(name)):
             return 0
         return aw.Rp
 
@@ -82,8 +85,8 @@ class LlamaLayer(nn.Module):
         if qw is not None:
             from ..ops.nf4 import qlora_linear
 
-            return qlora_linear(x.contiguous(), qw, pair.A if pair else None, pair.B if pair else None,
-                                pair.scale if pair else 1.0, pair.blocks if pair else None)
+            return qlora_linear(x, qw, pair.A if pair else None, pair.B if pair else None,
+                                pair.scale if pair else 1.0, pair.blocks if pair else None, pad=self.pad(name))
         W = self.base_weight(name)
         if pair is None:
             return ops.lora_linear(x, W)

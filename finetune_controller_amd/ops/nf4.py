@@ -22,7 +22,7 @@ from __future__ import annotations
 import torch
 
 from ._backend import ext, use_hip
-from .linear import _mask_blocks
+from .linear import _mask_blocks, _mm_into, _spare_cols, _tail, _wide
 
 NF4_CODE = torch.tensor([-1.0, -0.6961928009986877, -0.5250730514526367, -0.39491748809814453, -0.28444138169288635,
                          -0.18477343022823334, -0.09105003625154495, 0.0, 0.07958029955625534, 0.16093020141124725,
@@ -106,44 +106,116 @@ def nf4_matmul(x2: torch.Tensor, qw: NF4Weight) -> torch.Tensor:
     return x2 @ W.t()
 
 
+class _QScratch:
+    """Per-shape bf16 scratch for the augmented QLoRA GEMMs (shared by every layer of that shape --
+    layers run one after another on the stream, nothing here outlives a call):
+    ``fwd [N+Rp, K+Rp] = [[W | B 0], [s A ; 0 | 0]]`` and ``bwdT [K, N+Rp] = [W^T | (s A)^T 0]``."""
+
+    _cache: dict = {}
+
+    def __init__(self, N, K, Rp, device):
+        self.fwd = torch.zeros(N + Rp, K + Rp, dtype=torch.bfloat16, device=device)
+        self.bwdT = torch.zeros(K, N + Rp, dtype=torch.bfloat16, device=device)
+        self.Bp = torch.zeros(N, Rp, dtype=torch.bfloat16, device=device)
+
+    @classmethod
+    def get(cls, N, K, Rp, device):
+        key = (N, K, Rp, str(device))
+        sc = cls._cache.get(key)
+        if sc is None:
+            sc = cls._cache[key] = cls(N, K, Rp, device)
+        return sc
+
+
+def _dequant_into(qw: NF4Weight, out: torch.Tensor, transpose: bool):
+    ext().nf4_dequantize_into(qw.packed, qw.absmax_q, qw.absmax_scale, qw.absmax_offset, out, qw.shape[0],
+                              qw.shape[1], qw.block, qw.block2, transpose)
+
+
 class _QLoRALinearFn(torch.autograd.Function):
+    """y = x dequant(W)^T + s (x A^T) B^T with W in NF4.  On the GPU (LoRA present, padded producer
+    buffers) the same augmented GEMMs as ops.linear run: the weight is dequantised straight into the
+    augmented operand, and for the backward into its transposed (TN) form, so neither the rank-r
+    read-modify-writes nor a separate transpose pass exist."""
+
     @staticmethod
-    def forward(ctx, x, A, B, qw, scale, blocks):
+    def forward(ctx, x, A, B, qw, scale, blocks, Rp):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
-        y = nf4_matmul(x2, qw)
+        N, K = qw.shape
+        use_aug = (A is not None and Rp > 0 and use_hip(x2) and x2.dtype == torch.bfloat16
+                   and x2.shape[0] > FUSED_MAX_ROWS and K % 64 == 0 and N % 64 == 0 and qw.block == 64
+                   and _spare_cols(x2, K, Rp))
         xa = None
-        if A is not None:
-            xa = x2 @ A.t()
-            y.addmm_(xa, B.t(), alpha=scale)
+        if use_aug:
+            R = A.shape[0]
+            sc = _QScratch.get(N, K, Rp, x2.device)
+            _dequant_into(qw, sc.fwd[:N, :K], False)
+            sc.fwd[:N, K:K + R].copy_(B)
+            torch.mul(A, scale, out=sc.fwd[N:N + R, :K])
+            _mm_into(x2, sc.fwd[N:, :K].t(), _tail(x2, K, Rp))
+            xa = _tail(x2, K, R)  # s * x A^T
+            y = torch.mm(_wide(x2, K + Rp), sc.fwd[:N].t())
+        else:
+            y = nf4_matmul(x2 if x2.is_contiguous() else x2.contiguous(), qw)
+            if A is not None:
+                xa = x2 @ A.t()
+                y.addmm_(xa, B.t(), alpha=scale)
         ctx.save_for_backward(x2, A, B, xa)
-        ctx.qw, ctx.scale, ctx.blocks, ctx.shp = qw, scale, blocks, shp
+        ctx.qw, ctx.scale, ctx.blocks, ctx.shp, ctx.Rp, ctx.aug_fwd = qw, scale, blocks, shp, Rp, use_aug
         return y if x.dim() == 2 else y.reshape(*shp[:-1], qw.shape[0]).clone()
 
     @staticmethod
     def backward(ctx, dy):
         x2, A, B, xa = ctx.saved_tensors
         s = ctx.scale
+        qw = ctx.qw
+        N, K = qw.shape
+        Rp = ctx.Rp
         dy2 = dy.reshape(-1, dy.shape[-1])
-        dx = dA = dB = None
-        dyb = dy2 @ B if A is not None else None
+        dx = dA = dB = dyb = None
+        hip = use_hip(dy2) and dy2.dtype == torch.bfloat16 and qw.block == 64 and K % 64 == 0 and N % 64 == 0
         if ctx.needs_input_grad[0]:
-            W = ctx.qw.dequantize(dy2.dtype)
-            dx = dy2 @ W
-            del W
-            if dyb is not None:
-                dx.addmm_(dyb, A, alpha=s)
+            if hip and A is not None and Rp > 0 and _spare_cols(dy2, N, Rp):
+                R = A.shape[0]
+                sc = _QScratch.get(N, K, Rp, dy2.device)
+                sc.Bp[:, :R].copy_(B)
+                _mm_into(dy2, sc.Bp, _tail(dy2, N, Rp))
+                dyb = _tail(dy2, N, R)
+                _dequant_into(qw, sc.bwdT[:, :N], True)
+                sc.bwdT[:, N:N + R].copy_((A * s).t())
+                dx = torch.mm(_wide(dy2, N + Rp), sc.bwdT.t())
+            elif hip:
+                sc = _QScratch.get(N, K, 64, dy2.device)
+                _dequant_into(qw, sc.bwdT[:, :N], True)  # TN operand even without LoRA spare columns
+                dx = torch.mm(dy2, sc.bwdT[:, :N].t())
+                if A is not None:
+                    dyb = dy2 @ B
+                    dx.addmm_(dyb, A, alpha=s)
+            else:
+                W = qw.dequantize(dy2.dtype)
+                dx = dy2 @ W
+                del W
+                if A is not None:
+                    dyb = dy2 @ B
+                    dx.addmm_(dyb, A, alpha=s)
             dx = dx.view(ctx.shp)
         if A is not None:
             if ctx.needs_input_grad[2]:
-                dB = _mask_blocks(torch.mm(dy2.t(), xa) * s, ctx.blocks)
+                dB = torch.mm(dy2.t(), xa)
+                if not ctx.aug_fwd:
+                    dB.mul_(s)
+                dB = _mask_blocks(dB, ctx.blocks)
             if ctx.needs_input_grad[1]:
-                dA = torch.mm(dyb.t(), x2) * s
-        return dx, dA, dB, None, None, None
+                if dyb is None:
+                    dyb = dy2 @ B
+                dA = torch.mm(dyb.t(), x2).mul_(s)
+        return dx, dA, dB, None, None, None, None
 
 
-def qlora_linear(x, qw: NF4Weight, A=None, B=None, scale=1.0, blocks=None):
-    return _QLoRALinearFn.apply(x, A, B, qw, scale, blocks)
+def qlora_linear(x, qw: NF4Weight, A=None, B=None, scale=1.0, blocks=None, pad: int = 0):
+    """``pad``: spare columns the producer of ``x`` (and of the output gradient) provides."""
+    return _QLoRALinearFn.apply(x, A, B, qw, scale, blocks, int(pad))
 
 
 @torch.no_grad()

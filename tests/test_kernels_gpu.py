@@ -292,3 +292,60 @@ def test_nf4_fused_gemm_matches_dequant(C, M):
     torch.testing.assert_close(y.float(), ref, atol=2e-2, rtol=2e-2)
     # the ops-level dispatcher takes the fused path at this M
     torch.testing.assert_close(nf4.nf4_matmul(x, qw).float(), ref, atol=2e-2, rtol=2e-2)
+
+
+def test_nf4_dequantize_into_rows_and_transposed(C):
+    from finetune_controller_amd.ops import nf4
+
+    torch.manual_seed(3)
+    N, K = 192, 320
+    qw = nf4.NF4Weight.quantize(bf(torch.randn(N, K, device=DEV) * 0.05))
+    ref = qw.dequantize()
+    buf = torch.full((N, K + 64), 7.0, device=DEV, dtype=torch.bfloat16)
+    C.nf4_dequantize_into(qw.packed, qw.absmax_q, qw.absmax_scale, qw.absmax_offset, buf[:, :K], N, K, 64,
+                          qw.block2, False)
+    assert torch.equal(buf[:, :K], ref) and (buf[:, K:] == 7.0).all()
+    bufT = torch.full((K, N + 64), 7.0, device=DEV, dtype=torch.bfloat16)
+    C.nf4_dequantize_into(qw.packed, qw.absmax_q, qw.absmax_scale, qw.absmax_offset, bufT[:, :N], N, K, 64,
+                          qw.block2, True)
+    assert torch.equal(bufT[:, :N], ref.t()) and (bufT[:, N:] == 7.0).all()
+
+
+def test_qlora_step_hip_matches_torch_path(C, monkeypatch):
+    """Mistral-style trunk (sliding window) in QLoRA: NF4 base dequantised into the augmented operands
+    (forward) and their transposed form (backward) vs the stock-PyTorch path on the same NF4 weights."""
+    from finetune_controller_amd.models import LoRAConfig, build_model
+    from finetune_controller_amd.models.config import ModelConfig
+    from finetune_controller_amd.ops.nf4 import quantize_model_
+
+    cfg = ModelConfig("llama", 512, 256, 2, 4, 2, 512, 1024, 10000.0, sliding_window=128, name="mistral-test")
+    torch.manual_seed(0)
+    models = []
+    for _ in range(2):
+        m = build_model(cfg, LoRAConfig(r=8, alpha=16), device=DEV, dtype=torch.bfloat16)
+        m.init_weights(seed=9)
+        m.freeze_base()
+        models.append(m)
+    g = torch.Generator(device=DEV).manual_seed(2)
+    for layer in models[0].layers:
+        for p in layer.lora.values():
+            for _, _, B_s in p.segment_tensors():
+                B_s.data.normal_(0, 0.05, generator=g)
+    with torch.no_grad():
+        for p0, p1 in zip(models[0].parameters(), models[1].parameters()):
+            p1.copy_(p0)
+    for m in models:
+        quantize_model_(m)
+    ids = torch.randint(0, cfg.vocab_size, (2, 512), device=DEV)
+    labels = torch.roll(ids, -1, 1)
+    out = []
+    for mode, m in (("hip", models[0]), ("torch", models[1])):
+        monkeypatch.setenv("FTC_KERNELS", mode)
+        loss = m(ids, labels)
+        loss.backward()
+        out.append((loss.float().item(), {n: p.grad.float().clone() for n, p in m.named_parameters()
+                                          if p.grad is not None}))
+    (l0, g0), (l1, g1) = out
+    assert abs(l0 - l1) < 2e-2 * abs(l1), (l0, l1)
+    bad = [n for n in g0 if (g0[n] - g1[n]).abs().max() > 5e-2 * g1[n].abs().max() + 1e-3]
+    assert not bad and len(g0) > 0, bad
