@@ -153,14 +153,28 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
   }
 }
 
-// dw[c] = sum_b part[b][c]; one thread per column, coalesced across the row of partials.
+// dw[c] = sum_b part[b][c].  A workgroup owns 64 columns; its 4 waves take every 4th partial row with
+// 8 independent accumulators each (enough loads in flight to hide HBM latency), then reduce through
+// LDS.  Deterministic (fixed summation order), d/64 workgroups.
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, float* __restrict__ out,
                                                      int nrows, int d) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= d) return;
-  float s = 0.f;
-  for (int b = 0; b < nrows; ++b) s += part[(long long)b * d + c];
-  out[c] = s;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  if (c < d) {
+    int b = wv;
+    for (; b + 28 < nrows; b += 32) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += part[(long long)(b + 4 * j) * d + c];
+    }
+    for (; b < nrows; b += 4) acc[0] += part[(long long)b * d + c];
+  }
+  red[wv][lane] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  __syncthreads();
+  if (wv == 0 && c < d) out[c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
 static int pick_nv(int d) {
@@ -240,7 +254,7 @@ extern "C" int ftc_rmsnorm_bwd(const void* dy, const void* h, const void* w, con
 #undef FTC_LAUNCH_BWD_NV
 #undef FTC_LAUNCH_BWD
   if (need_dw) {
-    hipLaunchKernelGGL(colsum_kernel, dim3((d + 255) / 256), dim3(256), 0, stream, dw_part, dw, grid, d);
+    hipLaunchKernelGGL(colsum_kernel, dim3((d + 63) / 64), dim3(256), 0, stream, dw_part, dw, grid, d);
   }
   return (int)hipGetLastError();
 }

@@ -39,10 +39,23 @@ import torch
 
 _GRAD_READY_HOOK = None  # set by parallel.ddp to learn when a main_grad was written
 
+# Bumped by optimizers that rewrite parameters in place behind autograd's back (the flat AdamW kernel
+# writes param_flat directly, which moves no version counter): AugWeight re-copies A/B then.
+_PARAM_GENERATION = [0]
+
+
+def bump_param_generation():
+    _PARAM_GENERATION[0] += 1
+
 
 def set_grad_ready_hook(fn):
     global _GRAD_READY_HOOK
     _GRAD_READY_HOOK = fn
+
+
+def _grad_ready(p):
+    if _GRAD_READY_HOOK is not None:
+        _GRAD_READY_HOOK(p)
 
 
 def _mask_blocks(dB: torch.Tensor, blocks):
@@ -125,11 +138,23 @@ class AugWeight:
     def owns(self, W: torch.Tensor) -> bool:
         return W.data_ptr() == self.big.data_ptr() and W.shape == (self.N, self.K) and W.stride(0) == self.K + self.Rp
 
+    _key = None
+
     def refresh(self, A: torch.Tensor, B: torch.Tensor, scale: float):
-        """big[:N, K:K+R] = B ; big[N:N+R, :K] = s A (pad rows / columns stay zero)."""
+        """big[:N, K:K+R] = B ; big[N:N+R, :K] = s A (pad rows / columns stay zero); bigT follows.
+
+        Runs once per parameter update, not per call: forward and backward of every micro-batch
+        between two optimizer steps see the same A/B (key = optimizer generation + the tensors'
+        version counters and storage)."""
+        key = (_PARAM_GENERATION[0], A._version, B._version, A.data_ptr(), B.data_ptr(), float(scale))
+        if key == self._key:
+            return
         N, K, R = self.N, self.K, self.R
         self.big[:N, K:K + R].copy_(B)
         torch.mul(A, scale, out=self.big[N:N + R, :K])
+        if self.bigT is not None:
+            self.bigT[:, N:N + R].copy_(self.big[N:N + R, :K].t())
+        self._key = key
 
     # ---- backward operand in the "TN" layout.  hipBLASLt runs dx = [dy | dyB] . [W ; sA] 14-16 %
     # faster when the right operand is stored K-contiguous (tools/bench_gemm_layouts.py), so a
@@ -140,15 +165,48 @@ class AugWeight:
 
     def invalidate(self):
         self.bigT = None
+        self._key = None
 
-    def bwd_operand(self, A: torch.Tensor, scale: float) -> torch.Tensor:
-        """[N+Rp, K] view of [W ; s A ; 0] with unit stride along N+Rp (column-major for the GEMM)."""
-        N, K, R = self.N, self.K, self.R
+    def bwd_operand(self) -> torch.Tensor:
+        """[N+Rp, K] view of [W ; s A ; 0] with unit stride along N+Rp (column-major for the GEMM).
+        Call after refresh(): the s A rows are copied from big."""
+        N, K = self.N, self.K
         if self.bigT is None:
             self.bigT = torch.zeros(K, N + self.Rp, device=self.big.device, dtype=self.big.dtype)
-            self.bigT[:, :N].copy_(self.big[:N, :K].t())
-        self.bigT[:, N:N + R].copy_((A * scale).t())
+            self.bigT[:, :N + self.R].copy_(self.big[:N + self.R, :K].t())
         return self.bigT.t()
+
+
+def direct_grad_params(A, B, blocks):
+    """(A, B) when both have a flat-buffer ``main_grad`` and no structural block mask, else None."""
+    if (A is not None and blocks is None and getattr(A, "main_grad", None) is not None
+            and getattr(B, "main_grad", None) is not None):
+        return (A, B)
+    return None
+
+
+def lora_weight_grads(direct, dy2, xa, xa_scaled, dyb, xin, s, blocks, need_a, need_b):
+    """dB = dy^T (s x A^T), dA = s (dy B)^T x.  With ``direct`` = (A, B) homed in the flat grad buffer
+    they are accumulated in place by beta=1 GEMMs (alpha carries the scale) and the data-parallel
+    grad-ready hook fires; (None, None) is returned.  Otherwise fresh tensors are returned for
+    autograd to accumulate."""
+    dA = dB = None
+    if need_b:
+        if direct is not None:
+            direct[1].main_grad.addmm_(dy2.t(), xa, alpha=1.0 if xa_scaled else s)
+            _grad_ready(direct[1])
+        else:
+            dB = torch.mm(dy2.t(), xa)
+            if not xa_scaled:
+                dB.mul_(s)
+            dB = _mask_blocks(dB, blocks)
+    if need_a:
+        if direct is not None:
+            direct[0].main_grad.addmm_(dyb.t(), xin, alpha=s)
+            _grad_ready(direct[0])
+        else:
+            dA = torch.mm(dyb.t(), xin).mul_(s)
+    return dA, dB
 
 
 class _LoRALinearFn(torch.autograd.Function):
@@ -197,6 +255,10 @@ class _LoRALinearFn(torch.autograd.Function):
         ctx.scale, ctx.blocks, ctx.shp, ctx.has_bias, ctx.aug = scale, blocks, shp, bias is not None, aug
         ctx.aug_fwd = use_aug  # saved xa is s * x A^T
         ctx.mask, ctx.p_drop = mask, p_drop
+        # trainable A/B homed in a flat grad buffer (FlatAdamW sets .main_grad): their weight
+        # gradients are accumulated in place by beta=1 GEMMs instead of returned (no temporaries, no
+        # scale / accumulate kernels).  Block-masked packed pairs keep the returned-gradient path.
+        ctx.lora_params = direct_grad_params(A, B, blocks)
         return out
 
     @staticmethod
@@ -218,7 +280,7 @@ class _LoRALinearFn(torch.autograd.Function):
             aug.refresh(A, B, s)
             _mm_into(dy2, aug.big[:N, aug.K:], _tail(dy2, N, Rp))
             dyb = _tail(dy2, N, aug.R)
-            rhs = aug.bwd_operand(A, s) if _TN_BWD else aug.big[:, :aug.K]
+            rhs = aug.bwd_operand() if _TN_BWD else aug.big[:, :aug.K]
             dx = torch.mm(_wide(dy2, N + Rp), rhs).view(ctx.shp)
         else:
             if A is not None and (need_x or need_a):
@@ -235,23 +297,16 @@ class _LoRALinearFn(torch.autograd.Function):
             mg = getattr(W, "main_grad", None)
             if mg is not None:
                 mg.addmm_(dy2.t(), x2)
-                if _GRAD_READY_HOOK is not None:
-                    _GRAD_READY_HOOK(W)
+                _grad_ready(W)
             else:
                 dW = dy2.t() @ x2
         if need_b and ctx.has_bias:
             db = dy2.sum(0)
-        if A is not None:
-            if need_bb:
-                dB = torch.mm(dy2.t(), xa)
-                if not xa_scaled:
-                    dB.mul_(s)
-                dB = _mask_blocks(dB, ctx.blocks)
-            if need_a:
-                if dyb is None:
-                    dyb = dy2 @ B
-                xin = x2 if ctx.mask is None else x2 * ctx.mask / (1.0 - ctx.p_drop)
-                dA = torch.mm(dyb.t(), xin).mul_(s)
+        if A is not None and (need_a or need_bb):
+            if need_a and dyb is None:
+                dyb = dy2 @ B
+            xin = x2 if ctx.mask is None else x2 * ctx.mask / (1.0 - ctx.p_drop)
+            dA, dB = lora_weight_grads(ctx.lora_params, dy2, xa, xa_scaled, dyb, xin, s, ctx.blocks, need_a, need_bb)
         return dx, dW, db, dA, dB, None, None, None, None
 
 

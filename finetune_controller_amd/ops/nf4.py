@@ -22,7 +22,7 @@ from __future__ import annotations
 import torch
 
 from ._backend import ext, use_hip
-from .linear import _mask_blocks, _mm_into, _spare_cols, _tail, _wide
+from .linear import _mm_into, _spare_cols, _tail, _wide, direct_grad_params, lora_weight_grads
 
 NF4_CODE = torch.tensor([-1.0, -0.6961928009986877, -0.5250730514526367, -0.39491748809814453, -0.28444138169288635,
                          -0.18477343022823334, -0.09105003625154495, 0.0, 0.07958029955625534, 0.16093020141124725,
@@ -163,6 +163,7 @@ class _QLoRALinearFn(torch.autograd.Function):
                 y.addmm_(xa, B.t(), alpha=scale)
         ctx.save_for_backward(x2, A, B, xa)
         ctx.qw, ctx.scale, ctx.blocks, ctx.shp, ctx.Rp, ctx.aug_fwd = qw, scale, blocks, shp, Rp, use_aug
+        ctx.lora_params = direct_grad_params(A, B, blocks)
         return y if x.dim() == 2 else y.reshape(*shp[:-1], qw.shape[0]).clone()
 
     @staticmethod
@@ -200,16 +201,11 @@ class _QLoRALinearFn(torch.autograd.Function):
                     dyb = dy2 @ B
                     dx.addmm_(dyb, A, alpha=s)
             dx = dx.view(ctx.shp)
-        if A is not None:
-            if ctx.needs_input_grad[2]:
-                dB = torch.mm(dy2.t(), xa)
-                if not ctx.aug_fwd:
-                    dB.mul_(s)
-                dB = _mask_blocks(dB, ctx.blocks)
-            if ctx.needs_input_grad[1]:
-                if dyb is None:
-                    dyb = dy2 @ B
-                dA = torch.mm(dyb.t(), x2).mul_(s)
+        need_a, need_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        if A is not None and (need_a or need_b):
+            if need_a and dyb is None:
+                dyb = dy2 @ B
+            dA, dB = lora_weight_grads(ctx.lora_params, dy2, xa, ctx.aug_fwd, dyb, x2, s, ctx.blocks, need_a, need_b)
         return dx, dA, dB, None, None, None, None
 
 

@@ -23,6 +23,7 @@ import math
 import torch
 
 from ..ops._backend import ext, use_hip
+from ..ops.linear import bump_param_generation
 
 ALIGN = 64  # elements: keeps every view 128-byte aligned for 16-byte vector access
 
@@ -81,6 +82,7 @@ class FlatAdamW:
     def step(self, lr: float | None = None):
         lr = self.lr if lr is None else lr
         self.step_count += 1
+        bump_param_generation()  # the update below rewrites param_flat in place
         b1, b2 = self.betas
         if use_hip(self.grad_flat) and self.dtype in (torch.bfloat16, torch.float32):
             stats = ext().grad_sumsq(self.grad_flat, self.max_grad_norm, self.grad_scale)
@@ -119,6 +121,7 @@ class FlatAdamW:
         self.exp_avg.copy_(sd["exp_avg"])
         self.exp_avg_sq.copy_(sd["exp_avg_sq"])
         self.step_count = int(sd["step"])
+        bump_param_generation()
         if self.master is not self.param_flat:
             self.param_flat.copy_(self.master)
 

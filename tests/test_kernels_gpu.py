@@ -24,7 +24,7 @@ def bf(x):
     return x.to(torch.bfloat16)
 
 
-@pytest.mark.parametrize("rows,d", [(257, 4096), (64, 768), (33, 128), (8, 8192)])
+@pytest.mark.parametrize("rows,d", [(257, 4096), (64, 768), (33, 128), (8, 8192), (4096, 4096)])
 @pytest.mark.parametrize("with_res", [False, True])
 def test_rmsnorm_fwd_bwd(C, rows, d, with_res):
     torch.manual_seed(0)

@@ -100,6 +100,43 @@ def test_augmented_lora_gemms_match_two_gemm_path():
         torch.testing.assert_close(a_, b_)
 
 
+def test_augmented_lora_direct_main_grad_and_refresh_across_steps():
+    """A/B homed in FlatAdamW's flat buffers: their grads are accumulated in place (beta=1 GEMMs, grad
+    -ready hook fired, nothing returned to autograd), and the augmented operands are re-copied once
+    per optimizer step -- the second forward must see the updated A/B."""
+    from finetune_controller_amd.ops import linear as lin
+
+    torch.manual_seed(0)
+    T, K, N, R = 10, 16, 24, 8
+    aw = lin.AugWeight(N, K, R, dtype=torch.float32)
+    aw.W.copy_(torch.randn(N, K))
+    W = torch.nn.Parameter(aw.W, requires_grad=False)
+    A = torch.nn.Parameter(torch.randn(R, K))
+    B = torch.nn.Parameter(torch.randn(N, R))
+    opt = FlatAdamW([A, B], lr=1e-1, max_grad_norm=0.0)
+    ready = []
+    lin.set_grad_ready_hook(ready.append)
+    try:
+        for step in range(2):
+            x = torch.randn(T, K, requires_grad=True)
+            y = _PadGrad.apply(ops.lora_linear(_PadIdentity.apply(x, aw.Rp), W, A, B, 0.5, aug=aw), aw.Rp)
+            x2, A2, B2 = (t.detach().clone().requires_grad_(True) for t in (x, A, B))
+            ref = x2 @ W.detach().clone().t() + 0.5 * (x2 @ A2.t()) @ B2.t()
+            torch.testing.assert_close(y, ref)
+            g = torch.randn_like(y)
+            opt.zero_grad()
+            ready.clear()
+            y.backward(g)
+            ref.backward(g)
+            assert {id(p) for p in ready} == {id(A), id(B)}
+            torch.testing.assert_close(x.grad, x2.grad)
+            torch.testing.assert_close(A.main_grad, A2.grad)
+            torch.testing.assert_close(B.main_grad, B2.grad)
+            opt.step()
+    finally:
+        lin.set_grad_ready_hook(None)
+
+
 def test_fused_ce_matches_reference():
     torch.manual_seed(0)
     h = torch.randn(37, 16, requires_grad=True)

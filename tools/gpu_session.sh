@@ -2,7 +2,8 @@
 # One gpurun session: GPU tests -> smoke -> short benches -> rocprofv3 kernel stats.
 # Every GPU step has its own timeout; a crash/abort/timeout (rc >= 124 or signal) ends the session.
 # Usage (from the repo root, on the GPU box): bash tools/gpu_session.sh [steps...]
-#   steps: tests smoke bench1l bench bench_torch prof  (default: all)
+#   steps: tests smoke bench1l bench bench_full bench_qlora bench_torch prof prof_lora prof_full attn ...
+#   (default: tests smoke bench1l bench bench_torch prof)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -52,6 +53,18 @@ for s in "${STEPS[@]}"; do
     bench_b8)
       timeout -k 10 600 python bench.py --steps 8 --warmup 3 --batch-size 8 > gpurun_out/bench_b8.log 2>&1
       fatal $? bench_b8; tail -2 gpurun_out/bench_b8.log ;;
+    bench_full)
+      timeout -k 10 600 python bench.py --method full --steps 6 --warmup 2 > gpurun_out/bench_full.log 2>&1
+      fatal $? bench_full; tail -1 gpurun_out/bench_full.log | cut -c1-220 ;;
+    bench_qlora)
+      timeout -k 10 600 python bench.py --model mistral-7b --method qlora --steps 8 --warmup 3 > gpurun_out/bench_qlora.log 2>&1
+      fatal $? bench_qlora; tail -1 gpurun_out/bench_qlora.log | cut -c1-220 ;;
+    prof_lora)
+      bash tools/prof_bench.sh lora --steps 3 --warmup 2
+      fatal $? prof_lora ;;
+    prof_full)
+      bash tools/prof_bench.sh full --method full --steps 3 --warmup 2
+      fatal $? prof_full ;;
     bench_torch)
       timeout -k 10 600 python bench.py --steps 10 --warmup 3 --kernels torch > gpurun_out/bench_torch.log 2>&1
       fatal $? bench_torch; tail -2 gpurun_out/bench_torch.log ;;
