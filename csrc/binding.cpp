@@ -47,6 +47,10 @@ int ftc_nf4_gemm(const void* x, const uint8_t* packed, const uint8_t* absmax_q, 
                  float absmax_offset, void* y, int M, int N, int K, int block, int block2, hipStream_t stream);
 int ftc_lora_merge(void* w, const void* a, const void* b, int out_f, int in_f, int r, int seg_rows, float scale,
                    hipStream_t stream);
+int ftc_lora_wgrad_splits(int T, int M);
+int ftc_lora_wgrad(const void* x, long long ldx, const void* y, long long ldy, float* ws, int T, int M, int R,
+                   void* out, long long out_sm, long long out_sr, float alpha, float beta, int nseg, const int* m_end,
+                   const int* ycol, const int* ocol, hipStream_t stream);
 }
 
 namespace {
@@ -380,6 +384,50 @@ void lora_merge_(at::Tensor& w, const at::Tensor& a, const at::Tensor& b, double
         "lora_merge");
 }
 
+// ---------------- LoRA weight gradient ----------------
+// out[m, ocol(m) + r] = beta * out + alpha * sum_t X[t, m] Y[t, ycol(m) + r]  (r < R) for X [T, M] and Y [T, *]
+// (row-strided views, unit column stride).  Segments (m_end, ycol, ocol) describe the block-diagonal B of a
+// packed projection; empty lists = one segment (ycol = ocol = 0).  out is any strided 2-D bf16 view (pass
+// main_grad.t() for dA [R, K]).
+bool lora_wgrad_ok(const at::Tensor& x, const at::Tensor& y, int64_t R) {
+  auto al = [](const at::Tensor& t) {
+    return t.scalar_type() == at::kBFloat16 && t.is_cuda() && t.dim() == 2 && t.stride(1) == 1 &&
+           t.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0;
+  };
+  if (!al(x) || !al(y)) return false;
+  const int64_t T = x.size(0), M = x.size(1);
+  return y.size(0) == T && T % 64 == 0 && M % 128 == 0 && R % 8 == 0 && R > 0 && R <= 64 && R <= y.size(1);
+}
+
+void lora_wgrad_(at::Tensor& out, const at::Tensor& x, const at::Tensor& y, int64_t R, double alpha, double beta,
+                 std::vector<int64_t> m_end, std::vector<int64_t> ycol, std::vector<int64_t> ocol) {
+  TORCH_CHECK(lora_wgrad_ok(x, y, R), "lora_wgrad: unsupported operands (bf16, T%64, M%128, R%8, R<=64, aligned rows)");
+  need(out, at::kBFloat16, "out");
+  const int T = (int)x.size(0), M = (int)x.size(1);
+  if (m_end.empty()) {
+    m_end = {M};
+    ycol = {0};
+    ocol = {0};
+  }
+  const int nseg = (int)m_end.size();
+  TORCH_CHECK(nseg <= 4 && (int)ycol.size() == nseg && (int)ocol.size() == nseg, "lora_wgrad: <= 4 segments");
+  int me[4], yc[4], oc[4];
+  for (int i = 0; i < nseg; ++i) {
+    me[i] = (int)m_end[i];
+    yc[i] = (int)ycol[i];
+    oc[i] = (int)ocol[i];
+    TORCH_CHECK(yc[i] + R <= y.size(1), "lora_wgrad: segment reads past Y");
+    TORCH_CHECK(oc[i] + R <= out.size(1), "lora_wgrad: segment writes past out");
+  }
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == M, "lora_wgrad: out must have M rows");
+  const int splits = ftc_lora_wgrad_splits(T, M);
+  auto ws = at::empty({(int64_t)splits * M * R}, x.options().dtype(at::kFloat));
+  check(ftc_lora_wgrad(x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), ws.data_ptr<float>(), T, M, (int)R,
+                       out.data_ptr(), out.stride(0), out.stride(1), (float)alpha, (float)beta, nseg, me, yc, oc,
+                       cur_stream()),
+        "lora_wgrad");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -401,6 +449,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("nf4_dequantize", &nf4_dequantize);
   m.def("nf4_linear", &nf4_linear);
   m.def("lora_merge_", &lora_merge_);
+  m.def("lora_wgrad_ok", &lora_wgrad_ok);
+  m.def("lora_wgrad_", &lora_wgrad_, py::arg("out"), py::arg("x"), py::arg("y"), py::arg("R"), py::arg("alpha"),
+        py::arg("beta") = 1.0, py::arg("m_end") = std::vector<int64_t>{}, py::arg("ycol") = std::vector<int64_t>{},
+        py::arg("ocol") = std::vector<int64_t>{});
   m.def("nf4_gemm_ready", [] { return true; });
   m.def("nf4_dequantize_into", &nf4_dequantize_into);
 }

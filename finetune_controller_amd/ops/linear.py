@@ -37,6 +37,8 @@ import os
 
 import torch
 
+from ._backend import ext, use_hip
+
 _GRAD_READY_HOOK = None  # set by parallel.ddp to learn when a main_grad was written
 
 # Bumped by optimizers that rewrite parameters in place behind autograd's back (the flat AdamW kernel
@@ -178,11 +180,38 @@ class AugWeight:
 
 
 def direct_grad_params(A, B, blocks):
-    """(A, B) when both have a flat-buffer ``main_grad`` and no structural block mask, else None."""
-    if (A is not None and blocks is None and getattr(A, "main_grad", None) is not None
+    """(A, B) when both have a flat-buffer ``main_grad``, else None."""
+    if (A is not None and getattr(A, "main_grad", None) is not None
             and getattr(B, "main_grad", None) is not None):
         return (A, B)
     return None
+
+
+_HIP_WGRAD = os.environ.get("FTC_LORA_WGRAD", "1") != "0"
+
+
+def _accum_xty(out: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, alpha: float, blocks=None):
+    """out [M, R] += alpha * X^T Y for X [T, M], Y [T, R] with T = tokens: one streaming pass over X
+    (csrc/kernels/lora_wgrad.hip: split-T MFMA + deterministic split reduction) where supported,
+    else beta=1 GEMMs.  ``blocks`` (r0, r1, c0, c1): only those diagonal blocks of out are formed
+    (block-diagonal B of a packed projection) -- one launch for all of them."""
+    hip = _HIP_WGRAD and use_hip(X)
+    if blocks is None:
+        if hip and ext().lora_wgrad_ok(X, Y, Y.shape[1]):
+            ext().lora_wgrad_(out, X, Y, Y.shape[1], float(alpha), 1.0)
+        else:
+            out.addmm_(X.t(), Y, alpha=alpha)
+        return
+    R = blocks[0][3] - blocks[0][2]
+    segs_ok = (len(blocks) <= 4 and blocks[0][0] == 0 and blocks[-1][1] == X.shape[1]
+               and all(b[3] - b[2] == R and b[1] % 128 == 0 for b in blocks)
+               and all(blocks[i][0] == blocks[i - 1][1] for i in range(1, len(blocks))))
+    if hip and segs_ok and ext().lora_wgrad_ok(X, Y, R):
+        ext().lora_wgrad_(out, X, Y, R, float(alpha), 1.0, [b[1] for b in blocks], [b[2] for b in blocks],
+                          [b[2] for b in blocks])
+    else:
+        for r0, r1, c0, c1 in blocks:
+            _accum_xty(out[r0:r1, c0:c1], X[:, r0:r1], Y[:, c0:c1], alpha)
 
 
 def lora_weight_grads(direct, dy2, xa, xa_scaled, dyb, xin, s, blocks, need_a, need_b):
@@ -193,7 +222,9 @@ def lora_weight_grads(direct, dy2, xa, xa_scaled, dyb, xin, s, blocks, need_a, n
     dA = dB = None
     if need_b:
         if direct is not None:
-            direct[1].main_grad.addmm_(dy2.t(), xa, alpha=1.0 if xa_scaled else s)
+            mg, alpha = direct[1].main_grad, 1.0 if xa_scaled else s
+            # block-diagonal B of a packed projection: only the diagonal blocks have gradients
+            _accum_xty(mg, dy2, xa, alpha, blocks)
             _grad_ready(direct[1])
         else:
             dB = torch.mm(dy2.t(), xa)
@@ -202,7 +233,7 @@ def lora_weight_grads(direct, dy2, xa, xa_scaled, dyb, xin, s, blocks, need_a, n
             dB = _mask_blocks(dB, blocks)
     if need_a:
         if direct is not None:
-            direct[0].main_grad.addmm_(dyb.t(), xin, alpha=s)
+            _accum_xty(direct[0].main_grad.t(), xin, dyb, s)  # dA^T [K, R] += s x^T (dy B)
             _grad_ready(direct[0])
         else:
             dA = torch.mm(dyb.t(), xin).mul_(s)

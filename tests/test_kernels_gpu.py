@@ -349,3 +349,44 @@ def test_qlora_step_hip_matches_torch_path(C, monkeypatch):
     assert abs(l0 - l1) < 2e-2 * abs(l1), (l0, l1)
     bad = [n for n in g0 if (g0[n] - g1[n]).abs().max() > 5e-2 * g1[n].abs().max() + 1e-3]
     assert not bad and len(g0) > 0, bad
+
+
+@pytest.mark.parametrize("T,M,R,transposed,col0", [(1024, 4096, 16, False, 0), (512, 1024, 48, False, 16),
+                                                   (256, 14336, 16, True, 0), (4096, 128, 64, True, 8),
+                                                   (64, 256, 32, False, 0)])
+def test_lora_wgrad_matches_fp32(C, T, M, R, transposed, col0):
+    """out [M, R] += alpha X^T Y through csrc/kernels/lora_wgrad.hip (split-T MFMA + split reduction), with
+    X / Y as column views of wider row-padded buffers (the augmented-GEMM operands) and out either a
+    row-major [M, R] block or the transposed view of an [R, M] gradient (dA)."""
+    torch.manual_seed(0)
+    Xbuf = bf(torch.randn(T, M + 64, device=DEV))
+    Ybuf = bf(torch.randn(T, col0 + R + 24, device=DEV))
+    X, Y = Xbuf[:, :M], Ybuf[:, col0:col0 + R]
+    assert C.lora_wgrad_ok(X, Y, R)
+    if transposed:
+        base = bf(torch.randn(R, M, device=DEV))
+        out = base.t()
+    else:
+        base = bf(torch.randn(M, R + 8, device=DEV))
+        out = base[:, :R]
+    before = out.float().clone()
+    C.lora_wgrad_(out, X, Y, R, 0.5, 1.0)
+    ref = before + 0.5 * (X.float().t() @ Y.float())
+    torch.testing.assert_close(out.float(), ref, atol=0.05 + 2e-3 * math.sqrt(T), rtol=1e-2)
+
+
+def test_lora_wgrad_block_diagonal_segments(C):
+    """Packed q|k|v dB in one launch: rows of each segment use their own 16 columns of Y and of out; the
+    off-diagonal blocks of out are not touched."""
+    torch.manual_seed(0)
+    T, R = 512, 16
+    bounds = [(0, 512), (512, 640), (640, 768)]
+    X = bf(torch.randn(T, 768 + 64, device=DEV))[:, :768]
+    Y = bf(torch.randn(T, 64, device=DEV))  # s x A^T tail: 3 x 16 used columns + zero pad
+    out = bf(torch.randn(768, 3 * R, device=DEV))
+    before = out.float().clone()
+    C.lora_wgrad_(out, X, Y, R, 1.0, 1.0, [b[1] for b in bounds], [0, 16, 32], [0, 16, 32])
+    ref = before.clone()
+    for i, (r0, r1) in enumerate(bounds):
+        ref[r0:r1, 16 * i:16 * i + 16] += X[:, r0:r1].float().t() @ Y[:, 16 * i:16 * i + 16].float()
+    torch.testing.assert_close(out.float(), ref, atol=0.1, rtol=1e-2)

@@ -100,7 +100,8 @@ def test_augmented_lora_gemms_match_two_gemm_path():
         torch.testing.assert_close(a_, b_)
 
 
-def test_augmented_lora_direct_main_grad_and_refresh_across_steps():
+@pytest.mark.parametrize("packed", [False, True])
+def test_augmented_lora_direct_main_grad_and_refresh_across_steps(packed):
     """A/B homed in FlatAdamW's flat buffers: their grads are accumulated in place (beta=1 GEMMs, grad
     -ready hook fired, nothing returned to autograd), and the augmented operands are re-copied once
     per optimizer step -- the second forward must see the updated A/B."""
@@ -108,20 +109,28 @@ def test_augmented_lora_direct_main_grad_and_refresh_across_steps():
 
     torch.manual_seed(0)
     T, K, N, R = 10, 16, 24, 8
+    blocks = [(0, 16, 0, 4), (16, 24, 4, 8)] if packed else None  # packed projection: block-diagonal B
     aw = lin.AugWeight(N, K, R, dtype=torch.float32)
     aw.W.copy_(torch.randn(N, K))
     W = torch.nn.Parameter(aw.W, requires_grad=False)
     A = torch.nn.Parameter(torch.randn(R, K))
     B = torch.nn.Parameter(torch.randn(N, R))
+    if packed:
+        with torch.no_grad():
+            mask = torch.zeros(N, R)
+            for r0, r1, c0, c1 in blocks:
+                mask[r0:r1, c0:c1] = 1
+            B.mul_(mask)
     opt = FlatAdamW([A, B], lr=1e-1, max_grad_norm=0.0)
     ready = []
     lin.set_grad_ready_hook(ready.append)
     try:
         for step in range(2):
             x = torch.randn(T, K, requires_grad=True)
-            y = _PadGrad.apply(ops.lora_linear(_PadIdentity.apply(x, aw.Rp), W, A, B, 0.5, aug=aw), aw.Rp)
+            y = _PadGrad.apply(ops.lora_linear(_PadIdentity.apply(x, aw.Rp), W, A, B, 0.5, blocks=blocks, aug=aw),
+                               aw.Rp)
             x2, A2, B2 = (t.detach().clone().requires_grad_(True) for t in (x, A, B))
-            ref = x2 @ W.detach().clone().t() + 0.5 * (x2 @ A2.t()) @ B2.t()
+            ref = x2 @ W.detach().clone().t() + 0.5 * (x2 @ A2.t()) @ (B2 * mask if packed else B2).t()
             torch.testing.assert_close(y, ref)
             g = torch.randn_like(y)
             opt.zero_grad()
@@ -132,6 +141,8 @@ def test_augmented_lora_direct_main_grad_and_refresh_across_steps():
             torch.testing.assert_close(x.grad, x2.grad)
             torch.testing.assert_close(A.main_grad, A2.grad)
             torch.testing.assert_close(B.main_grad, B2.grad)
+            if packed:
+                assert (B.main_grad * (1 - mask)).abs().max() == 0 and (B.detach() * (1 - mask)).abs().max() == 0
             opt.step()
     finally:
         lin.set_grad_ready_hook(None)
