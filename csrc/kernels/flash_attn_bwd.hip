@@ -122,10 +122,32 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(BwdArgs a) {
 // under them (register staging into the other LDS slot, one barrier per slice).
 // Block order: heavy (early, causal) key blocks first; the key blocks of one (batch, kv head) pair
 // share an XCD so its Q/dO slices are L2 hits for the co-running blocks.
-template <int D>
-__global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(BwdArgs a) {
+// One slice's LDS-DMA for a dK/dV wave: NG 1 KiB pieces of Q and of dO (lane-linear destinations,
+// pre-swizzled per-lane source offsets qvo/dvo) and the 256-byte row-constant piece.  A device-only
+// function rather than a lambda in the kernel: the host pass cannot instantiate these builtins.
+template <int D, int NG, int RPG, int QBYTES>
+FTC_DEV void dkdv_dma(__amdgpu_buffer_rsrc_t qr, __amdgpu_buffer_rsrc_t dr, __amdgpu_buffer_rsrc_t cr, const int* qvo,
+                      const int* dvo, int cvo, int qso, int dso, int cso, char* base, int wave) {
+#pragma unroll
+  for (int i = 0; i < NG; ++i) {
+    const int r0 = (wave * NG + i) * RPG;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (__attribute__((address_space(3))) void*)(base + r0 * D * 2), 16,
+                                             qvo[i], qso, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(dr, (__attribute__((address_space(3))) void*)(base + QBYTES + r0 * D * 2),
+                                             16, dvo[i], dso, 0, 0);
+  }
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(cr, (__attribute__((address_space(3))) void*)(base + 2 * QBYTES), 4, cvo,
+                                           cso, 0, 0);
+}
+
+// HW = 32-key halves per wave: HW = 2 -> 4 waves x 64 keys, one wave per SIMD (512-register budget);
+// HW = 1 -> 8 waves x 32 keys, two waves per SIMD (256 registers each): one wave's softmax VALU then
+// runs under the other wave's MFMAs.
+template <int D, int HW>
+__global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
   constexpr int NCH = D / 8, DSTEPS = D / 16, DT = D / 32;
   constexpr int BKV = 256, BQ2 = 32;
+  constexpr int WAVES = 8 / HW, NT = 64 * WAVES;
   constexpr int KBYTES = BKV * D * 2, QBYTES = BQ2 * D * 2;
   constexpr int SLICE = 2 * QBYTES + 2 * BQ2 * 4;  // Q | dO | -lse/scale | -delta
   // K and the three ring slots are DISTINCT __shared__ objects: the compiler then knows (LDS alias
@@ -156,12 +178,12 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(BwdArgs a) {
   }
   const int kvh = pair % a.KV, b = pair / a.KV;
   const int kv0 = kb * BKV;
-  const int wkey0 = kv0 + wave * 64;  // this wave's first key
+  const int wkey0 = kv0 + wave * 32 * HW;  // this wave's first key
 
   // stage the block's K rows into LDS; V^T fragments (B operand of dP) to registers
   const uint16_t* kbase = a.k + ((long long)b * S) * a.kv_rs + (long long)kvh * D;
   {
-    constexpr int RPP = 256 / NCH;
+    constexpr int RPP = NT / NCH;
     const int lrow = tid / NCH, lch = tid % NCH;
     const auto krs = make_rsrc(kbase + (long long)kv0 * a.kv_rs);
     const int voff = (lrow * (int)a.kv_rs + lch * 8) * 2;
@@ -169,17 +191,17 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(BwdArgs a) {
     for (int p = 0; p < BKV / RPP; ++p)
       *reinterpret_cast<u32x4*>(Ks + lds_off<D>(p * RPP + lrow, lch)) = buf_load16(krs, voff, p * RPP * (int)a.kv_rs * 2);
   }
-  bf16x8 vf[2][DSTEPS];
+  bf16x8 vf[HW][DSTEPS];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < HW; ++j) {
     const uint16_t* vp = a.v + ((long long)b * S + wkey0 + 32 * j + lr) * a.kv_rs + (long long)kvh * D + 8 * hh;
 #pragma unroll
     for (int s = 0; s < DSTEPS; ++s) vf[j][s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(vp + 16 * s));
   }
 
-  f32x16 dv[2][DT], dk[2][DT];
+  f32x16 dv[HW][DT], dk[HW][DT];
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int j = 0; j < HW; ++j)
 #pragma unroll
     for (int t = 0; t < DT; ++t)
 #pragma unroll
@@ -195,32 +217,30 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(BwdArgs a) {
   // 3-slot ring, two slices ahead of the compute; one raw barrier per slice with a COUNTED vmcnt so the
   // next slice's DMA stays in flight across it (guide §5 "Pipelining across barriers").  The swizzled
   // LDS image is produced by pre-swizzling the per-lane global source (the DMA writes lane-linearly).
-  constexpr int NG = BQ2 * D * 2 / 1024 / 4;  // 1 KiB DMA pieces per wave per matrix (D=128: 2)
+  constexpr int NG = BQ2 * D * 2 / 1024 / WAVES;  // 1 KiB DMA pieces per wave per matrix
+  static_assert(NG >= 1, "each wave DMAs at least one 1 KiB piece of Q and of dO");
   constexpr int PER_SLICE = 2 * NG + 1;       // DMA instructions per wave per slice (+1: row constants)
   constexpr int RPG = 1024 / (D * 2);         // rows per 1 KiB piece
-  const float* ls_all = a.delta + (long long)a.B * a.H * S;  // workspace: [-delta | -lse/scale]
+  // DMA sources as buffer resources (SGPRs) + per-lane loop-invariant 32-bit offsets: the slice's head
+  // and row position go into the scalar offset, so no 64-bit address VGPRs stay live in the loop
+  const auto qrsrc = make_rsrc(a.q + (long long)b * S * a.q_rs);
+  const auto drsrc = make_rsrc(a.dout + (long long)b * S * a.do_rs);
+  const auto crsrc = make_rsrc(a.delta);  // workspace [-delta | -lse/scale]
+  int qvo[NG], dvo[NG];
+#pragma unroll
+  for (int i = 0; i < NG; ++i) {
+    const int row = (wave * NG + i) * RPG + lane / NCH, pc = lane % NCH;
+    const int lc = (pc ^ swz(row)) & (NCH - 1);  // pre-swizzled source, lane-linear destination
+    qvo[i] = (row * (int)a.q_rs + lc * 8) * 2;
+    dvo[i] = (row * (int)a.do_rs + lc * 8) * 2;
+  }
+  // lanes 0..31: -lse/scale of the 32 rows, lanes 32..63: -delta (every wave issues the same piece)
+  const int cvo = (lr + (hh ? 0 : a.B * a.H * S)) * 4;
   auto issue = [&](int it_, char* base_) {
     const int g_ = it_ / nqt, qt_ = qbeg + (it_ % nqt) * BQ2;
     const int hq_ = kvh * G + g_;
-    const long long row0 = (long long)b * S + qt_;
-#pragma unroll
-    for (int i = 0; i < NG; ++i) {
-      const int r0 = (wave * NG + i) * RPG;
-      const int row = r0 + lane / NCH, pc = lane % NCH;
-      const int lc = (pc ^ swz(row)) & (NCH - 1);
-      const uint16_t* qsrc = a.q + (row0 + row) * a.q_rs + (long long)hq_ * D + lc * 8;
-      const uint16_t* dsrc = a.dout + (row0 + row) * a.do_rs + (long long)hq_ * D + lc * 8;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)qsrc,
-                                       (__attribute__((address_space(3))) void*)(base_ + r0 * D * 2), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)dsrc,
-                                       (__attribute__((address_space(3))) void*)(base_ + QBYTES + r0 * D * 2), 16,
-                                       0, 0);
-    }
-    // lanes 0..31: -lse/scale of the 32 rows, lanes 32..63: -delta (every wave issues the same piece)
-    const long long ridx = ((long long)b * a.H + hq_) * S + qt_ + lr;
-    const float* csrc = hh ? a.delta + ridx : ls_all + ridx;
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)csrc,
-                                     (__attribute__((address_space(3))) void*)(base_ + 2 * QBYTES), 4, 0, 0);
+    dkdv_dma<D, NG, RPG, QBYTES>(qrsrc, drsrc, crsrc, qvo, dvo, cvo, (hq_ * D + qt_ * (int)a.q_rs) * 2,
+                                 (hq_ * D + qt_ * (int)a.do_rs) * 2, ((b * a.H + hq_) * S + qt_) * 4, base_, wave);
   };
   constexpr int VM_ONE = 0x0F70 | (PER_SLICE & 15) | ((PER_SLICE >> 4) << 14);  // vmcnt(PER_SLICE)
   constexpr int VM_ZERO = 0x0F70;                                               // vmcnt(0)
@@ -247,13 +267,13 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(BwdArgs a) {
     const float* dlt_s = lse_s + BQ2;
     // ---- S[q][k], dP'[q][k] for both 32-key halves in one k-loop (rows q in registers, key on the
     // lane): the Q / dO A-fragments are read once for both halves, four independent MFMA chains
-    f32x16 s[2], dp[2];
+    f32x16 s[HW], dp[HW];
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
       const float4 lv = *reinterpret_cast<const float4*>(lse_s + 8 * g4 + 4 * hh);
       const float4 dv4 = *reinterpret_cast<const float4*>(dlt_s + 8 * g4 + 4 * hh);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < HW; ++j) {
         s[j][4 * g4 + 0] = lv.x; s[j][4 * g4 + 1] = lv.y; s[j][4 * g4 + 2] = lv.z; s[j][4 * g4 + 3] = lv.w;
         dp[j][4 * g4 + 0] = dv4.x; dp[j][4 * g4 + 1] = dv4.y; dp[j][4 * g4 + 2] = dv4.z; dp[j][4 * g4 + 3] = dv4.w;
       }
@@ -262,25 +282,37 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(BwdArgs a) {
     for (int st = 0; st < DSTEPS; ++st) {
       const u32x4 qa = *reinterpret_cast<const u32x4*>(Qs + lds_off<D>(lr, 2 * st + hh));
       const u32x4 da = *reinterpret_cast<const u32x4*>(Ds + lds_off<D>(lr, 2 * st + hh));
-      const u32x4 k0 = *reinterpret_cast<const u32x4*>(Ks + lds_off<D>(wave * 64 + lr, 2 * st + hh));
-      const u32x4 k1 = *reinterpret_cast<const u32x4*>(Ks + lds_off<D>(wave * 64 + 32 + lr, 2 * st + hh));
-      s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, qa), __builtin_bit_cast(bf16x8, k0), s[0], 0, 0, 0);
-      s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, qa), __builtin_bit_cast(bf16x8, k1), s[1], 0, 0, 0);
-      dp[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, da), vf[0][st], dp[0], 0, 0, 0);
-      dp[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, da), vf[1][st], dp[1], 0, 0, 0);
-    }
-    // 8 fragment reads (two k-steps) in flight ahead of the MFMA chain
-    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+      u32x4 kk[HW];
 #pragma unroll
-    for (int i = 0; i < 4 * DSTEPS - 8; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      for (int j = 0; j < HW; ++j)
+        kk[j] = *reinterpret_cast<const u32x4*>(Ks + lds_off<D>(wave * 32 * HW + 32 * j + lr, 2 * st + hh));
+#pragma unroll
+      for (int j = 0; j < HW; ++j)
+        s[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, qa), __builtin_bit_cast(bf16x8, kk[j]), s[j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < HW; ++j)
+        dp[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, da), vf[j][st], dp[j], 0, 0, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    // fragment reads of two k-steps in flight ahead of the MFMA chain, the rest interleaved
+    {
+      constexpr int NDS = (2 + HW) * DSTEPS, NMF = 2 * HW * DSTEPS, PRE = (HW == 1 ? 1 : 2) * (2 + HW);
+      constexpr int REM = NDS - PRE, Q = REM / NMF, X = REM % NMF;
+      __builtin_amdgcn_sched_group_barrier(0x100, PRE, 0);
+#pragma unroll
+      for (int i = 0; i < X; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, Q + 1, 0);
+      }
+#pragma unroll
+      for (int i = X; i < NMF; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if constexpr (Q > 0) __builtin_amdgcn_sched_group_barrier(0x100, Q, 0);
+      }
+    }
     // ---- P, dS (bf16 B operands of the accumulating products)
-    bf16x8 pb[2][2], sb[2][2];
+    bf16x8 pb[HW][2], sb[HW][2];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < HW; ++j) {
       const int key = wkey0 + 32 * j + lr;
       const int kmin = wkey0 + 32 * j;
       const bool need_mask = (a.causal && qt < kmin + 31) || (a.window > 0 && qt + BQ2 - 1 - kmin >= a.window);
@@ -313,7 +345,7 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(BwdArgs a) {
       const bf16x8 q0v = tr_read<D>(Qs, 0, to);
       const bf16x8 q1v = tr_read<D>(Qs, 16, to);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < HW; ++j) {
         dv[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, pb[j][0], dv[j][dt], 0, 0, 0);
         dv[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, pb[j][1], dv[j][dt], 0, 0, 0);
         dk[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q0v, sb[j][0], dk[j][dt], 0, 0, 0);
@@ -329,7 +361,7 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(BwdArgs a) {
 
   // ---- epilogue: dK = scale * dK^T^T, dV; lane owns one key row per half
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < HW; ++j) {
     const int key = wkey0 + 32 * j + lr;
     uint16_t* dkp = a.dk + ((long long)b * S + key) * a.dkv_rs + (long long)kvh * D;
     uint16_t* dvp = a.dv + ((long long)b * S + key) * a.dkv_rs + (long long)kvh * D;
@@ -514,6 +546,8 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
                              long long dq_rs, long long dkv_rs, float scale, int causal, int window,
                              hipStream_t stream) {
   if (S % 256 != 0 || H % KV != 0 || (D != 128 && D != 64)) return -1;
+  // the dK/dV kernel addresses one batch's Q / dO rows and the workspace with 32-bit buffer offsets
+  if ((long long)S * (q_rs > do_rs ? q_rs : do_rs) * 2 >= (1LL << 31) || 2LL * B * H * S * 4 >= (1LL << 31)) return -1;
   BwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)o, (const uint16_t*)dout,
             lse, (float*)workspace, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, q_rs, kv_rs, o_rs, dq_rs, dkv_rs, do_rs,
             B, S, H, KV, scale, scale * LOG2E, causal, window};
@@ -526,9 +560,18 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
     const char* e = getenv("FTC_FLASH_BWD_OCC");
     return (e && e[0] == '1') ? 1 : 2;
   }();
+  // dK/dV workgroup shape at D=128: 8 waves x 32 keys (2 waves/SIMD, default: 1.20 vs 1.52 ms at the
+  // Llama-3-8B layer shape, profiles/) or 4 waves x 64 keys (1 wave/SIMD); FTC_FLASH_DKDV_WAVES=8|4
+  static const int dkdv_waves = [] {
+    const char* e = getenv("FTC_FLASH_DKDV_WAVES");
+    return (e && e[0] == '4') ? 4 : 8;
+  }();
   if (D == 128) {
     hipLaunchKernelGGL(bwd_delta_kernel<128>, dim3(grid_d), dim3(256), 0, stream, a);
-    hipLaunchKernelGGL(bwd_dkdv_kernel<128>, dim3(g_kv), dim3(256), 0, stream, a);
+    if (dkdv_waves == 8)
+      hipLaunchKernelGGL((bwd_dkdv_kernel<128, 1>), dim3(g_kv), dim3(512), 0, stream, a);
+    else
+      hipLaunchKernelGGL((bwd_dkdv_kernel<128, 2>), dim3(g_kv), dim3(256), 0, stream, a);
     if (occ == 1) {
       hipLaunchKernelGGL((bwd_dq_kernel<128, 1>), dim3(g_q), dim3(256), 0, stream, a);
     } else {
@@ -536,7 +579,7 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
     }
   } else {
     hipLaunchKernelGGL(bwd_delta_kernel<64>, dim3(grid_d), dim3(256), 0, stream, a);
-    hipLaunchKernelGGL(bwd_dkdv_kernel<64>, dim3(g_kv), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((bwd_dkdv_kernel<64, 2>), dim3(g_kv), dim3(256), 0, stream, a);
     hipLaunchKernelGGL((bwd_dq_kernel<64, 2>), dim3(g_q), dim3(256), 0, stream, a);
   }
   return (int)hipGetLastError();

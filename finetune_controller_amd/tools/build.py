@@ -82,6 +82,16 @@ def _host_obj(src: Path, extra_inc: list[str], defines: list[str], force: bool, 
     return out
 
 
+def _check_kernel_stubs(so: Path) -> None:
+    """A kernel whose host-side instantiation fails is dropped SILENTLY by hipcc (its launch then
+    references an undefined ``__device_stub__``): the .so links but cannot be loaded.  Fail here."""
+    r = subprocess.run(["nm", "-C", "-u", str(so)], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+    missing = [ln.strip() for ln in r.stdout.splitlines() if "__device_stub__" in ln]
+    if missing:
+        so.unlink()
+        raise RuntimeError("kernels without host stubs (host pass rejected their bodies):\n  " + "\n  ".join(missing))
+
+
 def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> dict[str, Path]:
     BUILD.mkdir(parents=True, exist_ok=True)
     inc, tlib, abi, pyb = _torch_paths()
@@ -110,6 +120,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
     if force or _newer(so, hip_objs + [bind_obj]):
         _run(["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(so), *map(str, hip_objs), str(bind_obj),
               *link_torch])
+        _check_kernel_stubs(so)
     products["_C"] = so
 
     if comm_objs:
