@@ -1,9 +1,9 @@
 // K1: flash-attention forward for gfx950 -- causal / sliding-window, GQA, bf16 in/out, fp32 LSE.
 //
 // Geometry: one 256-thread workgroup (4 waves) = 128 query rows of one (batch, q-head); each wave
-// owns 32 rows.  K/V stream through LDS in 64-key tiles, double buffered; the next tile's global
-// loads are issued before the current tile's MFMAs and written to LDS after them (register
-// staging, guide T14), one barrier per tile.
+// owns 32 rows.  K/V stream through LDS in 64-key tiles, double buffered; the next tile arrives by
+// LDS-DMA (buffer_load ... lds, pre-swizzled sources) issued right after the current tile's barrier,
+// so it flies under the whole tile's compute with no staging registers and no ds_write pass.
 //
 // MFMA orientation (v_mfma_f32_32x32x16_bf16, wave64):
 //   S^T[key][q] = K . Q^T      A = K rows from LDS (ds_read_b128), B = Q^T kept in registers.
@@ -94,19 +94,39 @@ FTC_DEV void decode_block(const FwdArgs& a, int& qb, int& b, int& hq, int& kvh) 
   hq = kvh * G + g;
 }
 
+// One tile's K and V by LDS-DMA (buffer_load ... lds): NGT 1 KiB pieces per matrix per wave, the
+// lane's 16 bytes landing lane-linearly, the source pre-swizzled (voff) so the LDS image is the
+// XOR-swizzled one; toff = the tile's first row (scalar).  A device-only function: the host pass of
+// hipcc cannot instantiate these builtins inside a kernel lambda.
+template <int D, int NGT, int RPG>
+FTC_DEV void fwd_dma(__amdgpu_buffer_rsrc_t kr, __amdgpu_buffer_rsrc_t vr, const int* voff, int toff, char* kdst,
+                     char* vdst, int wave) {
+#pragma unroll
+  for (int i = 0; i < NGT; ++i) {
+    const int r0 = (wave * NGT + i) * RPG;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(kr, (__attribute__((address_space(3))) void*)(kdst + r0 * D * 2), 16,
+                                             voff[i], toff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(vr, (__attribute__((address_space(3))) void*)(vdst + r0 * D * 2), 16,
+                                             voff[i], toff, 0, 0);
+  }
+}
+
 template <int D, int WAVES>
 __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArgs a) {
   constexpr int BQ = 32 * WAVES;
-  constexpr int NT = 64 * WAVES;       // threads
   constexpr int NCH = D / 8;           // 16-byte chunks per row
   constexpr int DSTEPS = D / 16;       // k-steps of the S MFMA
   constexpr int DT = D / 32;           // 32-wide d tiles of O
-  constexpr int RPP = NT / NCH;        // rows loaded per pass
-  constexpr int NPASS = BK / RPP;      // passes per tile
   constexpr int TILE_BYTES = BK * D * 2;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Kb = smem;                     // [2][TILE_BYTES]
-  char* Vb = smem + 2 * TILE_BYTES;    // [2][TILE_BYTES]
+  constexpr int NGT = TILE_BYTES / 1024 / WAVES;  // 1 KiB DMA pieces per wave per matrix
+  constexpr int RPG = 1024 / (D * 2);             // rows per piece
+  static_assert(NGT >= 1, "tile too small for the wave count");
+  // K/V tiles double-buffered in four DISTINCT __shared__ objects: reading one does not make the
+  // compiler drain the DMA still filling the other pair (LDS alias scopes)
+  __shared__ __attribute__((aligned(16))) char K0[TILE_BYTES];
+  __shared__ __attribute__((aligned(16))) char V0[TILE_BYTES];
+  __shared__ __attribute__((aligned(16))) char K1[TILE_BYTES];
+  __shared__ __attribute__((aligned(16))) char V1[TILE_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform -> scalar branches
@@ -142,30 +162,13 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
 
   const uint16_t* kbase = a.k + (long long)b * S * a.kv_rs + (long long)kvh * D;
   const uint16_t* vbase = a.v + (long long)b * S * a.kv_rs + (long long)kvh * D;
-  const int lrow = tid / NCH, lch = tid % NCH;
-
-  // register-staged K/V prefetch (plain macros: lambdas capturing the staging arrays by reference left
-  // them in scratch memory)
-  u32x4 kreg[NPASS], vreg[NPASS];
-  // per-thread row pointers (64-bit math hoisted out of the loop; a tile advances by BK rows)
-  // buffer loads: one VGPR row offset per thread, tile/pass offsets in SGPRs (rows of one (b, kv head)
-  // span < 2 GiB: S * kv_rs * 2 bytes)
+  // rows of one (b, kv head) span < 2 GiB (S * kv_rs * 2 bytes): 32-bit buffer offsets
   const auto krs = make_rsrc(kbase), vrs = make_rsrc(vbase);
-  const int voff = (lrow * (int)a.kv_rs + lch * 8) * 2;
-  const int pass_bytes = RPP * (int)a.kv_rs * 2;
-#define FTC_GLOAD(KV0)                                                                  \
-  {                                                                                     \
-    const int toff = (KV0) * (int)a.kv_rs * 2;                                          \
-    _Pragma("unroll") for (int p = 0; p < NPASS; ++p) {                                 \
-      kreg[p] = buf_load16(krs, voff, toff + p * pass_bytes);                           \
-      vreg[p] = buf_load16(vrs, voff, toff + p * pass_bytes);                           \
-    }                                                                                   \
-  }
-#define FTC_LSTORE(BUF)                                                                 \
-  _Pragma("unroll") for (int p = 0; p < NPASS; ++p) {                                   \
-    const int r = p * RPP + lrow;                                                       \
-    *reinterpret_cast<u32x4*>(Kb + (BUF) * TILE_BYTES + lds_off<D>(r, lch)) = kreg[p];  \
-    *reinterpret_cast<u32x4*>(Vb + (BUF) * TILE_BYTES + lds_off<D>(r, lch)) = vreg[p];  \
+  int voff[NGT];
+#pragma unroll
+  for (int i = 0; i < NGT; ++i) {
+    const int row = (wave * NGT + i) * RPG + lane / NCH, pc = lane % NCH;
+    voff[i] = (row * (int)a.kv_rs + ((pc ^ swz(row)) & (NCH - 1)) * 8) * 2;
   }
 
   f32x16 o[DT];
@@ -176,23 +179,22 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
   float m = -INFINITY, l = 0.f;
   const float c = a.scale_log2;
 
-  if (ntiles > 0) {
-    FTC_GLOAD(kv_begin);
-    FTC_LSTORE(0);
-  }
-  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // Q fragments (plain loads) retired before any DMA: vmcnt(0)
+  if (ntiles > 0) fwd_dma<D, NGT, RPG>(krs, vrs, voff, kv_begin * (int)a.kv_rs * 2, K0, V0, wave);
 
   // tr-read addressing (V^T A operand): 16-lane group gi = lane>>4 covers d cols [16*(gi&1), +16)
   // of the 32-wide d tile and key rows [16ks + 4*hh (+8), +4)
   const int gi = lane >> 4, li = lane & 15;
   const int trq = li >> 2, trp = li & 3;
 
-  int cur = 0;
-  for (int t = 0; t < ntiles; ++t) {
+  // tile t reads (Kc, Vc); tile t+1 is DMA'd into (Kn, Vn), which held tile t-1 -- free once every
+  // wave passed this tile's barrier
+  auto tile = [&](const int t, const char* Kc, const char* Vc, char* Kn, char* Vn) __attribute__((always_inline)) {
     const int kv0 = kv_begin + t * BK;
-    const bool more = t + 1 < ntiles;
-    const char* Kc = Kb + cur * TILE_BYTES;
-    const char* Vc = Vb + cur * TILE_BYTES;
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's pieces of tile t landed (vmcnt(0))
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();        // ... and everyone's
+    if (t + 1 < ntiles) fwd_dma<D, NGT, RPG>(krs, vrs, voff, (kv0 + BK) * (int)a.kv_rs * 2, Kn, Vn, wave);
 
     // ---- S^T = K Q^T : two 32-key blocks
     f32x16 s[2];
@@ -220,7 +222,6 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
     }
     __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
 
-    if (more) { FTC_GLOAD(kv0 + BK); }
     // ---- mask (wave-uniform branch, branch-free selects inside) + online softmax in the log2 domain
     const int qmin_w = q0 + wave * 32;
     const bool need_mask = (a.causal && kv0 + BK - 1 > qmin_w) || (a.window > 0 && qmin_w + 31 - kv0 >= a.window);
@@ -290,13 +291,12 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
         o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, va), pf[ks], o[dt], 0, 0, 0);
       }
     }
-    if (more) { FTC_LSTORE(cur ^ 1); }
-    __syncthreads();
-    cur ^= 1;
+  };
+  for (int t = 0; t < ntiles; t += 2) {
+    tile(t, K0, V0, K1, V1);
+    if (t + 1 < ntiles) tile(t + 1, K1, V1, K0, V0);
   }
 
-#undef FTC_GLOAD
-#undef FTC_LSTORE
   // ---- epilogue: normalise, store O (bf16) and LSE (natural log)
   const float ltot = l + __shfl_xor(l, 32, 64);
   const float inv = ltot > 0.f ? 1.0f / ltot : 0.f;
@@ -333,7 +333,7 @@ extern "C" int ftc_flash_fwd(const void* q, const void* k, const void* v, void* 
   FwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, q_rs, kv_rs, o_rs,
             B, S, H, KV, (S + BQ - 1) / BQ, scale * LOG2E, causal, window};
   const int nblocks = a.nqb * B * H;
-  const size_t lds = (size_t)4 * BK * D * 2;
+  const size_t lds = 0;  // static: K/V double buffers
   if (waves == 8) {
     if (D == 128)
       hipLaunchKernelGGL((flash_fwd_kernel<128, 8>), dim3(nblocks), dim3(512), lds, stream, a);
