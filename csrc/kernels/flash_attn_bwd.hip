@@ -382,6 +382,20 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
 }
 
 // ---------------------------------------------------------------- 3. dQ
+// One K/V tile by LDS-DMA: NGT 1 KiB pieces per matrix per wave (device-only: see dkdv_dma)
+template <int D, int NGT, int RPG>
+FTC_DEV void kv_dma(__amdgpu_buffer_rsrc_t kr, __amdgpu_buffer_rsrc_t vr, const int* voff, int toff, char* kdst,
+                    char* vdst, int wave) {
+#pragma unroll
+  for (int i = 0; i < NGT; ++i) {
+    const int r0 = (wave * NGT + i) * RPG;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(kr, (__attribute__((address_space(3))) void*)(kdst + r0 * D * 2), 16,
+                                             voff[i], toff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(vr, (__attribute__((address_space(3))) void*)(vdst + r0 * D * 2), 16,
+                                             voff[i], toff, 0, 0);
+  }
+}
+
 template <int D, int OCC>
 __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
   constexpr int NCH = D / 8, DSTEPS = D / 16, DT = D / 32;
@@ -430,18 +444,17 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
   const uint16_t* vbase = a.v + (long long)b * S * a.kv_rs + (long long)kvh * D;
   constexpr int NGT = TILE / 1024 / 4;  // 1 KiB DMA pieces per wave per matrix
   constexpr int RPG = 1024 / (D * 2);  // rows per piece
-  auto issue = [&](int kv0_, char* kdst, char* vdst) {
+  // buffer resources + per-lane loop-invariant 32-bit offsets (pre-swizzled source, lane-linear
+  // destination); the tile's first row goes into the scalar offset
+  const auto krs = make_rsrc(kbase), vrs = make_rsrc(vbase);
+  int voff[NGT];
 #pragma unroll
-    for (int i = 0; i < NGT; ++i) {
-      const int r0 = (wave * NGT + i) * RPG;
-      const int row = r0 + lane / NCH, pc = lane % NCH;
-      const int lc = (pc ^ swz(row)) & (NCH - 1);  // pre-swizzled source, lane-linear destination
-      const long long go = (long long)(kv0_ + row) * a.kv_rs + lc * 8;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(kbase + go),
-                                       (__attribute__((address_space(3))) void*)(kdst + r0 * D * 2), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(vbase + go),
-                                       (__attribute__((address_space(3))) void*)(vdst + r0 * D * 2), 16, 0, 0);
-    }
+  for (int i = 0; i < NGT; ++i) {
+    const int row = (wave * NGT + i) * RPG + lane / NCH, pc = lane % NCH;
+    voff[i] = (row * (int)a.kv_rs + ((pc ^ swz(row)) & (NCH - 1)) * 8) * 2;
+  }
+  auto issue = [&](int kv0_, char* kdst, char* vdst) {
+    kv_dma<D, NGT, RPG>(krs, vrs, voff, kv0_ * (int)a.kv_rs * 2, kdst, vdst, wave);
   };
 
   f32x16 dq[DT];
@@ -547,7 +560,8 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
                              hipStream_t stream) {
   if (S % 256 != 0 || H % KV != 0 || (D != 128 && D != 64)) return -1;
   // the dK/dV kernel addresses one batch's Q / dO rows and the workspace with 32-bit buffer offsets
-  if ((long long)S * (q_rs > do_rs ? q_rs : do_rs) * 2 >= (1LL << 31) || 2LL * B * H * S * 4 >= (1LL << 31)) return -1;
+  const long long max_rs = q_rs > do_rs ? (q_rs > kv_rs ? q_rs : kv_rs) : (do_rs > kv_rs ? do_rs : kv_rs);
+  if ((long long)S * max_rs * 2 >= (1LL << 31) || 2LL * B * H * S * 4 >= (1LL << 31)) return -1;
   BwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)o, (const uint16_t*)dout,
             lse, (float*)workspace, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, q_rs, kv_rs, o_rs, dq_rs, dkv_rs, do_rs,
             B, S, H, KV, scale, scale * LOG2E, causal, window};

@@ -161,23 +161,23 @@ __global__ __launch_bounds__(256) void lora_wgrad_kernel(const uint16_t* __restr
 }
 
 // out[m * out_sm + (ocol(m) + r) * out_sr] = beta * out + alpha * sum_s ws[s][m][r]; each thread owns 4
-// consecutive (m, r) entries (R % 8 == 0, so they share m) and keeps 8 split loads in flight.
-__global__ __launch_bounds__(256) void lora_wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int M, int R,
+// consecutive (m, r) entries (R % 8 == 0, so they share m).  SPLITS is a compile-time power of two: all
+// of a thread's split loads are issued before the first add (one memory round trip, not SPLITS / 8).
+template <int SPLITS>
+__global__ __launch_bounds__(256) void lora_wgrad_reduce_kernel(const float* __restrict__ ws, int M, int R,
                                                                 uint16_t* __restrict__ out, long long out_sm,
                                                                 long long out_sr, float alpha, float beta, Segs sg) {
   const long long n = (long long)M * R;
   const long long idx = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
   if (idx >= n) return;
-  f32x4 acc[8];
+  f32x4 v[SPLITS];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int k = 0;
-  for (; k + 8 <= splits; k += 8) {
+  for (int k = 0; k < SPLITS; ++k) v[k] = *reinterpret_cast<const f32x4*>(ws + (long long)k * n + idx);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += *reinterpret_cast<const f32x4*>(ws + (long long)(k + j) * n + idx);
-  }
-  for (; k < splits; ++k) acc[0] += *reinterpret_cast<const f32x4*>(ws + (long long)k * n + idx);
-  const f32x4 s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  for (int w = SPLITS / 2; w > 0; w /= 2)
+#pragma unroll
+    for (int k = 0; k < w; ++k) v[k] += v[k + w];
+  const f32x4 s = v[0];
   const int m = (int)(idx / R), r = (int)(idx - (long long)m * R);
   uint16_t* o = out + (long long)m * out_sm + (long long)(sg.ocol[seg_of(sg, m)] + r) * out_sr;
 #pragma unroll
@@ -193,7 +193,7 @@ __global__ __launch_bounds__(256) void lora_wgrad_reduce_kernel(const float* __r
 extern "C" int ftc_lora_wgrad_splits(int T, int M) {
   const int ncb = M / MB;
   int s = 1;
-  while (s * 2 * ncb <= 1024 && T % (s * 2 * TT) == 0 && T / (s * 2) >= 256) s *= 2;
+  while (s < 64 && s * 2 * ncb <= 1024 && T % (s * 2 * TT) == 0 && T / (s * 2) >= 256) s *= 2;
   return s;
 }
 
@@ -223,7 +223,17 @@ extern "C" int ftc_lora_wgrad(const void* x, long long ldx, const void* y, long 
     hipLaunchKernelGGL(lora_wgrad_kernel<1>, dim3(ncb * splits), dim3(256), 0, stream, (const uint16_t*)x, ldx,
                        (const uint16_t*)y, ldy, ws, M, R, rows, ncb, sg);
   const long long n = (long long)M * R;
-  hipLaunchKernelGGL(lora_wgrad_reduce_kernel, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, stream, ws, splits, M,
-                     R, (uint16_t*)out, out_sm, out_sr, alpha, beta, sg);
+  const dim3 rg((unsigned)((n / 4 + 255) / 256));
+  auto out16 = (uint16_t*)out;
+#define FTC_RED(SP)                                                                                       \
+  case SP:                                                                                                \
+    hipLaunchKernelGGL(lora_wgrad_reduce_kernel<SP>, rg, dim3(256), 0, stream, ws, M, R, out16, out_sm, out_sr, \
+                       alpha, beta, sg);                                                                  \
+    break;
+  switch (splits) {
+    FTC_RED(1) FTC_RED(2) FTC_RED(4) FTC_RED(8) FTC_RED(16) FTC_RED(32) FTC_RED(64)
+    default: return -1;
+  }
+#undef FTC_RED
   return (int)hipGetLastError();
 }
