@@ -20,6 +20,11 @@ int ftc_rope(void* qkv, const float* cosT, const float* sinT, const int* positio
 int ftc_swiglu_fwd(const void* gu, void* a, long long rows, int F, long long a_rs, hipStream_t stream);
 int ftc_swiglu_bwd(const void* da, const void* gu, void* dgu, long long rows, int F, long long dgu_rs,
                    hipStream_t stream);
+int ftc_swiglu_fwd_lora(const void* gu, void* h, long long rows, int F, long long h_rs, const void* Am, long long lda,
+                        int nct, int Rp, hipStream_t stream);
+int ftc_swiglu_bwd_lora(const void* da, long long da_rs, const void* gu, void* dgu, long long rows, int F,
+                        long long dgu_rs, const void* Bt, long long ldb, int nct, int split, int Rp,
+                        hipStream_t stream);
 int ftc_ce_fwd_bwd(void* logits, const long long* labels, float* loss, float* lse, long long rows, int V, long long ld,
                    float gscale, long long ignore_index, hipStream_t stream);
 int ftc_adamw(void* param_bf16, float* master, float* m, float* v, const void* grad, int grad_is_fp32, long long n,
@@ -195,6 +200,54 @@ at::Tensor swiglu_bwd(const at::Tensor& da, const at::Tensor& gu, int64_t pad) {
                        cur_stream()),
         "swiglu_bwd");
   return pad ? dbuf.narrow(1, 0, gu.size(1)) : dbuf;
+}
+
+// SwiGLU fused with the LoRA rank product of its output (fwd: h (sA)^T, bwd: dgu B) written into the
+// tail columns of the row-padded result (csrc/kernels/swiglu_lora.hip).  `am` / `bt` are row views
+// [>= 16 nct, F] / [>= 16 nct, 2F] with unit column stride; Rp = pad (all pad columns are written).
+inline void need_rowview(const at::Tensor& t, int64_t min_rows, int64_t cols, const char* name) {
+  need(t, at::kBFloat16, name);
+  TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1 && t.size(0) >= min_rows && t.size(1) == cols, name,
+              " must be a [>=", min_rows, ", ", cols, "] row view");
+  TORCH_CHECK(t.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name,
+              " rows must be 16-byte aligned");
+}
+
+at::Tensor swiglu_fwd_lora(const at::Tensor& gu, int64_t pad, const at::Tensor& am, int64_t nct) {
+  need(gu, at::kBFloat16, "gu");
+  need_rows(gu, "gu");
+  const long long rows = gu.size(0);
+  const int F = (int)(gu.size(1) / 2);
+  TORCH_CHECK(F % 128 == 0, "swiglu_fwd_lora: F must be a multiple of 128");
+  TORCH_CHECK(nct >= 1 && nct <= 4 && pad >= 16 * nct && pad % 16 == 0, "swiglu_fwd_lora: bad nct/pad");
+  need_rowview(am, 16 * nct, F, "am");
+  auto abuf = at::empty({rows, F + pad}, gu.options());
+  check(ftc_swiglu_fwd_lora(gu.data_ptr(), abuf.data_ptr(), rows, F, F + pad, am.data_ptr(), am.stride(0), (int)nct,
+                            (int)pad, cur_stream()),
+        "swiglu_fwd_lora");
+  return abuf.narrow(1, 0, F);
+}
+
+at::Tensor swiglu_bwd_lora(const at::Tensor& da, const at::Tensor& gu, int64_t pad, const at::Tensor& bt,
+                           int64_t nct, bool split) {
+  need(da, at::kBFloat16, "da");
+  need(gu, at::kBFloat16, "gu");
+  need_rows(gu, "gu");
+  TORCH_CHECK(da.dim() == 2 && da.stride(1) == 1 && da.stride(0) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(da.data_ptr()) % 16 == 0,
+              "swiglu_bwd_lora: da must be a 16-byte aligned row view");
+  TORCH_CHECK(da.size(0) == gu.size(0) && gu.size(1) == 2 * da.size(1), "swiglu_bwd_lora shapes");
+  const int F = (int)da.size(1);
+  TORCH_CHECK(F % 128 == 0, "swiglu_bwd_lora: F must be a multiple of 128");
+  TORCH_CHECK(!split || nct % 2 == 0, "swiglu_bwd_lora: split needs an even tile count");
+  TORCH_CHECK(nct >= 1 && nct <= 4 && pad >= 16 * nct && pad % 16 == 0, "swiglu_bwd_lora: bad nct/pad");
+  need_rowview(bt, 16 * nct, 2 * F, "bt");
+  auto dbuf = at::empty({gu.size(0), gu.size(1) + pad}, gu.options());
+  check(ftc_swiglu_bwd_lora(da.data_ptr(), da.stride(0), gu.data_ptr(), dbuf.data_ptr(), gu.size(0), F,
+                            gu.size(1) + pad, bt.data_ptr(), bt.stride(0), (int)nct, split ? 1 : 0, (int)pad,
+                            cur_stream()),
+        "swiglu_bwd_lora");
+  return dbuf.narrow(1, 0, gu.size(1));
 }
 
 // ---------------- cross entropy (in place on logits) ----------------
@@ -439,6 +492,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("rope_", &rope_);
   m.def("swiglu_fwd", &swiglu_fwd, py::arg("gu"), py::arg("pad") = 0);
   m.def("swiglu_bwd", &swiglu_bwd, py::arg("da"), py::arg("gu"), py::arg("pad") = 0);
+  m.def("swiglu_fwd_lora", &swiglu_fwd_lora, py::arg("gu"), py::arg("pad"), py::arg("am"), py::arg("nct"));
+  m.def("swiglu_bwd_lora", &swiglu_bwd_lora, py::arg("da"), py::arg("gu"), py::arg("pad"), py::arg("bt"),
+        py::arg("nct"), py::arg("split") = false);
   m.def("ce_fwd_bwd_", &ce_fwd_bwd_);
   m.def("adamw_", &adamw_);
   m.def("grad_sumsq", &grad_sumsq);

@@ -28,7 +28,7 @@ from torch.utils.checkpoint import checkpoint
 
 from .. import ops
 from .config import ModelConfig
-from ..ops.linear import AugWeight
+from ..ops.linear import AugWeight, LoRATail
 from .lora import LoRAConfig, make_pairs
 
 
@@ -79,6 +79,17 @@ class LlamaLayer(nn.Module):
             return 0
         return aw.Rp
 
+    def tail(self, name: str, pad: int):
+        """LoRATail of an augmented projection (its producer kernel may form the rank-r tail product),
+        or None where the consumer does not take the augmented path (QLoRA, LoRA dropout, no pad)."""
+        aw = self.aug.get(name)
+        if pad <= 0 or aw is None or name in self.qweights or name not in self.lora:
+            return None
+        pair = self.lora[name]
+        if self.training and pair.dropout > 0.0:
+            return None
+        return LoRATail(aw, pair.A, pair.B, pair.scale, pair.blocks)
+
     def proj(self, name: str, x: torch.Tensor) -> torch.Tensor:
         pair = self.lora[name] if name in self.lora else None
         qw = self.qweights.get(name)
@@ -106,7 +117,8 @@ class LlamaLayer(nn.Module):
         o = self.proj("o", a)
         h, x = ops.add_rms_norm(h, o, self.mlp_norm, cfg.norm_eps, pad=p_gu, grad_pad=p_o)
         gu = self.proj("gu", x)
-        act = ops.swiglu(gu, out_pad=p_down, grad_pad=p_gu)
+        act = ops.swiglu(gu, out_pad=p_down, grad_pad=p_gu, fwd_tail=self.tail("down", p_down),
+                         bwd_tail=self.tail("gu", p_gu))
         return h, self.proj("down", act)
 
 

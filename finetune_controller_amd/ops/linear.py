@@ -119,6 +119,41 @@ def _mm_into(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor):
         torch.mm(a, b, out=out)
 
 
+# Tail products already formed by the producer kernel of an operand (one slot per direction; every
+# augmented GEMM call of that direction consumes the slot, so a mark never outlives its consumer).
+_PREFILLED: dict[str, tuple] = {}
+
+
+def _operand_key(t: torch.Tensor, aug) -> tuple:
+    return (t.data_ptr(), t.stride(0), t.shape[0], id(aug), aug._key)
+
+
+def mark_prefilled(direction: str, t: torch.Tensor, aug) -> None:
+    """``t`` ([T, width] row view) already holds the tail product of ``aug`` in its spare columns."""
+    _PREFILLED[direction] = _operand_key(t, aug)
+
+
+def take_prefilled(direction: str, t: torch.Tensor, aug) -> bool:
+    v = _PREFILLED.pop(direction, None)
+    return v is not None and v == _operand_key(t, aug)
+
+
+class LoRATail:
+    """What a producer kernel needs to form the LoRA tail of its consumer's augmented GEMM."""
+
+    __slots__ = ("aug", "A", "B", "scale", "split")
+
+    def __init__(self, aug, A, B, scale, blocks=None):
+        self.aug, self.A, self.B, self.scale = aug, A, B, float(scale)
+        # two-segment block-diagonal B (packed gate|up) whose halves own 16-aligned tail column
+        # ranges: the producer feeds each half of its output only to its own tail tiles
+        R = aug.R
+        self.split = bool(blocks is not None and len(blocks) == 2 and R % 32 == 0
+                          and tuple(blocks[0][2:]) == (0, R // 2) and tuple(blocks[1][2:]) == (R // 2, R)
+                          and blocks[0][0] == 0 and blocks[0][1] == blocks[1][0] == aug.N // 2
+                          and blocks[1][1] == aug.N)
+
+
 def _wide(t: torch.Tensor, width: int) -> torch.Tensor:
     return t.as_strided((t.shape[0], width), (t.stride(0), 1), t.storage_offset())
 
@@ -156,7 +191,31 @@ class AugWeight:
         torch.mul(A, scale, out=self.big[N:N + R, :K])
         if self.bigT is not None:
             self.bigT[:, N:N + R].copy_(self.big[N:N + R, :K].t())
+        if self.bt is not None:
+            self.bt[:R].copy_(B.t())
         self._key = key
+
+    # ---- producer-side tail products (csrc/kernels/swiglu_lora.hip): the kernel that produces this
+    # projection's input (forward) or output gradient (backward) forms s x A^T / dy B itself.
+    bt: torch.Tensor | None = None  # B^T [Rp, N] (rows past R zero), kept only when a producer asks
+
+    @property
+    def nct(self) -> int:
+        """16-wide column tiles that hold the R live tail columns."""
+        return -(-self.R // 16)
+
+    def fwd_tail_operand(self, A: torch.Tensor, B: torch.Tensor, scale: float) -> torch.Tensor:
+        """[Rp, K] row view of [s A ; 0] (refreshed)."""
+        self.refresh(A, B, scale)
+        return self.big[self.N:, :self.K]
+
+    def bwd_tail_operand(self, A: torch.Tensor, B: torch.Tensor, scale: float) -> torch.Tensor:
+        """[Rp, N] contiguous B^T (refreshed)."""
+        if self.bt is None:
+            self.bt = torch.zeros(self.Rp, self.N, device=self.big.device, dtype=self.big.dtype)
+            self._key = None
+        self.refresh(A, B, scale)
+        return self.bt
 
     # ---- backward operand in the "TN" layout.  hipBLASLt runs dx = [dy | dyB] . [W ; sA] 14-16 %
     # faster when the right operand is stored K-contiguous (tools/bench_gemm_layouts.py), so a
@@ -167,6 +226,7 @@ class AugWeight:
 
     def invalidate(self):
         self.bigT = None
+        self.bt = None
         self._key = None
 
     def bwd_operand(self) -> torch.Tensor:
@@ -262,8 +322,10 @@ class _LoRALinearFn(torch.autograd.Function):
         if use_aug:
             Rp = aug.Rp
             aug.refresh(A, B, scale)
-            # [s x A^T | 0] straight into the spare columns of the producer's buffer
-            _mm_into(x2, aug.big[N:, :K].t(), _tail(x2, K, Rp))
+            # [s x A^T | 0] straight into the spare columns of the producer's buffer (unless the
+            # producer kernel already formed it: ops.activation.swiglu)
+            if not take_prefilled("fwd", x2, aug):
+                _mm_into(x2, aug.big[N:, :K].t(), _tail(x2, K, Rp))
             xa = _tail(x2, K, aug.R)  # = s * x A^T
             torch.mm(_wide(x2, K + Rp), aug.big[:N].t(), out=y)
         else:
@@ -309,7 +371,8 @@ class _LoRALinearFn(torch.autograd.Function):
             # dx = [dy | dy B | 0] . [W ; s A ; 0]: dy B lands in the spare columns of the producer's buffer
             Rp = aug.Rp
             aug.refresh(A, B, s)
-            _mm_into(dy2, aug.big[:N, aug.K:], _tail(dy2, N, Rp))
+            if not take_prefilled("bwd", dy2, aug):
+                _mm_into(dy2, aug.big[:N, aug.K:], _tail(dy2, N, Rp))
             dyb = _tail(dy2, N, aug.R)
             rhs = aug.bwd_operand() if _TN_BWD else aug.big[:, :aug.K]
             dx = torch.mm(_wide(dy2, N + Rp), rhs).view(ctx.shp)

@@ -82,6 +82,46 @@ def test_swiglu(C):
     torch.testing.assert_close(dgu.float(), gv.grad, atol=3e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("rows,F,R,pad,split", [(200, 384, 16, 64, False), (4096, 1024, 40, 64, False),
+                                                 (33, 128, 64, 64, False), (16, 256, 8, 16, False),
+                                                 (300, 512, 32, 64, True), (77, 640, 64, 64, True)])
+def test_swiglu_lora_tail(C, rows, F, R, pad, split):
+    """swiglu_{fwd,bwd}_lora (csrc/kernels/swiglu_lora.hip): the SwiGLU result plus its rank-R product
+    in the tail columns of the padded buffer, against fp32 products of the stored bf16 values."""
+    torch.manual_seed(0)
+    nct = -(-R // 16)
+    gu = bf(torch.randn(rows, 2 * F, device=DEV))
+    # forward: tail = h (sA)^T with sA the rows of a padded [pad, F (+ extra cols)] operand view
+    big = torch.zeros(pad + 3, F + 24, device=DEV, dtype=torch.bfloat16)
+    big[:R, :F] = bf(torch.randn(R, F, device=DEV) * 0.1)
+    am = big[:pad, :F]
+    a = C.swiglu_fwd_lora(gu, pad, am, nct)
+    assert a.shape == (rows, F) and a.stride(0) == F + pad
+    g, u = gu.float().chunk(2, -1)
+    torch.testing.assert_close(a.float(), torch.nn.functional.silu(g) * u, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(a, C.swiglu_fwd(gu), atol=0, rtol=0)  # bit-identical to the plain kernel
+    full = a.as_strided((rows, F + pad), (F + pad, 1))
+    tail = full[:, F:].float()
+    ref = a.float() @ am[:R].float().t()
+    torch.testing.assert_close(tail[:, :R], ref, atol=2e-2 * ref.abs().max().item() + 1e-3, rtol=2e-2)
+    assert torch.count_nonzero(tail[:, R:]) == 0
+    # backward: tail = dgu B with B^T [pad, 2F]
+    da = bf(torch.randn(rows, F, device=DEV))
+    bt = torch.zeros(pad, 2 * F, device=DEV, dtype=torch.bfloat16)
+    bt[:R] = bf(torch.randn(R, 2 * F, device=DEV) * 0.1)
+    if split:  # block-diagonal B: gate rows feed tail columns [0, R/2), up rows [R/2, R)
+        bt[:R // 2, F:] = 0
+        bt[R // 2:R, :F] = 0
+    dgu = C.swiglu_bwd_lora(da, gu, pad, bt, nct, split)
+    assert dgu.shape == (rows, 2 * F) and dgu.stride(0) == 2 * F + pad
+    torch.testing.assert_close(dgu, C.swiglu_bwd(da, gu), atol=0, rtol=0)
+    fullb = dgu.as_strided((rows, 2 * F + pad), (2 * F + pad, 1))
+    tailb = fullb[:, 2 * F:].float()
+    refb = dgu.float() @ bt[:R].float().t()
+    torch.testing.assert_close(tailb[:, :R], refb, atol=2e-2 * refb.abs().max().item() + 1e-3, rtol=2e-2)
+    assert torch.count_nonzero(tailb[:, R:]) == 0
+
+
 @pytest.mark.parametrize("V", [128256, 32000, 50257])
 def test_cross_entropy_inplace(C, V):
     torch.manual_seed(0)
