@@ -42,15 +42,19 @@ def init_distributed(device_type: str = "auto", timeout_s: int = 1800) -> DistIn
         # device_count() does not initialise the HIP runtime on this image; is_available() does
         device_type = "cuda" if torch.cuda.device_count() > 0 and torch.cuda.is_available() else "cpu"
     if device_type == "cuda":
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
+        # FTC_SHARE_GPU=1: several ranks on one card (rehearsing the multi-GPU path on a 1-GPU box)
+        idx = local % torch.cuda.device_count() if os.environ.get("FTC_SHARE_GPU") == "1" else local
+        torch.cuda.set_device(idx)
+        device = torch.device("cuda", idx)
     else:
         device = torch.device("cpu")
     backend = "none"
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
-        backend = "nccl" if device.type == "cuda" else "gloo"
+        # nccl (= RCCL over xGMI) for GPU ranks; FTC_DIST_BACKEND=gloo forces host collectives (CPU
+        # tests, shared-card rehearsals where RCCL refuses two ranks on one device)
+        backend = os.environ.get("FTC_DIST_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
         if not dist.is_initialized():
             kw = {}
             if backend == "nccl":
@@ -63,7 +67,7 @@ def init_distributed(device_type: str = "auto", timeout_s: int = 1800) -> DistIn
 def barrier(info: DistInfo):
     if info.distributed:
         if info.backend == "nccl":
-            dist.barrier(device_ids=[info.local_rank])
+            dist.barrier(device_ids=[info.device.index])
         else:
             dist.barrier()
 
