@@ -37,6 +37,8 @@ def main(argv=None) -> int:
     ap.add_argument("--lora-r", type=int, default=16)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--comm-engine", default="torch", choices=["torch", "native"])
+    ap.add_argument("--zero-stage", type=int, default=0, choices=[0, 1],
+                    help="1: ZeRO-1 -- AdamW state sharded over the data-parallel ranks (reduce-scatter + all-gather)")
     ap.add_argument("--checkpoint-layers", action="store_true")
     ap.add_argument("--kernels", default=None, choices=["hip", "torch"],
                     help="torch = stock PyTorch-ROCm ops (the 'before' row)")
@@ -57,7 +59,7 @@ def main(argv=None) -> int:
 
     tc = TrainConfig(model=a.model, method=a.method, lora_r=a.lora_r, lora_alpha=2.0 * a.lora_r,
                      batch_size=a.batch_size, seq_len=a.seq_len, synthetic=True, max_steps=a.warmup + a.steps,
-                     warmup_steps=0, schedule="constant", lr=1e-4, bucket_mb=a.bucket_mb, comm_engine=a.comm_engine,
+                     warmup_steps=0, schedule="constant", lr=1e-4, bucket_mb=a.bucket_mb, comm_engine=a.comm_engine, zero_stage=a.zero_stage,
                      checkpoint_layers=a.checkpoint_layers, save_model=False, resume=False, device="cuda")
     tr = Trainer(tc)
     info = tr.info
@@ -122,9 +124,10 @@ def main(argv=None) -> int:
                 "micro_batch_per_gpu": a.batch_size,
                 "seq_len": a.seq_len,
                 "tokens_per_step": a.batch_size * a.seq_len * n,
-                "parallelism": f"dp{n}",
+                "parallelism": f"dp{n}" + ("-zero1" if a.zero_stage and n > 1 else ""),
                 "kernels": _backend.kernel_mode(),
                 "comm_engine": a.comm_engine,
+                "zero_stage": a.zero_stage,
             },
             "loss": round(loss, 4),
             "model_tflops_per_gpu": round(value * flops_tok / n / 1e12, 1),

@@ -210,9 +210,10 @@ def load_hf_checkpoint(model, path: str) -> int:
 
 # ---------------- resume checkpoints ----------------
 
-def save_resume(path: str, step: int, opt, data_state: dict, extra: dict | None = None):
+def save_resume(path: str, step: int, opt, data_state: dict, extra: dict | None = None, opt_state: dict | None = None):
+    opt_state = opt.state_dict() if opt_state is None else opt_state
     st = {"step": step, "param_flat": opt.param_flat.detach().cpu(), "opt": {k: (v.detach().cpu() if torch.is_tensor(v) else v)
-                                                                            for k, v in opt.state_dict().items()},
+                                                                            for k, v in opt_state.items()},
           "data": data_state, "extra": extra or {}}
     tmp = path + ".tmp"
     torch.save(st, tmp)
@@ -230,5 +231,7 @@ def latest_resume(ckpt_dir: str) -> str | None:
 def load_resume(path: str, opt) -> dict:
     st = torch.load(path, map_location="cpu", weights_only=True)
     opt.param_flat.copy_(st["param_flat"])
-    opt.load_state_dict({k: (v.to(opt.device) if torch.is_tensor(v) else v) for k, v in st["opt"].items()})
+    # full-layout state; a sharded (ZeRO-1) optimizer slices out its own part
+    dev = "cpu" if hasattr(opt, "shard_ranges") else opt.device
+    opt.load_state_dict({k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in st["opt"].items()})
     return st

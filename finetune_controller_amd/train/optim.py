@@ -34,7 +34,7 @@ def _align(n: int) -> int:
 
 class FlatAdamW:
     def __init__(self, params, lr: float = 2e-4, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-                 max_grad_norm: float = 1.0, grad_scale: float = 1.0):
+                 max_grad_norm: float = 1.0, grad_scale: float = 1.0, bucket_elems: int = 0, pad_multiple: int = 1):
         seen, plist = set(), []
         for p in params:
             if p.requires_grad and id(p) not in seen:
@@ -49,10 +49,27 @@ class FlatAdamW:
         self.device = plist[0].device
         self.params = list(reversed(plist))
         self.offsets: list[tuple[int, int]] = []
-        off = 0
+        # bucket plan (ZeRO-1 sharding): contiguous [start, end) ranges closed once they reach
+        # bucket_elems, each padded to a multiple of pad_multiple elements so it splits evenly over ranks
+        self.buckets: list[tuple[int, int]] = []
+        self.bucket_params: list[list] = []
+        self.bucket_elems = bucket_elems
+        off = start = 0
+        members: list = []
+        quantum = ALIGN * max(1, pad_multiple)
         for p in self.params:
             self.offsets.append((off, p.numel()))
             off += _align(p.numel())
+            members.append(p)
+            if bucket_elems and off - start >= bucket_elems:
+                off = -(-off // quantum) * quantum
+                self.buckets.append((start, off))
+                self.bucket_params.append(members)
+                start, members = off, []
+        if bucket_elems and members:
+            off = -(-off // quantum) * quantum
+            self.buckets.append((start, off))
+            self.bucket_params.append(members)
         self.numel = off
         self.param_flat = torch.zeros(off, dtype=self.dtype, device=self.device)
         self.grad_flat = torch.zeros(off, dtype=self.dtype, device=self.device)
@@ -63,14 +80,23 @@ class FlatAdamW:
                 g = self.grad_flat[o:o + n].view_as(p)
                 p.grad = g
                 p.main_grad = g
-        self.master = self.param_flat.float() if self.dtype != torch.float32 else self.param_flat
-        self.exp_avg = torch.zeros(off, dtype=torch.float32, device=self.device)
-        self.exp_avg_sq = torch.zeros(off, dtype=torch.float32, device=self.device)
+        self._init_state()
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.max_grad_norm = max_grad_norm
         self.grad_scale = grad_scale  # e.g. 1/world_size when grads are summed by all-reduce
         self.step_count = 0
         self.last_grad_norm: torch.Tensor | None = None
+
+    def _init_state(self):
+        self.master = self.param_flat.float() if self.dtype != torch.float32 else self.param_flat
+        self.exp_avg = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        self.exp_avg_sq = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+
+    @torch.no_grad()
+    def sync_master(self):
+        """Re-derive the fp32 master copy from ``param_flat`` (after a broadcast / external load)."""
+        if self.master is not self.param_flat:
+            self.master.copy_(self.param_flat)
 
     def num_params(self) -> int:
         return sum(n for _, n in self.offsets)
@@ -124,6 +150,146 @@ class FlatAdamW:
         bump_param_generation()
         if self.master is not self.param_flat:
             self.param_flat.copy_(self.master)
+
+
+class ShardedFlatAdamW(FlatAdamW):
+    """ZeRO-1: the fp32 master weights and both AdamW moments are partitioned over the data-parallel
+    ranks (1/world of the optimizer state per GPU: 96 GB -> 12 GB for Llama-3-8B full fine-tuning on
+    8 x MI355X).
+
+    The flat layout is cut into buckets padded to a multiple of ``world`` (``bucket_elems``); rank r
+    owns slice r of every bucket.  ``parallel.ddp.GradBucketer`` reduce-scatters each bucket as soon
+    as backward has produced it (``grad_shard`` receives the summed slice -- same bytes on the wire as
+    half an all-reduce), ``step()`` updates the owned slices with the same HIP AdamW kernel (one launch
+    per bucket, writing bf16 straight into ``param_flat``) after an all-reduced global grad norm, and
+    the updated slices are all-gathered in place into every rank's ``param_flat``.
+
+    Checkpoints (``state_dict``) hold the gathered full-size state, so a run can resume on any world
+    size; ``state_dict`` / ``load_state_dict`` are collective calls."""
+
+    def __init__(self, params, world: int, rank: int, group=None, bucket_elems: int = 16 << 20, **kw):
+        self.world, self.rank, self.group = world, rank, group
+        super().__init__(params, bucket_elems=bucket_elems, pad_multiple=world, **kw)
+
+    def _init_state(self):
+        world, rank = self.world, self.rank
+        self.shard_ranges: list[tuple[int, int]] = []  # owned [lo, hi) of param_flat per bucket
+        self.shard_offsets: list[int] = []             # where each owned slice starts in the shard buffers
+        n = 0
+        for s, e in self.buckets:
+            L = (e - s) // world
+            self.shard_ranges.append((s + rank * L, s + (rank + 1) * L))
+            self.shard_offsets.append(n)
+            n += L
+        self.shard_numel = n
+        with torch.no_grad():
+            self.master = torch.empty(n, dtype=torch.float32, device=self.device)
+            for (lo, hi), o in zip(self.shard_ranges, self.shard_offsets):
+                self.master[o:o + hi - lo].copy_(self.param_flat[lo:hi])
+        self.exp_avg = torch.zeros(n, dtype=torch.float32, device=self.device)
+        self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=self.device)
+        self.grad_shard = torch.zeros(n, dtype=self.dtype, device=self.device)
+
+    @torch.no_grad()
+    def sync_master(self):
+        for b, (lo, hi) in enumerate(self.shard_ranges):
+            self.shard_view(b, self.master).copy_(self.param_flat[lo:hi])
+
+    def shard_view(self, b: int, t: torch.Tensor) -> torch.Tensor:
+        lo, hi = self.shard_ranges[b]
+        o = self.shard_offsets[b]
+        return t[o:o + hi - lo]
+
+    def _all_gather_params(self):
+        import torch.distributed as dist
+
+        gloo = dist.get_backend(self.group) == "gloo"
+        works = []
+        for b, (s, e) in enumerate(self.buckets):
+            lo, hi = self.shard_ranges[b]
+            src = self.param_flat[lo:hi]
+            # RCCL gathers in place (input == output + rank * count); gloo gets a private copy
+            works.append(dist.all_gather_into_tensor(self.param_flat[s:e], src.clone() if gloo else src,
+                                                     group=self.group, async_op=True))
+        for w in works:
+            w.wait()
+
+    @torch.no_grad()
+    def step(self, lr: float | None = None):
+        import torch.distributed as dist
+
+        lr = self.lr if lr is None else lr
+        self.step_count += 1
+        bump_param_generation()
+        b1, b2 = self.betas
+        g = self.grad_shard
+        if use_hip(g) and self.dtype in (torch.bfloat16, torch.float32):
+            stats = ext().grad_sumsq(g, 0.0, 1.0)  # local sum of squares of the owned slices
+            dist.all_reduce(stats[0:1], group=self.group)
+            norm = stats[0:1].sqrt() * self.grad_scale
+            coef = torch.ones_like(norm)
+            if self.max_grad_norm and self.max_grad_norm > 0:
+                coef = torch.where(norm > self.max_grad_norm, self.max_grad_norm / (norm + 1e-6), coef)
+            gscale = coef * self.grad_scale
+            self.last_grad_norm = stats[0:1]
+            for b in range(len(self.buckets)):
+                lo, hi = self.shard_ranges[b]
+                param = self.param_flat[lo:hi] if self.dtype == torch.bfloat16 else None
+                ext().adamw_(param, self.shard_view(b, self.master), self.shard_view(b, self.exp_avg),
+                             self.shard_view(b, self.exp_avg_sq), self.shard_view(b, g), lr, b1, b2, self.eps,
+                             self.wd, self.step_count, gscale)
+                if param is None:
+                    self.param_flat[lo:hi].copy_(self.shard_view(b, self.master))
+        else:
+            gf = g.float() * self.grad_scale
+            sq = (gf * gf).sum().reshape(1)
+            dist.all_reduce(sq, group=self.group)
+            self.last_grad_norm = sq / (self.grad_scale ** 2)
+            norm = sq.sqrt()
+            if self.max_grad_norm and self.max_grad_norm > 0:
+                gf = gf * torch.clamp(self.max_grad_norm / (norm + 1e-6), max=1.0)
+            bc1, bc2 = 1 - b1 ** self.step_count, 1 - b2 ** self.step_count
+            self.exp_avg.mul_(b1).add_(gf, alpha=1 - b1)
+            self.exp_avg_sq.mul_(b2).addcmul_(gf, gf, value=1 - b2)
+            self.master.mul_(1 - lr * self.wd)
+            self.master.addcdiv_(self.exp_avg / bc1, (self.exp_avg_sq / bc2).sqrt_().add_(self.eps), value=-lr)
+            for b in range(len(self.buckets)):
+                lo, hi = self.shard_ranges[b]
+                self.param_flat[lo:hi].copy_(self.shard_view(b, self.master))
+        self._all_gather_params()
+
+    def grad_norm(self) -> float:
+        if self.last_grad_norm is None:
+            return 0.0
+        return float(self.last_grad_norm.float().sqrt().item()) * self.grad_scale
+
+    def _gather_full(self, shard: torch.Tensor) -> torch.Tensor:
+        """Full-layout fp32 copy (CPU) of a sharded state tensor; zeros in the padding."""
+        import torch.distributed as dist
+
+        out = torch.zeros(self.numel, dtype=torch.float32)
+        for b, (s, e) in enumerate(self.buckets):
+            full = torch.empty(e - s, dtype=torch.float32, device=self.device)
+            dist.all_gather_into_tensor(full, self.shard_view(b, shard).contiguous(), group=self.group)
+            out[s:e].copy_(full.cpu())
+        return out
+
+    def state_dict(self) -> dict:
+        return {"master": self._gather_full(self.master), "exp_avg": self._gather_full(self.exp_avg),
+                "exp_avg_sq": self._gather_full(self.exp_avg_sq), "step": self.step_count, "lr": self.lr,
+                "numel": self.numel}
+
+    @torch.no_grad()
+    def load_state_dict(self, sd: dict):
+        if int(sd["numel"]) != self.numel:
+            raise ValueError("optimizer state does not match the parameter layout")
+        for name in ("master", "exp_avg", "exp_avg_sq"):
+            full, dst = sd[name], getattr(self, name)
+            for b in range(len(self.buckets)):
+                lo, hi = self.shard_ranges[b]
+                self.shard_view(b, dst).copy_(full[lo:hi])
+        self.step_count = int(sd["step"])
+        bump_param_generation()
 
 
 def lr_at(step: int, base_lr: float, warmup: int, total: int, schedule: str = "cosine", min_ratio: float = 0.1) -> float:

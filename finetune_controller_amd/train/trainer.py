@@ -32,7 +32,7 @@ from ..parallel import dist as pdist
 from ..parallel.ddp import GradBucketer
 from ..utils.metrics import MetricsCSV
 from .data import PackedTokenDataset, SyntheticTokens
-from .optim import FlatAdamW, lr_at
+from .optim import FlatAdamW, ShardedFlatAdamW, lr_at
 
 log = logging.getLogger("ftc.train")
 
@@ -65,6 +65,7 @@ class TrainConfig:
     synthetic: bool = False
     bucket_mb: float = 64.0
     comm_engine: str = "torch"  # torch | native
+    zero_stage: int = 0  # 1: ZeRO-1 (optimizer state sharded over data-parallel ranks, reduce-scatter grads)
     checkpoint_layers: bool = False
     init_from: str = ""
     dtype: str = "auto"  # auto: bf16 on GPU, fp32 on CPU
@@ -110,13 +111,20 @@ class Trainer:
 
             quantize_model_(self.model)
         self.model.train()
-        self.opt = FlatAdamW([p for p in self.model.parameters() if p.requires_grad], lr=tc.lr,
-                             weight_decay=tc.weight_decay, max_grad_norm=tc.max_grad_norm,
-                             grad_scale=1.0 / (self.info.world_size * tc.grad_accum))
         # the loss is a per-micro-batch mean; summing grads over accum x world and scaling once
         # in the optimizer gives the global mean
+        okw = dict(lr=tc.lr, weight_decay=tc.weight_decay, max_grad_norm=tc.max_grad_norm,
+                   grad_scale=1.0 / (self.info.world_size * tc.grad_accum))
+        trainable = [p for p in self.model.parameters() if p.requires_grad]
+        if tc.zero_stage >= 1 and self.info.distributed:
+            esize = torch.finfo(self.dtype).bits // 8
+            self.opt = ShardedFlatAdamW(trainable, self.info.world_size, self.info.rank,
+                                        bucket_elems=max(1, int(tc.bucket_mb * 2 ** 20 / esize)), **okw)
+        else:
+            self.opt = FlatAdamW(trainable, **okw)
         if self.info.distributed:
             torch.distributed.broadcast(self.opt.param_flat, src=0)
+            self.opt.sync_master()
             if tc.method == "full":
                 pdist.broadcast_params_([p for p in self.model.parameters() if not p.requires_grad], self.info)
         tied = [self.model.lm_head] if self.cfg.tie_embeddings and tc.method == "full" else []
@@ -263,10 +271,12 @@ class Trainer:
         return last
 
     def save_resume(self):
+        opt_state = self.opt.state_dict()  # collective under ZeRO-1 (gathers the sharded state)
         if not self.is_main:
             return
         p = os.path.join(self.tc.checkpoint_path, f"checkpoint_step{self.step}.pt")
-        ckpt.save_resume(p, self.step, self.opt, self.data().state(), {"config": asdict(self.tc)})
+        ckpt.save_resume(p, self.step, self.opt, self.data().state(), {"config": asdict(self.tc)},
+                         opt_state=opt_state)
         # keep only the newest resume point
         for old in os.listdir(self.tc.checkpoint_path):
             if old.startswith("checkpoint_step") and old.endswith(".pt") and old != os.path.basename(p):
