@@ -25,6 +25,18 @@ import time
 BASELINE_METRIC = "fine-tune tokens/sec (whole node), Llama-3-8B LoRA at 1/2/4/8 MI355X"
 
 
+def _mark(op: str):
+    import torch
+
+    try:
+        if op == "push":
+            torch.cuda.nvtx.range_push("ftc_timed")
+        else:
+            torch.cuda.nvtx.range_pop()
+    except Exception:  # no roctx in this build: profiles fall back to whole-run stats
+        pass
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -73,6 +85,7 @@ def main(argv=None) -> int:
     sync()
     pdist.barrier(info)
     sync()
+    _mark("push")  # roctx range "ftc_timed" (rocprofv3 --marker-trace; tools/kstats_md.py filters on it)
     t0 = time.perf_counter()
     last = None
     for _ in range(a.steps):
@@ -81,6 +94,7 @@ def main(argv=None) -> int:
     pdist.barrier(info)
     sync()
     elapsed = time.perf_counter() - t0
+    _mark("pop")
     elapsed = pdist.all_reduce_max(elapsed, info)
     loss = float(last.float().item()) if last is not None else float("nan")
 
