@@ -52,6 +52,8 @@ def main(argv=None) -> int:
     ap.add_argument("--zero-stage", type=int, default=0, choices=[0, 1],
                     help="1: ZeRO-1 -- AdamW state sharded over the data-parallel ranks (reduce-scatter + all-gather)")
     ap.add_argument("--checkpoint-layers", action="store_true")
+    ap.add_argument("--ce-chunk-rows", type=int, default=int(os.environ.get("FTC_CE_CHUNK", "4096")),
+                    help="rows per lm_head + cross-entropy chunk (the only vocab-sized buffer)")
     ap.add_argument("--kernels", default=None, choices=["hip", "torch"],
                     help="torch = stock PyTorch-ROCm ops (the 'before' row)")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (not timed)")
@@ -72,7 +74,7 @@ def main(argv=None) -> int:
     tc = TrainConfig(model=a.model, method=a.method, lora_r=a.lora_r, lora_alpha=2.0 * a.lora_r,
                      batch_size=a.batch_size, seq_len=a.seq_len, synthetic=True, max_steps=a.warmup + a.steps,
                      warmup_steps=0, schedule="constant", lr=1e-4, bucket_mb=a.bucket_mb, comm_engine=a.comm_engine, zero_stage=a.zero_stage,
-                     checkpoint_layers=a.checkpoint_layers, save_model=False, resume=False, device="cuda")
+                     checkpoint_layers=a.checkpoint_layers, ce_chunk_rows=a.ce_chunk_rows, save_model=False, resume=False, device="cuda")
     tr = Trainer(tc)
     info = tr.info
     dev = tr.device
