@@ -25,6 +25,7 @@ int ftc_swiglu_fwd_lora(const void* gu, void* h, long long rows, int F, long lon
 int ftc_swiglu_bwd_lora(const void* da, long long da_rs, const void* gu, void* dgu, long long rows, int F,
                         long long dgu_rs, const void* Bt, long long ldb, int nct, int split, int Rp,
                         hipStream_t stream);
+int ftc_transpose(const void* x, long long ldx, void* y, long long ldy, int R, int C, hipStream_t stream);
 int ftc_ce_fwd_bwd(void* logits, const long long* labels, float* loss, float* lse, long long rows, int V, long long ld,
                    float gscale, long long ignore_index, hipStream_t stream);
 int ftc_adamw(void* param_bf16, float* master, float* m, float* v, const void* grad, int grad_is_fp32, long long n,
@@ -248,6 +249,29 @@ at::Tensor swiglu_bwd_lora(const at::Tensor& da, const at::Tensor& gu, int64_t p
                             cur_stream()),
         "swiglu_bwd_lora");
   return dbuf.narrow(1, 0, gu.size(1));
+}
+
+// ---------------- transpose ----------------
+// out[C, R] = x[R, C]^T for a 2-D bf16 row view x (unit column stride); out: contiguous [C, R] or None
+at::Tensor transpose2d(const at::Tensor& x, const c10::optional<at::Tensor>& out) {
+  need(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "transpose2d: x must be a 2-D row view");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "transpose2d: x rows must be 16-byte aligned");
+  const int64_t R = x.size(0), C = x.size(1);
+  TORCH_CHECK(R % 8 == 0 && C % 8 == 0, "transpose2d: both dims must be multiples of 8");
+  at::Tensor y;
+  if (out.has_value()) {
+    y = *out;
+    need(y, at::kBFloat16, "out");
+    need_rows(y, "out");
+    TORCH_CHECK(y.size(0) == C && y.size(1) == R, "transpose2d: out must be [C, R]");
+  } else {
+    y = at::empty({C, R}, x.options());
+  }
+  check(ftc_transpose(x.data_ptr(), x.stride(0), y.data_ptr(), y.stride(0), (int)R, (int)C, cur_stream()),
+        "transpose2d");
+  return y;
 }
 
 // ---------------- cross entropy (in place on logits) ----------------
@@ -495,6 +519,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("swiglu_fwd_lora", &swiglu_fwd_lora, py::arg("gu"), py::arg("pad"), py::arg("am"), py::arg("nct"));
   m.def("swiglu_bwd_lora", &swiglu_bwd_lora, py::arg("da"), py::arg("gu"), py::arg("pad"), py::arg("bt"),
         py::arg("nct"), py::arg("split") = false);
+  m.def("transpose2d", &transpose2d, py::arg("x"), py::arg("out") = py::none());
   m.def("ce_fwd_bwd_", &ce_fwd_bwd_);
   m.def("adamw_", &adamw_);
   m.def("grad_sumsq", &grad_sumsq);

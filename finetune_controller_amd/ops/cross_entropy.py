@@ -53,12 +53,11 @@ class _FusedLinearCE(torch.autograd.Function):
             dW = torch.zeros(W.shape, dtype=torch.float32, device=W.device)
         losses = torch.empty(T, dtype=torch.float32, device=h2.device)
         buf = None
-        # frozen head (LoRA / QLoRA): dh = dlogits . W through a cached W^T (TN GEMM layout, ~15 % faster)
-        WT = None
-        if need_dh and hip and not W.requires_grad:
-            from .linear import _TN_BWD, frozen_t
+        # dh = dlogits . W through a cached W^T (TN GEMM layout, ~15 % faster): frozen heads keep one
+        # copy, a trainable head (full FT) is re-transposed once per optimizer step
+        from .linear import _TN_DW, transpose2d, transposed_weight
 
-            WT = frozen_t.get(W) if _TN_BWD else None
+        WT = transposed_weight(W) if (need_dh and hip) else None
         for r0 in range(0, T, chunk_rows):
             r1 = min(T, r0 + chunk_rows)
             hc = h2[r0:r1]
@@ -78,7 +77,7 @@ class _FusedLinearCE(torch.autograd.Function):
                 torch.mm(dlog, W if WT is None else WT.t(), out=dh[r0:r1])
             if need_dw:
                 if mg is not None:
-                    mg.addmm_(dlog.t(), hc)
+                    mg.addmm_(dlog.t(), transpose2d(hc).t() if (hip and _TN_DW) else hc)
                 else:
                     dW.addmm_(dlog.t().float(), hc.float())
         loss = losses.sum() * gscale
