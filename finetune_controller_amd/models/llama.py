@@ -28,7 +28,7 @@ from torch.utils.checkpoint import checkpoint
 
 from .. import ops
 from .config import ModelConfig
-from ..ops.linear import AugWeight, LoRATail
+from ..ops.linear import AugWeight, LoRATail, TailOperands
 from .lora import LoRAConfig, make_pairs
 
 
@@ -52,6 +52,7 @@ class LlamaLayer(nn.Module):
         }
         self.lora = make_pairs(self.shapes, lora, device=device, dtype=dtype) if lora else nn.ModuleDict()
         self.qweights: dict[str, object] = {}  # QLoRA: proj -> NF4Weight (replaces the bf16 Parameter)
+        self.qtails: dict[str, TailOperands] = {}  # QLoRA: LoRA tail operands for fused producers
         # LoRA: the frozen base weight lives inside an augmented [N+R, K+R] buffer (ops.linear.AugWeight)
         # so the rank-r update rides along in the big GEMMs; the Parameter is a view of it
         self.aug: dict[str, AugWeight] = {}
@@ -81,12 +82,21 @@ class LlamaLayer(nn.Module):
 
     def tail(self, name: str, pad: int):
         """LoRATail of an augmented projection (its producer kernel may form the rank-r tail product),
-        or None where the consumer does not take the augmented path (QLoRA, LoRA dropout, no pad)."""
-        aw = self.aug.get(name)
-        if pad <= 0 or aw is None or name in self.qweights or name not in self.lora:
+        or None where the consumer does not take the augmented path (LoRA dropout, no pad)."""
+        if pad <= 0 or name not in self.lora:
             return None
         pair = self.lora[name]
         if self.training and pair.dropout > 0.0:
+            return None
+        if name in self.qweights:  # QLoRA: stand-alone tail operands next to the NF4 weight
+            qt = self.qtails.get(name)
+            if qt is None or qt.Rp != pad:
+                N, K = self.qweights[name].shape
+                qt = self.qtails[name] = TailOperands(N, K, pair.A.shape[0], pad, device=pair.A.device,
+                                                      dtype=pair.A.dtype)
+            return LoRATail(qt, pair.A, pair.B, pair.scale, pair.blocks)
+        aw = self.aug.get(name)
+        if aw is None:
             return None
         return LoRATail(aw, pair.A, pair.B, pair.scale, pair.blocks)
 
@@ -97,7 +107,8 @@ class LlamaLayer(nn.Module):
             from ..ops.nf4 import qlora_linear
 
             return qlora_linear(x, qw, pair.A if pair else None, pair.B if pair else None,
-                                pair.scale if pair else 1.0, pair.blocks if pair else None, pad=self.pad(name))
+                                pair.scale if pair else 1.0, pair.blocks if pair else None, pad=self.pad(name),
+                                tails=self.qtails.get(name))
         W = self.base_weight(name)
         if pair is None:
             return ops.lora_linear(x, W)

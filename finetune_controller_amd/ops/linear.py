@@ -177,6 +177,39 @@ def take_prefilled(direction: str, t: torch.Tensor, aug) -> bool:
     return v is not None and v == _operand_key(t, aug)
 
 
+class TailOperands:
+    """Stand-alone tail operands for a projection whose weight is not an ``AugWeight`` (QLoRA: the NF4
+    weight is dequantised per call into a shared scratch): ``[s A ; 0]`` as [Rp, K] and ``B^T`` as
+    [Rp, N], refreshed once per optimizer generation -- the same interface as AugWeight's
+    ``fwd_tail_operand`` / ``bwd_tail_operand``."""
+
+    def __init__(self, N: int, K: int, R: int, Rp: int, device=None, dtype=torch.bfloat16):
+        self.N, self.K, self.R, self.Rp = N, K, R, Rp
+        self.fwd = torch.zeros(Rp, K, device=device, dtype=dtype)
+        self.bt = torch.zeros(Rp, N, device=device, dtype=dtype)
+        self._key = None
+
+    @property
+    def nct(self) -> int:
+        return -(-self.R // 16)
+
+    def refresh(self, A: torch.Tensor, B: torch.Tensor, scale: float):
+        key = (_PARAM_GENERATION[0], A._version, B._version, A.data_ptr(), B.data_ptr(), float(scale))
+        if key == self._key:
+            return
+        torch.mul(A, scale, out=self.fwd[:self.R])
+        self.bt[:self.R].copy_(B.t())
+        self._key = key
+
+    def fwd_tail_operand(self, A, B, scale):
+        self.refresh(A, B, scale)
+        return self.fwd
+
+    def bwd_tail_operand(self, A, B, scale):
+        self.refresh(A, B, scale)
+        return self.bt
+
+
 class LoRATail:
     """What a producer kernel needs to form the LoRA tail of its consumer's augmented GEMM."""
 

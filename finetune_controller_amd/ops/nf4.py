@@ -22,7 +22,7 @@ from __future__ import annotations
 import torch
 
 from ._backend import ext, use_hip
-from .linear import _mm_into, _spare_cols, _tail, _wide, direct_grad_params, lora_weight_grads
+from .linear import _mm_into, _spare_cols, _tail, _wide, direct_grad_params, lora_weight_grads, take_prefilled
 
 NF4_CODE = torch.tensor([-1.0, -0.6961928009986877, -0.5250730514526367, -0.39491748809814453, -0.28444138169288635,
                          -0.18477343022823334, -0.09105003625154495, 0.0, 0.07958029955625534, 0.16093020141124725,
@@ -139,7 +139,7 @@ class _QLoRALinearFn(torch.autograd.Function):
     read-modify-writes nor a separate transpose pass exist."""
 
     @staticmethod
-    def forward(ctx, x, A, B, qw, scale, blocks, Rp):
+    def forward(ctx, x, A, B, qw, scale, blocks, Rp, tails=None):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         N, K = qw.shape
@@ -153,7 +153,9 @@ class _QLoRALinearFn(torch.autograd.Function):
             _dequant_into(qw, sc.fwd[:N, :K], False)
             sc.fwd[:N, K:K + R].copy_(B)
             torch.mul(A, scale, out=sc.fwd[N:N + R, :K])
-            _mm_into(x2, sc.fwd[N:, :K].t(), _tail(x2, K, Rp))
+            # the producer kernel (fused SwiGLU) may already have formed s x A^T in the spare columns
+            if tails is None or not take_prefilled("fwd", x2, tails):
+                _mm_into(x2, sc.fwd[N:, :K].t(), _tail(x2, K, Rp))
             xa = _tail(x2, K, R)  # s * x A^T
             y = torch.mm(_wide(x2, K + Rp), sc.fwd[:N].t())
         else:
@@ -163,6 +165,7 @@ class _QLoRALinearFn(torch.autograd.Function):
                 y.addmm_(xa, B.t(), alpha=scale)
         ctx.save_for_backward(x2, A, B, xa)
         ctx.qw, ctx.scale, ctx.blocks, ctx.shp, ctx.Rp, ctx.aug_fwd = qw, scale, blocks, shp, Rp, use_aug
+        ctx.tails = tails
         ctx.lora_params = direct_grad_params(A, B, blocks)
         return y if x.dim() == 2 else y.reshape(*shp[:-1], qw.shape[0]).clone()
 
@@ -180,8 +183,9 @@ class _QLoRALinearFn(torch.autograd.Function):
             if hip and A is not None and Rp > 0 and _spare_cols(dy2, N, Rp):
                 R = A.shape[0]
                 sc = _QScratch.get(N, K, Rp, dy2.device)
-                sc.Bp[:, :R].copy_(B)
-                _mm_into(dy2, sc.Bp, _tail(dy2, N, Rp))
+                if ctx.tails is None or not take_prefilled("bwd", dy2, ctx.tails):
+                    sc.Bp[:, :R].copy_(B)
+                    _mm_into(dy2, sc.Bp, _tail(dy2, N, Rp))
                 dyb = _tail(dy2, N, R)
                 _dequant_into(qw, sc.bwdT[:, :N], True)
                 sc.bwdT[:, N:N + R].copy_((A * s).t())
@@ -206,12 +210,13 @@ class _QLoRALinearFn(torch.autograd.Function):
             if need_a and dyb is None:
                 dyb = dy2 @ B
             dA, dB = lora_weight_grads(ctx.lora_params, dy2, xa, ctx.aug_fwd, dyb, x2, s, ctx.blocks, need_a, need_b)
-        return dx, dA, dB, None, None, None, None
+        return dx, dA, dB, None, None, None, None, None
 
 
-def qlora_linear(x, qw: NF4Weight, A=None, B=None, scale=1.0, blocks=None, pad: int = 0):
-    """``pad``: spare columns the producer of ``x`` (and of the output gradient) provides."""
-    return _QLoRALinearFn.apply(x, A, B, qw, scale, blocks, int(pad))
+def qlora_linear(x, qw: NF4Weight, A=None, B=None, scale=1.0, blocks=None, pad: int = 0, tails=None):
+    """``pad``: spare columns the producer of ``x`` (and of the output gradient) provides.  ``tails``
+    (ops.linear.TailOperands): the producer kernels may form the rank-r tail products themselves."""
+    return _QLoRALinearFn.apply(x, A, B, qw, scale, blocks, int(pad), tails)
 
 
 @torch.no_grad()
