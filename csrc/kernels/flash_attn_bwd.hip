@@ -77,6 +77,7 @@ struct BwdArgs {
   int B, S, H, KV;
   float scale, c;  // c = scale * log2(e)
   int causal, window;
+  int prio_young;  // dK/dV, 8 waves: s_setprio 1 for the second-dispatched half (guide T5 static form)
 };
 
 // ---------------------------------------------------------------- 1. delta
@@ -247,6 +248,9 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
   constexpr int LGKM_ZERO = 0xC07F;                                             // lgkmcnt(0)
 
   const int total = G * nqt;
+  // two waves per SIMD: the younger half loses VALU arbitration on every segment; one static
+  // priority raise (no per-segment flips) hands it the older half's timing (guide T5, static form)
+  if (WAVES == 8 && a.prio_young && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
   // K staging and the V fragments are ordinary loads: retire them before the first DMA so no
   // compiler-inserted wait inside the loop has to count them
   __builtin_amdgcn_s_waitcnt(VM_ZERO);
@@ -564,7 +568,12 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
   if ((long long)S * max_rs * 2 >= (1LL << 31) || 2LL * B * H * S * 4 >= (1LL << 31)) return -1;
   BwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)o, (const uint16_t*)dout,
             lse, (float*)workspace, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, q_rs, kv_rs, o_rs, dq_rs, dkv_rs, do_rs,
-            B, S, H, KV, scale, scale * LOG2E, causal, window};
+            B, S, H, KV, scale, scale * LOG2E, causal, window, 0};
+  static const int prio = [] {
+    const char* e = getenv("FTC_FLASH_BWD_PRIO");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  a.prio_young = prio;
   const int grid_d = ftc::stream_grid((long long)B * S, 4);
   const int g_kv = B * KV * (S / 256);
   const int g_q = B * H * (S / 128);

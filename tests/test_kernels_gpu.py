@@ -234,10 +234,11 @@ def test_flash_lse(C):
     torch.testing.assert_close(lse.view(H, S), torch.logsumexp(s, -1), atol=2e-3, rtol=1e-3)
 
 
-@pytest.mark.parametrize("window,aug", [(0, "1"), (0, "0"), (96, "1")])
-def test_llama_lora_step_hip_matches_torch_path(C, monkeypatch, window, aug):
-    """Whole decoder with LoRA on the HIP path (flash attention, fused norms, SwiGLU, augmented LoRA
-    GEMMs over padded producer buffers) against the stock-PyTorch path on the same weights."""
+@pytest.mark.parametrize("window,aug,ckpt", [(0, "1", False), (0, "0", False), (96, "1", False), (0, "1", True)])
+def test_llama_lora_step_hip_matches_torch_path(C, monkeypatch, window, aug, ckpt):
+    """Whole decoder with LoRA on the HIP path (flash attention, fused norms, SwiGLU with fused LoRA
+    tails, augmented LoRA GEMMs over padded producer buffers; optionally per-layer activation
+    checkpointing, i.e. the forward recomputed inside backward) against the stock-PyTorch path."""
     from finetune_controller_amd.models import LoRAConfig, build_model
     from finetune_controller_amd.models.config import ModelConfig
 
@@ -245,8 +246,8 @@ def test_llama_lora_step_hip_matches_torch_path(C, monkeypatch, window, aug):
     lc = LoRAConfig(r=8, alpha=16)
     torch.manual_seed(0)
     models = []
-    for _ in range(2):
-        m = build_model(cfg, lc, device=DEV, dtype=torch.bfloat16)
+    for i in range(2):
+        m = build_model(cfg, lc, device=DEV, dtype=torch.bfloat16, checkpoint_layers=ckpt and i == 0)
         m.init_weights(seed=5)
         m.freeze_base()
         models.append(m)
