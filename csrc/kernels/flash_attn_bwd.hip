@@ -144,7 +144,13 @@ FTC_DEV void dkdv_dma(__amdgpu_buffer_rsrc_t qr, __amdgpu_buffer_rsrc_t dr, __am
 // HW = 32-key halves per wave: HW = 2 -> 4 waves x 64 keys, one wave per SIMD (512-register budget);
 // HW = 1 -> 8 waves x 32 keys, two waves per SIMD (256 registers each): one wave's softmax VALU then
 // runs under the other wave's MFMAs.
-template <int D, int HW>
+// PP (8 waves only): "ping-pong" -- the two waves sharing a SIMD (w, w + 4) run each query slice's
+// two phases in opposite order between the same pair of barriers: half 0 does A(j) then B(j), half 1
+// does B(j - 1) then A(j), where A = the S / dP' MFMA chains and B = softmax / masking VALU + the
+// dV / dK MFMAs.  One wave's exp / mask / pack work then issues under its partner's MFMAs instead of
+// both waves idling the matrix pipe at the same time (guide: MI355X_MICROARCH.md "Two waves per
+// SIMD").  Slice j is read by half 1 one barrier interval later, so the Q/dO ring has 4 slots.
+template <int D, int HW, bool PP = false>
 __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
   constexpr int NCH = D / 8, DSTEPS = D / 16, DT = D / 32;
   constexpr int BKV = 256, BQ2 = 32;
@@ -158,6 +164,7 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
   __shared__ __attribute__((aligned(16))) char slot0[SLICE];
   __shared__ __attribute__((aligned(16))) char slot1[SLICE];
   __shared__ __attribute__((aligned(16))) char slot2[SLICE];
+  __shared__ __attribute__((aligned(16))) char slot3[PP ? SLICE : 16];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -259,19 +266,13 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
   if (total > 1) issue(1, slot1);
   // slice it computes from slot it % 3 and DMAs slice it + 2 into slot (it + 2) % 3, which held
   // slice it - 1 (finished by every wave before this slice's barrier)
-  auto body = [&](const int it, const char* Qs, char* dma_slot) __attribute__((always_inline)) {
-    const int qt = qbeg + (it % nqt) * BQ2;
-    if (it + 1 < total) __builtin_amdgcn_s_waitcnt(VM_ONE);  // slice it landed, it+1 may fly on
-    else __builtin_amdgcn_s_waitcnt(VM_ZERO);
-    __builtin_amdgcn_s_waitcnt(LGKM_ZERO);
-    __builtin_amdgcn_s_barrier();  // every wave's pieces of slice it are in
-    if (it + 2 < total) issue(it + 2, dma_slot);
+  f32x16 s[HW], dp[HW];  // S / dP' of the slice between phase A and phase B (registers)
+  // phase A: S[q][k], dP'[q][k] for both 32-key halves in one k-loop (rows q in registers, key on the
+  // lane): the Q / dO A-fragments are read once for both halves, four independent MFMA chains
+  auto phaseA = [&](const char* Qs) __attribute__((always_inline)) {
     const char* Ds = Qs + QBYTES;
     const float* lse_s = reinterpret_cast<const float*>(Ds + QBYTES);
     const float* dlt_s = lse_s + BQ2;
-    // ---- S[q][k], dP'[q][k] for both 32-key halves in one k-loop (rows q in registers, key on the
-    // lane): the Q / dO A-fragments are read once for both halves, four independent MFMA chains
-    f32x16 s[HW], dp[HW];
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
       const float4 lv = *reinterpret_cast<const float4*>(lse_s + 8 * g4 + 4 * hh);
@@ -313,8 +314,11 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
         if constexpr (Q > 0) __builtin_amdgcn_sched_group_barrier(0x100, Q, 0);
       }
     }
-    // ---- P, dS (bf16 B operands of the accumulating products)
-    bf16x8 pb[HW][2], sb[HW][2];
+  };
+  // phase B1: P, dS (bf16 B operands of the accumulating products) -- exp / mask / pack VALU work
+  bf16x8 pb[HW][2], sb[HW][2];
+  auto phaseB1 = [&](const int it) __attribute__((always_inline)) {
+    const int qt = qbeg + (it % nqt) * BQ2;
 #pragma unroll
     for (int j = 0; j < HW; ++j) {
       const int key = wkey0 + 32 * j + lr;
@@ -339,8 +343,11 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
       sb[j][0] = pack8_bf(dp[j], 0);
       sb[j][1] = pack8_bf(dp[j], 8);
     }
-    // ---- dV^T += dO^T P ; dK^T += Q^T dS for both halves (k of these MFMAs = the 32 query rows);
-    // the dO^T / Q^T tr-operands are read once and used by both halves
+  };
+  // phase B2: dV^T += dO^T P ; dK^T += Q^T dS for both halves (k of these MFMAs = the 32 query rows);
+  // the dO^T / Q^T tr-operands are read once and used by both halves
+  auto phaseB2 = [&](const char* Qs) __attribute__((always_inline)) {
+    const char* Ds = Qs + QBYTES;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
       const int2 to = tr_offsets<D>(dt * 32, lane);
@@ -357,10 +364,65 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
       }
     }
   };
-  for (int it = 0; it < total; it += 3) {
-    body(it, slot0, slot2);
-    if (it + 1 < total) body(it + 1, slot1, slot0);
-    if (it + 2 < total) body(it + 2, slot2, slot1);
+  // one barrier per slice: slice it is in LDS for every wave, the DMA of slice it + 2 goes out
+  auto sync_slice = [&](const int it, char* dma_slot) __attribute__((always_inline)) {
+    if (it + 1 < total) __builtin_amdgcn_s_waitcnt(VM_ONE);  // slice it landed, it+1 may fly on
+    else __builtin_amdgcn_s_waitcnt(VM_ZERO);
+    __builtin_amdgcn_s_waitcnt(LGKM_ZERO);
+    __builtin_amdgcn_s_barrier();  // every wave's pieces of slice it are in
+    if (it + 2 < total) issue(it + 2, dma_slot);
+  };
+  if constexpr (!PP) {
+    // slice it computes from slot it % 3 and DMAs slice it + 2 into slot (it + 2) % 3, which held
+    // slice it - 1 (finished by every wave before this slice's barrier)
+    auto body = [&](const int it, const char* Qs, char* dma_slot) __attribute__((always_inline)) {
+      sync_slice(it, dma_slot);
+      phaseA(Qs);
+      phaseB1(it);
+      phaseB2(Qs);
+    };
+    for (int it = 0; it < total; it += 3) {
+      body(it, slot0, slot2);
+      if (it + 1 < total) body(it + 1, slot1, slot0);
+      if (it + 2 < total) body(it + 2, slot2, slot1);
+    }
+  } else {
+    // 4-slot ring: slice it in slot it % 4; the DMA of slice it + 2 reuses the slot of slice it - 2,
+    // whose last reader (half 1's phase B2) finished before this slice's barrier.  Half 1 carries only
+    // the packed P / dS operands (16 VGPRs) across the barrier: A2 ... [B2(it-1) A(it) B1(it)] ...
+    // the halves run separate straight-line loops (one branch outside the loop, not one per slice:
+    // the register allocator then sees two independent paths) with the same barrier count
+    if (wave < 4) {  // waves w and w + 4 share a SIMD
+      auto body = [&](const int it, const char* Qs, char* dma_slot) __attribute__((always_inline)) {
+        sync_slice(it, dma_slot);
+        phaseA(Qs);
+        phaseB1(it);
+        phaseB2(Qs);
+      };
+      for (int it = 0; it < total; it += 4) {
+        body(it, slot0, slot2);
+        if (it + 1 < total) body(it + 1, slot1, slot3);
+        if (it + 2 < total) body(it + 2, slot2, slot0);
+        if (it + 3 < total) body(it + 3, slot3, slot1);
+      }
+    } else {
+      auto body = [&](const int it, const char* Qs, const char* Qprev, char* dma_slot) __attribute__((always_inline)) {
+        sync_slice(it, dma_slot);
+        if (it > 0) phaseB2(Qprev);
+        phaseA(Qs);
+        phaseB1(it);
+      };
+      for (int it = 0; it < total; it += 4) {
+        body(it, slot0, slot3, slot2);
+        if (it + 1 < total) body(it + 1, slot1, slot0, slot3);
+        if (it + 2 < total) body(it + 2, slot2, slot1, slot0);
+        if (it + 3 < total) body(it + 3, slot3, slot2, slot1);
+      }
+      if (total > 0) {
+        const int last = total - 1;
+        phaseB2((last & 3) == 0 ? slot0 : (last & 3) == 1 ? slot1 : (last & 3) == 2 ? slot2 : slot3);
+      }
+    }
   }
 
   // ---- epilogue: dK = scale * dK^T^T, dV; lane owns one key row per half
@@ -591,7 +653,15 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
   }();
   if (D == 128) {
     hipLaunchKernelGGL(bwd_delta_kernel<128>, dim3(grid_d), dim3(256), 0, stream, a);
-    if (dkdv_waves == 8)
+    // ping-pong phase order for the two waves of a SIMD (default; FTC_FLASH_DKDV_PP=0 turns it off):
+    // bwd 2.00 -> 1.97 ms at the Llama-3-8B layer shape (profiles/r1_attn_dkdv_pp.log)
+    static const bool pp = [] {
+      const char* e = getenv("FTC_FLASH_DKDV_PP");
+      return !(e && e[0] == '0');
+    }();
+    if (dkdv_waves == 8 && pp)
+      hipLaunchKernelGGL((bwd_dkdv_kernel<128, 1, true>), dim3(g_kv), dim3(512), 0, stream, a);
+    else if (dkdv_waves == 8)
       hipLaunchKernelGGL((bwd_dkdv_kernel<128, 1>), dim3(g_kv), dim3(512), 0, stream, a);
     else
       hipLaunchKernelGGL((bwd_dkdv_kernel<128, 2>), dim3(g_kv), dim3(256), 0, stream, a);
