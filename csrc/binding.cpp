@@ -25,6 +25,11 @@ int ftc_swiglu_fwd_lora(const void* gu, void* h, long long rows, int F, long lon
 int ftc_swiglu_bwd_lora(const void* da, long long da_rs, const void* gu, void* dgu, long long rows, int F,
                         long long dgu_rs, const void* Bt, long long ldb, int nct, int split, int Rp,
                         hipStream_t stream);
+int ftc_swiglu_wgrad_plan(long long T, int F, int* rb, long long* ws_floats);
+int ftc_swiglu_bwd_wgrad(const void* da, long long da_rs, const void* gu, void* dgu, long long dgu_rs, long long T,
+                         int F, const void* bt, long long ldb, const void* xa, long long xa_rs, const void* dyb,
+                         long long dyb_rs, float* ws, void* mgB, long long ldB, float alphaB, void* mgA, long long ldA,
+                         float alphaA, int Rp, hipStream_t stream);
 int ftc_transpose(const void* x, long long ldx, void* y, long long ldy, int R, int C, hipStream_t stream);
 int ftc_ce_fwd_bwd(void* logits, const long long* labels, float* loss, float* lse, long long rows, int V, long long ld,
                    float gscale, long long ignore_index, hipStream_t stream);
@@ -249,6 +254,56 @@ at::Tensor swiglu_bwd_lora(const at::Tensor& da, const at::Tensor& gu, int64_t p
                             cur_stream()),
         "swiglu_bwd_lora");
   return dbuf.narrow(1, 0, gu.size(1));
+}
+
+// SwiGLU backward + row tail dgu B_gu + LoRA weight gradients dB_gu (+=) and dA_down (+=) in one pass
+// (csrc/kernels/swiglu_lora.hip).  Per-segment rank 16: bt [>=32, 2F], xa [T, 32] view, dyb [T, 16] view,
+// mgB = B_gu.main_grad [2F, 32], mgA = A_down.main_grad [16, F] (both bf16, updated in place).
+bool swiglu_wgrad_ok(const at::Tensor& gu, int64_t pad) {
+  int rb;
+  long long wsf;
+  const long long T = gu.size(0), F = gu.size(1) / 2;
+  return gu.dim() == 2 && ftc_swiglu_wgrad_plan(T, (int)F, &rb, &wsf) == 0 && pad >= 32 && pad % 8 == 0 &&
+         T * 4LL * F < (1LL << 31) && T * (2 * F + pad) * 2 < (1LL << 31);
+}
+
+at::Tensor swiglu_bwd_wgrad(const at::Tensor& da, const at::Tensor& gu, int64_t pad, const at::Tensor& bt,
+                            const at::Tensor& xa, const at::Tensor& dyb, at::Tensor& mgB, at::Tensor& mgA,
+                            double alphaB, double alphaA) {
+  need(gu, at::kBFloat16, "gu");
+  need_rows(gu, "gu");
+  const long long T = gu.size(0);
+  const int F = (int)(gu.size(1) / 2);
+  TORCH_CHECK(swiglu_wgrad_ok(gu, pad), "swiglu_bwd_wgrad: unsupported shape");
+  TORCH_CHECK(da.dim() == 2 && da.size(0) == T && da.size(1) == F && da.stride(1) == 1 && da.stride(0) % 8 == 0,
+              "swiglu_bwd_wgrad: da must be a [T, F] row view");
+  need(da, at::kBFloat16, "da");
+  need_rowview(bt, 32, 2 * F, "bt");
+  need(xa, at::kBFloat16, "xa");
+  need(dyb, at::kBFloat16, "dyb");
+  TORCH_CHECK(xa.dim() == 2 && xa.size(0) == T && xa.size(1) == 32 && xa.stride(1) == 1 && xa.stride(0) % 8 == 0,
+              "swiglu_bwd_wgrad: xa must be a [T, 32] row view");
+  TORCH_CHECK(dyb.dim() == 2 && dyb.size(0) == T && dyb.size(1) == 16 && dyb.stride(1) == 1 && dyb.stride(0) % 8 == 0,
+              "swiglu_bwd_wgrad: dyb must be a [T, 16] row view");
+  for (const at::Tensor* t : {&da, &xa, &dyb})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "swiglu_bwd_wgrad: 16-byte aligned rows");
+  need(mgB, at::kBFloat16, "mgB");
+  need(mgA, at::kBFloat16, "mgA");
+  TORCH_CHECK(mgB.dim() == 2 && mgB.size(0) == 2 * F && mgB.size(1) == 32 && mgB.stride(1) == 1,
+              "swiglu_bwd_wgrad: mgB must be [2F, 32]");
+  TORCH_CHECK(mgA.dim() == 2 && mgA.size(0) == 16 && mgA.size(1) == F && mgA.stride(1) == 1,
+              "swiglu_bwd_wgrad: mgA must be [16, F]");
+  int rb;
+  long long wsf;
+  ftc_swiglu_wgrad_plan(T, F, &rb, &wsf);
+  auto ws = at::empty({wsf}, gu.options().dtype(at::kFloat));
+  auto dbuf = at::empty({T, 2 * F + pad}, gu.options());
+  check(ftc_swiglu_bwd_wgrad(da.data_ptr(), da.stride(0), gu.data_ptr(), dbuf.data_ptr(), dbuf.stride(0), T, F,
+                             bt.data_ptr(), bt.stride(0), xa.data_ptr(), xa.stride(0), dyb.data_ptr(), dyb.stride(0),
+                             ws.data_ptr<float>(), mgB.data_ptr(), mgB.stride(0), (float)alphaB, mgA.data_ptr(),
+                             mgA.stride(0), (float)alphaA, (int)pad, cur_stream()),
+        "swiglu_bwd_wgrad");
+  return dbuf.narrow(1, 0, 2 * F);
 }
 
 // ---------------- transpose ----------------
@@ -519,6 +574,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("swiglu_fwd_lora", &swiglu_fwd_lora, py::arg("gu"), py::arg("pad"), py::arg("am"), py::arg("nct"));
   m.def("swiglu_bwd_lora", &swiglu_bwd_lora, py::arg("da"), py::arg("gu"), py::arg("pad"), py::arg("bt"),
         py::arg("nct"), py::arg("split") = false);
+  m.def("swiglu_wgrad_ok", &swiglu_wgrad_ok);
+  m.def("swiglu_bwd_wgrad", &swiglu_bwd_wgrad);
   m.def("transpose2d", &transpose2d, py::arg("x"), py::arg("out") = py::none());
   m.def("ce_fwd_bwd_", &ce_fwd_bwd_);
   m.def("adamw_", &adamw_);

@@ -259,3 +259,284 @@ extern "C" int ftc_swiglu_bwd_lora(const void* da, long long da_rs, const void* 
   }
   return (int)hipGetLastError();
 }
+
+// ====================================================================================================
+// SwiGLU backward fused with the LoRA weight-gradient partials of BOTH neighbouring projections.
+//
+// Besides dgu and its row tail dgu B_gu (above), the weight gradients that need the MLP's big
+// tensors are formed here from the values in registers / LDS instead of by separate streaming passes
+// (csrc/kernels/lora_wgrad.hip re-reading dgu, 940 MB, and h, 470 MB, per Llama-3-8B layer):
+//
+//   dB_gu[c, r]   = sum_t dgu[t, c] xa[t, seg(c) * 16 + r]     xa = s x A_gu^T (gate | up tails, 2 x 16)
+//   dA_down^T[f, r] = sum_t h[t, f] dyb[t, r]                  h = silu(g) u recomputed, dyb = dy_down B_down
+//
+// Both reduce over tokens, the row tail over columns, so the grid tiles BOTH: a workgroup owns RB
+// token rows x 512 gate|up column pairs (4 waves x 128) and writes fp32 partials -- row tail per
+// column block, dB / dA per row block -- that two small reduction launches fold (deterministic, no
+// atomics).  Per 16-row sub-tile and wave: coalesced g / u / da loads (256 B per row and
+// instruction), dg / du / h into wave-private swizzled LDS tiles, then
+//   * row tail:  v_mfma_f32_16x16x32_bf16, A = dg / du row fragments, B = B^T rows held in registers
+//                for the whole row loop (the wave's columns never change),
+//   * dB, dA:    v_mfma_f32_16x16x16_bf16 with BOTH operands read column-wise by ds_read_b64_tr_b16
+//                (4 rows x 16 columns per 16-lane group: k = token) from the dg / du / h tiles and
+//                from the wave's small xa / dyb tiles.
+// Per-segment LoRA rank 16 (the all-linear r = 16 configuration); other ranks take the unfused path.
+namespace {
+
+typedef short s16x4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4v lds_s16x4v;
+
+FTC_DEV f32x4 mfma16k16(const s16x4v& a, const s16x4v& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+// transposed 4-row x 16-column read: lane 4q+p of each 16-lane group addresses row q, columns 4p..4p+3
+FTC_DEV s16x4v tr4(const char* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4v*)p); }
+
+struct WgArgs {
+  const uint16_t* gu;
+  const uint16_t* da;
+  long long da_rs;
+  uint16_t* dgu;
+  long long dgu_rs;
+  const uint16_t* bt;  // B^T [32, 2F]: rows 0..15 gate (over gate columns), 16..31 up (over up columns)
+  long long ldb;
+  const uint16_t* xa;  // [T, 32] (row stride xa_rs): s x A_gu^T, gate tail | up tail
+  long long xa_rs;
+  const uint16_t* dyb;  // [T, 16] (row stride dyb_rs): dy_down B_down
+  long long dyb_rs;
+  float* p_tail;  // [ncb][T][32]
+  float* p_b;     // [nrb][2F][16]
+  float* p_a;     // [nrb][F][16]
+  int T, F, RB, ncb;
+};
+
+constexpr int kCB = 512;  // gate|up column pairs per workgroup (128 per wave)
+
+// byte offset of (row, col) in a wave tile [16][128] bf16 with the 16-byte chunk swizzle of tile_off
+FTC_DEV int tcol_off(int row, int col) { return row * 256 + ((((col >> 3) ^ (row & 15)) & 15) << 4) + (col & 7) * 2; }
+
+__global__ __launch_bounds__(256, 2) void swiglu_bwd_wgrad_kernel(WgArgs a) {
+  __shared__ __attribute__((aligned(16))) char tiles[kWaves][3][16 * 256];  // dg, du, h
+  __shared__ __attribute__((aligned(16))) char xat[kWaves][16 * 64];       // xa sub-tile [16][32]
+  __shared__ __attribute__((aligned(16))) char dyt[kWaves][16 * 32];       // dyb sub-tile [16][16]
+  __shared__ float red[2][kWaves * 2 * 4 * 64];                            // row-tail partials, 2 buffers
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int F = a.F;
+  const int cb = blockIdx.x % a.ncb, rb = blockIdx.x / a.ncb;
+  const int cw = cb * kCB + 128 * wave;  // this wave's first gate column
+  const long long rbeg = (long long)rb * a.RB;
+  const long long rend = rbeg + a.RB < a.T ? rbeg + a.RB : a.T;
+  const int cq = lane & 15, rq = lane >> 4;  // coalesced: 16-byte chunk, row within 4
+  const int fr = lane & 15, fq = lane >> 4;  // fragment: row / column, k group
+  char* my = tiles[wave][0];
+
+  // row-tail B fragments (16x16x32): lane holds bt[tile][col = k0 + 8 fq .. +8] with tile row fr
+  uint4 bfg[4], bfu[4];
+  {
+    const __amdgpu_buffer_rsrc_t rb_ = make_rsrc_n(a.bt, 0x7fffffffu);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      bfg[m] = bload16(rb_, (int)((fr * a.ldb + cw + 32 * m + 8 * fq) * 2), 0);
+      bfu[m] = bload16(rb_, (int)(((16 + fr) * a.ldb + F + cw + 32 * m + 8 * fq) * 2), 0);
+    }
+  }
+  f32x4 accb[16], acca[8];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) accb[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acca[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int sub = 0;
+  for (long long r0 = rbeg; r0 < rend; r0 += 16, ++sub) {
+    const long long nrows = rend - r0 < 16 ? rend - r0 : 16;
+    // this sub-tile's rows as buffer resources: rows past the block read as zero, stores are dropped
+    const __amdgpu_buffer_rsrc_t rg = make_rsrc_n(a.gu + r0 * 2LL * F, (unsigned)(nrows * 4LL * F));
+    const __amdgpu_buffer_rsrc_t rd = make_rsrc_n(a.da + r0 * a.da_rs, (unsigned)(nrows * a.da_rs * 2));
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc_n(a.dgu + r0 * a.dgu_rs, (unsigned)(nrows * a.dgu_rs * 2));
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc_n(a.xa + r0 * a.xa_rs, (unsigned)(nrows * a.xa_rs * 2));
+    const __amdgpu_buffer_rsrc_t ry = make_rsrc_n(a.dyb + r0 * a.dyb_rs, (unsigned)(nrows * a.dyb_rs * 2));
+    uint4 gv[4], uv[4], dv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 4 * i + rq;
+      gv[i] = bload16(rg, (int)((row * 2LL * F + cw + 8 * cq) * 2), 0);
+      uv[i] = bload16(rg, (int)((row * 2LL * F + F + cw + 8 * cq) * 2), 0);
+      dv[i] = bload16(rd, (int)((row * a.da_rs + cw + 8 * cq) * 2), 0);
+    }
+    // xa [16][32]: lane -> row lane >> 2, chunk lane & 3;  dyb [16][16]: lanes 0..31 -> row lane >> 1, chunk lane & 1
+    const uint4 xv = bload16(rx, (int)(((lane >> 2) * a.xa_rs + 8 * (lane & 3)) * 2), 0);
+    const uint4 yv = lane < 32 ? bload16(ry, (int)(((lane >> 1) * a.dyb_rs + 8 * (lane & 1)) * 2), 0)
+                               : make_uint4(0u, 0u, 0u, 0u);
+    asm volatile("" ::: "memory");  // previous sub-tile's LDS reads stay above these writes
+    *reinterpret_cast<uint4*>(xat[wave] + (lane >> 2) * 64 + 16 * (lane & 3)) = xv;
+    if (lane < 32) *reinterpret_cast<uint4*>(dyt[wave] + (lane >> 1) * 32 + 16 * (lane & 1)) = yv;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 4 * i + rq;
+      float g[8], u[8], d[8], dg[8], du[8], h[8];
+      unpack8(gv[i], g);
+      unpack8(uv[i], u);
+      unpack8(dv[i], d);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float sg = 1.0f / (1.0f + __expf(-g[e]));
+        const float sl = g[e] * sg;
+        du[e] = d[e] * sl;
+        dg[e] = d[e] * u[e] * sg * (1.0f + g[e] * (1.0f - sg));
+        h[e] = silu_f(g[e]) * u[e];  // the forward's h, bit for bit
+      }
+      const uint4 gq = pack8(dg), uq = pack8(du), hq = pack8(h);
+      bstore16(gq, ro, (int)((row * a.dgu_rs + cw + 8 * cq) * 2), 0);
+      bstore16(uq, ro, (int)((row * a.dgu_rs + F + cw + 8 * cq) * 2), 0);
+      const int off = tile_off(row, cq);
+      *reinterpret_cast<uint4*>(my + off) = gq;
+      *reinterpret_cast<uint4*>(my + 16 * 256 + off) = uq;
+      *reinterpret_cast<uint4*>(my + 2 * 16 * 256 + off) = hq;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private tiles complete
+
+    // ---- row tail: [16 rows] x (gate tile 0, up tile 1)
+    f32x4 tg = f32x4{0.f, 0.f, 0.f, 0.f}, tu = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int off = tile_off(fr, 4 * m + fq);
+      tg = mfma16(*reinterpret_cast<const uint4*>(my + off), bfg[m], tg);
+      tu = mfma16(*reinterpret_cast<const uint4*>(my + 16 * 256 + off), bfu[m], tu);
+    }
+    // ---- dB (gate / up) and dA: k = the 16 token rows, operands read column-wise
+    const int q = (lane & 15) >> 2, p = lane & 3, g4 = lane >> 4;
+    const int trow = 4 * g4 + q;  // the row this lane addresses in a tr read
+    const s16x4v xg = tr4(xat[wave] + trow * 64 + (4 * p) * 2);
+    const s16x4v xu = tr4(xat[wave] + trow * 64 + (16 + 4 * p) * 2);
+    const s16x4v yb = tr4(dyt[wave] + trow * 32 + (4 * p) * 2);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int off = tcol_off(trow, 16 * j + 4 * p);
+      accb[j] = mfma16k16(tr4(my + off), xg, accb[j]);
+      accb[8 + j] = mfma16k16(tr4(my + 16 * 256 + off), xu, accb[8 + j]);
+      acca[j] = mfma16k16(tr4(my + 2 * 16 * 256 + off), yb, acca[j]);
+    }
+    // ---- row-tail reduction over the 4 waves (double-buffered LDS, one barrier per sub-tile)
+    float* rbuf = red[sub & 1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      rbuf[((wave * 2 + 0) * 4 + i) * 64 + lane] = tg[i];
+      rbuf[((wave * 2 + 1) * 4 + i) * 64 + lane] = tu[i];
+    }
+    __syncthreads();
+    for (int idx = tid; idx < 2 * 4 * 64; idx += 256) {  // (tile, i, lane) -> row 4 (ln >> 4) + i, col tile*16 + (ln & 15)
+      const int t = idx >> 8, i = (idx >> 6) & 3, ln = idx & 63;
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) s += rbuf[((w * 2 + t) * 4 + i) * 64 + ln];
+      const long long row = r0 + 4 * (ln >> 4) + i;
+      if (row < rend) a.p_tail[((long long)cb * a.T + row) * 32 + t * 16 + (ln & 15)] = s;
+    }
+  }
+  // ---- dB / dA partials of this row block: C[m = column][n = r], lane: r = lane & 15, m = 4 (lane >> 4) + i
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = cw + 16 * j + 4 * (lane >> 4) + i;
+      a.p_b[((long long)rb * 2 * F + c) * 16 + (lane & 15)] = accb[j][i];
+      a.p_b[((long long)rb * 2 * F + F + c) * 16 + (lane & 15)] = accb[8 + j][i];
+      a.p_a[((long long)rb * F + c) * 16 + (lane & 15)] = acca[j][i];
+    }
+}
+
+// dgu tail[t][r] = bf16(sum_cb p_tail[cb][t][r]) for r < 32, zeros for 32 <= r < Rp
+__global__ __launch_bounds__(256) void wgrad_tail_reduce_kernel(const float* __restrict__ p, int ncb, int T,
+                                                                uint16_t* __restrict__ dgu, long long dgu_rs,
+                                                                int col0, int Rp) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;  // one (t, 8-column chunk)
+  const int nch = Rp / 8;
+  if (idx >= (long long)T * nch) return;
+  const long long t = idx / nch;
+  const int ch = (int)(idx - t * nch);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (ch < 4) {
+    for (int k = 0; k < ncb; ++k) {
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(p + ((long long)k * T + t) * 32 + 8 * ch);
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(p + ((long long)k * T + t) * 32 + 8 * ch + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s[e] += v0[e];
+        s[4 + e] += v1[e];
+      }
+    }
+  }
+  *reinterpret_cast<uint4*>(dgu + t * dgu_rs + col0 + 8 * ch) = pack8(s);
+}
+
+// mgB[c][seg(c) * 16 + r] += alpha * sum_rb p_b[rb][c][r]   (c < 2F; seg = c >= F)
+// mgA[r][f] (row stride ldA)  += alphaA * sum_rb p_a[rb][f][r]
+__global__ __launch_bounds__(256) void wgrad_col_reduce_kernel(const float* __restrict__ pb, const float* __restrict__ pa,
+                                                               int nrb, int F, uint16_t* __restrict__ mgB,
+                                                               long long ldB, float alphaB, uint16_t* __restrict__ mgA,
+                                                               long long ldA, float alphaA) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;  // one (row, 4 r) of B then of A
+  const long long nB = 2LL * F * 4, nA = (long long)F * 4;
+  if (idx < nB) {
+    const long long c = idx >> 2;
+    const int r = 4 * (int)(idx & 3);
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < nrb; ++k) s += *reinterpret_cast<const f32x4*>(pb + ((long long)k * 2 * F + c) * 16 + r);
+    uint16_t* o = mgB + c * ldB + (c >= F ? 16 : 0) + r;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = f2bf(bf2f(o[e]) + alphaB * s[e]);
+  } else if (idx < nB + nA) {
+    const long long i2 = idx - nB;
+    const long long f = i2 >> 2;
+    const int r = 4 * (int)(i2 & 3);
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < nrb; ++k) s += *reinterpret_cast<const f32x4*>(pa + ((long long)k * F + f) * 16 + r);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      uint16_t* o = mgA + (long long)(r + e) * ldA + f;
+      *o = f2bf(bf2f(*o) + alphaA * s[e]);
+    }
+  }
+}
+
+}  // namespace
+
+// Row-block size and workspace (floats) of the fused backward for T tokens and F = ffn width.
+extern "C" int ftc_swiglu_wgrad_plan(long long T, int F, int* rb, long long* ws_floats) {
+  if (F % kCB != 0 || T <= 0) return -1;
+  const int ncb = F / kCB;
+  long long nrb = (1024 + ncb - 1) / ncb;  // ~1k workgroups
+  long long r = (T + nrb - 1) / nrb;
+  r = (r + 15) / 16 * 16;
+  if (r < 64) r = 64;
+  nrb = (T + r - 1) / r;
+  *rb = (int)r;
+  *ws_floats = (long long)ncb * T * 32 + nrb * 2LL * F * 16 + nrb * (long long)F * 16;
+  return 0;
+}
+
+extern "C" int ftc_swiglu_bwd_wgrad(const void* da, long long da_rs, const void* gu, void* dgu, long long dgu_rs,
+                                    long long T, int F, const void* bt, long long ldb, const void* xa, long long xa_rs,
+                                    const void* dyb, long long dyb_rs, float* ws, void* mgB, long long ldB,
+                                    float alphaB, void* mgA, long long ldA, float alphaA, int Rp, hipStream_t stream) {
+  int RB;
+  long long wsf;
+  if (ftc_swiglu_wgrad_plan(T, F, &RB, &wsf) != 0) return -1;
+  if (Rp < 32 || Rp % 8 != 0 || dgu_rs < 2LL * F + Rp || da_rs % 8 || dgu_rs % 8 || ldb % 8 || xa_rs % 8 ||
+      dyb_rs % 8 || T * 4LL * F >= (1LL << 31) || T * dgu_rs * 2 >= (1LL << 31))
+    return -1;
+  const int ncb = F / kCB;
+  const int nrb = (int)((T + RB - 1) / RB);
+  WgArgs a{(const uint16_t*)gu, (const uint16_t*)da, da_rs, (uint16_t*)dgu, dgu_rs, (const uint16_t*)bt, ldb,
+           (const uint16_t*)xa, xa_rs, (const uint16_t*)dyb, dyb_rs, ws, ws + (long long)ncb * T * 32,
+           ws + (long long)ncb * T * 32 + (long long)nrb * 2 * F * 16, (int)T, F, RB, ncb};
+  hipLaunchKernelGGL(swiglu_bwd_wgrad_kernel, dim3(ncb * nrb), dim3(256), 0, stream, a);
+  const long long nt = T * (Rp / 8);
+  hipLaunchKernelGGL(wgrad_tail_reduce_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, a.p_tail,
+                     ncb, (int)T, (uint16_t*)dgu, dgu_rs, 2 * F, Rp);
+  const long long nc = 2LL * F * 4 + (long long)F * 4;
+  hipLaunchKernelGGL(wgrad_col_reduce_kernel, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, stream, a.p_b, a.p_a,
+                     nrb, F, (uint16_t*)mgB, ldB, alphaB, (uint16_t*)mgA, ldA, alphaA);
+  return (int)hipGetLastError();
+}

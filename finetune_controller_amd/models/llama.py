@@ -29,6 +29,7 @@ from torch.utils.checkpoint import checkpoint
 from .. import ops
 from .config import ModelConfig
 from ..ops.linear import AugWeight, LoRATail, TailOperands
+from ..ops.mlp import fused_mlp_supported, lora_mlp
 from .lora import LoRAConfig, make_pairs
 
 
@@ -127,6 +128,11 @@ class LlamaLayer(nn.Module):
                                  out_pad=p_o, grad_pad=p_qkv)
         o = self.proj("o", a)
         h, x = ops.add_rms_norm(h, o, self.mlp_norm, cfg.norm_eps, pad=p_gu, grad_pad=p_o)
+        if "gu" in self.lora and "down" in self.lora and not self.qweights and fused_mlp_supported(
+                x, self.aug.get("gu"), self.lora["gu"], self.aug.get("down"), self.lora["down"], p_gu, p_down,
+                self.training):
+            # the whole LoRA MLP as one autograd function: SwiGLU backward also forms dB_gu / dA_down
+            return h, lora_mlp(x, self.aug["gu"], self.lora["gu"], self.aug["down"], self.lora["down"])
         gu = self.proj("gu", x)
         act = ops.swiglu(gu, out_pad=p_down, grad_pad=p_gu, fwd_tail=self.tail("down", p_down),
                          bwd_tail=self.tail("gu", p_gu))

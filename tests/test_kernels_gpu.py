@@ -122,6 +122,47 @@ def test_swiglu_lora_tail(C, rows, F, R, pad, split):
     assert torch.count_nonzero(tailb[:, R:]) == 0
 
 
+@pytest.mark.parametrize("T,F", [(1000, 1024), (4096, 512), (77, 512)])
+def test_swiglu_bwd_wgrad(C, T, F):
+    """swiglu_bwd_wgrad (csrc/kernels/swiglu_lora.hip): dgu, its row tail dgu B and the LoRA weight
+    gradients dB_gu += dgu^T xa (block-diagonal gate|up) and dA_down += s dyb^T h in one pass, against
+    fp32 products of the stored bf16 values (h = the forward SwiGLU output)."""
+    torch.manual_seed(0)
+    pad = 64
+    gu = bf(torch.randn(T, 2 * F, device=DEV))
+    da = bf(torch.randn(T, F, device=DEV))
+    bt = torch.zeros(pad, 2 * F, device=DEV, dtype=torch.bfloat16)
+    bt[:16, :F] = bf(torch.randn(16, F, device=DEV) * 0.1)
+    bt[16:32, F:] = bf(torch.randn(16, F, device=DEV) * 0.1)
+    xbuf = bf(torch.randn(T, 104, device=DEV))
+    xa = xbuf[:, 40:72]
+    ybuf = bf(torch.randn(T, 40, device=DEV))
+    dyb = ybuf[:, 8:24]
+    mgB = torch.zeros(2 * F, 32, device=DEV, dtype=torch.bfloat16)
+    mgB[:F, :16] = bf(torch.randn(F, 16, device=DEV))
+    mgB[F:, 16:] = bf(torch.randn(F, 16, device=DEV))
+    mgA = bf(torch.randn(16, F, device=DEV))
+    mgB0, mgA0 = mgB.float().clone(), mgA.float().clone()
+    dgu = C.swiglu_bwd_wgrad(da, gu, pad, bt, xa, dyb, mgB, mgA, 1.0, 0.5)
+    assert dgu.shape == (T, 2 * F) and dgu.stride(0) == 2 * F + pad
+    torch.testing.assert_close(dgu, C.swiglu_bwd(da, gu), atol=0, rtol=0)
+    full = dgu.as_strided((T, 2 * F + pad), (2 * F + pad, 1))
+    tail = full[:, 2 * F:].float()
+    ref_tail = dgu.float() @ bt[:32].float().t()
+    torch.testing.assert_close(tail[:, :32], ref_tail, atol=2e-2 * ref_tail.abs().max().item() + 1e-3, rtol=2e-2)
+    assert torch.count_nonzero(tail[:, 32:]) == 0
+    dgf = dgu.float()
+    refB = mgB0.clone()
+    refB[:F, :16] += dgf[:, :F].t() @ xa[:, :16].float()
+    refB[F:, 16:] += dgf[:, F:].t() @ xa[:, 16:].float()
+    tolB = 2e-2 * refB.abs().max().item()
+    torch.testing.assert_close(mgB.float(), refB, atol=tolB, rtol=2e-2)
+    assert torch.count_nonzero(mgB[:F, 16:]) == 0 and torch.count_nonzero(mgB[F:, :16]) == 0
+    h = C.swiglu_fwd(gu).float()
+    refA = mgA0 + 0.5 * (dyb.float().t() @ h)
+    torch.testing.assert_close(mgA.float(), refA, atol=2e-2 * refA.abs().max().item(), rtol=2e-2)
+
+
 @pytest.mark.parametrize("V", [128256, 32000, 50257])
 def test_cross_entropy_inplace(C, V):
     torch.manual_seed(0)
@@ -480,3 +521,47 @@ def test_full_ft_steps_hip_match_torch_path(C, monkeypatch):
     # parameters after three AdamW steps: every element moved by ~lr per step; compare the drift
     err = (ph - pt).abs().max().item()
     assert err < 1e-2, err
+
+
+def test_llama_fused_lora_mlp_matches_torch_path(C, monkeypatch):
+    """The fused LoRA MLP block (ops/mlp.py: SwiGLU backward forming dB_gu / dA_down, augmented GEMMs)
+    on adapters homed in FlatAdamW's flat gradient buffer, against the stock-PyTorch path: loss and
+    every adapter gradient of a whole decoder."""
+    import finetune_controller_amd.models.llama as llama_mod
+    from finetune_controller_amd.models import LoRAConfig, build_model
+    from finetune_controller_amd.models.config import ModelConfig
+    from finetune_controller_amd.train.optim import FlatAdamW
+
+    cfg = ModelConfig("llama", 512, 256, 2, 4, 2, 1024, 512, 10000.0, name="llama-test")
+    lc = LoRAConfig(r=16, alpha=32)
+    calls = []
+    real = llama_mod.lora_mlp
+    monkeypatch.setattr(llama_mod, "lora_mlp", lambda *a, **k: calls.append(1) or real(*a, **k))
+    ids = torch.randint(0, cfg.vocab_size, (2, 256), device=DEV)
+    labels = torch.roll(ids, -1, 1)
+    res = {}
+    for mode in ("hip", "torch"):
+        monkeypatch.setenv("FTC_KERNELS", mode)
+        torch.manual_seed(0)
+        m = build_model(cfg, lc, device=DEV, dtype=torch.bfloat16)
+        m.init_weights(seed=5)
+        m.freeze_base()
+        g = torch.Generator(device=DEV).manual_seed(1)
+        for layer in m.layers:
+            for p in layer.lora.values():
+                for _, _, B_s in p.segment_tensors():
+                    B_s.data.normal_(0, 0.05, generator=g)
+        opt = FlatAdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3)
+        opt.zero_grad()
+        loss = m(ids, labels)
+        loss.backward()
+        res[mode] = (loss.float().item(), opt.grad_flat.float().clone(), [(o, n) for o, n in opt.offsets])
+    assert len(calls) == cfg.n_layers  # the fused block ran in every layer on the HIP path
+    (lh, gh, offs), (lt, gt, _) = res["hip"], res["torch"]
+    assert abs(lh - lt) < 2e-2 * abs(lt)
+    bad = []
+    for o, n in offs:
+        a, b = gh[o:o + n], gt[o:o + n]
+        if (a - b).abs().max().item() > 5e-2 * b.abs().max().item() + 1e-3:
+            bad.append((o, n, (a - b).abs().max().item(), b.abs().max().item()))
+    assert not bad, bad

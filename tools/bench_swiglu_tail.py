@@ -49,6 +49,17 @@ def main():
         full = d.as_strided((T, 2 * F + Rp), (2 * F + Rp, 1))
         torch.mm(d, B, out=full[:, 2 * F:])
 
+    xa = torch.randn(T, 4160, device="cuda", dtype=bf)[:, 4096:4128]
+    dyb = torch.randn(T, 4160, device="cuda", dtype=bf)[:, 4096:4112]
+    mgB = torch.zeros(2 * F, 32, device="cuda", dtype=bf)
+    mgA = torch.zeros(16, F, device="cuda", dtype=bf)
+    h = torch.randn(T, F + Rp, device="cuda", dtype=bf)[:, :F]
+
+    def bwd_split_wgrad():
+        d = C.swiglu_bwd_lora(da, gu, Rp, bt, 2, True)
+        C.lora_wgrad_(mgB, d, xa, 16, 1.0, 1.0, [F, 2 * F], [0, 16], [0, 16])
+        C.lora_wgrad_(mgA.t(), h, dyb, 16, 0.5, 1.0)
+
     variants = {
         "fwd_swiglu_only": lambda: C.swiglu_fwd(gu, Rp),
         "fwd_plain+gemm": fwd_plain,
@@ -57,6 +68,8 @@ def main():
         "bwd_plain+gemm": bwd_plain,
         "bwd_fused_nct2": lambda: C.swiglu_bwd_lora(da, gu, Rp, bt, 2, False),
         "bwd_fused_nct2_split": lambda: C.swiglu_bwd_lora(da, gu, Rp, bt, 2, True),
+        "bwd_split+lora_wgrad_dB_gu_dA_down": bwd_split_wgrad,
+        "bwd_fused_wgrad": lambda: C.swiglu_bwd_wgrad(da, gu, Rp, bt, xa, dyb, mgB, mgA, 1.0, 0.5),
     }
     for name, fn in variants.items():
         ms = timeit(fn)
