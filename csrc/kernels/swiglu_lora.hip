@@ -22,6 +22,8 @@
 //   written as zeros (the augmented GEMM reads all Rp spare columns).
 #include "common.h"
 
+#include <cstdlib>
+
 using namespace ftc;
 
 namespace {
@@ -506,7 +508,13 @@ __global__ __launch_bounds__(256) void wgrad_col_reduce_kernel(const float* __re
 extern "C" int ftc_swiglu_wgrad_plan(long long T, int F, int* rb, long long* ws_floats) {
   if (F % kCB != 0 || T <= 0) return -1;
   const int ncb = F / kCB;
-  long long nrb = (1024 + ncb - 1) / ncb;  // ~1k workgroups
+  // workgroup target: partial traffic grows with ncb + nrb, balance wants whole rounds of the
+  // 2-per-CU residency (FTC_WGRAD_WGS, default 512 = one round on 256 CUs)
+  static const int target = [] {
+    const char* e = getenv("FTC_WGRAD_WGS");
+    return e ? atoi(e) : 512;
+  }();
+  long long nrb = target / ncb > 0 ? target / ncb : 1;
   long long r = (T + nrb - 1) / nrb;
   r = (r + 15) / 16 * 16;
   if (r < 64) r = 64;
