@@ -14,6 +14,8 @@
 // (deterministic: no float atomics).
 #include "common.h"
 
+#include <cstdlib>
+
 using namespace ftc;
 
 template <int NV, bool RES>
@@ -153,6 +155,82 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_kernel(
   }
 }
 
+// Frozen-weight backward (no dw: LoRA / QLoRA norms), tuned for occupancy: TWO waves per row (each
+// lane holds NV2 16-byte chunks, half of the one-wave layout), w staged once per workgroup in LDS, and
+// dres loaded together with dy / h so each row needs a single memory round trip.  The row dot product
+// meets in LDS (one barrier per pair of rows).  ~100 VGPRs instead of 178: 4+ waves per SIMD.
+template <int NV2, bool DRES>
+__global__ __launch_bounds__(256) void rmsnorm_bwd2_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ h, const uint16_t* __restrict__ w,
+    const float* __restrict__ rstd, const uint16_t* __restrict__ dres, uint16_t* __restrict__ dx, int rows, int d,
+    long long dres_rs, long long dx_rs) {
+  extern __shared__ __attribute__((aligned(16))) uint4 wl[];  // w: d / 8 chunks, then 4 floats of partial dots
+  float* part = reinterpret_cast<float*>(wl + (d >> 3));
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int pair = wid >> 1, half = wid & 1;  // rows: 2 per iteration, 2 waves per row
+  const int nvec = d >> 3;
+  const float inv_d = 1.0f / (float)d;
+  for (int i = tid; i < nvec; i += 256) wl[i] = reinterpret_cast<const uint4*>(w)[i];
+  __syncthreads();
+  const int lane2 = half * 64 + lane;  // 0..127 within the row
+  for (long long base = (long long)blockIdx.x * 2; base < rows; base += (long long)gridDim.x * 2) {
+    const long long row = base + pair;
+    const bool ok = row < rows;
+    uint4 dyv[NV2], hv[NV2], drv[DRES ? NV2 : 1];
+    float dot = 0.f, r = 0.f;
+    if (ok) {
+      r = rstd[row];
+#pragma unroll
+      for (int i = 0; i < NV2; ++i) {
+        const int idx = lane2 + i * 128;
+        if (idx < nvec) {
+          dyv[i] = reinterpret_cast<const uint4*>(dy + row * d)[idx];
+          hv[i] = reinterpret_cast<const uint4*>(h + row * d)[idx];
+          if constexpr (DRES) drv[i] = reinterpret_cast<const uint4*>(dres + row * dres_rs)[idx];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NV2; ++i) {
+        const int idx = lane2 + i * 128;
+        if (idx < nvec) {
+          float dy8[8], h8[8], w8[8];
+          unpack8(dyv[i], dy8);
+          unpack8(hv[i], h8);
+          unpack8(wl[idx], w8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dot += dy8[j] * w8[j] * (h8[j] * r);
+        }
+      }
+    }
+    dot = wave_sum(dot);
+    if (lane == 0) part[wid] = dot;
+    __syncthreads();
+    dot = (part[2 * pair] + part[2 * pair + 1]) * inv_d;
+    __syncthreads();  // part is rewritten next iteration
+    if (ok) {
+#pragma unroll
+      for (int i = 0; i < NV2; ++i) {
+        const int idx = lane2 + i * 128;
+        if (idx < nvec) {
+          float dy8[8], h8[8], w8[8], o[8];
+          unpack8(dyv[i], dy8);
+          unpack8(hv[i], h8);
+          unpack8(wl[idx], w8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = r * (dy8[j] * w8[j] - h8[j] * r * dot);
+          if constexpr (DRES) {
+            float d8[8];
+            unpack8(drv[i], d8);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] += d8[j];
+          }
+          reinterpret_cast<uint4*>(dx + row * dx_rs)[idx] = pack8(o);
+        }
+      }
+    }
+  }
+}
+
 // dw[c] = sum_b part[b][c].  A workgroup owns 64 columns; its 4 waves take every 4th partial row with
 // 8 independent accumulators each (enough loads in flight to hide HBM latency), then reduce through
 // LDS.  Deterministic (fixed summation order), d/64 workgroups.
@@ -242,6 +320,31 @@ extern "C" int ftc_rmsnorm_bwd(const void* dy, const void* h, const void* w, con
   } else {                                        \
     if (dres) FTC_LAUNCH_BWD(NV, false, true);    \
     else FTC_LAUNCH_BWD(NV, false, false);        \
+  }
+  // frozen norms: the two-waves-per-row variant (FTC_RMSNORM_BWD2=0 selects the one-wave kernel)
+  static const bool two = [] {
+    const char* e = getenv("FTC_RMSNORM_BWD2");
+    return !(e && e[0] == '0');
+  }();
+  if (!need_dw && two && nv >= 2) {
+    const int g2 = ftc::stream_grid(rows, 2);
+    const size_t l2 = (size_t)(d / 8) * 16 + 4 * sizeof(float);
+#define FTC_LAUNCH_BWD2(NV2)                                                                                  \
+  if (dres)                                                                                                   \
+    hipLaunchKernelGGL((rmsnorm_bwd2_kernel<NV2, true>), dim3(g2), dim3(256), l2, stream, DY, Hh, W, rstd, DR, DX, \
+                       rows, d, dres_rs, dx_rs);                                                              \
+  else                                                                                                        \
+    hipLaunchKernelGGL((rmsnorm_bwd2_kernel<NV2, false>), dim3(g2), dim3(256), l2, stream, DY, Hh, W, rstd, DR,  \
+                       DX, rows, d, dres_rs, dx_rs);
+    switch (nv) {
+      case 2: FTC_LAUNCH_BWD2(1); break;
+      case 4: FTC_LAUNCH_BWD2(2); break;
+      case 8: FTC_LAUNCH_BWD2(4); break;
+      case 16: FTC_LAUNCH_BWD2(8); break;
+      default: return -1;
+    }
+#undef FTC_LAUNCH_BWD2
+    return (int)hipGetLastError();
   }
   switch (nv) {
     case 1: FTC_LAUNCH_BWD_NV(1); break;

@@ -48,6 +48,11 @@ def test_rmsnorm_fwd_bwd(C, rows, d, with_res):
     dx, dw = C.rmsnorm_bwd(dy, h if with_res else x, w, rstd, dres, True)
     torch.testing.assert_close(dx.float(), hv.grad + dres.float(), atol=3e-2, rtol=3e-2)
     torch.testing.assert_close(dw, wv.grad, atol=5e-2 * math.sqrt(rows), rtol=2e-2)
+    # frozen-weight backward (two waves per row kernel), with and without the residual gradient
+    dx2 = C.rmsnorm_bwd(dy, h if with_res else x, w, rstd, dres, False)[0]
+    torch.testing.assert_close(dx2.float(), hv.grad + dres.float(), atol=3e-2, rtol=3e-2)
+    dx3 = C.rmsnorm_bwd(dy, h if with_res else x, w, rstd, None, False)[0]
+    torch.testing.assert_close(dx3.float(), hv.grad, atol=3e-2, rtol=3e-2)
 
 
 def test_rope_roundtrip_and_reference(C):
