@@ -67,6 +67,75 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_kernel(
   }
 }
 
+// Forward with TWO waves per row (each lane NV2 16-byte chunks): half the registers of the one-wave
+// layout, so twice the rows in flight for this HBM-bound pass; the sum of squares meets in LDS.
+template <int NV2, bool RES>
+__global__ __launch_bounds__(256) void rmsnorm_fwd2_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ res, const uint16_t* __restrict__ w,
+    uint16_t* __restrict__ h_out, uint16_t* __restrict__ y, float* __restrict__ rstd, int rows, int d,
+    float eps, long long y_rs) {
+  __shared__ float part[4];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int pair = wid >> 1, half = wid & 1;
+  const int nvec = d >> 3;
+  const float inv_d = 1.0f / (float)d;
+  const int lane2 = half * 64 + lane;
+  for (long long base = (long long)blockIdx.x * 2; base < rows; base += (long long)gridDim.x * 2) {
+    const long long row = base + pair;
+    const bool ok = row < rows;
+    float v[NV2][8];
+    float ss = 0.f;
+    if (ok) {
+      uint4 xv[NV2], rv[RES ? NV2 : 1];
+#pragma unroll
+      for (int i = 0; i < NV2; ++i) {
+        const int idx = lane2 + i * 128;
+        if (idx < nvec) {
+          xv[i] = reinterpret_cast<const uint4*>(x + row * d)[idx];
+          if constexpr (RES) rv[i] = reinterpret_cast<const uint4*>(res + row * d)[idx];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NV2; ++i) {
+        const int idx = lane2 + i * 128;
+        if (idx < nvec) {
+          unpack8(xv[i], v[i]);
+          if constexpr (RES) {
+            float r8[8];
+            unpack8(rv[i], r8);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[i][j] += r8[j];
+            const uint4 hv = pack8(v[i]);
+            reinterpret_cast<uint4*>(h_out + row * d)[idx] = hv;
+            unpack8(hv, v[i]);  // statistics on the stored (rounded) residual stream
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+        }
+      }
+    }
+    ss = wave_sum(ss);
+    if (lane == 0) part[wid] = ss;
+    __syncthreads();
+    const float r = rsqrtf((part[2 * pair] + part[2 * pair + 1]) * inv_d + eps);
+    __syncthreads();
+    if (ok) {
+#pragma unroll
+      for (int i = 0; i < NV2; ++i) {
+        const int idx = lane2 + i * 128;
+        if (idx < nvec) {
+          float w8[8], o[8];
+          unpack8(reinterpret_cast<const uint4*>(w)[idx], w8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = v[i][j] * r * w8[j];
+          reinterpret_cast<uint4*>(y + row * y_rs)[idx] = pack8(o);
+        }
+      }
+      if (half == 0 && lane == 0) rstd[row] = r;
+    }
+  }
+}
+
 // One wave per row.  dy / h rows stay in registers as packed bf16 (4 VGPRs per 8 elements) and are
 // re-expanded in the second pass, and w is loaded once per wave: ~100 VGPRs at d = 4096 instead of
 // ~180 for fp32 copies, i.e. twice the waves in flight for this HBM-bound kernel.
@@ -281,6 +350,29 @@ extern "C" int ftc_rmsnorm_fwd(const void* x, const void* res, const void* w, vo
   else                                                                                                        \
     hipLaunchKernelGGL((rmsnorm_fwd_kernel<NV, false>), dim3(grid), dim3(256), 0, stream, X, R, W, H, Y,     \
                        rstd, rows, d, eps, y_rs);
+  static const bool two = [] {
+    const char* e = getenv("FTC_RMSNORM_FWD2");
+    return !(e && e[0] == '0');
+  }();
+  if (two && nv >= 2) {
+    const int g2 = ftc::stream_grid(rows, 2);
+#define FTC_LAUNCH_FWD2(NV2)                                                                                     \
+  if (res)                                                                                                       \
+    hipLaunchKernelGGL((rmsnorm_fwd2_kernel<NV2, true>), dim3(g2), dim3(256), 0, stream, X, R, W, H, Y, rstd, rows, \
+                       d, eps, y_rs);                                                                            \
+  else                                                                                                           \
+    hipLaunchKernelGGL((rmsnorm_fwd2_kernel<NV2, false>), dim3(g2), dim3(256), 0, stream, X, R, W, H, Y, rstd,     \
+                       rows, d, eps, y_rs);
+    switch (nv) {
+      case 2: FTC_LAUNCH_FWD2(1); break;
+      case 4: FTC_LAUNCH_FWD2(2); break;
+      case 8: FTC_LAUNCH_FWD2(4); break;
+      case 16: FTC_LAUNCH_FWD2(8); break;
+      default: return -1;
+    }
+#undef FTC_LAUNCH_FWD2
+    return (int)hipGetLastError();
+  }
   switch (nv) {
     case 1: FTC_LAUNCH_FWD(1); break;
     case 2: FTC_LAUNCH_FWD(2); break;
