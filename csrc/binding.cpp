@@ -30,6 +30,8 @@ int ftc_swiglu_bwd_wgrad(const void* da, long long da_rs, const void* gu, void* 
                          int F, const void* bt, long long ldb, const void* xa, long long xa_rs, const void* dyb,
                          long long dyb_rs, float* ws, void* mgB, long long ldB, float alphaB, void* mgA, long long ldA,
                          float alphaA, int Rp, hipStream_t stream);
+int ftc_tail_gemm(void* x, long long ldx, long long rows, int K, const void* Bm, long long ldb, int nct, int Rp,
+                  hipStream_t stream);
 int ftc_transpose(const void* x, long long ldx, void* y, long long ldy, int R, int C, hipStream_t stream);
 int ftc_ce_fwd_bwd(void* logits, const long long* labels, float* loss, float* lse, long long rows, int V, long long ld,
                    float gscale, long long ignore_index, hipStream_t stream);
@@ -306,6 +308,22 @@ at::Tensor swiglu_bwd_wgrad(const at::Tensor& da, const at::Tensor& gu, int64_t 
   return dbuf.narrow(1, 0, 2 * F);
 }
 
+// tail[:, 0:Rp] = x[:, 0:K] Bm[0:Rp]^T into x's own spare columns (x: [T, K] view with row stride >= K + Rp)
+bool tail_gemm_ok(const at::Tensor& x, int64_t Rp) {
+  return x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.stride(1) == 1 &&
+         x.size(1) % 128 == 0 && x.stride(0) % 8 == 0 && x.stride(0) >= x.size(1) + Rp &&
+         reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && x.size(0) * x.stride(0) * 2 < (1LL << 31);
+}
+
+void tail_gemm_(at::Tensor& x, const at::Tensor& bm, int64_t nct, int64_t Rp) {
+  TORCH_CHECK(tail_gemm_ok(x, Rp), "tail_gemm_: x must be a [T, K] bf16 row view with Rp spare columns");
+  TORCH_CHECK(nct >= 1 && nct <= 4 && Rp >= 16 * nct && Rp % 16 == 0, "tail_gemm_: bad nct / Rp");
+  need_rowview(bm, 16 * nct, x.size(1), "bm");
+  check(ftc_tail_gemm(x.data_ptr(), x.stride(0), x.size(0), (int)x.size(1), bm.data_ptr(), bm.stride(0), (int)nct,
+                      (int)Rp, cur_stream()),
+        "tail_gemm_");
+}
+
 // ---------------- transpose ----------------
 // out[C, R] = x[R, C]^T for a 2-D bf16 row view x (unit column stride); out: contiguous [C, R] or None
 at::Tensor transpose2d(const at::Tensor& x, const c10::optional<at::Tensor>& out) {
@@ -576,6 +594,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("nct"), py::arg("split") = false);
   m.def("swiglu_wgrad_ok", &swiglu_wgrad_ok);
   m.def("swiglu_bwd_wgrad", &swiglu_bwd_wgrad);
+  m.def("tail_gemm_ok", &tail_gemm_ok);
+  m.def("tail_gemm_", &tail_gemm_);
   m.def("transpose2d", &transpose2d, py::arg("x"), py::arg("out") = py::none());
   m.def("ce_fwd_bwd_", &ce_fwd_bwd_);
   m.def("adamw_", &adamw_);

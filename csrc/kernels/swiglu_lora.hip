@@ -548,3 +548,84 @@ extern "C" int ftc_swiglu_bwd_wgrad(const void* da, long long da_rs, const void*
                      nrb, F, (uint16_t*)mgB, ldB, alphaB, (uint16_t*)mgA, ldA, alphaA);
   return (int)hipGetLastError();
 }
+
+// ====================================================================================================
+// Skinny "tail" GEMM: tail[t, 0:Rp] = X[t, 0:K] . Bm[0:Rp, 0:K]^T written into X's own spare columns
+// (X row stride ldx >= K + Rp; rows of Bm past 16 * nct are treated as zero and their columns written
+// as zeros).  This is the rank-r product of an augmented LoRA GEMM when its producer is a kernel that
+// cannot form it (flash attention output, RMSNorm output / residual gradient, ...): a pure stream of X
+// at HBM rate -- hipBLASLt's 64x64 tiles run these [T, K] x [K, 64] shapes at ~4.3 TB/s.  Same
+// structure as the SwiGLU kernels above: 32 rows x 4 waves (K split in 128-column chunks), coalesced
+// 256-byte row loads, a wave-private swizzled LDS tile into 16x16x32 MFMA fragments, LDS reduction.
+namespace {
+
+template <int NCT>
+__global__ __launch_bounds__(256) void tail_gemm_kernel(uint16_t* __restrict__ X, long long ldx, long long rows, int K,
+                                                        const uint16_t* __restrict__ Bm, long long ldb, int Rp) {
+  constexpr int RT = 2, NL = RT * 4;
+  __shared__ __attribute__((aligned(16))) char lds[kWaves * RT * 16 * 256];
+  __shared__ float red[kWaves * RT * NCT * 4 * 64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  char* my = lds + wave * (RT * 16 * 256);
+  const long long r0 = (long long)blockIdx.x * (RT * 16);
+  const int cq = lane & 15, rq = lane >> 4;
+  const int fr = lane & 15, fq = lane >> 4;
+  const long long nrows = rows - r0 < RT * 16 ? rows - r0 : RT * 16;
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc_n(X + r0 * ldx, (unsigned)(nrows * ldx * 2LL));
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc_n(Bm, 0x7fffffffu);
+  const int vx = (int)(rq * ldx + 8 * cq) * 2;
+  const int vb = (int)(fr * ldb + 8 * fq) * 2;
+  f32x4 acc[RT][NCT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int t = 0; t < NCT; ++t) acc[r][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nch = K / 128;
+  const int c0 = (nch * wave) / kWaves, c1 = (nch * (wave + 1)) / kWaves;
+  for (int c = c0; c < c1; ++c) {
+    const int k0 = c * 128;
+    uint4 xv[NL];
+#pragma unroll
+    for (int i = 0; i < NL; ++i) xv[i] = bload16(rx, vx + 2 * k0, (int)(i * 8 * ldx));
+    uint4 bf[4][NCT];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) bf[m][t] = bload16(rb, vb + 2 * (k0 + 32 * m), (int)(t * 16 * ldb * 2));
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < NL; ++i) *reinterpret_cast<uint4*>(my + tile_off(4 * i + rq, cq)) = xv[i];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        const uint4 a = *reinterpret_cast<const uint4*>(my + tile_off(r * 16 + fr, 4 * m + fq));
+#pragma unroll
+        for (int t = 0; t < NCT; ++t) acc[r][t] = mfma16(a, bf[m][t], acc[r][t]);
+      }
+  }
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+    write_tail<NCT>(acc[r], red + r * (kWaves * NCT * 4 * 64), X, ldx, r0 + 16 * r, rows, K, Rp);
+}
+
+}  // namespace
+
+extern "C" int ftc_tail_gemm(void* x, long long ldx, long long rows, int K, const void* Bm, long long ldb, int nct,
+                             int Rp, hipStream_t stream) {
+  if (K % 128 != 0 || ldx % 8 != 0 || ldb % 8 != 0 || ldx < (long long)K + Rp || nct < 1 || nct > 4 ||
+      Rp < 16 * nct || Rp % 16 != 0 || rows <= 0 || rows * ldx * 2 >= (1LL << 31))
+    return -1;
+  const dim3 grid((unsigned)((rows + 31) / 32)), block(256);
+  auto X = (uint16_t*)x;
+  auto B = (const uint16_t*)Bm;
+  switch (nct) {
+    case 1: hipLaunchKernelGGL(tail_gemm_kernel<1>, grid, block, 0, stream, X, ldx, rows, K, B, ldb, Rp); break;
+    case 2: hipLaunchKernelGGL(tail_gemm_kernel<2>, grid, block, 0, stream, X, ldx, rows, K, B, ldb, Rp); break;
+    case 3: hipLaunchKernelGGL(tail_gemm_kernel<3>, grid, block, 0, stream, X, ldx, rows, K, B, ldb, Rp); break;
+    default: hipLaunchKernelGGL(tail_gemm_kernel<4>, grid, block, 0, stream, X, ldx, rows, K, B, ldb, Rp); break;
+  }
+  return (int)hipGetLastError();
+}

@@ -226,6 +226,23 @@ class LoRATail:
                           and blocks[1][1] == aug.N)
 
 
+_HIP_TAIL = os.environ.get("FTC_TAIL_GEMM", "1") != "0"  # A/B switch: hipBLASLt for the skinny tail GEMMs
+
+
+def tail_product(x2: torch.Tensor, width: int, Rp: int, operand: torch.Tensor, nct: int) -> None:
+    """``x2[:, width:width+Rp] = x2[:, :width] . operand^T`` (operand: [Rp, width] row view, rows past
+    16*nct zero) -- the rank-r product of an augmented GEMM written into the operand's own spare
+    columns.  The HIP skinny-GEMM kernel streams x2 once at HBM rate (csrc/kernels/swiglu_lora.hip
+    ``tail_gemm``); elsewhere a GEMM into the strided tail."""
+    xv = x2[:, :width] if x2.shape[1] != width else x2
+    # up to 32 live columns the kernel streams at 6.3 TB/s vs hipBLASLt's 5.4; at 48 (packed q|k|v
+    # forward, nct = 3) its L2 fragment traffic loses (tools/bench_rmsnorm.py)
+    if _HIP_TAIL and nct <= 2 and use_hip(x2) and ext().tail_gemm_ok(xv, Rp):
+        ext().tail_gemm_(xv, operand, nct, Rp)
+    else:
+        _mm_into(x2, operand.t(), _tail(x2, width, Rp))
+
+
 def _wide(t: torch.Tensor, width: int) -> torch.Tensor:
     return t.as_strided((t.shape[0], width), (t.stride(0), 1), t.storage_offset())
 
@@ -397,7 +414,7 @@ class _LoRALinearFn(torch.autograd.Function):
             # [s x A^T | 0] straight into the spare columns of the producer's buffer (unless the
             # producer kernel already formed it: ops.activation.swiglu)
             if not take_prefilled("fwd", x2, aug):
-                _mm_into(x2, aug.big[N:, :K].t(), _tail(x2, K, Rp))
+                tail_product(x2, K, Rp, aug.big[N:, :K], aug.nct)
             xa = _tail(x2, K, aug.R)  # = s * x A^T
             torch.mm(_wide(x2, K + Rp), aug.big[:N].t(), out=y)
         else:
@@ -444,7 +461,7 @@ class _LoRALinearFn(torch.autograd.Function):
             Rp = aug.Rp
             aug.refresh(A, B, s)
             if not take_prefilled("bwd", dy2, aug):
-                _mm_into(dy2, aug.big[:N, aug.K:], _tail(dy2, N, Rp))
+                tail_product(dy2, N, Rp, aug.bwd_tail_operand(A, B, s), aug.nct)
             dyb = _tail(dy2, N, aug.R)
             rhs = aug.bwd_operand() if _TN_BWD else aug.big[:, :aug.K]
             dx = torch.mm(_wide(dy2, N + Rp), rhs).view(ctx.shp)

@@ -27,7 +27,7 @@ import os
 import torch
 
 from ._backend import ext, use_hip
-from .linear import _TN_BWD, _accum_xty, _grad_ready, _mm_into, _spare_cols, _tail, _wide
+from .linear import _TN_BWD, _accum_xty, _grad_ready, _spare_cols, _tail, _wide, tail_product
 
 _OFF = os.environ.get("FTC_FUSED_MLP", "1") == "0"  # A/B switch: unfused composition
 
@@ -69,7 +69,7 @@ class _LoRAMLPFn(torch.autograd.Function):
         F, d = aug_dn.K, aug_dn.N
         # 1. gate|up projection, LoRA folded in through x's spare columns
         aug_gu.refresh(A_gu, B_gu, s_gu)
-        _mm_into(x2, aug_gu.big[N:, :K].t(), _tail(x2, K, aug_gu.Rp))
+        tail_product(x2, K, aug_gu.Rp, aug_gu.big[N:, :K], aug_gu.nct)
         gu = torch.mm(_wide(x2, K + aug_gu.Rp), aug_gu.big[:N].t())
         # 2. SwiGLU + s h A_down^T into h's spare columns
         h = ext().swiglu_fwd_lora(gu, aug_dn.Rp, aug_dn.fwd_tail_operand(A_dn, B_dn, s_dn), aug_dn.nct)
@@ -96,7 +96,7 @@ class _LoRAMLPFn(torch.autograd.Function):
             dy2 = buf[:, :d]
         # 4. dy B_down into dy's spare columns, dh through the augmented TN operand
         aug_dn.refresh(A_dn, B_dn, s_dn)
-        _mm_into(dy2, aug_dn.big[:d, F:], _tail(dy2, d, aug_dn.Rp))
+        tail_product(dy2, d, aug_dn.Rp, aug_dn.bwd_tail_operand(A_dn, B_dn, s_dn), aug_dn.nct)
         dyb_dn = _tail(dy2, d, aug_dn.R)
         rhs = aug_dn.bwd_operand() if _TN_BWD else aug_dn.big[:, :F]
         dh = torch.mm(_wide(dy2, d + aug_dn.Rp), rhs)

@@ -168,6 +168,22 @@ def test_swiglu_bwd_wgrad(C, T, F):
     torch.testing.assert_close(mgA.float(), refA, atol=2e-2 * refA.abs().max().item(), rtol=2e-2)
 
 
+@pytest.mark.parametrize("T,K,R,Rp", [(16384, 4096, 48, 64), (1000, 6144, 16, 64), (33, 128, 64, 64), (64, 256, 8, 16)])
+def test_tail_gemm(C, T, K, R, Rp):
+    """tail_gemm_ (csrc/kernels/swiglu_lora.hip): x[:, K:K+Rp] = x[:, :K] . Bm^T in place, zero past R."""
+    torch.manual_seed(0)
+    buf = bf(torch.randn(T, K + Rp + 8, device=DEV))
+    x = buf[:, :K]
+    bm = torch.zeros(Rp, K + 24, device=DEV, dtype=torch.bfloat16)
+    bm[:R, :K] = bf(torch.randn(R, K, device=DEV) * 0.05)
+    keep = buf[:, K + Rp:].clone()
+    C.tail_gemm_(x, bm[:, :K], -(-R // 16), Rp)
+    ref = x.float() @ bm[:R, :K].float().t()
+    torch.testing.assert_close(buf[:, K:K + R].float(), ref, atol=2e-2 * ref.abs().max().item() + 1e-3, rtol=2e-2)
+    assert torch.count_nonzero(buf[:, K + R:K + Rp]) == 0
+    assert torch.equal(buf[:, K + Rp:], keep)  # nothing written past the tail
+
+
 @pytest.mark.parametrize("V", [128256, 32000, 50257])
 def test_cross_entropy_inplace(C, V):
     torch.manual_seed(0)

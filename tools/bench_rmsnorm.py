@@ -24,6 +24,14 @@ def main():
     dy = torch.randn(T, d, device="cuda", dtype=bf)
     dres = torch.randn(T, d + 64, device="cuda", dtype=bf)[:, :d]
     nb = T * d * 2
+    xt = torch.randn(T, d + 64, device="cuda", dtype=bf)
+    bm = torch.zeros(64, d, device="cuda", dtype=bf)
+    bm[:48] = 0.05 * torch.randn(48, d, device="cuda", dtype=bf)
+    for nct in (1, 3):
+        ms = timeit(lambda: C.tail_gemm_(xt[:, :d], bm, nct, 64))
+        ms2 = timeit(lambda: torch.mm(xt[:, :d], bm.t(), out=torch.empty(T, 64, device="cuda", dtype=bf)))
+        print(json.dumps({"kernel": f"tail_gemm_nct{nct}", "ms": round(ms, 4), "TBps": round(nb / ms / 1e9, 2),
+                          "hipblaslt_ms": round(ms2, 4)}), flush=True)
     for name, fn, nbytes in (("fwd_res", lambda: C.rmsnorm_fwd(x, r, w, 1e-5, 64), 4 * nb),
                              ("bwd_dres_frozen", lambda: C.rmsnorm_bwd(dy, h, w, rstd, dres, False, 64), 4 * nb),
                              ("bwd_dres_dw", lambda: C.rmsnorm_bwd(dy, h, w, rstd, dres, True, 64), 4 * nb)):
