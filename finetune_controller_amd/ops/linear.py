@@ -235,8 +235,9 @@ def tail_product(x2: torch.Tensor, width: int, Rp: int, operand: torch.Tensor, n
     columns.  The HIP skinny-GEMM kernel streams x2 once at HBM rate (csrc/kernels/swiglu_lora.hip
     ``tail_gemm``); elsewhere a GEMM into the strided tail."""
     xv = x2[:, :width] if x2.shape[1] != width else x2
-    # up to 32 live columns the kernel streams at 6.3 TB/s vs hipBLASLt's 5.4; at 48 (packed q|k|v
-    # forward, nct = 3) its L2 fragment traffic loses (tools/bench_rmsnorm.py)
+    # up to 32 live columns the kernel streams at 6.3 TB/s vs hipBLASLt's 5.4 in isolation; at 48
+    # (packed q|k|v forward, nct = 3) its L2 fragment traffic loses (tools/bench_rmsnorm.py).  End to
+    # end the difference is within box noise (profiles/r1_tail_gemm_ab.log)
     if _HIP_TAIL and nct <= 2 and use_hip(x2) and ext().tail_gemm_ok(xv, Rp):
         ext().tail_gemm_(xv, operand, nct, Rp)
     else:
