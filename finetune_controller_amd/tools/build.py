@@ -72,7 +72,7 @@ def _hip_obj(src: Path, headers: list[Path], force: bool) -> Path:
 
 def _host_obj(src: Path, extra_inc: list[str], defines: list[str], force: bool, torch_headers: bool) -> Path:
     out = BUILD / (src.stem + ".cpp.o")
-    if force or _newer(out, [src]):
+    if force or _newer(out, [src, *sorted(src.parent.glob("*.h"))]):  # + headers next to the source
         cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-c", str(src), "-o", str(out), "-D__HIP_PLATFORM_AMD__=1",
                "-DUSE_ROCM=1", f"-I{ROCM}/include", f"-I{sysconfig.get_paths()['include']}"]
         cmd += [f"-I{p}" for p in extra_inc] + defines
