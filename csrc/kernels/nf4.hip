@@ -27,6 +27,14 @@ __constant__ float kNF4[16] = {-1.0f,
                                0.7229568362236023f,
                                1.0f};
 
+// The codebook indexed per lane from __constant__ memory compiles to one global load per element (16
+// vector-memory loads per 8 bytes of codes: the dequant kernels ran at 2.5 TB/s).  Each workgroup
+// copies it to LDS once; a lookup is then one conflict-free ds_read (16 entries, 16 banks).
+FTC_DEV void nf4_lut_load(float* lut) {
+  if (threadIdx.x < 16) lut[threadIdx.x] = kNF4[threadIdx.x];
+  __syncthreads();
+}
+
 FTC_DEV int nf4_encode(float x) {
   // nearest codebook entry (midpoints between consecutive codes)
   int best = 0;
@@ -63,6 +71,8 @@ __global__ __launch_bounds__(256) void nf4_dequant_kernel(const uint8_t* __restr
                                                           uint16_t* __restrict__ out, long long n, int block,
                                                           int block2) {
   // each thread: 16 codes (8 bytes) -> 16 bf16 (32 bytes)
+  __shared__ float lut[16];
+  nf4_lut_load(lut);
   const long long n16 = n >> 4;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long long)gridDim.x * 256) {
     const uint2 p = reinterpret_cast<const uint2*>(packed)[i];
@@ -76,8 +86,8 @@ __global__ __launch_bounds__(256) void nf4_dequant_kernel(const uint8_t* __restr
 #pragma unroll
       for (int bt = 0; bt < 4; ++bt) {
         const uint32_t byte = (words[wd] >> (8 * bt)) & 0xffu;
-        f[wd * 8 + bt * 2] = kNF4[byte >> 4] * a;
-        f[wd * 8 + bt * 2 + 1] = kNF4[byte & 0xf] * a;
+        f[wd * 8 + bt * 2] = lut[byte >> 4] * a;
+        f[wd * 8 + bt * 2 + 1] = lut[byte & 0xf] * a;
       }
     }
     uint4* o = reinterpret_cast<uint4*>(out + e0);
@@ -92,6 +102,8 @@ __global__ __launch_bounds__(256) void nf4_dequant_rows_kernel(const uint8_t* __
                                                                const float* __restrict__ s2, float off,
                                                                uint16_t* __restrict__ out, long long n, int cols,
                                                                long long ldo, int block, int block2) {
+  __shared__ float lut[16];
+  nf4_lut_load(lut);
   const long long n16 = n >> 4;
   const int c16 = cols >> 4;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long long)gridDim.x * 256) {
@@ -106,8 +118,8 @@ __global__ __launch_bounds__(256) void nf4_dequant_rows_kernel(const uint8_t* __
 #pragma unroll
       for (int bt = 0; bt < 4; ++bt) {
         const uint32_t byte = (words[wd] >> (8 * bt)) & 0xffu;
-        f[wd * 8 + bt * 2] = kNF4[byte >> 4] * a;
-        f[wd * 8 + bt * 2 + 1] = kNF4[byte & 0xf] * a;
+        f[wd * 8 + bt * 2] = lut[byte >> 4] * a;
+        f[wd * 8 + bt * 2 + 1] = lut[byte & 0xf] * a;
       }
     const long long row = i / c16;
     const int c = (int)(i - row * c16) * 16;
@@ -126,6 +138,8 @@ __global__ __launch_bounds__(256) void nf4_dequant_t_kernel(const uint8_t* __res
                                                             uint16_t* __restrict__ outT, int N, int K, long long ldo,
                                                             int block2) {
   __shared__ uint16_t tile[64][64 + 2];
+  __shared__ float lut[16];
+  nf4_lut_load(lut);
   const int n0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
   const int t = threadIdx.x;
   {
@@ -141,8 +155,8 @@ __global__ __launch_bounds__(256) void nf4_dequant_t_kernel(const uint8_t* __res
       for (int bt = 0; bt < 4; ++bt) {
         const uint32_t byte = (words[wd] >> (8 * bt)) & 0xffu;
         const int kk = kq + wd * 8 + bt * 2;
-        tile[kk][nl] = f2bf(kNF4[byte >> 4] * a);
-        tile[kk + 1][nl] = f2bf(kNF4[byte & 0xf] * a);
+        tile[kk][nl] = f2bf(lut[byte >> 4] * a);
+        tile[kk + 1][nl] = f2bf(lut[byte & 0xf] * a);
       }
   }
   __syncthreads();
