@@ -111,7 +111,14 @@ FTC_DEV void fwd_dma(__amdgpu_buffer_rsrc_t kr, __amdgpu_buffer_rsrc_t vr, const
   }
 }
 
-template <int D, int WAVES>
+// PP (WAVES = 8 only): ping-pong phase order for the two waves sharing a SIMD (w, w + 4): half 0 runs
+// A(t) B1(t) B2(t) and half 1 runs B2(t-1) A(t) B1(t) between the same barriers (A = S MFMAs, B1 =
+// mask / online softmax / pack VALU, B2 = PV MFMAs), so one wave's softmax issues under the other's
+// MFMAs.  Half 1 reads V of tile t-1 one interval late: V has a 4-slot ring (K keeps 2).  Measured
+// at the Llama-3-8B layer shape: 0.64 ms vs 0.617 (8 waves) and 0.604 (4 waves, the default) -- unlike
+// the dK/dV kernel, the forward's softmax already overlaps across the two co-resident 4-wave
+// workgroups, so PP stays opt-in (FTC_FLASH_FWD_WAVES=8 FTC_FLASH_FWD_PP=1; profiles/r1_attn_fwd_pp.log).
+template <int D, int WAVES, bool PP = false>
 __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArgs a) {
   constexpr int BQ = 32 * WAVES;
   constexpr int NCH = D / 8;           // 16-byte chunks per row
@@ -127,6 +134,8 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
   __shared__ __attribute__((aligned(16))) char V0[TILE_BYTES];
   __shared__ __attribute__((aligned(16))) char K1[TILE_BYTES];
   __shared__ __attribute__((aligned(16))) char V1[TILE_BYTES];
+  __shared__ __attribute__((aligned(16))) char V2[PP ? TILE_BYTES : 16];
+  __shared__ __attribute__((aligned(16))) char V3[PP ? TILE_BYTES : 16];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform -> scalar branches
@@ -187,17 +196,17 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
   const int gi = lane >> 4, li = lane & 15;
   const int trq = li >> 2, trp = li & 3;
 
-  // tile t reads (Kc, Vc); tile t+1 is DMA'd into (Kn, Vn), which held tile t-1 -- free once every
-  // wave passed this tile's barrier
-  auto tile = [&](const int t, const char* Kc, const char* Vc, char* Kn, char* Vn) __attribute__((always_inline)) {
-    const int kv0 = kv_begin + t * BK;
+  f32x16 s[2];   // S^T of the current tile, then its P (registers between the phases)
+  bf16x8 pf[4];  // packed P^T operand of the PV MFMAs (carried across a barrier by PP's half 1)
+  // wait for tile t, barrier, then DMA tile t+1 into the slots that held tile t-1 (PP: V of t-3)
+  auto sync_tile = [&](const int t, char* Kn, char* Vn) __attribute__((always_inline)) {
     __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's pieces of tile t landed (vmcnt(0))
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     __builtin_amdgcn_s_barrier();        // ... and everyone's
-    if (t + 1 < ntiles) fwd_dma<D, NGT, RPG>(krs, vrs, voff, (kv0 + BK) * (int)a.kv_rs * 2, Kn, Vn, wave);
-
-    // ---- S^T = K Q^T : two 32-key blocks
-    f32x16 s[2];
+    if (t + 1 < ntiles) fwd_dma<D, NGT, RPG>(krs, vrs, voff, (kv_begin + (t + 1) * BK) * (int)a.kv_rs * 2, Kn, Vn, wave);
+  };
+  // ---- phase A: S^T = K Q^T, two 32-key blocks
+  auto phaseA = [&](const char* Kc) __attribute__((always_inline)) {
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       // issue all LDS reads of this 32-key block before its MFMA chain (no read->wait->mfma serialisation)
@@ -221,8 +230,11 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
     __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-
-    // ---- mask (wave-uniform branch, branch-free selects inside) + online softmax in the log2 domain
+  };
+  // ---- phase B1: mask (wave-uniform branch, branch-free selects inside) + online softmax in the log2
+  // domain; P packed as the bf16 B operand of the PV MFMAs
+  auto phaseB1 = [&](const int t) __attribute__((always_inline)) {
+    const int kv0 = kv_begin + t * BK;
     const int qmin_w = q0 + wave * 32;
     const bool need_mask = (a.causal && kv0 + BK - 1 > qmin_w) || (a.window > 0 && qmin_w + 31 - kv0 >= a.window);
     if (need_mask) {
@@ -268,11 +280,11 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
         rs += p;
       }
     l += rs;
-
-    // ---- O^T += V^T P^T : 4 k-steps of 16 keys
-    bf16x8 pf[4];
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) pf[ks] = pack_p(s[ks >> 1], 8 * (ks & 1));
+  };
+  // ---- phase B2: O^T += V^T P^T, 4 k-steps of 16 keys
+  auto phaseB2 = [&](const char* Vc) __attribute__((always_inline)) {
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
       const int col = dt * 32 + 16 * (gi & 1) + 4 * trp;
@@ -292,9 +304,53 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
       }
     }
   };
-  for (int t = 0; t < ntiles; t += 2) {
-    tile(t, K0, V0, K1, V1);
-    if (t + 1 < ntiles) tile(t + 1, K1, V1, K0, V0);
+  if constexpr (!PP) {
+    // tile t reads (Kc, Vc); tile t+1 is DMA'd into (Kn, Vn), which held tile t-1 -- free once every
+    // wave passed this tile's barrier
+    auto tile = [&](const int t, const char* Kc, const char* Vc, char* Kn, char* Vn) __attribute__((always_inline)) {
+      sync_tile(t, Kn, Vn);
+      phaseA(Kc);
+      phaseB1(t);
+      phaseB2(Vc);
+    };
+    for (int t = 0; t < ntiles; t += 2) {
+      tile(t, K0, V0, K1, V1);
+      if (t + 1 < ntiles) tile(t + 1, K1, V1, K0, V0);
+    }
+  } else {
+    // K ring of 2 (K of tile t-1 is free after its interval), V ring of 4 (half 1 reads V of t-1 in
+    // interval t); separate straight-line loops per half, equal barrier counts
+    if (wave < 4) {
+      auto tile = [&](const int t, const char* Kc, const char* Vc, char* Kn, char* Vn) __attribute__((always_inline)) {
+        sync_tile(t, Kn, Vn);
+        phaseA(Kc);
+        phaseB1(t);
+        phaseB2(Vc);
+      };
+      for (int t = 0; t < ntiles; t += 4) {
+        tile(t, K0, V0, K1, V1);
+        if (t + 1 < ntiles) tile(t + 1, K1, V1, K0, V2);
+        if (t + 2 < ntiles) tile(t + 2, K0, V2, K1, V3);
+        if (t + 3 < ntiles) tile(t + 3, K1, V3, K0, V0);
+      }
+    } else {
+      auto tile = [&](const int t, const char* Kc, const char* Vprev, char* Kn, char* Vn) __attribute__((always_inline)) {
+        sync_tile(t, Kn, Vn);
+        if (t > 0) phaseB2(Vprev);
+        phaseA(Kc);
+        phaseB1(t);
+      };
+      for (int t = 0; t < ntiles; t += 4) {
+        tile(t, K0, V3, K1, V1);
+        if (t + 1 < ntiles) tile(t + 1, K1, V0, K0, V2);
+        if (t + 2 < ntiles) tile(t + 2, K0, V1, K1, V3);
+        if (t + 3 < ntiles) tile(t + 3, K1, V2, K0, V0);
+      }
+      if (ntiles > 0) {
+        const int last = ntiles - 1;
+        phaseB2((last & 3) == 0 ? V0 : (last & 3) == 1 ? V1 : (last & 3) == 2 ? V2 : V3);
+      }
+    }
   }
 
   // ---- epilogue: normalise, store O (bf16) and LSE (natural log)
@@ -334,7 +390,13 @@ extern "C" int ftc_flash_fwd(const void* q, const void* k, const void* v, void* 
             B, S, H, KV, (S + BQ - 1) / BQ, scale * LOG2E, causal, window};
   const int nblocks = a.nqb * B * H;
   const size_t lds = 0;  // static: K/V double buffers
-  if (waves == 8) {
+  static const bool pp = [] {
+    const char* e = getenv("FTC_FLASH_FWD_PP");
+    return e && e[0] == '1';
+  }();
+  if (waves == 8 && pp && D == 128) {
+    hipLaunchKernelGGL((flash_fwd_kernel<128, 8, true>), dim3(nblocks), dim3(512), lds, stream, a);
+  } else if (waves == 8) {
     if (D == 128)
       hipLaunchKernelGGL((flash_fwd_kernel<128, 8>), dim3(nblocks), dim3(512), lds, stream, a);
     else
