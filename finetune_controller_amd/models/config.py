@@ -8,7 +8,8 @@ the fine-tune targets named by BASELINE.json are built here from their public co
 * ``mistral-7b`` -- same trunk, vocab 32000, RoPE 1e4, sliding window 4096 (v0.1)
 * ``gpt2-small`` -- d 768, 12 layers, 12 heads x 64, FFN 3072, vocab 50257, LayerNorm + GELU, learned positions
 
-plus ``*-tiny`` variants of the same families used by CPU tests and the FakeCluster e2e job.
+plus Llama-3.1 / 3.2 / 70B and Mistral v0.3 members of the same trunk, and ``*-tiny`` variants of
+each family used by CPU tests and the FakeCluster e2e job.
 """
 from __future__ import annotations
 
@@ -103,11 +104,25 @@ class ModelConfig:
                    cfg.get("tie_word_embeddings", False), name=name or mt)
 
 
+_L31 = {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+        "original_max_position_embeddings": 8192}
+
 PRESETS: dict[str, ModelConfig] = {
     "llama3-8b": ModelConfig("llama", 128256, 4096, 32, 32, 8, 14336, 8192, 500000.0, name="llama3-8b"),
     "mistral-7b": ModelConfig("llama", 32000, 4096, 32, 32, 8, 14336, 32768, 10000.0, sliding_window=4096,
                               name="mistral-7b"),
     "gpt2-small": ModelConfig("gpt2", 50257, 768, 12, 12, 12, 3072, 1024, tie_embeddings=True, name="gpt2-small"),
+    # further members of the Llama trunk (public configs): Llama-3.1 frequency scaling, Llama-3.2's tied
+    # embeddings and head_dim 64 (1B) / 24-head GQA 3:1 (3B), the 80-layer 70B (QLoRA fits one
+    # 288 GB MI355X), Mistral v0.3 (full attention, 32768 vocab)
+    "llama3.1-8b": ModelConfig("llama", 128256, 4096, 32, 32, 8, 14336, 131072, 500000.0, name="llama3.1-8b",
+                               rope_scaling=_L31),
+    "llama3.2-1b": ModelConfig("llama", 128256, 2048, 16, 32, 8, 8192, 131072, 500000.0, tie_embeddings=True,
+                               name="llama3.2-1b", rope_scaling={**_L31, "factor": 32.0}),
+    "llama3.2-3b": ModelConfig("llama", 128256, 3072, 28, 24, 8, 8192, 131072, 500000.0, tie_embeddings=True,
+                               name="llama3.2-3b", rope_scaling={**_L31, "factor": 32.0}),
+    "llama3-70b": ModelConfig("llama", 128256, 8192, 80, 64, 8, 28672, 8192, 500000.0, name="llama3-70b"),
+    "mistral-7b-v0.3": ModelConfig("llama", 32768, 4096, 32, 32, 8, 14336, 32768, 1000000.0, name="mistral-7b-v0.3"),
     # test-sized members of each family (same code paths, seconds on CPU)
     "llama-tiny": ModelConfig("llama", 512, 128, 2, 4, 2, 256, 512, 500000.0, name="llama-tiny"),
     "mistral-tiny": ModelConfig("llama", 384, 128, 2, 4, 2, 256, 512, 10000.0, sliding_window=64, name="mistral-tiny"),

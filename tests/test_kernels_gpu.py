@@ -586,3 +586,44 @@ def test_llama_fused_lora_mlp_matches_torch_path(C, monkeypatch):
         if (a - b).abs().max().item() > 5e-2 * b.abs().max().item() + 1e-3:
             bad.append((o, n, (a - b).abs().max().item(), b.abs().max().item()))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("name", ["llama3.2-1b", "llama3.2-3b", "llama3-70b", "mistral-7b-v0.3", "llama3.1-8b"])
+def test_llama_family_presets_hip_match_torch(C, monkeypatch, name):
+    """One full-width layer of each Llama-trunk preset (head_dim 64 flash path, GQA 3:1, tied
+    embeddings, Llama-3.1 rope scaling, the 70B width) with LoRA r=16 on adapters homed in a flat
+    gradient buffer: HIP path (fused MLP block included) against the stock-PyTorch path."""
+    import dataclasses
+
+    from finetune_controller_amd.models import LoRAConfig, build_model
+    from finetune_controller_amd.models.config import get_config
+    from finetune_controller_amd.train.optim import FlatAdamW
+
+    cfg = dataclasses.replace(get_config(name), n_layers=1, max_seq_len=512)
+    lc = LoRAConfig(r=16, alpha=32)
+    ids = torch.randint(0, cfg.vocab_size, (1, 512), device=DEV)
+    labels = torch.roll(ids, -1, 1)
+    res = {}
+    for mode in ("hip", "torch"):
+        monkeypatch.setenv("FTC_KERNELS", mode)
+        torch.manual_seed(0)
+        m = build_model(cfg, lc, device=DEV, dtype=torch.bfloat16)
+        m.init_weights(seed=5)
+        m.freeze_base()
+        g = torch.Generator(device=DEV).manual_seed(1)
+        for layer in m.layers:
+            for p in layer.lora.values():
+                for _, _, B_s in p.segment_tensors():
+                    B_s.data.normal_(0, 0.05, generator=g)
+        opt = FlatAdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3)
+        opt.zero_grad()
+        loss = m(ids, labels)
+        loss.backward()
+        res[mode] = (loss.float().item(), opt.grad_flat.float().clone(), list(opt.offsets))
+        del m, opt
+        torch.cuda.empty_cache()
+    (lh, gh, offs), (lt, gt, _) = res["hip"], res["torch"]
+    assert abs(lh - lt) < 2e-2 * abs(lt), (lh, lt)
+    for o, n in offs:
+        a, b = gh[o:o + n], gt[o:o + n]
+        assert (a - b).abs().max().item() <= 5e-2 * b.abs().max().item() + 1e-3, (name, o, n)

@@ -484,3 +484,32 @@ def test_zero1_sharded_optimizer_matches_ddp(tmp_path, world):
     live1 = p1[p1 != 0]
     # reduction orders differ (reduce-scatter vs all-reduce); AdamW steps are lr = 1e-2 per element
     torch.testing.assert_close(live1, live0, atol=1e-4, rtol=1e-3)
+
+
+@pytest.mark.parametrize("name", ["llama3.1-8b", "llama3.2-1b", "llama3.2-3b", "llama3-70b", "mistral-7b-v0.3"])
+def test_llama_family_presets(name):
+    """Llama-trunk presets: public parameter counts, HF config round trip (rope scaling, tied
+    embeddings), and a LoRA step of a width-reduced copy on the CPU reference path."""
+    import dataclasses
+
+    from finetune_controller_amd.models import LoRAConfig, build_model
+    from finetune_controller_amd.models.config import ModelConfig, get_config
+
+    expect = {"llama3.1-8b": 8.03, "llama3.2-1b": 1.24, "llama3.2-3b": 3.21, "llama3-70b": 70.55,
+              "mistral-7b-v0.3": 7.25}
+    cfg = get_config(name)
+    assert abs(cfg.num_params() / 1e9 - expect[name]) < 0.01
+    back = ModelConfig.from_hf_config(cfg.to_hf_config(), name=name)
+    assert (back.rope_scaling, back.tie_embeddings, back.n_kv_heads, back.rope_theta) == \
+        (cfg.rope_scaling, cfg.tie_embeddings, cfg.n_kv_heads, cfg.rope_theta)
+    small = dataclasses.replace(cfg, vocab_size=512, dim=cfg.head_dim * 4, n_layers=1, n_heads=4,
+                                n_kv_heads=4 // max(1, cfg.n_heads // cfg.n_kv_heads) or 1, ffn_dim=256,
+                                max_seq_len=64)
+    torch.manual_seed(0)
+    m = build_model(small, LoRAConfig(r=4, alpha=8), dtype=torch.float32)
+    m.init_weights(seed=1)
+    m.freeze_base()
+    ids = torch.randint(0, 512, (2, 32))
+    loss = m(ids, torch.roll(ids, -1, 1))
+    loss.backward()
+    assert torch.isfinite(loss) and all(p.grad is not None for p in m.parameters() if p.requires_grad)
