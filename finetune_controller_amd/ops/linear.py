@@ -88,6 +88,17 @@ _TUNABLEOP = os.environ.get("PYTORCH_TUNABLEOP_ENABLED", "0") == "1"
 _TN_BWD = os.environ.get("FTC_TN_BWD", "1") != "0"  # transposed frozen-weight copies for backward GEMMs
 
 
+def set_tn_backward(on: bool) -> None:
+    """Enable / disable the W^T copies of the TN backward GEMMs (+2 B per weight element of HBM);
+    the trainer turns them off when the copies would not fit next to the model (e.g. 70B bf16)."""
+    global _TN_BWD
+    _TN_BWD = bool(on) and os.environ.get("FTC_TN_BWD", "1") != "0"
+
+
+def tn_backward() -> bool:
+    return _TN_BWD
+
+
 class FrozenTransposed:
     """Cache of ``W^T`` (contiguous) for frozen 2-D weights used as the right operand of ``x @ W`` in a
     backward pass (TN layout, see AugWeight.bwd_operand).  Keyed by the parameter; rebuilt when the

@@ -27,7 +27,7 @@ import os
 import torch
 
 from ._backend import ext, use_hip
-from .linear import _TN_BWD, _accum_xty, _grad_ready, _spare_cols, _tail, _wide, tail_product
+from .linear import _accum_xty, _grad_ready, _spare_cols, _tail, _wide, tail_product, tn_backward
 
 _OFF = os.environ.get("FTC_FUSED_MLP", "1") == "0"  # A/B switch: unfused composition
 
@@ -98,7 +98,7 @@ class _LoRAMLPFn(torch.autograd.Function):
         aug_dn.refresh(A_dn, B_dn, s_dn)
         tail_product(dy2, d, aug_dn.Rp, aug_dn.bwd_tail_operand(A_dn, B_dn, s_dn), aug_dn.nct)
         dyb_dn = _tail(dy2, d, aug_dn.R)
-        rhs = aug_dn.bwd_operand() if _TN_BWD else aug_dn.big[:, :F]
+        rhs = aug_dn.bwd_operand() if tn_backward() else aug_dn.big[:, :F]
         dh = torch.mm(_wide(dy2, d + aug_dn.Rp), rhs)
         # 5. dB_down += dy^T (s h A_down^T)
         _accum_xty(B_dn.main_grad, dy2, _tail(h, F, aug_dn.R), 1.0)
@@ -112,7 +112,7 @@ class _LoRAMLPFn(torch.autograd.Function):
         # 7. dx and dA_gu += s x^T (dgu B_gu)
         dx = None
         if ctx.needs_input_grad[0]:
-            rhs = aug_gu.bwd_operand() if _TN_BWD else aug_gu.big[:, :K]
+            rhs = aug_gu.bwd_operand() if tn_backward() else aug_gu.big[:, :K]
             dx = torch.mm(_wide(dgu, N + aug_gu.Rp), rhs).view(ctx.shp)
         _accum_xty(A_gu.main_grad.t(), x2, _tail(dgu, N, aug_gu.R), s_gu)
         _grad_ready(A_gu)

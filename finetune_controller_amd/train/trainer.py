@@ -111,6 +111,7 @@ class Trainer:
 
             quantize_model_(self.model)
         self.model.train()
+        self._memory_policy()
         # the loss is a per-micro-batch mean; summing grads over accum x world and scaling once
         # in the optimizer gives the global mean
         okw = dict(lr=tc.lr, weight_decay=tc.weight_decay, max_grad_norm=tc.max_grad_norm,
@@ -133,6 +134,21 @@ class Trainer:
         self.step = 0
         self.is_main = self.info.is_main
         self._timing: list[tuple] = []  # per-step (start, fwd, bwd, comm, optim) device events
+
+    def _memory_policy(self):
+        """HBM budget decisions that depend on the model size: the TN backward GEMMs keep a transposed
+        copy of every bf16 weight (+2 B/param); skip them when weights + copies would take more than
+        45 % of the device (e.g. Llama-3-70B in bf16: 141 GB of weights on a 288 GB MI355X)."""
+        if self.device.type != "cuda":
+            return
+        from ..ops.linear import set_tn_backward
+
+        total = torch.cuda.get_device_properties(self.device).total_memory
+        wbytes = sum(p.numel() * p.element_size() for p in self.model.parameters() if p.dim() == 2)
+        on = 2 * wbytes <= 0.45 * total
+        set_tn_backward(on)
+        if not on and self.info.is_main:
+            log.info("TN backward copies off: %.0f GB of 2-D weights on a %.0f GB device", wbytes / 1e9, total / 1e9)
 
     # ------------------------------------------------------------------ data
     def data(self):
