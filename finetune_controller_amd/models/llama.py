@@ -29,7 +29,7 @@ from torch.utils.checkpoint import checkpoint
 from .. import ops
 from .config import ModelConfig
 from ..ops.linear import AugWeight, LoRATail, TailOperands
-from ..ops.mlp import fused_mlp_supported, lora_mlp
+from ..ops.mlp import AugProj, NF4Proj, fused_mlp_supported, lora_mlp
 from .lora import LoRAConfig, make_pairs
 
 
@@ -101,6 +101,25 @@ class LlamaLayer(nn.Module):
             return None
         return LoRATail(aw, pair.A, pair.B, pair.scale, pair.blocks)
 
+    def mlp_projs(self, p_gu: int, p_down: int):
+        """(gate|up, down) projections for ops.mlp.lora_mlp: AugProj (bf16) or NF4Proj (QLoRA), or None."""
+        if "gu" not in self.lora or "down" not in self.lora or p_gu <= 0 or p_down <= 0:
+            return None
+        out = []
+        for name, pad in (("gu", p_gu), ("down", p_down)):
+            pair = self.lora[name]
+            if name in self.qweights:
+                t = self.tail(name, pad)  # creates the TailOperands
+                if t is None:
+                    return None
+                out.append(NF4Proj(self.qweights[name], self.qtails[name], pair))
+            else:
+                aw = self.aug.get(name)
+                if aw is None or not aw.owns(self.base_weight(name)):
+                    return None
+                out.append(AugProj(aw, pair))
+        return tuple(out)
+
     def proj(self, name: str, x: torch.Tensor) -> torch.Tensor:
         pair = self.lora[name] if name in self.lora else None
         qw = self.qweights.get(name)
@@ -128,11 +147,11 @@ class LlamaLayer(nn.Module):
                                  out_pad=p_o, grad_pad=p_qkv)
         o = self.proj("o", a)
         h, x = ops.add_rms_norm(h, o, self.mlp_norm, cfg.norm_eps, pad=p_gu, grad_pad=p_o)
-        if "gu" in self.lora and "down" in self.lora and not self.qweights and fused_mlp_supported(
-                x, self.aug.get("gu"), self.lora["gu"], self.aug.get("down"), self.lora["down"], p_gu, p_down,
-                self.training):
+        mlp = self.mlp_projs(p_gu, p_down)
+        if mlp is not None and fused_mlp_supported(x, mlp[0], mlp[1], self.lora["gu"], self.lora["down"], p_gu,
+                                                   p_down, self.training):
             # the whole LoRA MLP as one autograd function: SwiGLU backward also forms dB_gu / dA_down
-            return h, lora_mlp(x, self.aug["gu"], self.lora["gu"], self.aug["down"], self.lora["down"])
+            return h, lora_mlp(x, mlp[0], mlp[1])
         gu = self.proj("gu", x)
         act = ops.swiglu(gu, out_pad=p_down, grad_pad=p_gu, fwd_tail=self.tail("down", p_down),
                          bwd_tail=self.tail("gu", p_gu))

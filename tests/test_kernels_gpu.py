@@ -627,3 +627,44 @@ def test_llama_family_presets_hip_match_torch(C, monkeypatch, name):
     for o, n in offs:
         a, b = gh[o:o + n], gt[o:o + n]
         assert (a - b).abs().max().item() <= 5e-2 * b.abs().max().item() + 1e-3, (name, o, n)
+
+
+def test_qlora_fused_mlp_matches_torch_path(C, monkeypatch):
+    """QLoRA through the fused MLP block (NF4Proj: dequantised augmented / TN operands, SwiGLU backward
+    forming dB_gu / dA_down) against the stock-PyTorch QLoRA path, adapters in flat gradient buffers."""
+    import finetune_controller_amd.models.llama as llama_mod
+    from finetune_controller_amd.models import LoRAConfig, build_model
+    from finetune_controller_amd.models.config import ModelConfig
+    from finetune_controller_amd.ops.nf4 import quantize_model_
+    from finetune_controller_amd.train.optim import FlatAdamW
+
+    cfg = ModelConfig("llama", 512, 256, 2, 4, 2, 1024, 512, 10000.0, name="llama-test")
+    calls = []
+    real = llama_mod.lora_mlp
+    monkeypatch.setattr(llama_mod, "lora_mlp", lambda *a, **k: calls.append(1) or real(*a, **k))
+    ids = torch.randint(0, cfg.vocab_size, (2, 256), device=DEV)
+    labels = torch.roll(ids, -1, 1)
+    res = {}
+    for mode in ("hip", "torch"):
+        monkeypatch.setenv("FTC_KERNELS", mode)
+        torch.manual_seed(0)
+        m = build_model(cfg, LoRAConfig(r=16, alpha=32), device=DEV, dtype=torch.bfloat16)
+        m.init_weights(seed=5)
+        m.freeze_base()
+        quantize_model_(m)
+        g = torch.Generator(device=DEV).manual_seed(1)
+        for layer in m.layers:
+            for p in layer.lora.values():
+                for _, _, B_s in p.segment_tensors():
+                    B_s.data.normal_(0, 0.05, generator=g)
+        opt = FlatAdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3)
+        opt.zero_grad()
+        loss = m(ids, labels)
+        loss.backward()
+        res[mode] = (loss.float().item(), opt.grad_flat.float().clone(), list(opt.offsets))
+    assert len(calls) == cfg.n_layers
+    (lh, gh, offs), (lt, gt, _) = res["hip"], res["torch"]
+    assert abs(lh - lt) < 2e-2 * abs(lt)
+    for o, n in offs:
+        a, b = gh[o:o + n], gt[o:o + n]
+        assert (a - b).abs().max().item() <= 5e-2 * b.abs().max().item() + 1e-3, (o, n)
