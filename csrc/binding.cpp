@@ -265,8 +265,7 @@ bool swiglu_wgrad_ok(const at::Tensor& gu, int64_t pad) {
   int rb;
   long long wsf;
   const long long T = gu.size(0), F = gu.size(1) / 2;
-  return gu.dim() == 2 && ftc_swiglu_wgrad_plan(T, (int)F, &rb, &wsf) == 0 && pad >= 32 && pad % 8 == 0 &&
-         T * 4LL * F < (1LL << 31) && T * (2 * F + pad) * 2 < (1LL << 31);
+  return gu.dim() == 2 && ftc_swiglu_wgrad_plan(T, (int)F, &rb, &wsf) == 0 && pad >= 32 && pad % 8 == 0;
 }
 
 at::Tensor swiglu_bwd_wgrad(const at::Tensor& da, const at::Tensor& gu, int64_t pad, const at::Tensor& bt,
@@ -312,7 +311,7 @@ at::Tensor swiglu_bwd_wgrad(const at::Tensor& da, const at::Tensor& gu, int64_t 
 bool tail_gemm_ok(const at::Tensor& x, int64_t Rp) {
   return x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.stride(1) == 1 &&
          x.size(1) % 128 == 0 && x.stride(0) % 8 == 0 && x.stride(0) >= x.size(1) + Rp &&
-         reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && x.size(0) * x.stride(0) * 2 < (1LL << 31);
+         reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0;
 }
 
 void tail_gemm_(at::Tensor& x, const at::Tensor& bm, int64_t nct, int64_t Rp) {

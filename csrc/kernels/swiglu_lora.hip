@@ -531,8 +531,9 @@ extern "C" int ftc_swiglu_bwd_wgrad(const void* da, long long da_rs, const void*
   int RB;
   long long wsf;
   if (ftc_swiglu_wgrad_plan(T, F, &RB, &wsf) != 0) return -1;
+  // buffer resources are made per 16-row sub-tile: no 2 GiB limit on the tensors themselves
   if (Rp < 32 || Rp % 8 != 0 || dgu_rs < 2LL * F + Rp || da_rs % 8 || dgu_rs % 8 || ldb % 8 || xa_rs % 8 ||
-      dyb_rs % 8 || T * 4LL * F >= (1LL << 31) || T * dgu_rs * 2 >= (1LL << 31))
+      dyb_rs % 8 || T >= (1LL << 31))
     return -1;
   const int ncb = F / kCB;
   const int nrb = (int)((T + RB - 1) / RB);
@@ -616,7 +617,7 @@ __global__ __launch_bounds__(256) void tail_gemm_kernel(uint16_t* __restrict__ X
 extern "C" int ftc_tail_gemm(void* x, long long ldx, long long rows, int K, const void* Bm, long long ldb, int nct,
                              int Rp, hipStream_t stream) {
   if (K % 128 != 0 || ldx % 8 != 0 || ldb % 8 != 0 || ldx < (long long)K + Rp || nct < 1 || nct > 4 ||
-      Rp < 16 * nct || Rp % 16 != 0 || rows <= 0 || rows * ldx * 2 >= (1LL << 31))
+      Rp < 16 * nct || Rp % 16 != 0 || rows <= 0)  // per-block buffer resources: no 2 GiB limit
     return -1;
   const dim3 grid((unsigned)((rows + 31) / 32)), block(256);
   auto X = (uint16_t*)x;

@@ -124,9 +124,8 @@ def fused_mlp_supported(x2: torch.Tensor, gu, dn, pair_gu, pair_down, p_gu: int,
         if (q.qw.block != 64 or gu.K % 64 or gu.N % 64 or dn.K % 64 or dn.N % 64
                 or x2.shape[0] <= FUSED_MAX_ROWS):  # few rows: the fused NF4 GEMM path is faster
             return False
-    # swiglu_bwd_wgrad's limits (csrc/kernels/swiglu_lora.hip): 512-column blocks, 32-bit buffer offsets
-    T, Rp = x2.shape[0], gu.Rp
-    return F % 512 == 0 and T * 4 * F < 2 ** 31 and T * (2 * F + Rp) * 2 < 2 ** 31 and Rp % 8 == 0
+    # swiglu_bwd_wgrad's shape limits (csrc/kernels/swiglu_lora.hip): 512-column blocks
+    return F % 512 == 0 and gu.Rp % 8 == 0
 
 
 class _LoRAMLPFn(torch.autograd.Function):
