@@ -150,8 +150,9 @@ FTC_DEV void dkdv_dma(__amdgpu_buffer_rsrc_t qr, __amdgpu_buffer_rsrc_t dr, __am
 // dV / dK MFMAs.  One wave's exp / mask / pack work then issues under its partner's MFMAs instead of
 // both waves idling the matrix pipe at the same time (guide: MI355X_MICROARCH.md "Two waves per
 // SIMD").  Slice j is read by half 1 one barrier interval later, so the Q/dO ring has 4 slots.
-template <int D, int HW, bool PP = false>
+template <int D, int HW, bool PP = false, int DIST = 2>
 __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
+  static_assert(DIST == 2 || (PP && DIST == 3), "DMA distance 3 needs the ping-pong 5-slot ring");
   constexpr int NCH = D / 8, DSTEPS = D / 16, DT = D / 32;
   constexpr int BKV = 256, BQ2 = 32;
   constexpr int WAVES = 8 / HW, NT = 64 * WAVES;
@@ -165,6 +166,7 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
   __shared__ __attribute__((aligned(16))) char slot1[SLICE];
   __shared__ __attribute__((aligned(16))) char slot2[SLICE];
   __shared__ __attribute__((aligned(16))) char slot3[PP ? SLICE : 16];
+  __shared__ __attribute__((aligned(16))) char slot4[DIST == 3 ? SLICE : 16];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -251,6 +253,7 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
                                  (hq_ * D + qt_ * (int)a.do_rs) * 2, ((b * a.H + hq_) * S + qt_) * 4, base_, wave);
   };
   constexpr int VM_ONE = 0x0F70 | (PER_SLICE & 15) | ((PER_SLICE >> 4) << 14);  // vmcnt(PER_SLICE)
+  constexpr int VM_TWO = 0x0F70 | ((2 * PER_SLICE) & 15) | (((2 * PER_SLICE) >> 4) << 14);  // vmcnt(2 PER_SLICE)
   constexpr int VM_ZERO = 0x0F70;                                               // vmcnt(0)
   constexpr int LGKM_ZERO = 0xC07F;                                             // lgkmcnt(0)
 
@@ -264,6 +267,7 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
   __syncthreads();  // K staged (no DMA in flight yet: a plain barrier is fine here)
   if (total > 0) issue(0, slot0);
   if (total > 1) issue(1, slot1);
+  if (DIST == 3 && total > 2) issue(2, slot2);
   // slice it computes from slot it % 3 and DMAs slice it + 2 into slot (it + 2) % 3, which held
   // slice it - 1 (finished by every wave before this slice's barrier)
   f32x16 s[HW], dp[HW];  // S / dP' of the slice between phase A and phase B (registers)
@@ -366,11 +370,12 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
   };
   // one barrier per slice: slice it is in LDS for every wave, the DMA of slice it + 2 goes out
   auto sync_slice = [&](const int it, char* dma_slot) __attribute__((always_inline)) {
-    if (it + 1 < total) __builtin_amdgcn_s_waitcnt(VM_ONE);  // slice it landed, it+1 may fly on
+    if (DIST == 3 && it + 2 < total) __builtin_amdgcn_s_waitcnt(VM_TWO);  // slices it+1, it+2 may fly on
+    else if (it + 1 < total) __builtin_amdgcn_s_waitcnt(VM_ONE);       // slice it landed, it+1 may fly on
     else __builtin_amdgcn_s_waitcnt(VM_ZERO);
     __builtin_amdgcn_s_waitcnt(LGKM_ZERO);
     __builtin_amdgcn_s_barrier();  // every wave's pieces of slice it are in
-    if (it + 2 < total) issue(it + 2, dma_slot);
+    if (it + DIST < total) issue(it + DIST, dma_slot);
   };
   if constexpr (!PP) {
     // slice it computes from slot it % 3 and DMAs slice it + 2 into slot (it + 2) % 3, which held
@@ -392,7 +397,42 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
     // the packed P / dS operands (16 VGPRs) across the barrier: A2 ... [B2(it-1) A(it) B1(it)] ...
     // the halves run separate straight-line loops (one branch outside the loop, not one per slice:
     // the register allocator then sees two independent paths) with the same barrier count
-    if (wave < 4) {  // waves w and w + 4 share a SIMD
+    if constexpr (DIST == 3) {
+      // 5-slot ring, DMA three slices ahead: slice it + 3 reuses the slot of slice it - 2
+      if (wave < 4) {
+        auto body = [&](const int it, const char* Qs, char* dma_slot) __attribute__((always_inline)) {
+          sync_slice(it, dma_slot);
+          phaseA(Qs);
+          phaseB1(it);
+          phaseB2(Qs);
+        };
+        for (int it = 0; it < total; it += 5) {
+          body(it, slot0, slot3);
+          if (it + 1 < total) body(it + 1, slot1, slot4);
+          if (it + 2 < total) body(it + 2, slot2, slot0);
+          if (it + 3 < total) body(it + 3, slot3, slot1);
+          if (it + 4 < total) body(it + 4, slot4, slot2);
+        }
+      } else {
+        auto body = [&](const int it, const char* Qs, const char* Qprev, char* dma_slot) __attribute__((always_inline)) {
+          sync_slice(it, dma_slot);
+          if (it > 0) phaseB2(Qprev);
+          phaseA(Qs);
+          phaseB1(it);
+        };
+        for (int it = 0; it < total; it += 5) {
+          body(it, slot0, slot4, slot3);
+          if (it + 1 < total) body(it + 1, slot1, slot0, slot4);
+          if (it + 2 < total) body(it + 2, slot2, slot1, slot0);
+          if (it + 3 < total) body(it + 3, slot3, slot2, slot1);
+          if (it + 4 < total) body(it + 4, slot4, slot3, slot2);
+        }
+        if (total > 0) {
+          const int r = (total - 1) % 5;
+          phaseB2(r == 0 ? slot0 : r == 1 ? slot1 : r == 2 ? slot2 : r == 3 ? slot3 : slot4);
+        }
+      }
+    } else if (wave < 4) {  // waves w and w + 4 share a SIMD
       auto body = [&](const int it, const char* Qs, char* dma_slot) __attribute__((always_inline)) {
         sync_slice(it, dma_slot);
         phaseA(Qs);
@@ -659,7 +699,15 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
       const char* e = getenv("FTC_FLASH_DKDV_PP");
       return !(e && e[0] == '0');
     }();
-    if (dkdv_waves == 8 && pp)
+    // Q/dO slices DMA'd three slices ahead (5-slot ring; default, FTC_FLASH_DKDV_DIST=2 for two):
+    // bwd 1.99 -> 1.96 ms at the Llama-3-8B layer shape (profiles/r1_attn_dkdv_pp.log)
+    static const bool dist3 = [] {
+      const char* e = getenv("FTC_FLASH_DKDV_DIST");
+      return !(e && e[0] == '2');
+    }();
+    if (dkdv_waves == 8 && pp && dist3)
+      hipLaunchKernelGGL((bwd_dkdv_kernel<128, 1, true, 3>), dim3(g_kv), dim3(512), 0, stream, a);
+    else if (dkdv_waves == 8 && pp)
       hipLaunchKernelGGL((bwd_dkdv_kernel<128, 1, true>), dim3(g_kv), dim3(512), 0, stream, a);
     else if (dkdv_waves == 8)
       hipLaunchKernelGGL((bwd_dkdv_kernel<128, 1>), dim3(g_kv), dim3(512), 0, stream, a);
