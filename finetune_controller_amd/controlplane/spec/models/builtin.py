@@ -95,6 +95,8 @@ class LMTrainingArguments(TrainingArguments):
     log_interval: int = Field(default=10, ge=1, description="Steps between metrics.csv rows / Epoch log lines")
     save_every: int = Field(default=0, ge=0, description="Resume checkpoint every N steps (0 = only at the end)")
     checkpoint_layers: bool = Field(default=False, description="Activation checkpointing per decoder layer")
+    zero_stage: int = Field(default=0, ge=0, le=1,
+                            description="1: ZeRO-1 -- AdamW state sharded over the data-parallel ranks")
 
 
 class LoRAArguments(LMTrainingArguments):
@@ -216,4 +218,83 @@ class Mistral7B_QLoRA(_WorkerSpec):
     training_arguments: LoRAArguments = LoRAArguments()
 
 
-BUILTIN_MODELS = [MNIST, GPT2SmallFT, Llama3_8B_LoRA, Llama3_8B_Full, Mistral7B_QLoRA]
+class Llama31_8B_LoRA(Llama3_8B_LoRA):
+    """Llama-3.1-8B LoRA (Llama-3.1 RoPE frequency scaling; 128k positions)."""
+
+    name: str = "Llama3.1-8B-LoRA"
+    inference_name: str | None = "Llama3.1-8B"
+    description: str = "Llama-3.1-8B LoRA fine-tune on one MI355X (long-context capable: 32k tokens without checkpointing)"
+    project_url: str = "https://huggingface.co/meta-llama/Llama-3.1-8B"
+    promotion_path: str = Field(default="language/llama3.1-8b/lora", description="s3 promotion prefix")
+    model_preset: ClassVar[str] = "llama3.1-8b"
+
+
+class Llama32_3B_LoRA(Llama3_8B_LoRA):
+    """Llama-3.2-3B LoRA (tied embeddings, GQA 3:1)."""
+
+    name: str = "Llama3.2-3B-LoRA"
+    inference_name: str | None = "Llama3.2-3B"
+    description: str = "Llama-3.2-3B LoRA fine-tune on one MI355X"
+    project_url: str = "https://huggingface.co/meta-llama/Llama-3.2-3B"
+    resources: TrainingResources = TrainingResources(requests={"cpu": 8, "memory": "64Gi"},
+                                                     limits={"cpu": 16, "memory": "128Gi"})
+    promotion_path: str = Field(default="language/llama3.2-3b/lora", description="s3 promotion prefix")
+    model_preset: ClassVar[str] = "llama3.2-3b"
+
+
+class Llama32_1B_LoRA(Llama32_3B_LoRA):
+    """Llama-3.2-1B LoRA (tied embeddings, head_dim 64)."""
+
+    name: str = "Llama3.2-1B-LoRA"
+    inference_name: str | None = "Llama3.2-1B"
+    description: str = "Llama-3.2-1B LoRA fine-tune on one MI355X"
+    project_url: str = "https://huggingface.co/meta-llama/Llama-3.2-1B"
+    promotion_path: str = Field(default="language/llama3.2-1b/lora", description="s3 promotion prefix")
+    model_preset: ClassVar[str] = "llama3.2-1b"
+
+
+class Llama3_70B_QLoRA(_WorkerSpec):
+    """Llama-3-70B QLoRA on ONE MI355X (NF4 base in 288 GB of HBM)."""
+
+    name: str = "Llama3-70B-QLoRA"
+    inference_name: str | None = "Llama3-70B"
+    description: str = "Llama-3-70B QLoRA on a single MI355X (NF4 base weights, bf16 adapters, ~4k tokens/s)"
+    project_url: str = "https://huggingface.co/meta-llama/Meta-Llama-3-70B"
+    resources: TrainingResources = TrainingResources(requests={"cpu": 16, "memory": "256Gi"},
+                                                     limits={"cpu": 32, "memory": "512Gi"})
+    accelerator_count: int = Field(default=1, ge=1, description="MI355X GPUs per worker")
+    promotion_path: str = Field(default="language/llama3-70b/qlora", description="s3 promotion prefix")
+    model_preset: ClassVar[str] = "llama3-70b"
+    method: ClassVar[str] = "qlora"
+    training_arguments: LoRAArguments = LoRAArguments(batch_size=2)
+
+
+class Llama3_70B_LoRA(_WorkerSpec):
+    """Llama-3-70B bf16 LoRA, data parallel over 8 x MI355X (all 141 GB of weights resident per GPU)."""
+
+    name: str = "Llama3-70B-LoRA"
+    inference_name: str | None = "Llama3-70B"
+    description: str = "Llama-3-70B bf16 LoRA, 8 x MI355X data parallel (no weight sharding needed at 288 GB/GPU)"
+    project_url: str = "https://huggingface.co/meta-llama/Meta-Llama-3-70B"
+    resources: TrainingResources = TrainingResources(requests={"cpu": 64, "memory": "1024Gi"},
+                                                     limits={"cpu": 128, "memory": "1536Gi"})
+    accelerator_count: int = Field(default=8, ge=1, description="MI355X GPUs per worker")
+    promotion_path: str = Field(default="language/llama3-70b/lora", description="s3 promotion prefix")
+    model_preset: ClassVar[str] = "llama3-70b"
+    method: ClassVar[str] = "lora"
+    training_arguments: LoRAArguments = LoRAArguments(batch_size=1)
+
+
+class Mistral7B_v03_LoRA(Llama3_8B_LoRA):
+    """Mistral-7B-v0.3 LoRA (full attention, 32768 vocab)."""
+
+    name: str = "Mistral-7B-v0.3-LoRA"
+    inference_name: str | None = "Mistral-7B-v0.3"
+    description: str = "Mistral-7B-v0.3 LoRA fine-tune on one MI355X"
+    project_url: str = "https://huggingface.co/mistralai/Mistral-7B-v0.3"
+    promotion_path: str = Field(default="language/mistral-7b-v0.3/lora", description="s3 promotion prefix")
+    model_preset: ClassVar[str] = "mistral-7b-v0.3"
+
+
+BUILTIN_MODELS = [MNIST, GPT2SmallFT, Llama3_8B_LoRA, Llama3_8B_Full, Mistral7B_QLoRA, Llama31_8B_LoRA,
+                  Llama32_3B_LoRA, Llama32_1B_LoRA, Llama3_70B_QLoRA, Llama3_70B_LoRA, Mistral7B_v03_LoRA]

@@ -256,3 +256,26 @@ def test_deploy_manifests_are_valid_yaml_with_amd_gpu_quota():
     assert gpu and gpu[0]["nominalQuota"] == 8
     assert ("LocalQueue", "finetune-queue") in docs and ("Role", "ftc-controlplane") in docs
     assert not any(d["kind"] == "ClusterRoleBinding" for d in docs.values())  # no cluster-admin
+
+
+@pytest.mark.parametrize("name,preset,method,gpus", [("Llama3.1-8B-LoRA", "llama3.1-8b", "lora", 1),
+                                                     ("Llama3.2-1B-LoRA", "llama3.2-1b", "lora", 1),
+                                                     ("Llama3.2-3B-LoRA", "llama3.2-3b", "lora", 1),
+                                                     ("Llama3-70B-QLoRA", "llama3-70b", "qlora", 1),
+                                                     ("Llama3-70B-LoRA", "llama3-70b", "lora", 8),
+                                                     ("Mistral-7B-v0.3-LoRA", "mistral-7b-v0.3", "lora", 1)])
+def test_family_specs_render_worker_commands(name, preset, method, gpus):
+    """Every built-in worker spec renders a trainer command the worker CLI parses (preset, method,
+    launcher for its GPU count, ZeRO flag)."""
+    from finetune_controller_amd.train import cli
+
+    cls = ModelRegistry().get(name)
+    spec = cls()
+    cmd = spec.run_cmd()[-1]
+    assert f"--model={preset}" in cmd and f"--method={method}" in cmd and "--zero-stage=0" in cmd
+    if gpus > 1:
+        assert cmd.startswith(f"torchrun --standalone --nproc-per-node={gpus} ")
+    argv = cmd.split(" -m finetune_controller_amd.train.cli ", 1)[-1].split() if gpus > 1 else \
+        cmd.split("python -m finetune_controller_amd.train.cli ", 1)[-1].split()
+    a = cli.build_parser().parse_args(argv)
+    assert a.model == preset and a.method == method and a.zero_stage == 0
