@@ -97,6 +97,9 @@ class LMTrainingArguments(TrainingArguments):
     checkpoint_layers: bool = Field(default=False, description="Activation checkpointing per decoder layer")
     zero_stage: int = Field(default=0, ge=0, le=1,
                             description="1: ZeRO-1 -- AdamW state sharded over the data-parallel ranks")
+    eval_every: int = Field(default=0, ge=0, description="Held-out loss every N steps (0 = off)")
+    eval_batches: int = Field(default=4, ge=1, description="Micro-batches per GPU per evaluation")
+    eval_holdout: float = Field(default=0.01, gt=0, description="Held-out share of the dataset (>= 1: windows)")
 
 
 class LoRAArguments(LMTrainingArguments):

@@ -36,7 +36,7 @@ def _ce_chunk_ref(logits: torch.Tensor, labels: torch.Tensor, gscale: float, ign
 
 class _FusedLinearCE(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h, W, labels, chunk_rows, ignore_index, n_valid_override):
+    def forward(ctx, h, W, labels, chunk_rows, ignore_index, n_valid_override, grad_enabled=True):
         d = h.shape[-1]
         h2 = h.reshape(-1, d)
         lab = labels.reshape(-1)
@@ -44,8 +44,10 @@ class _FusedLinearCE(torch.autograd.Function):
         n_valid = int(n_valid_override) if n_valid_override else int((lab != ignore_index).sum().item())
         gscale = 1.0 / max(n_valid, 1)
         hip = use_hip(h2) and h2.dtype == torch.bfloat16
-        need_dh = ctx.needs_input_grad[0]
-        need_dw = ctx.needs_input_grad[1]
+        # gradients are produced in this pass: only when the caller runs with autograd on (an eval
+        # forward under no_grad must neither compute dh nor touch W.main_grad)
+        need_dh = ctx.needs_input_grad[0] and grad_enabled
+        need_dw = ctx.needs_input_grad[1] and grad_enabled
         dh = torch.empty_like(h2) if need_dh else None
         mg = getattr(W, "main_grad", None) if need_dw else None
         dW = None
@@ -97,13 +99,13 @@ class _FusedLinearCE(torch.autograd.Function):
         if dh is not None:
             gh = dh.mul_(g.to(dh.dtype)).view(ctx.shp)  # in place: dh is ours and used once
         gw = (dW * g).to(ctx.wdtype) if dW is not None else None
-        return gh, gw, None, None, None, None
+        return gh, gw, None, None, None, None, None
 
 
 def fused_linear_cross_entropy(h: torch.Tensor, W: torch.Tensor, labels: torch.Tensor, chunk_rows: int = 4096,
                                ignore_index: int = -100, n_valid: int | None = None) -> torch.Tensor:
     """Mean CE over non-ignored labels. ``n_valid`` (optional) avoids a host sync per step."""
-    return _FusedLinearCE.apply(h, W, labels, chunk_rows, ignore_index, n_valid or 0)
+    return _FusedLinearCE.apply(h, W, labels, chunk_rows, ignore_index, n_valid or 0, torch.is_grad_enabled())
 
 
 def cross_entropy_reference(h, W, labels, ignore_index=-100):

@@ -149,7 +149,7 @@ class PackedTokenDataset:
     """
 
     def __init__(self, path: str, vocab: int, batch: int, seq_len: int, device, rank: int = 0, world: int = 1,
-                 seed: int = 0):
+                 seed: int = 0, holdout: float = 0):
         self.tokens = load_token_array(path, vocab)
         self.vocab, self.batch, self.seq_len, self.device = vocab, batch, seq_len, device
         self.rank, self.world, self.seed = rank, world, seed
@@ -157,7 +157,14 @@ class PackedTokenDataset:
         if n_windows < 1:
             raise ValueError(f"dataset has {len(self.tokens)} tokens; need > seq_len={seq_len}")
         self.n_windows = n_windows
-        self.steps_per_epoch = max(1, n_windows // (batch * world))
+        # the last windows are an evaluation split (EvalWindows), never trained on: `holdout` is a share
+        # of the windows (< 1) or a count, at least one micro-batch per rank
+        want = 0
+        if holdout > 0:
+            want = max(int(holdout) if holdout >= 1 else int(round(n_windows * holdout)), batch * world)
+        self.holdout = max(0, min(want, n_windows - 1))
+        self.n_use = n_windows - self.holdout
+        self.steps_per_epoch = max(1, self.n_use // (batch * world))
         self.epoch = 0
         self.pos = 0
         self._native = None
@@ -166,14 +173,14 @@ class PackedTokenDataset:
 
             if isinstance(self.tokens, np.memmap) and os.environ.get("FTC_NATIVE_LOADER", "1") != "0":
                 self._native = NativeTokenLoader(self.tokens.filename, self.tokens.dtype.itemsize, seq_len, batch,
-                                                 rank, world, seed)
+                                                 rank, world, seed, n_use=self.n_use)
         except ImportError:  # _rt.so not built: numpy path
             self._native = None
         self._perm()
 
     def _perm(self):
         rng = np.random.default_rng(self.seed + self.epoch)
-        self.order = rng.permutation(self.n_windows)
+        self.order = rng.permutation(self.n_use)
 
     def __iter__(self):
         return self
@@ -189,7 +196,7 @@ class PackedTokenDataset:
                 self.pos, self.epoch = 0, self.epoch + 1
                 self._perm()
             base = (self.pos * self.world + self.rank) * self.batch
-            idx = [self.order[(base + i) % self.n_windows] for i in range(self.batch)]
+            idx = [self.order[(base + i) % self.n_use] for i in range(self.batch)]
             S = self.seq_len
             arr = np.stack([np.asarray(self.tokens[j * S: j * S + S + 1], dtype=np.int64) for j in idx])
             arr = torch.from_numpy(arr)
@@ -212,3 +219,24 @@ class PackedTokenDataset:
         self._perm()
         if self._native is not None:
             self._native.seek(self.epoch, self.pos)
+
+
+class EvalWindows:
+    """The held-out tail windows of a PackedTokenDataset as fixed evaluation batches: batch i of rank r
+    takes windows ``n_use + ((i * world + r) * batch + j) % holdout`` -- the same every evaluation, so
+    successive eval losses are comparable."""
+
+    def __init__(self, ds: "PackedTokenDataset", n_batches: int):
+        self.ds, self.n_batches = ds, max(1, int(n_batches))
+
+    def batches(self):
+        ds = self.ds
+        if ds.holdout <= 0:
+            return
+        S = ds.seq_len
+        for i in range(self.n_batches):
+            base = (i * ds.world + ds.rank) * ds.batch
+            idx = [ds.n_use + (base + j) % ds.holdout for j in range(ds.batch)]
+            arr = np.stack([np.asarray(ds.tokens[w * S: w * S + S + 1], dtype=np.int64) for w in idx])
+            t = torch.from_numpy(arr).to(ds.device, non_blocking=True)
+            yield t[:, :-1], t[:, 1:]

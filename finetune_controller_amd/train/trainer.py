@@ -31,7 +31,7 @@ from ..models import checkpoint as ckpt
 from ..parallel import dist as pdist
 from ..parallel.ddp import GradBucketer
 from ..utils.metrics import MetricsCSV
-from .data import PackedTokenDataset, SyntheticTokens
+from .data import EvalWindows, PackedTokenDataset, SyntheticTokens
 from .optim import FlatAdamW, ShardedFlatAdamW, lr_at
 
 log = logging.getLogger("ftc.train")
@@ -74,6 +74,9 @@ class TrainConfig:
     save_model: bool = True
     timers: bool = False  # per-phase device timers (fwd/bwd/comm/optim) -> metrics.csv
     profile_steps: int = 0  # >0: torch.profiler chrome trace of that many steps -> trace_rank<r>.json
+    eval_every: int = 0  # >0: held-out loss every that many optimizer steps (and after the last one)
+    eval_batches: int = 4  # micro-batches per rank per evaluation
+    eval_holdout: float = 0.01  # held-out share of the dataset's windows (>= 1: a window count)
 
     def lora_config(self) -> LoRAConfig | None:
         if self.method not in ("lora", "qlora"):
@@ -131,6 +134,7 @@ class Trainer:
         tied = [self.model.lm_head] if self.cfg.tie_embeddings and tc.method == "full" else []
         self.ddp = GradBucketer(self.opt, tc.bucket_mb, engine=tc.comm_engine, multi_use_params=tied)
         self._data = None
+        self._eval_synth = None
         self.step = 0
         self.is_main = self.info.is_main
         self._timing: list[tuple] = []  # per-step (start, fwd, bwd, comm, optim) device events
@@ -161,7 +165,8 @@ class Trainer:
                 self.steps_per_epoch = 100
             else:
                 self._data = PackedTokenDataset(tc.dataset_path, self.cfg.vocab_size, tc.batch_size, tc.seq_len,
-                                                self.device, self.info.rank, self.info.world_size, tc.seed)
+                                                self.device, self.info.rank, self.info.world_size, tc.seed,
+                                                holdout=tc.eval_holdout if tc.eval_every > 0 else 0)
                 self.steps_per_epoch = max(1, self._data.steps_per_epoch // tc.grad_accum)
         return self._data
 
@@ -199,6 +204,38 @@ class Trainer:
             ev[4].record()
             self._timing.append(tuple(ev))
         return total / tc.grad_accum
+
+    # ------------------------------------------------------------------ evaluation
+    def eval_batches(self):
+        """Fixed held-out batches of this rank: the dataset's tail windows, or (synthetic data) a
+        separate pool drawn from another seed."""
+        data = self.data()
+        if isinstance(data, PackedTokenDataset):
+            return EvalWindows(data, self.tc.eval_batches).batches()
+        if self._eval_synth is None:
+            self._eval_synth = SyntheticTokens(self.cfg.vocab_size, self.tc.batch_size, self.tc.seq_len, self.device,
+                                               seed=self.tc.seed + 7919 + self.info.rank)
+        self._eval_synth.i = 0  # the same batches every evaluation
+        return (next(self._eval_synth) for _ in range(self.tc.eval_batches))
+
+    def evaluate(self) -> float | None:
+        """Mean next-token loss over the held-out batches of every rank (forward only, no gradients:
+        the fused CE computes none under ``no_grad``).  None when there is nothing held out."""
+        tc = self.tc
+        was = self.model.training
+        self.model.eval()
+        tot = torch.zeros(2, dtype=torch.float64, device=self.device)
+        try:
+            with torch.no_grad():
+                for x, y in self.eval_batches():
+                    tot[0] += self.model(x, y, n_valid=x.numel()).double()
+                    tot[1] += 1
+        finally:
+            self.model.train(was)
+        pdist.all_reduce_mean_(tot, self.info)
+        if float(tot[1]) == 0:
+            return None
+        return float(tot[0] / tot[1])
 
     def _phase_ms(self) -> dict:
         """Mean fwd/bwd/comm/optim milliseconds of the steps since the last call (after a sync)."""
@@ -278,6 +315,15 @@ class Trainer:
                           f"mem {mem:.1f} GB", flush=True)
                 losses = []
                 t0 = time.perf_counter()
+            if tc.eval_every and (self.step % tc.eval_every == 0 or self.step == total):
+                ev_loss = self.evaluate()
+                if ev_loss is not None:
+                    last["eval_loss"] = round(ev_loss, 6)
+                    if self.is_main:
+                        metrics.write({"epoch": step // max(1, self.steps_per_epoch), "step": self.step,
+                                       "eval_loss": last["eval_loss"], "world_size": self.info.world_size})
+                        print(f"Epoch {step // max(1, self.steps_per_epoch)} | step {self.step}/{total} | "
+                              f"eval_loss {ev_loss:.4f}", flush=True)
             if tc.save_every and self.step % tc.save_every == 0 and self.step < total:
                 self.save_resume()
         metrics.close()

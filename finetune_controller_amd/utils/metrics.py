@@ -13,7 +13,7 @@ import csv
 import os
 
 COLUMNS = ["epoch", "step", "loss", "lr", "tokens_per_sec", "step_time_ms", "grad_norm", "world_size", "mem_gb",
-           "tflops_per_gpu", "fwd_ms", "bwd_ms", "comm_ms", "optim_ms"]
+           "tflops_per_gpu", "fwd_ms", "bwd_ms", "comm_ms", "optim_ms", "eval_loss"]
 
 
 class MetricsCSV:

@@ -22,13 +22,15 @@ def load_rt():
 
 class NativeTokenLoader:
     def __init__(self, filename: str, itemsize: int, seq_len: int, batch: int, rank: int = 0, world: int = 1,
-                 seed: int = 0, depth: int = 4, threads: int = 2, pin: bool | None = None):
+                 seed: int = 0, depth: int = 4, threads: int = 2, pin: bool | None = None, n_use: int | None = None):
         rt = load_rt()
         self.L = rt.TokenLoader(str(filename), int(itemsize), int(seq_len), int(batch), int(rank), int(world),
                                 int(threads))
         self.seq_len, self.batch, self.world, self.seed = seq_len, batch, world, seed
         self.n_windows = int(self.L.n_windows)
-        self.steps_per_epoch = max(1, self.n_windows // (batch * world))
+        # train on the first n_use windows only (the tail is a held-out evaluation split)
+        self.n_use = min(self.n_windows, int(n_use)) if n_use else self.n_windows
+        self.steps_per_epoch = max(1, self.n_use // (batch * world))
         if pin is None:
             pin = torch.cuda.is_available()
         self.bufs = [torch.empty(batch, seq_len + 1, dtype=torch.int64, pin_memory=pin) for _ in range(depth)]
@@ -39,7 +41,11 @@ class NativeTokenLoader:
         self._start()
 
     def _order(self, epoch: int) -> np.ndarray:
-        return np.random.default_rng(self.seed + epoch).permutation(self.n_windows).astype(np.int64)
+        perm = np.random.default_rng(self.seed + epoch).permutation(self.n_use).astype(np.int64)
+        if self.n_use == self.n_windows:
+            return perm
+        # batches only index the first n_use entries; the rest pads the array to the loader's length
+        return np.concatenate([perm, np.arange(self.n_use, self.n_windows, dtype=np.int64)])
 
     def _start(self):
         self.L.start(self._order(self.epoch), self.pos, self.steps_per_epoch)

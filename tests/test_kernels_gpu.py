@@ -668,3 +668,29 @@ def test_qlora_fused_mlp_matches_torch_path(C, monkeypatch):
     for o, n in offs:
         a, b = gh[o:o + n], gt[o:o + n]
         assert (a - b).abs().max().item() <= 5e-2 * b.abs().max().item() + 1e-3, (o, n)
+
+
+@pytest.mark.parametrize("method", ["lora", "full"])
+def test_trainer_evaluate_hip_no_grad(C, tmp_path, method):
+    """Trainer.evaluate on the HIP path: a forward under no_grad through the fused LoRA MLP / fused CE
+    leaves every gradient buffer untouched, returns the same loss twice, and matches a training-mode
+    forward of the same batch (the eval forward computes the same function)."""
+    from finetune_controller_amd.train.trainer import Trainer, TrainConfig
+
+    tr = Trainer(TrainConfig(model="llama-smoke", method=method, batch_size=2, seq_len=256, synthetic=True,
+                             max_steps=1, eval_batches=2, checkpoint_path=str(tmp_path), resume=False,
+                             device="cuda", save_model=False, warmup_steps=0))
+    tr.train_step(1e-4)
+    torch.cuda.synchronize()
+    g0 = tr.opt.grad_flat.detach().clone()
+    a, b = tr.evaluate(), tr.evaluate()
+    torch.cuda.synchronize()
+    assert torch.equal(tr.opt.grad_flat, g0)
+    assert a == b and math.isfinite(a)
+    batches = list(tr.eval_batches())
+    ref = 0.0
+    for x, y in batches:
+        with torch.no_grad():
+            ref += float(tr.model(x, y))  # training mode, no grad: same function as eval
+    assert abs(a - ref / len(batches)) < 1e-3 * abs(a)
+    tr.close()

@@ -15,7 +15,8 @@ from finetune_controller_amd.models import LoRAConfig, build_model, get_config
 from finetune_controller_amd.models import checkpoint as ckpt
 from finetune_controller_amd.models.lora import merge_pair_into
 from finetune_controller_amd.ops import nf4
-from finetune_controller_amd.train.data import PackedTokenDataset, load_token_array
+from finetune_controller_amd.train.data import EvalWindows, PackedTokenDataset, load_token_array
+from finetune_controller_amd.utils.metrics import read_metrics_csv
 from finetune_controller_amd.train.optim import FlatAdamW, lr_at
 from finetune_controller_amd.train.trainer import TrainConfig, Trainer
 
@@ -349,6 +350,68 @@ def test_native_token_loader_matches_numpy_path(tmp_path, monkeypatch, dtype, vo
         for _ in range(3):
             assert torch.equal(next(nat)[0], next(ref)[0])
         nat._native.close()
+
+
+@pytest.mark.parametrize("native", ["0", "1"])
+def test_holdout_windows_never_trained_on(tmp_path, monkeypatch, native):
+    """With a held-out split the training order (numpy and native loader) only visits the leading
+    windows and EvalWindows only the tail ones."""
+    if native == "1":
+        pytest.importorskip("finetune_controller_amd._rt")
+    monkeypatch.setenv("FTC_NATIVE_LOADER", native)
+    S = 16
+    np.arange(4000, dtype=np.uint16).tofile(tmp_path / "t.bin")  # window w starts with token w * S
+    for rank in (0, 1):
+        ds = PackedTokenDataset(str(tmp_path / "t.bin"), vocab=8192, batch=2, seq_len=S, device="cpu", rank=rank,
+                                world=2, seed=3, holdout=0.1)
+        assert ds.holdout == round(ds.n_windows * 0.1) and ds.n_use + ds.holdout == ds.n_windows
+        seen = set()
+        for _ in range(3 * ds.steps_per_epoch):
+            x, _ = next(ds)
+            seen |= {int(v) // S for v in x[:, 0]}
+        assert max(seen) < ds.n_use
+        ev = [int(v) // S for x, _ in EvalWindows(ds, 3).batches() for v in x[:, 0]]
+        assert len(ev) == 6 and all(ds.n_use <= w < ds.n_windows for w in ev)
+        if ds._native is not None:
+            ds._native.close()
+
+
+def test_trainer_eval_loss_no_grad_side_effects(tmp_path):
+    """Trainer.evaluate: mean held-out loss equal to a direct forward over the tail windows, no
+    gradient written (full fine-tuning: the fused CE would otherwise fill lm_head's main_grad), rows in
+    metrics.csv."""
+    vocab = 512
+    (np.arange(6000, dtype=np.int64) * 7919 % vocab).astype(np.uint16).tofile(tmp_path / "t.bin")
+    tc = TrainConfig(model="llama-tiny", method="full", batch_size=2, seq_len=32, dataset_path=str(tmp_path / "t.bin"),
+                     max_steps=4, log_interval=2, eval_every=2, eval_batches=2, eval_holdout=0.05,
+                     checkpoint_path=str(tmp_path / "out"), resume=False, device="cpu", lr=1e-3, warmup_steps=0,
+                     save_model=False)
+    tr = Trainer(tc)
+    tr.train_step(1e-3)
+    g0 = tr.opt.grad_flat.detach().clone()
+    ev = tr.evaluate()
+    assert torch.equal(tr.opt.grad_flat, g0) and tr.model.training
+    ds = tr.data()
+    ref = []
+    with torch.no_grad():
+        for x, y in EvalWindows(ds, 2).batches():
+            ref.append(float(tr.model(x, y)))
+    assert ev == pytest.approx(sum(ref) / len(ref), rel=1e-5)
+    last = tr.run()
+    tr.close()
+    rows = read_metrics_csv(str(tmp_path / "out" / "metrics.csv"))
+    evals = [r for r in rows if r["eval_loss"]]
+    assert [r["step"] for r in evals] == [2, 4] and all(0 < r["eval_loss"] < 20 for r in evals)
+    assert last["eval_loss"] == evals[-1]["eval_loss"]
+
+
+def test_trainer_eval_synthetic(tmp_path):
+    tr = Trainer(TrainConfig(model="llama-tiny", method="lora", batch_size=2, seq_len=16, synthetic=True,
+                             max_steps=1, eval_batches=3, checkpoint_path=str(tmp_path), resume=False, device="cpu",
+                             save_model=False))
+    a, b = tr.evaluate(), tr.evaluate()
+    tr.close()
+    assert a == b and a == pytest.approx(np.log(512), rel=0.1)
 
 
 def _ddp_worker(rank, world, port, tmp, q):
