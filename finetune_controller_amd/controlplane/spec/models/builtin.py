@@ -77,6 +77,26 @@ class MNIST(BaseFineTuneModel):
         return self.append_args(args)
 
 
+class MNIST_MI355X(MNIST):
+    """The reference's MNIST example on this repository's worker image: the same form and command line,
+    run by ``finetune_controller_amd.train.mnist`` (one process per GPU under torchrun; CPU when
+    ``accelerator_count`` is 0)."""
+
+    name: str = "MNIST-MI355X"
+    description: str = "Example MNIST classifier on the MI355X worker image"
+    image: str = WORKER_IMAGE
+    command: list[str] = ["/bin/bash", "-c", "python -m finetune_controller_amd.train.mnist"]
+    store_asset_patterns: list[str] = Field(default=["*.json", "*.yaml", "*.csv", "*.pt", "*.ckpt"],
+                                            description="Pattern match a list of files to store.")
+
+    def run_cmd(self) -> list[str]:
+        cmd = super().run_cmd()
+        n = max(1, int(self.accelerator_count or 0))
+        if n > 1:
+            cmd[-1] = cmd[-1].replace("python -m", f"torchrun --standalone --nproc-per-node={n} -m", 1)
+        return cmd
+
+
 # ------------------------------------------------------------------ MI355X worker-runtime specs
 class LMTrainingArguments(TrainingArguments):
     """Flags of ``finetune_controller_amd.train.cli`` exposed to the UI form."""
@@ -299,5 +319,5 @@ class Mistral7B_v03_LoRA(Llama3_8B_LoRA):
     model_preset: ClassVar[str] = "mistral-7b-v0.3"
 
 
-BUILTIN_MODELS = [MNIST, GPT2SmallFT, Llama3_8B_LoRA, Llama3_8B_Full, Mistral7B_QLoRA, Llama31_8B_LoRA,
+BUILTIN_MODELS = [MNIST, MNIST_MI355X, GPT2SmallFT, Llama3_8B_LoRA, Llama3_8B_Full, Mistral7B_QLoRA, Llama31_8B_LoRA,
                   Llama32_3B_LoRA, Llama32_1B_LoRA, Llama3_70B_QLoRA, Llama3_70B_LoRA, Mistral7B_v03_LoRA]

@@ -694,3 +694,13 @@ def test_trainer_evaluate_hip_no_grad(C, tmp_path, method):
             ref += float(tr.model(x, y))  # training mode, no grad: same function as eval
     assert abs(a - ref / len(batches)) < 1e-3 * abs(a)
     tr.close()
+
+
+def test_mnist_example_on_gpu(tmp_path):
+    """The reference's example job runs on the MI355X worker (MIOpen convolutions, one process)."""
+    from finetune_controller_amd.train import mnist
+
+    last = mnist.run(mnist.build_parser().parse_args(
+        ["--epochs", "1", "--train-size", "4000", "--test-size", "1000", "--log-interval", "50",
+         "--dataset_path", str(tmp_path / "none"), "--checkpoint_path", str(tmp_path / "out")]))
+    assert last["accuracy"] > 90.0
