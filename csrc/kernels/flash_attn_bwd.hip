@@ -126,19 +126,36 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(BwdArgs a) {
 // One slice's LDS-DMA for a dK/dV wave: NG 1 KiB pieces of Q and of dO (lane-linear destinations,
 // pre-swizzled per-lane source offsets qvo/dvo) and the 256-byte row-constant piece.  A device-only
 // function rather than a lambda in the kernel: the host pass cannot instantiate these builtins.
-template <int D, int NG, int RPG, int QBYTES>
+// SPLIT (a slice of fewer 1 KiB pieces per matrix than waves, D = 64 with 8 waves): each wave DMAs ONE
+// piece -- waves [0, P) a piece of Q, waves [P, 2P) the same piece of dO -- so every wave still issues
+// the same number of DMA instructions per slice (the counted vmcnt stays wave-uniform).
+// QR = 2 (64-row slices): the row constants are two 256-byte pieces (-lse/scale rows, then -delta rows).
+template <int D, int NG, int RPG, int QBYTES, bool SPLIT = false, int QR = 1>
 FTC_DEV void dkdv_dma(__amdgpu_buffer_rsrc_t qr, __amdgpu_buffer_rsrc_t dr, __amdgpu_buffer_rsrc_t cr, const int* qvo,
-                      const int* dvo, int cvo, int qso, int dso, int cso, char* base, int wave) {
+                      const int* dvo, int cvo, int cvo2, int qso, int dso, int cso, char* base, int wave) {
+  if constexpr (SPLIT) {
+    constexpr int P = QBYTES / 1024;
+    if (wave < P)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (__attribute__((address_space(3))) void*)(base + wave * 1024), 16,
+                                               qvo[0], qso, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          dr, (__attribute__((address_space(3))) void*)(base + QBYTES + (wave - P) * 1024), 16, dvo[0], dso, 0, 0);
+  } else {
 #pragma unroll
-  for (int i = 0; i < NG; ++i) {
-    const int r0 = (wave * NG + i) * RPG;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (__attribute__((address_space(3))) void*)(base + r0 * D * 2), 16,
-                                             qvo[i], qso, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(dr, (__attribute__((address_space(3))) void*)(base + QBYTES + r0 * D * 2),
-                                             16, dvo[i], dso, 0, 0);
+    for (int i = 0; i < NG; ++i) {
+      const int r0 = (wave * NG + i) * RPG;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (__attribute__((address_space(3))) void*)(base + r0 * D * 2), 16,
+                                               qvo[i], qso, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          dr, (__attribute__((address_space(3))) void*)(base + QBYTES + r0 * D * 2), 16, dvo[i], dso, 0, 0);
+    }
   }
   __builtin_amdgcn_raw_ptr_buffer_load_lds(cr, (__attribute__((address_space(3))) void*)(base + 2 * QBYTES), 4, cvo,
                                            cso, 0, 0);
+  if constexpr (QR == 2)  // second piece: -delta of the 64 rows (cvo addressed the -lse/scale rows)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(cr, (__attribute__((address_space(3))) void*)(base + 2 * QBYTES + 256), 4,
+                                             cvo2, cso, 0, 0);
 }
 
 // HW = 32-key halves per wave: HW = 2 -> 4 waves x 64 keys, one wave per SIMD (512-register budget);
@@ -150,11 +167,14 @@ FTC_DEV void dkdv_dma(__amdgpu_buffer_rsrc_t qr, __amdgpu_buffer_rsrc_t dr, __am
 // dV / dK MFMAs.  One wave's exp / mask / pack work then issues under its partner's MFMAs instead of
 // both waves idling the matrix pipe at the same time (guide: MI355X_MICROARCH.md "Two waves per
 // SIMD").  Slice j is read by half 1 one barrier interval later, so the Q/dO ring has 4 slots.
-template <int D, int HW, bool PP = false, int DIST = 2>
+// QR = 32-row query blocks per slice: QR = 2 (D = 64) doubles the MFMA work between two barriers,
+// which at D = 64 is otherwise half of D = 128's (the per-slice barrier / DMA cost stays the same).
+template <int D, int HW, bool PP = false, int DIST = 2, int QR = 1>
 __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
   static_assert(DIST == 2 || (PP && DIST == 3), "DMA distance 3 needs the ping-pong 5-slot ring");
+  static_assert(QR == 1 || QR == 2, "one or two 32-row query blocks per slice");
   constexpr int NCH = D / 8, DSTEPS = D / 16, DT = D / 32;
-  constexpr int BKV = 256, BQ2 = 32;
+  constexpr int BKV = 256, BQ2 = 32 * QR;
   constexpr int WAVES = 8 / HW, NT = 64 * WAVES;
   constexpr int KBYTES = BKV * D * 2, QBYTES = BQ2 * D * 2;
   constexpr int SLICE = 2 * QBYTES + 2 * BQ2 * 4;  // Q | dO | -lse/scale | -delta
@@ -227,10 +247,13 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
   // 3-slot ring, two slices ahead of the compute; one raw barrier per slice with a COUNTED vmcnt so the
   // next slice's DMA stays in flight across it (guide §5 "Pipelining across barriers").  The swizzled
   // LDS image is produced by pre-swizzling the per-lane global source (the DMA writes lane-linearly).
-  constexpr int NG = BQ2 * D * 2 / 1024 / WAVES;  // 1 KiB DMA pieces per wave per matrix
+  constexpr int PIECES = BQ2 * D * 2 / 1024;         // 1 KiB pieces per matrix per slice
+  constexpr bool SPLIT = PIECES < WAVES;             // D = 64, 8 waves: one piece of Q OR dO per wave
+  static_assert(!SPLIT || 2 * PIECES == WAVES, "split DMA: one piece per wave");
+  constexpr int NG = SPLIT ? 1 : PIECES / WAVES;     // 1 KiB DMA pieces per wave per matrix
   static_assert(NG >= 1, "each wave DMAs at least one 1 KiB piece of Q and of dO");
-  constexpr int PER_SLICE = 2 * NG + 1;       // DMA instructions per wave per slice (+1: row constants)
-  constexpr int RPG = 1024 / (D * 2);         // rows per 1 KiB piece
+  constexpr int PER_SLICE = (SPLIT ? 1 : 2 * NG) + QR;  // DMA instructions per wave per slice (+ row constants)
+  constexpr int RPG = 1024 / (D * 2);                // rows per 1 KiB piece
   // DMA sources as buffer resources (SGPRs) + per-lane loop-invariant 32-bit offsets: the slice's head
   // and row position go into the scalar offset, so no 64-bit address VGPRs stay live in the loop
   const auto qrsrc = make_rsrc(a.q + (long long)b * S * a.q_rs);
@@ -239,17 +262,19 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
   int qvo[NG], dvo[NG];
 #pragma unroll
   for (int i = 0; i < NG; ++i) {
-    const int row = (wave * NG + i) * RPG + lane / NCH, pc = lane % NCH;
+    const int row = ((SPLIT ? wave % PIECES : wave * NG) + i) * RPG + lane / NCH, pc = lane % NCH;
     const int lc = (pc ^ swz(row)) & (NCH - 1);  // pre-swizzled source, lane-linear destination
     qvo[i] = (row * (int)a.q_rs + lc * 8) * 2;
     dvo[i] = (row * (int)a.do_rs + lc * 8) * 2;
   }
-  // lanes 0..31: -lse/scale of the 32 rows, lanes 32..63: -delta (every wave issues the same piece)
-  const int cvo = (lr + (hh ? 0 : a.B * a.H * S)) * 4;
+  // QR = 1: lanes 0..31 -lse/scale of the 32 rows, lanes 32..63 -delta (every wave issues the same
+  // piece); QR = 2: one piece of the 64 rows' -lse/scale (cvo) and one of their -delta (cvo2)
+  const int cvo = QR == 1 ? (lr + (hh ? 0 : a.B * a.H * S)) * 4 : (lane + a.B * a.H * S) * 4;
+  const int cvo2 = lane * 4;
   auto issue = [&](int it_, char* base_) {
     const int g_ = it_ / nqt, qt_ = qbeg + (it_ % nqt) * BQ2;
     const int hq_ = kvh * G + g_;
-    dkdv_dma<D, NG, RPG, QBYTES>(qrsrc, drsrc, crsrc, qvo, dvo, cvo, (hq_ * D + qt_ * (int)a.q_rs) * 2,
+    dkdv_dma<D, NG, RPG, QBYTES, SPLIT, QR>(qrsrc, drsrc, crsrc, qvo, dvo, cvo, cvo2, (hq_ * D + qt_ * (int)a.q_rs) * 2,
                                  (hq_ * D + qt_ * (int)a.do_rs) * 2, ((b * a.H + hq_) * S + qt_) * 4, base_, wave);
   };
   constexpr int VM_ONE = 0x0F70 | (PER_SLICE & 15) | ((PER_SLICE >> 4) << 14);  // vmcnt(PER_SLICE)
@@ -270,41 +295,54 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
   if (DIST == 3 && total > 2) issue(2, slot2);
   // slice it computes from slot it % 3 and DMAs slice it + 2 into slot (it + 2) % 3, which held
   // slice it - 1 (finished by every wave before this slice's barrier)
-  f32x16 s[HW], dp[HW];  // S / dP' of the slice between phase A and phase B (registers)
+  f32x16 s[QR][HW], dp[QR][HW];  // S / dP' of the slice between phase A and phase B (registers)
   // phase A: S[q][k], dP'[q][k] for both 32-key halves in one k-loop (rows q in registers, key on the
-  // lane): the Q / dO A-fragments are read once for both halves, four independent MFMA chains
+  // lane): the Q / dO A-fragments are read once for both halves, the K fragments once for all row
+  // blocks -- 2 QR HW independent MFMA chains
   auto phaseA = [&](const char* Qs) __attribute__((always_inline)) {
     const char* Ds = Qs + QBYTES;
     const float* lse_s = reinterpret_cast<const float*>(Ds + QBYTES);
     const float* dlt_s = lse_s + BQ2;
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const float4 lv = *reinterpret_cast<const float4*>(lse_s + 8 * g4 + 4 * hh);
-      const float4 dv4 = *reinterpret_cast<const float4*>(dlt_s + 8 * g4 + 4 * hh);
+    for (int r = 0; r < QR; ++r)
 #pragma unroll
-      for (int j = 0; j < HW; ++j) {
-        s[j][4 * g4 + 0] = lv.x; s[j][4 * g4 + 1] = lv.y; s[j][4 * g4 + 2] = lv.z; s[j][4 * g4 + 3] = lv.w;
-        dp[j][4 * g4 + 0] = dv4.x; dp[j][4 * g4 + 1] = dv4.y; dp[j][4 * g4 + 2] = dv4.z; dp[j][4 * g4 + 3] = dv4.w;
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 lv = *reinterpret_cast<const float4*>(lse_s + 32 * r + 8 * g4 + 4 * hh);
+        const float4 dv4 = *reinterpret_cast<const float4*>(dlt_s + 32 * r + 8 * g4 + 4 * hh);
+#pragma unroll
+        for (int j = 0; j < HW; ++j) {
+          s[r][j][4 * g4 + 0] = lv.x; s[r][j][4 * g4 + 1] = lv.y; s[r][j][4 * g4 + 2] = lv.z; s[r][j][4 * g4 + 3] = lv.w;
+          dp[r][j][4 * g4 + 0] = dv4.x; dp[r][j][4 * g4 + 1] = dv4.y; dp[r][j][4 * g4 + 2] = dv4.z;
+          dp[r][j][4 * g4 + 3] = dv4.w;
+        }
       }
-    }
 #pragma unroll
     for (int st = 0; st < DSTEPS; ++st) {
-      const u32x4 qa = *reinterpret_cast<const u32x4*>(Qs + lds_off<D>(lr, 2 * st + hh));
-      const u32x4 da = *reinterpret_cast<const u32x4*>(Ds + lds_off<D>(lr, 2 * st + hh));
+      u32x4 qa[QR], da[QR];
+#pragma unroll
+      for (int r = 0; r < QR; ++r) {
+        qa[r] = *reinterpret_cast<const u32x4*>(Qs + lds_off<D>(32 * r + lr, 2 * st + hh));
+        da[r] = *reinterpret_cast<const u32x4*>(Ds + lds_off<D>(32 * r + lr, 2 * st + hh));
+      }
       u32x4 kk[HW];
 #pragma unroll
       for (int j = 0; j < HW; ++j)
         kk[j] = *reinterpret_cast<const u32x4*>(Ks + lds_off<D>(wave * 32 * HW + 32 * j + lr, 2 * st + hh));
 #pragma unroll
-      for (int j = 0; j < HW; ++j)
-        s[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, qa), __builtin_bit_cast(bf16x8, kk[j]), s[j], 0, 0, 0);
+      for (int r = 0; r < QR; ++r)
 #pragma unroll
-      for (int j = 0; j < HW; ++j)
-        dp[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, da), vf[j][st], dp[j], 0, 0, 0);
+        for (int j = 0; j < HW; ++j)
+          s[r][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, qa[r]), __builtin_bit_cast(bf16x8, kk[j]),
+                                                            s[r][j], 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < QR; ++r)
+#pragma unroll
+        for (int j = 0; j < HW; ++j)
+          dp[r][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, da[r]), vf[j][st], dp[r][j], 0, 0, 0);
     }
     // fragment reads of two k-steps in flight ahead of the MFMA chain, the rest interleaved
     {
-      constexpr int NDS = (2 + HW) * DSTEPS, NMF = 2 * HW * DSTEPS, PRE = (HW == 1 ? 1 : 2) * (2 + HW);
+      constexpr int NDS = (2 * QR + HW) * DSTEPS, NMF = 2 * HW * QR * DSTEPS, PRE = (HW == 1 ? 1 : 2) * (2 * QR + HW);
       constexpr int REM = NDS - PRE, Q = REM / NMF, X = REM % NMF;
       __builtin_amdgcn_sched_group_barrier(0x100, PRE, 0);
 #pragma unroll
@@ -320,51 +358,57 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
     }
   };
   // phase B1: P, dS (bf16 B operands of the accumulating products) -- exp / mask / pack VALU work
-  bf16x8 pb[HW][2], sb[HW][2];
+  bf16x8 pb[QR][HW][2], sb[QR][HW][2];
   auto phaseB1 = [&](const int it) __attribute__((always_inline)) {
-    const int qt = qbeg + (it % nqt) * BQ2;
 #pragma unroll
-    for (int j = 0; j < HW; ++j) {
-      const int key = wkey0 + 32 * j + lr;
-      const int kmin = wkey0 + 32 * j;
-      const bool need_mask = (a.causal && qt < kmin + 31) || (a.window > 0 && qt + BQ2 - 1 - kmin >= a.window);
+    for (int r = 0; r < QR; ++r) {
+      const int qt = qbeg + (it % nqt) * BQ2 + 32 * r;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) s[j][i] = __builtin_amdgcn_exp2f(a.c * s[j][i]);
-      if (need_mask) {  // wave-uniform; query q = qt + (i&3) + 8(i>>2) + 4hh valid iff key <= q < key + window
-        const int base = qt + 4 * hh;
-        const int lo = (a.causal ? key : -0x3fffffff) - base;
-        const int hi = (a.window > 0 ? key + a.window - 1 : 0x3fffffff) - base;
+      for (int j = 0; j < HW; ++j) {
+        const int key = wkey0 + 32 * j + lr;
+        const int kmin = wkey0 + 32 * j;
+        const bool need_mask = (a.causal && qt < kmin + 31) || (a.window > 0 && qt + 31 - kmin >= a.window);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int off = (i & 3) + 8 * (i >> 2);
-          s[j][i] = (off >= lo && off <= hi) ? s[j][i] : 0.f;
+        for (int i = 0; i < 16; ++i) s[r][j][i] = __builtin_amdgcn_exp2f(a.c * s[r][j][i]);
+        if (need_mask) {  // wave-uniform; query q = qt + (i&3) + 8(i>>2) + 4hh valid iff key <= q < key + window
+          const int base = qt + 4 * hh;
+          const int lo = (a.causal ? key : -0x3fffffff) - base;
+          const int hi = (a.window > 0 ? key + a.window - 1 : 0x3fffffff) - base;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int off = (i & 3) + 8 * (i >> 2);
+            s[r][j][i] = (off >= lo && off <= hi) ? s[r][j][i] : 0.f;
+          }
         }
-      }
 #pragma unroll
-      for (int i = 0; i < 16; ++i) dp[j][i] = s[j][i] * dp[j][i];
-      pb[j][0] = pack8_bf(s[j], 0);
-      pb[j][1] = pack8_bf(s[j], 8);
-      sb[j][0] = pack8_bf(dp[j], 0);
-      sb[j][1] = pack8_bf(dp[j], 8);
+        for (int i = 0; i < 16; ++i) dp[r][j][i] = s[r][j][i] * dp[r][j][i];
+        pb[r][j][0] = pack8_bf(s[r][j], 0);
+        pb[r][j][1] = pack8_bf(s[r][j], 8);
+        sb[r][j][0] = pack8_bf(dp[r][j], 0);
+        sb[r][j][1] = pack8_bf(dp[r][j], 8);
+      }
     }
   };
-  // phase B2: dV^T += dO^T P ; dK^T += Q^T dS for both halves (k of these MFMAs = the 32 query rows);
-  // the dO^T / Q^T tr-operands are read once and used by both halves
+  // phase B2: dV^T += dO^T P ; dK^T += Q^T dS for both halves (k of these MFMAs = the slice's query
+  // rows); the dO^T / Q^T tr-operands are read once and used by both halves
   auto phaseB2 = [&](const char* Qs) __attribute__((always_inline)) {
     const char* Ds = Qs + QBYTES;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
       const int2 to = tr_offsets<D>(dt * 32, lane);
-      const bf16x8 a0 = tr_read<D>(Ds, 0, to);
-      const bf16x8 a1 = tr_read<D>(Ds, 16, to);
-      const bf16x8 q0v = tr_read<D>(Qs, 0, to);
-      const bf16x8 q1v = tr_read<D>(Qs, 16, to);
 #pragma unroll
-      for (int j = 0; j < HW; ++j) {
-        dv[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, pb[j][0], dv[j][dt], 0, 0, 0);
-        dv[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, pb[j][1], dv[j][dt], 0, 0, 0);
-        dk[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q0v, sb[j][0], dk[j][dt], 0, 0, 0);
-        dk[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q1v, sb[j][1], dk[j][dt], 0, 0, 0);
+      for (int r = 0; r < QR; ++r) {
+        const bf16x8 a0 = tr_read<D>(Ds, 32 * r, to);
+        const bf16x8 a1 = tr_read<D>(Ds, 32 * r + 16, to);
+        const bf16x8 q0v = tr_read<D>(Qs, 32 * r, to);
+        const bf16x8 q1v = tr_read<D>(Qs, 32 * r + 16, to);
+#pragma unroll
+        for (int j = 0; j < HW; ++j) {
+          dv[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, pb[r][j][0], dv[j][dt], 0, 0, 0);
+          dv[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, pb[r][j][1], dv[j][dt], 0, 0, 0);
+          dk[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q0v, sb[r][j][0], dk[j][dt], 0, 0, 0);
+          dk[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(q1v, sb[r][j][1], dk[j][dt], 0, 0, 0);
+        }
       }
     }
   };
@@ -651,6 +695,28 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
     }
 }
 
+
+// dK/dV variant: 8 waves x 32 keys (2 waves/SIMD) with ping-pong and the 5-slot ring by default, or
+// 4 waves x 64 keys (1 wave/SIMD)
+template <int D>
+void launch_dkdv(const BwdArgs& a, int grid, int waves, bool pp, bool dist3, hipStream_t stream) {
+  // D = 64: 64-row query slices (FTC_FLASH_DKDV_QR=1 for 32)
+  static const bool qr2 = [] {
+    const char* e = getenv("FTC_FLASH_DKDV_QR");
+    return !(e && e[0] == '1');
+  }();
+  if (D == 64 && qr2 && waves == 8 && pp && dist3)
+    hipLaunchKernelGGL((bwd_dkdv_kernel<64, 1, true, 3, 2>), dim3(grid), dim3(512), 0, stream, a);
+  else if (waves == 8 && pp && dist3)
+    hipLaunchKernelGGL((bwd_dkdv_kernel<D, 1, true, 3>), dim3(grid), dim3(512), 0, stream, a);
+  else if (waves == 8 && pp)
+    hipLaunchKernelGGL((bwd_dkdv_kernel<D, 1, true>), dim3(grid), dim3(512), 0, stream, a);
+  else if (waves == 8)
+    hipLaunchKernelGGL((bwd_dkdv_kernel<D, 1>), dim3(grid), dim3(512), 0, stream, a);
+  else
+    hipLaunchKernelGGL((bwd_dkdv_kernel<D, 2>), dim3(grid), dim3(256), 0, stream, a);
+}
+
 }  // namespace
 
 extern "C" int ftc_flash_bwd_workspace(int B, int S, int H, int D, long long* bytes) {
@@ -691,28 +757,21 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
     const char* e = getenv("FTC_FLASH_DKDV_WAVES");
     return (e && e[0] == '4') ? 4 : 8;
   }();
+  // ping-pong phase order for the two waves of a SIMD (default; FTC_FLASH_DKDV_PP=0 turns it off):
+  // bwd 2.00 -> 1.97 ms at the Llama-3-8B layer shape (profiles/r1_attn_dkdv_pp.log)
+  static const bool pp = [] {
+    const char* e = getenv("FTC_FLASH_DKDV_PP");
+    return !(e && e[0] == '0');
+  }();
+  // Q/dO slices DMA'd three slices ahead (5-slot ring; default, FTC_FLASH_DKDV_DIST=2 for two):
+  // bwd 1.99 -> 1.96 ms at the Llama-3-8B layer shape (profiles/r1_attn_dkdv_pp.log)
+  static const bool dist3 = [] {
+    const char* e = getenv("FTC_FLASH_DKDV_DIST");
+    return !(e && e[0] == '2');
+  }();
   if (D == 128) {
     hipLaunchKernelGGL(bwd_delta_kernel<128>, dim3(grid_d), dim3(256), 0, stream, a);
-    // ping-pong phase order for the two waves of a SIMD (default; FTC_FLASH_DKDV_PP=0 turns it off):
-    // bwd 2.00 -> 1.97 ms at the Llama-3-8B layer shape (profiles/r1_attn_dkdv_pp.log)
-    static const bool pp = [] {
-      const char* e = getenv("FTC_FLASH_DKDV_PP");
-      return !(e && e[0] == '0');
-    }();
-    // Q/dO slices DMA'd three slices ahead (5-slot ring; default, FTC_FLASH_DKDV_DIST=2 for two):
-    // bwd 1.99 -> 1.96 ms at the Llama-3-8B layer shape (profiles/r1_attn_dkdv_pp.log)
-    static const bool dist3 = [] {
-      const char* e = getenv("FTC_FLASH_DKDV_DIST");
-      return !(e && e[0] == '2');
-    }();
-    if (dkdv_waves == 8 && pp && dist3)
-      hipLaunchKernelGGL((bwd_dkdv_kernel<128, 1, true, 3>), dim3(g_kv), dim3(512), 0, stream, a);
-    else if (dkdv_waves == 8 && pp)
-      hipLaunchKernelGGL((bwd_dkdv_kernel<128, 1, true>), dim3(g_kv), dim3(512), 0, stream, a);
-    else if (dkdv_waves == 8)
-      hipLaunchKernelGGL((bwd_dkdv_kernel<128, 1>), dim3(g_kv), dim3(512), 0, stream, a);
-    else
-      hipLaunchKernelGGL((bwd_dkdv_kernel<128, 2>), dim3(g_kv), dim3(256), 0, stream, a);
+    launch_dkdv<128>(a, g_kv, dkdv_waves, pp, dist3, stream);
     if (occ == 1) {
       hipLaunchKernelGGL((bwd_dq_kernel<128, 1>), dim3(g_q), dim3(256), 0, stream, a);
     } else {
@@ -720,7 +779,7 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
     }
   } else {
     hipLaunchKernelGGL(bwd_delta_kernel<64>, dim3(grid_d), dim3(256), 0, stream, a);
-    hipLaunchKernelGGL((bwd_dkdv_kernel<64, 2>), dim3(g_kv), dim3(256), 0, stream, a);
+    launch_dkdv<64>(a, g_kv, dkdv_waves, pp, dist3, stream);
     hipLaunchKernelGGL((bwd_dq_kernel<64, 2>), dim3(g_q), dim3(256), 0, stream, a);
   }
   return (int)hipGetLastError();

@@ -259,6 +259,9 @@ def test_lora_merge(C):
     (1, 1024, 8, 2, 128, True, 0),
     (1, 512, 8, 2, 128, True, 192),
     (2, 256, 4, 4, 64, True, 0),
+    (1, 1024, 8, 2, 64, True, 0),
+    (1, 512, 8, 2, 64, False, 0),
+    (1, 768, 8, 4, 64, True, 320),
 ])
 def test_flash_attention_fwd_bwd(C, B, S, H, KV, D, causal, window):
     from finetune_controller_amd.ops.attention import _FlashPacked, attention_reference
