@@ -56,6 +56,8 @@ def main(argv=None) -> int:
                     help="rows per lm_head + cross-entropy chunk (the only vocab-sized buffer)")
     ap.add_argument("--kernels", default=None, choices=["hip", "torch"],
                     help="torch = stock PyTorch-ROCm ops (the 'before' row)")
+    ap.add_argument("--doc-len", type=int, default=0,
+                    help="packed documents of this many tokens (document-masked attention; 0: one per row)")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (not timed)")
     a = ap.parse_args(argv)
     if a.kernels:
@@ -74,7 +76,8 @@ def main(argv=None) -> int:
     tc = TrainConfig(model=a.model, method=a.method, lora_r=a.lora_r, lora_alpha=2.0 * a.lora_r,
                      batch_size=a.batch_size, seq_len=a.seq_len, synthetic=True, max_steps=a.warmup + a.steps,
                      warmup_steps=0, schedule="constant", lr=1e-4, bucket_mb=a.bucket_mb, comm_engine=a.comm_engine, zero_stage=a.zero_stage,
-                     checkpoint_layers=a.checkpoint_layers, ce_chunk_rows=a.ce_chunk_rows, save_model=False, resume=False, device="cuda")
+                     checkpoint_layers=a.checkpoint_layers, ce_chunk_rows=a.ce_chunk_rows, save_model=False, resume=False, device="cuda",
+                     pack_documents=a.doc_len > 0, eos_id=2, synthetic_doc_len=a.doc_len)
     tr = Trainer(tc)
     info = tr.info
     dev = tr.device
@@ -144,6 +147,7 @@ def main(argv=None) -> int:
                 "kernels": _backend.kernel_mode(),
                 "comm_engine": a.comm_engine,
                 "zero_stage": a.zero_stage,
+                **({"packed_doc_len": a.doc_len} if a.doc_len else {}),
             },
             "loss": round(loss, 4),
             "model_tflops_per_gpu": round(value * flops_tok / n / 1e12, 1),

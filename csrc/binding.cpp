@@ -43,13 +43,14 @@ int ftc_sumsq(const void* x, int is_fp32, long long n, float* partial, float* ou
               float scale, hipStream_t stream);
 int ftc_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H, int KV, int D,
                   long long q_row_stride, long long kv_row_stride, long long o_row_stride, float scale, int causal,
-                  int window, hipStream_t stream);
+                  int window, const int* doc_start, hipStream_t stream);
 int ftc_flash_bwd_workspace(int B, int S, int H, int D, long long* bytes);
 int ftc_flash_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
                   void* dq, void* dk, void* dv, void* workspace, int B, int S, int H, int KV, int D,
                   long long q_row_stride, long long kv_row_stride, long long o_row_stride, long long do_row_stride,
                   long long dq_row_stride,
-                  long long dkv_row_stride, float scale, int causal, int window, hipStream_t stream);
+                  long long dkv_row_stride, float scale, int causal, int window, const int* doc_start,
+                  const int* doc_end, hipStream_t stream);
 int ftc_nf4_dequant(const uint8_t* packed, const uint8_t* absmax_q, const float* absmax_scale, float absmax_offset,
                     void* out, long long n, int block, int block2, hipStream_t stream);
 int ftc_nf4_quant(const void* w, uint8_t* packed, float* absmax, long long n, int block, hipStream_t stream);
@@ -403,10 +404,19 @@ at::Tensor grad_sumsq(const at::Tensor& g, double max_norm, double scale) {
 }
 
 // ---------------- flash attention ----------------
+// optional packed-sequence document bounds: int32 [B*S], doc_start[t] = first position of t's document,
+// doc_end[t] = one past its last position (causal attention only)
+static const int* doc_ptr(const c10::optional<at::Tensor>& t, int64_t n, const char* what) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kInt && t->is_contiguous() && t->numel() == n, what,
+              ": int32 contiguous [B*S] device tensor");
+  return t->data_ptr<int>();
+}
+
 // q: [B*S, >=H*D] view (row stride q_rs), k/v: [B*S, >=KV*D] views; all bf16 with unit column stride.
 std::vector<at::Tensor> flash_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, int64_t B, int64_t S,
                                   int64_t H, int64_t KV, int64_t D, double scale, bool causal, int64_t window,
-                                  int64_t pad) {
+                                  int64_t pad, const c10::optional<at::Tensor>& doc_start) {
   need(q, at::kBFloat16, "q");
   need(k, at::kBFloat16, "k");
   need(v, at::kBFloat16, "v");
@@ -425,7 +435,7 @@ std::vector<at::Tensor> flash_fwd(const at::Tensor& q, const at::Tensor& k, cons
   auto lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
   check(ftc_flash_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), (int)B, (int)S,
                       (int)H, (int)KV, (int)D, q.stride(0), k.stride(0), o.stride(0), (float)scale, causal ? 1 : 0,
-                      (int)window, cur_stream()),
+                      (int)window, doc_ptr(doc_start, B * S, "doc_start"), cur_stream()),
         "flash_fwd");
   return {o, lse};
 }
@@ -433,7 +443,9 @@ std::vector<at::Tensor> flash_fwd(const at::Tensor& q, const at::Tensor& k, cons
 // writes dq/dk/dv into the given views (packed dqkv buffer)
 void flash_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
                const at::Tensor& dout, const at::Tensor& lse, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv,
-               int64_t B, int64_t S, int64_t H, int64_t KV, int64_t D, double scale, bool causal, int64_t window) {
+               int64_t B, int64_t S, int64_t H, int64_t KV, int64_t D, double scale, bool causal, int64_t window,
+               const c10::optional<at::Tensor>& doc_start, const c10::optional<at::Tensor>& doc_end) {
+  TORCH_CHECK(doc_start.has_value() == doc_end.has_value(), "flash_bwd: doc_start and doc_end go together");
   for (auto* t : {&q, &k, &v, &o, &dout}) need(*t, at::kBFloat16, "flash_bwd input");
   need(lse, at::kFloat, "lse");
   TORCH_CHECK(D == 128 || D == 64, "flash_bwd: head_dim");
@@ -449,7 +461,8 @@ void flash_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, co
                       dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), work.data_ptr(), (int)B, (int)S, (int)H, (int)KV,
                       (int)D, q.stride(0), k.stride(0), o.stride(0), dout.stride(0), dq.stride(0), dk.stride(0),
                       (float)scale,
-                      causal ? 1 : 0, (int)window, cur_stream()),
+                      causal ? 1 : 0, (int)window, doc_ptr(doc_start, B * S, "doc_start"),
+                      doc_ptr(doc_end, B * S, "doc_end"), cur_stream()),
         "flash_bwd");
 }
 
@@ -600,8 +613,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("adamw_", &adamw_);
   m.def("grad_sumsq", &grad_sumsq);
   m.def("flash_fwd", &flash_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("B"), py::arg("S"), py::arg("H"),
-        py::arg("KV"), py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("pad") = 0);
-  m.def("flash_bwd", &flash_bwd);
+        py::arg("KV"), py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("pad") = 0,
+        py::arg("doc_start") = py::none());
+  m.def("flash_bwd", &flash_bwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("dout"),
+        py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("B"), py::arg("S"), py::arg("H"),
+        py::arg("KV"), py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("window"),
+        py::arg("doc_start") = py::none(), py::arg("doc_end") = py::none());
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequantize", &nf4_dequantize);
   m.def("nf4_linear", &nf4_linear);

@@ -77,7 +77,9 @@ struct BwdArgs {
   int B, S, H, KV;
   float scale, c;  // c = scale * log2(e)
   int causal, window;
-  int prio_young;  // dK/dV, 8 waves: s_setprio 1 for the second-dispatched half (guide T5 static form)
+  int prio_young;
+  const int* doc_start;  // [B*S] packed-sequence document bounds (null: one document per sequence):
+  const int* doc_end;    //   key k visible to query q iff doc_start[q] <= k, i.e. q < doc_end[k]  // dK/dV, 8 waves: s_setprio 1 for the second-dispatched half (guide T5 static form)
 };
 
 // ---------------------------------------------------------------- 1. delta
@@ -241,6 +243,20 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
   int qbeg = a.causal ? kv0 : 0;
   int qend = S;
   if (a.window > 0) qend = min(S, kv0 + BKV - 1 + a.window);
+  // packed documents: queries past the end of the block's last key's document see none of its keys;
+  // per half, the lane's key bound (dend) and the half's smallest one (dmin: mask needed beyond it)
+  int dend[HW], dmin[HW];
+#pragma unroll
+  for (int j = 0; j < HW; ++j) dend[j] = dmin[j] = 0x3fffffff;
+  if (a.doc_end) {
+    const int* de = a.doc_end + (long long)b * S;
+    qend = min(qend, de[kv0 + BKV - 1]);
+#pragma unroll
+    for (int j = 0; j < HW; ++j) {
+      dend[j] = de[wkey0 + 32 * j + lr];
+      dmin[j] = de[wkey0 + 32 * j];
+    }
+  }
   qbeg = (qbeg / BQ2) * BQ2;
   const int nqt = (qend - qbeg + BQ2 - 1) / BQ2;
   // Q / dO / row-constant slices arrive by LDS-DMA (global_load_lds_dwordx4: no staging VGPRs) into a
@@ -367,13 +383,14 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
       for (int j = 0; j < HW; ++j) {
         const int key = wkey0 + 32 * j + lr;
         const int kmin = wkey0 + 32 * j;
-        const bool need_mask = (a.causal && qt < kmin + 31) || (a.window > 0 && qt + 31 - kmin >= a.window);
+        const bool need_mask = (a.causal && qt < kmin + 31) || (a.window > 0 && qt + 31 - kmin >= a.window) ||
+                               qt + 31 >= dmin[j];
 #pragma unroll
         for (int i = 0; i < 16; ++i) s[r][j][i] = __builtin_amdgcn_exp2f(a.c * s[r][j][i]);
         if (need_mask) {  // wave-uniform; query q = qt + (i&3) + 8(i>>2) + 4hh valid iff key <= q < key + window
           const int base = qt + 4 * hh;
           const int lo = (a.causal ? key : -0x3fffffff) - base;
-          const int hi = (a.window > 0 ? key + a.window - 1 : 0x3fffffff) - base;
+          const int hi = min(a.window > 0 ? key + a.window - 1 : 0x3fffffff, dend[j] - 1) - base;
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const int off = (i & 3) + 8 * (i >> 2);
@@ -589,6 +606,13 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
   int kv_end = a.causal ? q0 + BQ : S;
   int kv_begin = 0;
   if (a.window > 0) kv_begin = (max(0, q0 - a.window + 1) / BK) * BK;
+  int dlo = -0x3fffffff, wdmax = -0x3fffffff;  // packed documents: as in the forward
+  if (a.doc_start) {
+    const int* ds = a.doc_start + (long long)b * S;
+    dlo = ds[qrow];
+    wdmax = ds[q0 + wave * 32 + 31];
+    kv_begin = max(kv_begin, (ds[q0] / BK) * BK);
+  }
   const int ntiles = (kv_end - kv_begin + BK - 1) / BK;
   const uint16_t* kbase = a.k + (long long)b * S * a.kv_rs + (long long)kvh * D;
   const uint16_t* vbase = a.v + (long long)b * S * a.kv_rs + (long long)kvh * D;
@@ -648,11 +672,12 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[kt][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(a.c, s[kt][i], -lse2));
     const int qmin_w = q0 + wave * 32;
-    const bool need_mask = (a.causal && kv0 + BK - 1 > qmin_w) || (a.window > 0 && qmin_w + 31 - kv0 >= a.window);
+    const bool need_mask = (a.causal && kv0 + BK - 1 > qmin_w) || (a.window > 0 && qmin_w + 31 - kv0 >= a.window) ||
+                           kv0 < wdmax;
     if (need_mask) {  // wave-uniform; selects inside
       const int base = kv0 + 4 * hh;
       const int hi = (a.causal ? qrow : 0x3fffffff) - base;
-      const int lo = (a.window > 0 ? qrow - a.window + 1 : -0x3fffffff) - base;
+      const int lo = max(a.window > 0 ? qrow - a.window + 1 : -0x3fffffff, dlo) - base;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -729,14 +754,14 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
                              const float* lse, void* dq, void* dk, void* dv, void* workspace, int B, int S, int H,
                              int KV, int D, long long q_rs, long long kv_rs, long long o_rs, long long do_rs,
                              long long dq_rs, long long dkv_rs, float scale, int causal, int window,
-                             hipStream_t stream) {
+                             const int* doc_start, const int* doc_end, hipStream_t stream) {
   if (S % 256 != 0 || H % KV != 0 || (D != 128 && D != 64)) return -1;
   // the dK/dV kernel addresses one batch's Q / dO rows and the workspace with 32-bit buffer offsets
   const long long max_rs = q_rs > do_rs ? (q_rs > kv_rs ? q_rs : kv_rs) : (do_rs > kv_rs ? do_rs : kv_rs);
   if ((long long)S * max_rs * 2 >= (1LL << 31) || 2LL * B * H * S * 4 >= (1LL << 31)) return -1;
   BwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)o, (const uint16_t*)dout,
             lse, (float*)workspace, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, q_rs, kv_rs, o_rs, dq_rs, dkv_rs, do_rs,
-            B, S, H, KV, scale, scale * LOG2E, causal, window, 0};
+            B, S, H, KV, scale, scale * LOG2E, causal, window, 0, doc_start, doc_end};
   static const int prio = [] {
     const char* e = getenv("FTC_FLASH_BWD_PRIO");
     return (e && e[0] == '1') ? 1 : 0;

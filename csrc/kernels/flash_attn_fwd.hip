@@ -70,6 +70,7 @@ struct FwdArgs {
   int B, S, H, KV, nqb;
   float scale_log2;
   int causal, window;
+  const int* doc_start;  // [B*S] first position of each token's document (packed sequences), or null
 };
 
 // logical block -> (qb, b, kvh, g) with heavy-first order and GQA groups co-located on one XCD
@@ -167,6 +168,16 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
     kv_begin = max(0, q0 - a.window + 1);
     kv_begin = (kv_begin / BK) * BK;
   }
+  // document-masked packing: key k is visible to query q only when doc_start[q] <= k.  doc_start is
+  // non-decreasing along a sequence, so the block's first row bounds the key range and the wave's
+  // last row tells whether a tile needs the per-element mask.
+  int dlo = -0x3fffffff, wdmax = -0x3fffffff;
+  if (a.doc_start) {
+    const int* ds = a.doc_start + (long long)b * S;
+    dlo = ds[qvalid ? qrow : S - 1];
+    wdmax = ds[min(S - 1, q0 + wave * 32 + 31)];
+    kv_begin = max(kv_begin, (ds[q0] / BK) * BK);
+  }
   const int ntiles = (kv_end - kv_begin + BK - 1) / BK;
 
   const uint16_t* kbase = a.k + (long long)b * S * a.kv_rs + (long long)kvh * D;
@@ -236,12 +247,13 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
   auto phaseB1 = [&](const int t) __attribute__((always_inline)) {
     const int kv0 = kv_begin + t * BK;
     const int qmin_w = q0 + wave * 32;
-    const bool need_mask = (a.causal && kv0 + BK - 1 > qmin_w) || (a.window > 0 && qmin_w + 31 - kv0 >= a.window);
+    const bool need_mask = (a.causal && kv0 + BK - 1 > qmin_w) || (a.window > 0 && qmin_w + 31 - kv0 >= a.window) ||
+                           kv0 < wdmax;
     if (need_mask) {
       // key k of element (kt, i) = kv0 + kt*32 + (i&3) + 8*(i>>2) + 4*hh; valid iff lo <= k <= hi
       const int base = kv0 + 4 * hh;
       const int hi = (a.causal ? qrow : 0x3fffffff) - base;
-      const int lo = (a.window > 0 ? qrow - a.window + 1 : -0x3fffffff) - base;
+      const int lo = max(a.window > 0 ? qrow - a.window + 1 : -0x3fffffff, dlo) - base;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -379,7 +391,7 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
 
 extern "C" int ftc_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H,
                              int KV, int D, long long q_rs, long long kv_rs, long long o_rs, float scale, int causal,
-                             int window, hipStream_t stream) {
+                             int window, const int* doc_start, hipStream_t stream) {
   if (S % BK != 0 || H % KV != 0 || (D != 128 && D != 64)) return -1;
   static const int waves = [] {
     const char* e = getenv("FTC_FLASH_FWD_WAVES");
@@ -387,7 +399,7 @@ extern "C" int ftc_flash_fwd(const void* q, const void* k, const void* v, void* 
   }();
   const int BQ = 32 * waves;
   FwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, q_rs, kv_rs, o_rs,
-            B, S, H, KV, (S + BQ - 1) / BQ, scale * LOG2E, causal, window};
+            B, S, H, KV, (S + BQ - 1) / BQ, scale * LOG2E, causal, window, doc_start};
   const int nblocks = a.nqb * B * H;
   const size_t lds = 0;  // static: K/V double buffers
   static const bool pp = [] {

@@ -45,11 +45,11 @@ class GPT2Block(nn.Module):
         return ops.lora_linear(x, W, p.A, p.B, p.scale, bias=b, blocks=p.blocks,
                                dropout=p.dropout if self.training else 0.0)
 
-    def forward(self, h, B, S):
+    def forward(self, h, B, S, docs=None):
         cfg = self.cfg
         x = ops.layer_norm(h, self.ln1_w, self.ln1_b, cfg.norm_eps)
         qkv = self._lin("qkv", x, self.attn_w, self.attn_b)
-        a = ops.attention_packed(qkv, B, S, cfg.n_heads, cfg.n_heads, cfg.head_dim, True, 0)
+        a = ops.attention_packed(qkv, B, S, cfg.n_heads, cfg.n_heads, cfg.head_dim, True, 0, docs=docs)
         h = h + self._lin("o", a, self.proj_w, self.proj_b)
         x = ops.layer_norm(h, self.ln2_w, self.ln2_b, cfg.norm_eps)
         x = ops.gelu_tanh(self._lin("gu", x, self.fc_w, self.fc_b))
@@ -94,19 +94,23 @@ class GPT2ForCausalLM(nn.Module):
         for name, p in self.named_parameters():
             p.requires_grad_(".lora." in name)
 
-    def hidden(self, input_ids, positions=None):
+    def hidden(self, input_ids, positions=None, segments=None):
         B, S = input_ids.shape
-        pos = torch.arange(S, device=input_ids.device)
-        h = (self.wte[input_ids] + self.wpe[pos][None]).reshape(B * S, -1)
+        if segments is not None:  # packed documents: positions restart per document
+            pos = segments.positions.view(B, S).long()
+            h = (self.wte[input_ids] + self.wpe[pos]).reshape(B * S, -1)
+        else:
+            pos = torch.arange(S, device=input_ids.device) if positions is None else positions.long()
+            h = (self.wte[input_ids] + self.wpe[pos].view(-1, S, self.wpe.shape[1])).reshape(B * S, -1)
         for blk in self.blocks:
             if self.checkpoint_layers and self.training and torch.is_grad_enabled():
-                h = checkpoint(blk, h, B, S, use_reentrant=False)
+                h = checkpoint(blk, h, B, S, segments, use_reentrant=False)
             else:
-                h = blk(h, B, S)
+                h = blk(h, B, S, segments)
         return ops.layer_norm(h, self.lnf_w, self.lnf_b, self.cfg.norm_eps)
 
-    def forward(self, input_ids, labels=None, positions=None, n_valid=None):
-        x = self.hidden(input_ids)
+    def forward(self, input_ids, labels=None, positions=None, n_valid=None, segments=None):
+        x = self.hidden(input_ids, positions, segments)
         if labels is None:
             return x @ self.wte.t()
         return ops.fused_linear_cross_entropy(x, self.wte, labels, self.ce_chunk_rows, -100, n_valid)

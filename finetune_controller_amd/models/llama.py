@@ -135,7 +135,7 @@ class LlamaLayer(nn.Module):
         return ops.lora_linear(x, W, pair.A, pair.B, pair.scale, blocks=pair.blocks, aug=self.aug.get(name),
                                dropout=pair.dropout if self.training else 0.0)
 
-    def forward(self, h, delta, rope: ops.RotaryTable, B: int, S: int, positions=None):
+    def forward(self, h, delta, rope: ops.RotaryTable, B: int, S: int, positions=None, docs=None):
         cfg = self.cfg
         p_qkv, p_o, p_gu, p_down = (self.pad(n) for n in ("qkv", "o", "gu", "down"))
         # grad_pad: delta came from the previous layer's down projection (same LoRA shape in every layer;
@@ -144,7 +144,7 @@ class LlamaLayer(nn.Module):
         qkv = self.proj("qkv", x)
         qkv = ops.apply_rope_packed(qkv, rope, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, S, positions)
         a = ops.attention_packed(qkv, B, S, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, True, cfg.sliding_window,
-                                 out_pad=p_o, grad_pad=p_qkv)
+                                 out_pad=p_o, grad_pad=p_qkv, docs=docs)
         o = self.proj("o", a)
         h, x = ops.add_rms_norm(h, o, self.mlp_norm, cfg.norm_eps, pad=p_gu, grad_pad=p_o)
         mlp = self.mlp_projs(p_gu, p_down)
@@ -205,22 +205,26 @@ class LlamaForCausalLM(nn.Module):
         for name, p in self.named_parameters():
             p.requires_grad_(".lora." in name)
 
-    def hidden(self, input_ids: torch.Tensor, positions=None) -> torch.Tensor:
+    def hidden(self, input_ids: torch.Tensor, positions=None, segments=None) -> torch.Tensor:
+        """``segments`` (``ops.Segments``): packed documents -- RoPE positions restart and attention
+        stays inside each document."""
         B, S = input_ids.shape
+        if segments is not None:
+            positions = segments.positions
         h = F.embedding(input_ids.reshape(-1), self.embed)
         delta = None
         for layer in self.layers:
             if self.checkpoint_layers and self.training and torch.is_grad_enabled():
-                h, delta = checkpoint(layer, h, delta, self.rope, B, S, positions, use_reentrant=False)
+                h, delta = checkpoint(layer, h, delta, self.rope, B, S, positions, segments, use_reentrant=False)
             else:
-                h, delta = layer(h, delta, self.rope, B, S, positions)
+                h, delta = layer(h, delta, self.rope, B, S, positions, segments)
         gp = self.layers[-1].pad("down") if len(self.layers) else 0
         _, x = ops.add_rms_norm(h, delta, self.final_norm, self.cfg.norm_eps, grad_pad=gp)
         return x
 
     def forward(self, input_ids: torch.Tensor, labels: torch.Tensor | None = None, positions=None,
-                n_valid: int | None = None):
-        x = self.hidden(input_ids, positions)
+                n_valid: int | None = None, segments=None):
+        x = self.hidden(input_ids, positions, segments)
         if labels is None:
             return x @ self.lm_head.t()
         return ops.fused_linear_cross_entropy(x, self.lm_head, labels, self.ce_chunk_rows, -100, n_valid)

@@ -11,10 +11,16 @@ The backward writes dq/dk/dv straight into ONE packed ``dqkv`` buffer, which is 
 packed projection output -- again no concatenation.
 
 CPU / ``FTC_KERNELS=torch``: ``torch.nn.functional.scaled_dot_product_attention``.
+
+Packed sequences (several documents per row, ``Segments``): a query sees only keys of its own
+document.  The kernels take per-token document bounds -- ``doc_start`` for the query-on-lane passes
+(forward, dQ), ``doc_end`` for the key-on-lane dK/dV pass -- skip key / query tiles outside the
+document range and mask per element only on tiles that straddle a boundary.
 """
 from __future__ import annotations
 
 import math
+from dataclasses import dataclass
 
 import torch
 import torch.nn.functional as F
@@ -30,6 +36,42 @@ def flash_supported(D: int, S: int) -> bool:
     return FLASH_READY and D in (64, 128) and S % 256 == 0
 
 
+@dataclass
+class Segments:
+    """Document layout of a packed [B, S] batch, int32 flat [B*S] (positions within the row):
+    ``doc_start[t]`` first position of t's document, ``doc_end[t]`` one past its last, ``positions[t]``
+    = t - doc_start[t] (RoPE / learned positions restart per document)."""
+
+    doc_start: torch.Tensor
+    doc_end: torch.Tensor
+    positions: torch.Tensor
+
+
+def segments_from_eos(ids: torch.Tensor, eos_id: int) -> Segments:
+    """Documents end at (and include) each ``eos_id`` token; computed on the ids' device (cummax /
+    cummin scans, no host sync)."""
+    B, S = ids.shape
+    t = torch.arange(S, device=ids.device, dtype=torch.int64).expand(B, S)
+    is_eos = ids == eos_id
+    starts = torch.zeros_like(is_eos)
+    starts[:, 0] = True
+    starts[:, 1:] = is_eos[:, :-1]
+    doc_start = torch.where(starts, t, torch.zeros_like(t)).cummax(dim=1).values
+    ends = is_eos.clone()
+    ends[:, -1] = True
+    last = torch.where(ends, t, torch.full_like(t, S)).flip(1).cummin(dim=1).values.flip(1)
+    doc_end = last + 1
+    return Segments(doc_start.to(torch.int32).reshape(-1).contiguous(), doc_end.to(torch.int32).reshape(-1).contiguous(),
+                    (t - doc_start).to(torch.int32).reshape(-1).contiguous())
+
+
+def _doc_mask(docs: Segments, B: int, S: int) -> torch.Tensor:
+    """[B, 1, S, S] bool: causal and same document."""
+    ds = docs.doc_start.view(B, S).long()
+    k = torch.arange(S, device=ds.device)
+    return ((k[None, None, :] <= k[None, :, None]) & (k[None, None, :] >= ds[:, :, None])).unsqueeze(1)
+
+
 def _split(qkv, B, S, H, KV, D):
     q = qkv[:, : H * D]
     k = qkv[:, H * D : (H + KV) * D]
@@ -37,7 +79,7 @@ def _split(qkv, B, S, H, KV, D):
     return q, k, v
 
 
-def _sdpa_packed(qkv, B, S, H, KV, D, causal, window, scale):
+def _sdpa_packed(qkv, B, S, H, KV, D, causal, window, scale, docs: Segments | None = None):
     q, k, v = _split(qkv, B, S, H, KV, D)
     q = q.reshape(B, S, H, D).transpose(1, 2)
     k = k.reshape(B, S, KV, D).transpose(1, 2)
@@ -47,7 +89,13 @@ def _sdpa_packed(qkv, B, S, H, KV, D, causal, window, scale):
         k = k.repeat_interleave(rep, dim=1)
         v = v.repeat_interleave(rep, dim=1)
     mask = None
-    if window and window > 0 and window < S:
+    if docs is not None:
+        mask = _doc_mask(docs, B, S)
+        if window and window > 0:
+            i = torch.arange(S, device=qkv.device)
+            mask = mask & ((i[:, None] - i[None, :]) < window)
+        o = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, scale=scale)
+    elif window and window > 0 and window < S:
         i = torch.arange(S, device=qkv.device)
         allowed = (i[None, :] <= i[:, None]) & (i[:, None] - i[None, :] < window)
         mask = allowed
@@ -59,9 +107,10 @@ def _sdpa_packed(qkv, B, S, H, KV, D, causal, window, scale):
 
 class _FlashPacked(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, B, S, H, KV, D, causal, window, scale, out_pad=0, grad_pad=0):
+    def forward(ctx, qkv, B, S, H, KV, D, causal, window, scale, out_pad=0, grad_pad=0, docs=None):
         q, k, v = _split(qkv, B, S, H, KV, D)
-        o, lse = ext().flash_fwd(q, k, v, B, S, H, KV, D, scale, causal, window, out_pad)
+        o, lse = ext().flash_fwd(q, k, v, B, S, H, KV, D, scale, causal, window, out_pad,
+                                 docs.doc_start if docs is not None else None)
         # o is kept outside save_for_backward: with out_pad the consumer writes its LoRA activations
         # into the spare columns of o's buffer, which bumps the shared version counter (the [:, :H*D]
         # values themselves never change)
@@ -69,6 +118,7 @@ class _FlashPacked(torch.autograd.Function):
         ctx.o = o.detach()
         ctx.cfg = (B, S, H, KV, D, causal, window, scale)
         ctx.grad_pad = grad_pad
+        ctx.docs = docs
         return o
 
     @staticmethod
@@ -84,24 +134,29 @@ class _FlashPacked(torch.autograd.Function):
         # LoRA backward GEMM of the qkv projection)
         dqkv = torch.empty(qkv.shape[0], Wd + ctx.grad_pad, dtype=qkv.dtype, device=qkv.device)[:, :Wd]
         dq, dk, dv = _split(dqkv, B, S, H, KV, D)
-        ext().flash_bwd(q, k, v, o, do, lse, dq, dk, dv, B, S, H, KV, D, scale, causal, window)
-        return dqkv, None, None, None, None, None, None, None, None, None, None
+        docs = ctx.docs
+        ext().flash_bwd(q, k, v, o, do, lse, dq, dk, dv, B, S, H, KV, D, scale, causal, window,
+                        docs.doc_start if docs is not None else None, docs.doc_end if docs is not None else None)
+        return dqkv, None, None, None, None, None, None, None, None, None, None, None
 
 
 def attention_packed(qkv: torch.Tensor, B: int, S: int, H: int, KV: int, D: int, causal: bool = True,
                      window: int = 0, scale: float | None = None, out_pad: int = 0,
-                     grad_pad: int = 0) -> torch.Tensor:
+                     grad_pad: int = 0, docs: Segments | None = None) -> torch.Tensor:
     """Causal / sliding-window GQA attention on a packed ``[B*S, (H+2KV)*D]`` projection.
 
     ``out_pad`` / ``grad_pad``: the output / the gradient of ``qkv`` are column views of
-    row-padded buffers (spare columns for the augmented LoRA GEMMs, ``ops.linear``)."""
+    row-padded buffers (spare columns for the augmented LoRA GEMMs, ``ops.linear``).  ``docs``: packed
+    documents (causal only)."""
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if docs is not None and not causal:
+        raise ValueError("document-masked attention is causal")
     if use_hip(qkv) and qkv.dtype == torch.bfloat16 and flash_supported(D, S):
-        return _FlashPacked.apply(qkv, B, S, H, KV, D, causal, int(window or 0), scale, out_pad, grad_pad)
-    return _sdpa_packed(qkv, B, S, H, KV, D, causal, window, scale)
+        return _FlashPacked.apply(qkv, B, S, H, KV, D, causal, int(window or 0), scale, out_pad, grad_pad, docs)
+    return _sdpa_packed(qkv, B, S, H, KV, D, causal, window, scale, docs)
 
 
-def attention_reference(qkv, B, S, H, KV, D, causal=True, window=0, scale=None):
+def attention_reference(qkv, B, S, H, KV, D, causal=True, window=0, scale=None, docs: Segments | None = None):
     """fp32 math reference used by the kernel numerics tests."""
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     q, k, v = (t.float() for t in _split(qkv, B, S, H, KV, D))
@@ -115,6 +170,8 @@ def attention_reference(qkv, B, S, H, KV, D, causal=True, window=0, scale=None):
         allowed &= i[None, :] <= i[:, None]
     if window and window > 0:
         allowed &= (i[:, None] - i[None, :]) < window
+    if docs is not None:
+        allowed = allowed & _doc_mask(docs, B, S)
     s = s.masked_fill(~allowed, float("-inf"))
     p = s.softmax(-1)
     return (p @ v).transpose(1, 2).reshape(B * S, H * D)

@@ -28,11 +28,19 @@ import torch
 class SyntheticTokens:
     """Uniform random token ids of the configured shape (the benchmark contract's synthetic data)."""
 
-    def __init__(self, vocab: int, batch: int, seq_len: int, device, seed: int = 0):
+    def __init__(self, vocab: int, batch: int, seq_len: int, device, seed: int = 0, doc_len: int = 0,
+                 eos_id: int = 2):
         self.vocab, self.batch, self.seq_len, self.device = vocab, batch, seq_len, device
         self.gen = torch.Generator(device="cpu").manual_seed(seed)
         # a small pool of pre-generated batches on device: no host->device copy in the timed loop
-        self.pool = [torch.randint(0, vocab, (batch, seq_len + 1), generator=self.gen).to(device) for _ in range(4)]
+        pool = [torch.randint(0, vocab, (batch, seq_len + 1), generator=self.gen) for _ in range(4)]
+        self.last_eos = None
+        if doc_len:  # packed documents of doc_len tokens: EOS at the end of each, none elsewhere
+            for t in pool:
+                t[t == eos_id] = (eos_id + 1) % vocab
+                t[:, doc_len - 1::doc_len] = eos_id
+            self.last_eos = int((pool[0][:, :-1] == eos_id).sum())
+        self.pool = [t.to(device) for t in pool]
         self.i = 0
 
     def __iter__(self):
@@ -110,6 +118,11 @@ class Tokenizer:
             from tokenizers import Tokenizer as HFTok
 
             self.tk = HFTok.from_file(cand)
+            for name in ("<|end_of_text|>", "</s>", "<|endoftext|>", "<eos>", "<|eot_id|>"):
+                i = self.tk.token_to_id(name)
+                if i is not None:
+                    self.eos = int(i)
+                    break
         elif vocab < 259:
             raise ValueError("byte-level fallback tokenizer needs vocab >= 259")
 
@@ -149,7 +162,7 @@ class PackedTokenDataset:
     """
 
     def __init__(self, path: str, vocab: int, batch: int, seq_len: int, device, rank: int = 0, world: int = 1,
-                 seed: int = 0, holdout: float = 0):
+                 seed: int = 0, holdout: float = 0, eos_id: int | None = None):
         self.tokens = load_token_array(path, vocab)
         self.vocab, self.batch, self.seq_len, self.device = vocab, batch, seq_len, device
         self.rank, self.world, self.seed = rank, world, seed
@@ -164,6 +177,9 @@ class PackedTokenDataset:
             want = max(int(holdout) if holdout >= 1 else int(round(n_windows * holdout)), batch * world)
         self.holdout = max(0, min(want, n_windows - 1))
         self.n_use = n_windows - self.holdout
+        # packed documents: EOS tokens among the inputs of the last batch (their next-token labels are
+        # masked), counted on the host so the loss normaliser needs no device sync
+        self.eos_id, self.last_eos = eos_id, 0
         self.steps_per_epoch = max(1, self.n_use // (batch * world))
         self.epoch = 0
         self.pos = 0
@@ -201,6 +217,8 @@ class PackedTokenDataset:
             arr = np.stack([np.asarray(self.tokens[j * S: j * S + S + 1], dtype=np.int64) for j in idx])
             arr = torch.from_numpy(arr)
             self.pos += 1
+        if self.eos_id is not None:
+            self.last_eos = int((arr[:, :-1] == self.eos_id).sum())
         if self._native is not None:
             if torch.device(self.device).type == "cpu":
                 t = arr.clone()  # the ring buffer is refilled after the next call

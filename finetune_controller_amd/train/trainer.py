@@ -26,12 +26,13 @@ from dataclasses import asdict, dataclass, field
 
 import torch
 
+from .. import ops
 from ..models import LoRAConfig, build_model, get_config
 from ..models import checkpoint as ckpt
 from ..parallel import dist as pdist
 from ..parallel.ddp import GradBucketer
 from ..utils.metrics import MetricsCSV
-from .data import EvalWindows, PackedTokenDataset, SyntheticTokens
+from .data import EvalWindows, PackedTokenDataset, SyntheticTokens, Tokenizer
 from .optim import FlatAdamW, ShardedFlatAdamW, lr_at
 
 log = logging.getLogger("ftc.train")
@@ -77,6 +78,9 @@ class TrainConfig:
     eval_every: int = 0  # >0: held-out loss every that many optimizer steps (and after the last one)
     eval_batches: int = 4  # micro-batches per rank per evaluation
     eval_holdout: float = 0.01  # held-out share of the dataset's windows (>= 1: a window count)
+    pack_documents: bool = False  # EOS-separated documents in a window attend only within themselves
+    eos_id: int = -1  # -1: the dataset tokenizer's EOS (tokenizer.json, or the byte-level fallback's 2)
+    synthetic_doc_len: int = 0  # synthetic data: EOS every that many tokens (packed-document benchmarks)
 
     def lora_config(self) -> LoRAConfig | None:
         if self.method not in ("lora", "qlora"):
@@ -161,14 +165,41 @@ class Trainer:
             if tc.synthetic or not tc.dataset_path or not os.path.exists(tc.dataset_path) or not os.listdir(
                     tc.dataset_path if os.path.isdir(tc.dataset_path) else os.path.dirname(tc.dataset_path)):
                 self._data = SyntheticTokens(self.cfg.vocab_size, tc.batch_size, tc.seq_len, self.device,
-                                             seed=tc.seed + self.info.rank)
+                                             seed=tc.seed + self.info.rank, doc_len=tc.synthetic_doc_len,
+                                             eos_id=self.eos_id() if tc.pack_documents else 2)
                 self.steps_per_epoch = 100
             else:
                 self._data = PackedTokenDataset(tc.dataset_path, self.cfg.vocab_size, tc.batch_size, tc.seq_len,
                                                 self.device, self.info.rank, self.info.world_size, tc.seed,
-                                                holdout=tc.eval_holdout if tc.eval_every > 0 else 0)
+                                                holdout=tc.eval_holdout if tc.eval_every > 0 else 0,
+                                                eos_id=self.eos_id())
                 self.steps_per_epoch = max(1, self._data.steps_per_epoch // tc.grad_accum)
         return self._data
+
+    def eos_id(self) -> int | None:
+        """The document separator when ``pack_documents`` is on."""
+        tc = self.tc
+        if not tc.pack_documents:
+            return None
+        if getattr(self, "_eos", None) is None:
+            self._eos = tc.eos_id if tc.eos_id >= 0 else Tokenizer(
+                tc.dataset_path if tc.dataset_path and os.path.exists(tc.dataset_path) else None,
+                max(self.cfg.vocab_size, 259)).eos
+        return self._eos
+
+    def _batch(self, x, y, data):
+        """(x, labels, segments, n_valid) of one micro-batch: with packed documents the labels that would
+        predict across a document boundary (inputs equal to EOS) are ignored and attention / positions
+        follow the documents."""
+        tc = self.tc
+        n_valid = x.numel()
+        eos = self.eos_id()
+        if eos is None:
+            return x, y, None, n_valid
+        seg = ops.segments_from_eos(x, eos)
+        y = y.masked_fill(x == eos, -100)
+        n_eos = getattr(data, "last_eos", None)
+        return x, y, seg, (n_valid - n_eos) if n_eos is not None else None
 
     def total_steps(self) -> int:
         self.data()
@@ -185,11 +216,10 @@ class Trainer:
             ev[0].record()
         self.opt.zero_grad()
         total = None
-        n_valid = tc.batch_size * tc.seq_len
         for micro in range(tc.grad_accum):
-            x, y = next(data)
+            x, y, seg, n_valid = self._batch(*next(data), data)
             self.ddp.armed = micro == tc.grad_accum - 1
-            loss = self.model(x, y, n_valid=n_valid)
+            loss = self.model(x, y, n_valid=n_valid, segments=seg)
             if ev:
                 ev[1].record()  # (last micro-batch's forward end)
             loss.backward()
@@ -228,7 +258,8 @@ class Trainer:
         try:
             with torch.no_grad():
                 for x, y in self.eval_batches():
-                    tot[0] += self.model(x, y, n_valid=x.numel()).double()
+                    x, y, seg, _ = self._batch(x, y, None)
+                    tot[0] += self.model(x, y, segments=seg).double()
                     tot[1] += 1
         finally:
             self.model.train(was)

@@ -35,8 +35,9 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--window", type=int, default=0)
+    ap.add_argument("--doc-len", type=int, default=0, help="packed documents of this many tokens (0: one per row)")
     a = ap.parse_args()
-    from finetune_controller_amd.ops.attention import _FlashPacked, _sdpa_packed
+    from finetune_controller_amd.ops.attention import _FlashPacked, _sdpa_packed, segments_from_eos
 
     B, S, H, KV, D = a.B, a.S, a.H, a.KV, a.D
     dev = "cuda"
@@ -45,14 +46,19 @@ def main():
     do = torch.randn(B * S, H * D, device=dev, dtype=torch.bfloat16)
     scale = 1 / math.sqrt(D)
     flops_fwd = 4 * B * H * S * S * D / 2  # causal
+    seg = None
+    if a.doc_len:
+        ids = torch.zeros(B, S, dtype=torch.long, device=dev)
+        ids[:, a.doc_len - 1::a.doc_len] = 2
+        seg = segments_from_eos(ids, 2)
     x1 = qkv.clone().requires_grad_(True)
     x2 = qkv.clone().requires_grad_(True)
 
     def ours_fwd():
-        return _FlashPacked.apply(x1, B, S, H, KV, D, True, a.window, scale)
+        return _FlashPacked.apply(x1, B, S, H, KV, D, True, a.window, scale, 0, 0, seg)
 
     def sdpa_fwd():
-        return _sdpa_packed(x2, B, S, H, KV, D, True, a.window, scale)
+        return _sdpa_packed(x2, B, S, H, KV, D, True, a.window, scale, seg)
 
     def ours_fb():
         ours_fwd().backward(do)
@@ -68,11 +74,13 @@ def main():
         pass
     for _ in range(a.rounds):
         with torch.no_grad():
-            res["ours_fwd"].append(timeit(lambda: _FlashPacked.apply(qkv, B, S, H, KV, D, True, a.window, scale), a.iters))
-            res["sdpa_fwd"].append(timeit(lambda: _sdpa_packed(qkv, B, S, H, KV, D, True, a.window, scale), a.iters))
+            res["ours_fwd"].append(timeit(lambda: _FlashPacked.apply(qkv, B, S, H, KV, D, True, a.window, scale, 0, 0,
+                                                                     seg), a.iters))
+            res["sdpa_fwd"].append(timeit(lambda: _sdpa_packed(qkv, B, S, H, KV, D, True, a.window, scale, seg),
+                                          a.iters))
         res["ours_fwdbwd"].append(timeit(ours_fb, a.iters))
         res["sdpa_fwdbwd"].append(timeit(sdpa_fb, a.iters))
-    out = {"shape": dict(B=B, S=S, H=H, KV=KV, D=D, causal=True, window=a.window)}
+    out = {"shape": dict(B=B, S=S, H=H, KV=KV, D=D, causal=True, window=a.window, doc_len=a.doc_len)}
     for k, v in res.items():
         ms = min(v)
         fl = flops_fwd * (1 if "bwd" not in k else 3.5)
