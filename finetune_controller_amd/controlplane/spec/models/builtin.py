@@ -121,6 +121,7 @@ class LMTrainingArguments(TrainingArguments):
     eval_batches: int = Field(default=4, ge=1, description="Micro-batches per GPU per evaluation")
     eval_holdout: float = Field(default=0.01, gt=0, description="Held-out share of the dataset (>= 1: windows)")
     pack_documents: bool = Field(default=False, description="Packed documents attend only within themselves")
+    completion_only: bool = Field(default=False, description="prompt/completion data: loss on completions only")
 
 
 class LoRAArguments(LMTrainingArguments):

@@ -53,6 +53,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--profile-steps", type=int, default=0, help="torch.profiler chrome trace of N steps")
     ap.add_argument("--pack-documents", action="store_true",
                     help="EOS-separated documents in a window attend only within themselves (positions restart)")
+    ap.add_argument("--completion-only", action="store_true",
+                    help="prompt/completion records: no loss on prompt tokens")
     ap.add_argument("--eos-id", type=int, default=-1, help="document separator (-1: the dataset tokenizer's EOS)")
     ap.add_argument("--eval-every", type=int, default=0, help="held-out loss every N steps (0: off)")
     ap.add_argument("--eval-batches", type=int, default=4, help="micro-batches per rank per evaluation")
@@ -73,7 +75,8 @@ def config_from_args(a) -> TrainConfig:
                        comm_engine=a.comm_engine, zero_stage=a.zero_stage, checkpoint_layers=a.checkpoint_layers, init_from=a.init_from,
                        dtype=a.dtype, device=a.device, timers=a.timers, profile_steps=a.profile_steps,
                        eval_every=a.eval_every, eval_batches=a.eval_batches, eval_holdout=a.eval_holdout,
-                       pack_documents=a.pack_documents, eos_id=a.eos_id)
+                       pack_documents=a.pack_documents, eos_id=a.eos_id,
+                       completion_only=a.completion_only)
 
 
 def main(argv=None) -> int:

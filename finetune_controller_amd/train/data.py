@@ -34,12 +34,13 @@ class SyntheticTokens:
         self.gen = torch.Generator(device="cpu").manual_seed(seed)
         # a small pool of pre-generated batches on device: no host->device copy in the timed loop
         pool = [torch.randint(0, vocab, (batch, seq_len + 1), generator=self.gen) for _ in range(4)]
-        self.last_eos = None
-        if doc_len:  # packed documents of doc_len tokens: EOS at the end of each, none elsewhere
+        self.last_n_valid, self.labels = None, None
+        if doc_len:  # packed documents of doc_len tokens: EOS at the end of each (its label ignored)
             for t in pool:
                 t[t == eos_id] = (eos_id + 1) % vocab
                 t[:, doc_len - 1::doc_len] = eos_id
-            self.last_eos = int((pool[0][:, :-1] == eos_id).sum())
+            self.labels = [t[:, 1:].masked_fill(t[:, :-1] == eos_id, -100).to(device) for t in pool]
+            self.last_n_valid = int((self.labels[0] != -100).sum().item())
         self.pool = [t.to(device) for t in pool]
         self.i = 0
 
@@ -48,8 +49,9 @@ class SyntheticTokens:
 
     def __next__(self):
         t = self.pool[self.i % len(self.pool)]
+        y = t[:, 1:] if self.labels is None else self.labels[self.i % len(self.pool)]
         self.i += 1
-        return t[:, :-1], t[:, 1:]
+        return t[:, :-1], y
 
     def state(self):
         return {"i": self.i}
@@ -70,7 +72,8 @@ def _find_data_file(path: str) -> str | None:
     return cands[0] if cands else None
 
 
-def _texts(path: str):
+def _records(path: str):
+    """(prompt, completion) per record: ``prompt`` is "" for plain text (loss on every token)."""
     ext = Path(path).suffix.lower()
     if ext in (".jsonl", ".json"):
         with open(path, encoding="utf-8") as f:
@@ -79,11 +82,11 @@ def _texts(path: str):
             rows = json.load(f) if (ext == ".json" and head == "[") else (json.loads(l) for l in f if l.strip())
             for r in rows:
                 if isinstance(r, str):
-                    yield r
+                    yield "", r
                 elif "text" in r:
-                    yield str(r["text"])
+                    yield "", str(r["text"])
                 else:
-                    yield str(r.get("prompt", "")) + str(r.get("completion", r.get("response", "")))
+                    yield str(r.get("prompt", "")), str(r.get("completion", r.get("response", "")))
     elif ext == ".csv":
         with open(path, encoding="utf-8", newline="") as f:
             rd = csv.reader(f)
@@ -96,12 +99,12 @@ def _texts(path: str):
                         break
             for row in rd:
                 if row:
-                    yield row[col]
+                    yield "", row[col]
     else:
         with open(path, encoding="utf-8", errors="replace") as f:
             for line in f:
                 if line.strip():
-                    yield line.rstrip("\n")
+                    yield "", line.rstrip("\n")
 
 
 class Tokenizer:
@@ -134,24 +137,36 @@ class Tokenizer:
 
 def load_token_array(path: str, vocab: int) -> np.ndarray:
     """Return a 1-D int array of token ids for a dataset path (memory-mapped when binary)."""
+    return load_tokens_and_mask(path, vocab)[0]
+
+
+def load_tokens_and_mask(path: str, vocab: int, completion_only: bool = False):
+    """(ids, loss_mask): ``loss_mask`` (uint8, same length, or None) is 0 on prompt tokens of
+    prompt/completion records when ``completion_only`` -- their next-token labels are not trained on."""
     f = _find_data_file(path)
     if f is None:
         raise FileNotFoundError(f"no dataset file under {path!r}")
     ext = Path(f).suffix.lower()
     if ext in (".bin", ".tokens"):
         dt = np.uint32 if f.endswith(".u32.bin") or vocab > 65536 else np.uint16
-        return np.memmap(f, dtype=dt, mode="r")
+        return np.memmap(f, dtype=dt, mode="r"), None
     if ext == ".npy":
-        return np.load(f, mmap_mode="r", allow_pickle=False)
+        return np.load(f, mmap_mode="r", allow_pickle=False), None
     tok = Tokenizer(path, vocab)
     ids: list[int] = []
-    for t in _texts(f):
-        ids.extend(tok.encode(t))
-        ids.append(tok.eos)
+    mask: list[int] = []
+    for prompt, completion in _records(f):
+        p = tok.encode(prompt) if prompt else []
+        c = tok.encode(completion) + [tok.eos]
+        ids.extend(p)
+        ids.extend(c)
+        mask.extend([0] * len(p))
+        mask.extend([1] * len(c))
     arr = np.asarray(ids, dtype=np.int64)
     if arr.size and int(arr.max()) >= vocab:
         arr = arr % vocab
-    return arr
+    m = np.asarray(mask, dtype=np.uint8) if completion_only else None
+    return arr, (m if m is not None and not m.all() else None)
 
 
 class PackedTokenDataset:
@@ -162,8 +177,8 @@ class PackedTokenDataset:
     """
 
     def __init__(self, path: str, vocab: int, batch: int, seq_len: int, device, rank: int = 0, world: int = 1,
-                 seed: int = 0, holdout: float = 0, eos_id: int | None = None):
-        self.tokens = load_token_array(path, vocab)
+                 seed: int = 0, holdout: float = 0, eos_id: int | None = None, completion_only: bool = False):
+        self.tokens, self.loss_mask = load_tokens_and_mask(path, vocab, completion_only)
         self.vocab, self.batch, self.seq_len, self.device = vocab, batch, seq_len, device
         self.rank, self.world, self.seed = rank, world, seed
         n_windows = (len(self.tokens) - 1) // seq_len
@@ -177,9 +192,10 @@ class PackedTokenDataset:
             want = max(int(holdout) if holdout >= 1 else int(round(n_windows * holdout)), batch * world)
         self.holdout = max(0, min(want, n_windows - 1))
         self.n_use = n_windows - self.holdout
-        # packed documents: EOS tokens among the inputs of the last batch (their next-token labels are
-        # masked), counted on the host so the loss normaliser needs no device sync
-        self.eos_id, self.last_eos = eos_id, 0
+        # label masking (host side, so the loss normaliser ``last_n_valid`` needs no device sync):
+        # packed documents ignore the label of every EOS input (it would predict across a document
+        # boundary), completion-only training the labels of prompt tokens
+        self.eos_id, self.last_n_valid = eos_id, None
         self.steps_per_epoch = max(1, self.n_use // (batch * world))
         self.epoch = 0
         self.pos = 0
@@ -187,7 +203,8 @@ class PackedTokenDataset:
         try:
             from ..utils.native import NativeTokenLoader
 
-            if isinstance(self.tokens, np.memmap) and os.environ.get("FTC_NATIVE_LOADER", "1") != "0":
+            if (isinstance(self.tokens, np.memmap) and self.loss_mask is None
+                    and os.environ.get("FTC_NATIVE_LOADER", "1") != "0"):
                 self._native = NativeTokenLoader(self.tokens.filename, self.tokens.dtype.itemsize, seq_len, batch,
                                                  rank, world, seed, n_use=self.n_use)
         except ImportError:  # _rt.so not built: numpy path
@@ -213,12 +230,15 @@ class PackedTokenDataset:
                 self._perm()
             base = (self.pos * self.world + self.rank) * self.batch
             idx = [self.order[(base + i) % self.n_use] for i in range(self.batch)]
-            S = self.seq_len
-            arr = np.stack([np.asarray(self.tokens[j * S: j * S + S + 1], dtype=np.int64) for j in idx])
-            arr = torch.from_numpy(arr)
+            arr = self._windows(idx)
             self.pos += 1
-        if self.eos_id is not None:
-            self.last_eos = int((arr[:, :-1] == self.eos_id).sum())
+        labels = self._labels(arr, idx if self._native is None else None)
+        if labels is not None:
+            cpu = torch.device(self.device).type == "cpu"
+            x = arr[:, :-1].clone() if cpu else arr[:, :-1].to(self.device, non_blocking=True)
+            if self._native is not None and not cpu:
+                self._native.copied()
+            return x, labels.to(self.device, non_blocking=True)
         if self._native is not None:
             if torch.device(self.device).type == "cpu":
                 t = arr.clone()  # the ring buffer is refilled after the next call
@@ -228,6 +248,24 @@ class PackedTokenDataset:
         else:
             t = arr.to(self.device, non_blocking=True)
         return t[:, :-1], t[:, 1:]
+
+    def _windows(self, idx) -> torch.Tensor:
+        S = self.seq_len
+        return torch.from_numpy(np.stack([np.asarray(self.tokens[j * S: j * S + S + 1], dtype=np.int64) for j in idx]))
+
+    def _labels(self, arr: torch.Tensor, idx) -> torch.Tensor | None:
+        """Masked labels of a [batch, S+1] host window batch (None: no masking configured)."""
+        if self.eos_id is None and self.loss_mask is None:
+            return None
+        y = arr[:, 1:].clone()
+        if self.loss_mask is not None:
+            S = self.seq_len
+            m = torch.from_numpy(np.stack([self.loss_mask[j * S + 1: j * S + S + 1] for j in idx]))
+            y[m == 0] = -100
+        if self.eos_id is not None:
+            y[arr[:, :-1] == self.eos_id] = -100
+        self.last_n_valid = int((y != -100).sum())
+        return y
 
     def state(self):
         return {"epoch": self.epoch, "pos": self.pos}
@@ -255,6 +293,7 @@ class EvalWindows:
         for i in range(self.n_batches):
             base = (i * ds.world + ds.rank) * ds.batch
             idx = [ds.n_use + (base + j) % ds.holdout for j in range(ds.batch)]
-            arr = np.stack([np.asarray(ds.tokens[w * S: w * S + S + 1], dtype=np.int64) for w in idx])
-            t = torch.from_numpy(arr).to(ds.device, non_blocking=True)
-            yield t[:, :-1], t[:, 1:]
+            arr = ds._windows(idx)
+            y = ds._labels(arr, idx)
+            t = arr.to(ds.device, non_blocking=True)
+            yield t[:, :-1], (t[:, 1:] if y is None else y.to(ds.device, non_blocking=True))

@@ -80,6 +80,7 @@ class TrainConfig:
     eval_holdout: float = 0.01  # held-out share of the dataset's windows (>= 1: a window count)
     pack_documents: bool = False  # EOS-separated documents in a window attend only within themselves
     eos_id: int = -1  # -1: the dataset tokenizer's EOS (tokenizer.json, or the byte-level fallback's 2)
+    completion_only: bool = False  # prompt/completion records: loss on the completion tokens only
     synthetic_doc_len: int = 0  # synthetic data: EOS every that many tokens (packed-document benchmarks)
 
     def lora_config(self) -> LoRAConfig | None:
@@ -172,7 +173,7 @@ class Trainer:
                 self._data = PackedTokenDataset(tc.dataset_path, self.cfg.vocab_size, tc.batch_size, tc.seq_len,
                                                 self.device, self.info.rank, self.info.world_size, tc.seed,
                                                 holdout=tc.eval_holdout if tc.eval_every > 0 else 0,
-                                                eos_id=self.eos_id())
+                                                eos_id=self.eos_id(), completion_only=tc.completion_only)
                 self.steps_per_epoch = max(1, self._data.steps_per_epoch // tc.grad_accum)
         return self._data
 
@@ -188,18 +189,16 @@ class Trainer:
         return self._eos
 
     def _batch(self, x, y, data):
-        """(x, labels, segments, n_valid) of one micro-batch: with packed documents the labels that would
-        predict across a document boundary (inputs equal to EOS) are ignored and attention / positions
-        follow the documents."""
-        tc = self.tc
-        n_valid = x.numel()
+        """(x, labels, segments, n_valid) of one micro-batch.  The data source masks the labels (packed
+        documents: EOS inputs; completion-only: prompt tokens) and reports their count host-side
+        (``last_n_valid``), so the loss normaliser needs no device sync; packed documents also get
+        their segment bounds (attention stays inside a document, positions restart)."""
         eos = self.eos_id()
-        if eos is None:
-            return x, y, None, n_valid
-        seg = ops.segments_from_eos(x, eos)
-        y = y.masked_fill(x == eos, -100)
-        n_eos = getattr(data, "last_eos", None)
-        return x, y, seg, (n_valid - n_eos) if n_eos is not None else None
+        seg = ops.segments_from_eos(x, eos) if eos is not None else None
+        n_valid = getattr(data, "last_n_valid", None) if data is not None else None
+        if n_valid is None and data is not None and eos is None and not self.tc.completion_only:
+            n_valid = x.numel()  # nothing masked
+        return x, y, seg, n_valid
 
     def total_steps(self) -> int:
         self.data()

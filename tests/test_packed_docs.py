@@ -86,9 +86,61 @@ def test_trainer_pack_documents_masks_boundary_labels(tmp_path):
     x, y = next(data)
     x2, y2, seg, n_valid = tr._batch(x, y, data)
     n_eos = int((x == 2).sum())
-    assert n_eos > 0 and n_valid == x.numel() - n_eos == x.numel() - data.last_eos
-    assert bool((y2[x == 2] == -100).all()) and bool((y2[x != 2] == y[x != 2]).all())
+    assert n_eos > 0 and n_valid == x.numel() - n_eos == data.last_n_valid
+    assert bool((y2[x == 2] == -100).all()) and bool((y2[x != 2] != -100).all())
+    keep = x[:, :-1] != 2
+    assert bool((y2[:, :-1][keep] == x[:, 1:][keep]).all())  # kept labels are the next inputs
     assert seg.positions.max() < 64
     last = tr.run()
     tr.close()
     assert math.isfinite(last["loss"])
+
+
+def test_completion_only_masks_prompt_labels(tmp_path):
+    import json
+
+    from finetune_controller_amd.train.data import PackedTokenDataset, load_tokens_and_mask
+
+    rows = [{"prompt": "Q: what is %d+%d? A:" % (i, i), "completion": " %d" % (2 * i)} for i in range(60)]
+    (tmp_path / "d.jsonl").write_text("\n".join(json.dumps(r) for r in rows))
+    ids, mask = load_tokens_and_mask(str(tmp_path / "d.jsonl"), 512, completion_only=True)
+    assert mask is not None and len(mask) == len(ids) and 0 < mask.sum() < len(mask)
+    # byte-level fallback: the first record's prompt bytes are masked, its completion + EOS are not
+    n_p = len("Q: what is 0+0? A:".encode())
+    assert mask[:n_p].sum() == 0 and mask[n_p:n_p + 3].tolist() == [1, 1, 1] and ids[n_p + 2] == 2
+    assert load_tokens_and_mask(str(tmp_path / "d.jsonl"), 512)[1] is None
+    ds = PackedTokenDataset(str(tmp_path / "d.jsonl"), 512, batch=2, seq_len=32, device="cpu", completion_only=True)
+    x, y = next(ds)
+    assert ds._native is None and ds.last_n_valid == int((y != -100).sum()) < y.numel()
+    # a label is kept iff the token it predicts is a completion token
+    S = 32
+    j = int(ds.order[0])
+    keep = torch.from_numpy(mask[j * S + 1: j * S + S + 1].astype(bool))
+    assert torch.equal(y[0] != -100, keep)
+    tr = Trainer(TrainConfig(model="llama-tiny", method="lora", batch_size=2, seq_len=32,
+                             dataset_path=str(tmp_path / "d.jsonl"), max_steps=2, completion_only=True,
+                             checkpoint_path=str(tmp_path / "out"), resume=False, device="cpu", save_model=False,
+                             warmup_steps=0))
+    assert math.isfinite(tr.run()["loss"])
+    tr.close()
+
+
+def test_native_loader_label_masking_matches_numpy(tmp_path, monkeypatch):
+    import numpy as np
+
+    pytest.importorskip("finetune_controller_amd._rt")
+    from finetune_controller_amd.train.data import PackedTokenDataset
+
+    toks = (np.arange(6000) * 7919 % 300).astype(np.uint16)
+    toks[::37] = 2
+    toks.tofile(tmp_path / "t.bin")
+    out = {}
+    for native in ("1", "0"):
+        monkeypatch.setenv("FTC_NATIVE_LOADER", native)
+        ds = PackedTokenDataset(str(tmp_path / "t.bin"), 512, batch=3, seq_len=64, device="cpu", seed=5, eos_id=2)
+        assert (ds._native is not None) == (native == "1")
+        out[native] = [(*next(ds), ds.last_n_valid) for _ in range(5)]
+        if ds._native is not None:
+            ds._native.close()
+    for (xa, ya, na), (xb, yb, nb) in zip(out["1"], out["0"]):
+        assert torch.equal(xa, xb) and torch.equal(ya, yb) and na == nb and bool((ya[xa == 2] == -100).all())
