@@ -244,18 +244,16 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
   int qend = S;
   if (a.window > 0) qend = min(S, kv0 + BKV - 1 + a.window);
   // packed documents: queries past the end of the block's last key's document see none of its keys;
-  // per half, the lane's key bound (dend) and the half's smallest one (dmin: mask needed beyond it)
-  int dend[HW], dmin[HW];
+  // per half, the smallest doc_end of its keys (dmin, wave-uniform: per-element masks needed beyond
+  // it).  The lane's own doc_end is loaded only inside the masked branch (no loop-long register).
+  int dmin[HW];
 #pragma unroll
-  for (int j = 0; j < HW; ++j) dend[j] = dmin[j] = 0x3fffffff;
-  if (a.doc_end) {
-    const int* de = a.doc_end + (long long)b * S;
-    qend = min(qend, de[kv0 + BKV - 1]);
+  for (int j = 0; j < HW; ++j) dmin[j] = 0x3fffffff;
+  const int* de_row = a.doc_end ? a.doc_end + (long long)b * S : nullptr;
+  if (de_row) {
+    qend = min(qend, de_row[kv0 + BKV - 1]);
 #pragma unroll
-    for (int j = 0; j < HW; ++j) {
-      dend[j] = de[wkey0 + 32 * j + lr];
-      dmin[j] = de[wkey0 + 32 * j];
-    }
+    for (int j = 0; j < HW; ++j) dmin[j] = de_row[wkey0 + 32 * j];
   }
   qbeg = (qbeg / BQ2) * BQ2;
   const int nqt = (qend - qbeg + BQ2 - 1) / BQ2;
@@ -390,7 +388,8 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
         if (need_mask) {  // wave-uniform; query q = qt + (i&3) + 8(i>>2) + 4hh valid iff key <= q < key + window
           const int base = qt + 4 * hh;
           const int lo = (a.causal ? key : -0x3fffffff) - base;
-          const int hi = min(a.window > 0 ? key + a.window - 1 : 0x3fffffff, dend[j] - 1) - base;
+          const int dend = de_row ? de_row[key] : 0x40000000;
+          const int hi = min(a.window > 0 ? key + a.window - 1 : 0x3fffffff, dend - 1) - base;
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const int off = (i & 3) + 8 * (i >> 2);
