@@ -56,6 +56,7 @@ def main(argv=None) -> int:
                     help="rows per lm_head + cross-entropy chunk (the only vocab-sized buffer)")
     ap.add_argument("--kernels", default=None, choices=["hip", "torch"],
                     help="torch = stock PyTorch-ROCm ops (the 'before' row)")
+    ap.add_argument("--graph", action="store_true", help="whole training step captured in a hipGraph (1 GPU)")
     ap.add_argument("--doc-len", type=int, default=0,
                     help="packed documents of this many tokens (document-masked attention; 0: one per row)")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (not timed)")
@@ -77,7 +78,7 @@ def main(argv=None) -> int:
                      batch_size=a.batch_size, seq_len=a.seq_len, synthetic=True, max_steps=a.warmup + a.steps,
                      warmup_steps=0, schedule="constant", lr=1e-4, bucket_mb=a.bucket_mb, comm_engine=a.comm_engine, zero_stage=a.zero_stage,
                      checkpoint_layers=a.checkpoint_layers, ce_chunk_rows=a.ce_chunk_rows, save_model=False, resume=False, device="cuda",
-                     pack_documents=a.doc_len > 0, eos_id=2, synthetic_doc_len=a.doc_len)
+                     pack_documents=a.doc_len > 0, eos_id=2, synthetic_doc_len=a.doc_len, graph=a.graph)
     tr = Trainer(tc)
     info = tr.info
     dev = tr.device
@@ -148,6 +149,7 @@ def main(argv=None) -> int:
                 "comm_engine": a.comm_engine,
                 "zero_stage": a.zero_stage,
                 **({"packed_doc_len": a.doc_len} if a.doc_len else {}),
+                **({"hipgraph": True} if tr.graph_ok() else {}),
             },
             "loss": round(loss, 4),
             "model_tflops_per_gpu": round(value * flops_tok / n / 1e12, 1),

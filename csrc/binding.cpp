@@ -37,7 +37,7 @@ int ftc_ce_fwd_bwd(void* logits, const long long* labels, float* loss, float* ls
                    float gscale, long long ignore_index, hipStream_t stream);
 int ftc_adamw(void* param_bf16, float* master, float* m, float* v, const void* grad, int grad_is_fp32, long long n,
               float lr, float b1, float b2, float eps, float wd, float bc1, float bc2, const float* gscale,
-              hipStream_t stream);
+              const float* hpdev, hipStream_t stream);
 int ftc_sumsq_partials();
 int ftc_sumsq(const void* x, int is_fp32, long long n, float* partial, float* out, float* coef, float max_norm,
               float scale, hipStream_t stream);
@@ -363,7 +363,7 @@ at::Tensor ce_fwd_bwd_(at::Tensor& logits, const at::Tensor& labels, double gsca
 // ---------------- AdamW / grad norm ----------------
 void adamw_(const c10::optional<at::Tensor>& param, at::Tensor& master, at::Tensor& m, at::Tensor& v,
             const at::Tensor& grad, double lr, double b1, double b2, double eps, double wd, int64_t step,
-            const c10::optional<at::Tensor>& gscale) {
+            const c10::optional<at::Tensor>& gscale, const c10::optional<at::Tensor>& hpdev) {
   need(master, at::kFloat, "master");
   need(m, at::kFloat, "m");
   need(v, at::kFloat, "v");
@@ -383,11 +383,17 @@ void adamw_(const c10::optional<at::Tensor>& param, at::Tensor& master, at::Tens
     need(*gscale, at::kFloat, "gscale");
     gs = gscale->data_ptr<float>();
   }
+  const float* hp = nullptr;
+  if (hpdev.has_value() && hpdev->defined()) {
+    need(*hpdev, at::kFloat, "hp");
+    TORCH_CHECK(hpdev->is_contiguous() && hpdev->numel() == 3, "adamw: hp = [lr, 1 - b1^t, 1 - b2^t]");
+    hp = hpdev->data_ptr<float>();
+  }
   const double bc1 = 1.0 - std::pow(b1, (double)step);
   const double bc2 = 1.0 - std::pow(b2, (double)step);
   check(ftc_adamw(pp, master.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), grad.data_ptr(),
                   grad.scalar_type() == at::kFloat, n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd,
-                  (float)bc1, (float)bc2, gs, cur_stream()),
+                  (float)bc1, (float)bc2, gs, hp, cur_stream()),
         "adamw");
 }
 
@@ -610,7 +616,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("tail_gemm_", &tail_gemm_);
   m.def("transpose2d", &transpose2d, py::arg("x"), py::arg("out") = py::none());
   m.def("ce_fwd_bwd_", &ce_fwd_bwd_);
-  m.def("adamw_", &adamw_);
+  m.def("adamw_", &adamw_, py::arg("param"), py::arg("master"), py::arg("m"), py::arg("v"), py::arg("grad"),
+        py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("step"),
+        py::arg("gscale") = py::none(), py::arg("hp") = py::none());
   m.def("grad_sumsq", &grad_sumsq);
   m.def("flash_fwd", &flash_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("B"), py::arg("S"), py::arg("H"),
         py::arg("KV"), py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("pad") = 0,

@@ -48,8 +48,14 @@ template <typename G>
 __global__ __launch_bounds__(256) void adamw_kernel(uint16_t* __restrict__ param, float* __restrict__ master,
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     const G* __restrict__ grad, long long n, AdamHP hp,
-                                                    const float* __restrict__ gscale) {
+                                                    const float* __restrict__ gscale,
+                                                    const float* __restrict__ hpdev) {
   const float sc = gscale ? gscale[0] : 1.0f;
+  if (hpdev) {  // [lr, 1 - b1^t, 1 - b2^t] from device memory: a captured step replays with new values
+    hp.lr = hpdev[0];
+    hp.bc1 = hpdev[1];
+    hp.bc2 = hpdev[2];
+  }
   const long long n4 = n >> 2;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
     float g[4];
@@ -83,15 +89,15 @@ __global__ __launch_bounds__(256) void adamw_kernel(uint16_t* __restrict__ param
 
 extern "C" int ftc_adamw(void* param_bf16, float* master, float* m, float* v, const void* grad, int grad_is_fp32,
                          long long n, float lr, float b1, float b2, float eps, float wd, float bc1, float bc2,
-                         const float* gscale, hipStream_t stream) {
+                         const float* gscale, const float* hpdev, hipStream_t stream) {
   AdamHP hp{lr, b1, b2, eps, wd, bc1, bc2};
   const int grid = ftc::stream_grid((n + 3) / 4, 256);
   if (grad_is_fp32)
     hipLaunchKernelGGL((adamw_kernel<float>), dim3(grid), dim3(256), 0, stream, (uint16_t*)param_bf16, master, m, v,
-                       (const float*)grad, n, hp, gscale);
+                       (const float*)grad, n, hp, gscale, hpdev);
   else
     hipLaunchKernelGGL((adamw_kernel<uint16_t>), dim3(grid), dim3(256), 0, stream, (uint16_t*)param_bf16, master, m,
-                       v, (const uint16_t*)grad, n, hp, gscale);
+                       v, (const uint16_t*)grad, n, hp, gscale, hpdev);
   return (int)hipGetLastError();
 }
 

@@ -51,6 +51,7 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--checkpoint_path", "--checkpoint-path", dest="checkpoint_path", default="/data/artifacts")
     ap.add_argument("--timers", action="store_true", help="per-phase device timers (fwd/bwd/comm/optim) in metrics.csv")
     ap.add_argument("--profile-steps", type=int, default=0, help="torch.profiler chrome trace of N steps")
+    ap.add_argument("--graph", action="store_true", help="capture the training step in a hipGraph (1 GPU)")
     ap.add_argument("--pack-documents", action="store_true",
                     help="EOS-separated documents in a window attend only within themselves (positions restart)")
     ap.add_argument("--completion-only", action="store_true",
@@ -76,7 +77,7 @@ def config_from_args(a) -> TrainConfig:
                        dtype=a.dtype, device=a.device, timers=a.timers, profile_steps=a.profile_steps,
                        eval_every=a.eval_every, eval_batches=a.eval_batches, eval_holdout=a.eval_holdout,
                        pack_documents=a.pack_documents, eos_id=a.eos_id,
-                       completion_only=a.completion_only)
+                       completion_only=a.completion_only, graph=a.graph)
 
 
 def main(argv=None) -> int:

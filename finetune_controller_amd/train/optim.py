@@ -86,6 +86,19 @@ class FlatAdamW:
         self.grad_scale = grad_scale  # e.g. 1/world_size when grads are summed by all-reduce
         self.step_count = 0
         self.last_grad_norm: torch.Tensor | None = None
+        self._hp_table: torch.Tensor | None = None  # device schedule (graph-captured steps)
+        self._hp_idx: torch.Tensor | None = None
+
+    def use_device_schedule(self, lrs: list[float]):
+        """Read lr and the bias corrections from a device table, one row per coming step, indexed by a
+        device counter the step itself advances: a step captured in a hipGraph then replays with the
+        schedule instead of the capture-time constants.  Row i: [lrs[i], 1 - b1^t, 1 - b2^t] with
+        t = step_count + 1 + i."""
+        b1, b2 = self.betas
+        rows = [[lr, 1.0 - b1 ** (self.step_count + 1 + i), 1.0 - b2 ** (self.step_count + 1 + i)]
+                for i, lr in enumerate(lrs)]
+        self._hp_table = torch.tensor(rows, dtype=torch.float32, device=self.device)
+        self._hp_idx = torch.zeros(1, dtype=torch.long, device=self.device)
 
     def _init_state(self):
         self.master = self.param_flat.float() if self.dtype != torch.float32 else self.param_flat
@@ -114,8 +127,12 @@ class FlatAdamW:
             stats = ext().grad_sumsq(self.grad_flat, self.max_grad_norm, self.grad_scale)
             self.last_grad_norm = stats[0:1]
             param = self.param_flat if self.dtype == torch.bfloat16 else None
+            hp = None
+            if self._hp_table is not None:
+                hp = self._hp_table.index_select(0, self._hp_idx.clamp(max=self._hp_table.shape[0] - 1)).reshape(3)
+                self._hp_idx += 1
             ext().adamw_(param, self.master, self.exp_avg, self.exp_avg_sq, self.grad_flat, lr, b1, b2, self.eps,
-                         self.wd, self.step_count, stats[1:2])
+                         self.wd, self.step_count, stats[1:2], hp)
             return
         g = self.grad_flat.float() * self.grad_scale
         norm = g.norm()

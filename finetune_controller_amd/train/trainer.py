@@ -75,6 +75,7 @@ class TrainConfig:
     save_model: bool = True
     timers: bool = False  # per-phase device timers (fwd/bwd/comm/optim) -> metrics.csv
     profile_steps: int = 0  # >0: torch.profiler chrome trace of that many steps -> trace_rank<r>.json
+    graph: bool = False  # capture the whole training step in a hipGraph after 2 eager steps (1 GPU)
     eval_every: int = 0  # >0: held-out loss every that many optimizer steps (and after the last one)
     eval_batches: int = 4  # micro-batches per rank per evaluation
     eval_holdout: float = 0.01  # held-out share of the dataset's windows (>= 1: a window count)
@@ -205,8 +206,58 @@ class Trainer:
         return self.tc.max_steps or self.tc.epochs * self.steps_per_epoch
 
     # ------------------------------------------------------------------ one step
+    def graph_ok(self) -> bool:
+        """Whole-step capture needs a step whose every launch argument is fixed: one rank (no
+        collectives in the graph), the flat HIP AdamW (device-side schedule), a constant loss
+        normaliser (no per-batch label masking) and no host-side timers."""
+        tc = self.tc
+        return (tc.graph and self.device.type == "cuda" and self.info.world_size == 1 and not tc.timers
+                and type(self.opt) is FlatAdamW and ops.use_hip(self.opt.grad_flat) and not tc.pack_documents
+                and not tc.completion_only)
+
     def train_step(self, lr: float) -> torch.Tensor:
         """fwd + bwd (+accum) + overlapped all-reduce + optimizer. Returns the loss (device tensor)."""
+        if self.graph_ok():
+            return self._graph_step(lr)
+        return self._eager_step(lr)
+
+    def _graph_step(self, lr: float) -> torch.Tensor:
+        """Step through a captured hipGraph: launch-bound configurations (small models, short
+        sequences) lose the host's per-kernel launch cost.  Two eager steps warm every cache (aug
+        buffers, Wᵀ copies, hipBLASLt heuristics), the third is captured -- inputs copied into static
+        buffers, lr / bias corrections read from the optimizer's device table -- and every step from
+        then on is one graph launch.  Host-side bookkeeping the replay skips (optimizer step count,
+        parameter generation for the eager caches) is advanced here."""
+        from ..ops.linear import bump_param_generation
+
+        tc = self.tc
+        data = self.data()
+        self._n_graph_calls = getattr(self, "_n_graph_calls", 0) + 1
+        if self._n_graph_calls <= 2:
+            return self._eager_step(lr)
+        batches = [next(data) for _ in range(tc.grad_accum)]
+        if getattr(self, "_graph", None) is None:
+            self._gin = [(x.clone(), y.clone()) for x, y in batches]
+            total = self.total_steps()
+            lrs = [lr_at(s, tc.lr, tc.warmup_steps, total, tc.schedule) for s in range(self.step, max(total, self.step + 1))]
+            self.opt.use_device_schedule(lrs + [lrs[-1]] * 1024)
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._gout = self._eager_step(lr, inputs=self._gin)
+            self._graph = g
+            # the capture ran nothing: host state moved as if the step had run, the replay below runs it
+            self.opt.step_count -= 1
+        else:
+            for (sx, sy), (x, y) in zip(self._gin, batches):
+                sx.copy_(x, non_blocking=True)
+                sy.copy_(y, non_blocking=True)
+        self._graph.replay()
+        self.opt.step_count += 1
+        bump_param_generation()  # eager code after this step must re-read the updated adapters
+        return self._gout.clone()
+
+    def _eager_step(self, lr: float, inputs=None) -> torch.Tensor:
         tc = self.tc
         data = self.data()
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if (tc.timers and self.device.type == "cuda") \
@@ -216,7 +267,7 @@ class Trainer:
         self.opt.zero_grad()
         total = None
         for micro in range(tc.grad_accum):
-            x, y, seg, n_valid = self._batch(*next(data), data)
+            x, y, seg, n_valid = self._batch(*(next(data) if inputs is None else inputs[micro]), data)
             self.ddp.armed = micro == tc.grad_accum - 1
             loss = self.model(x, y, n_valid=n_valid, segments=seg)
             if ev:
