@@ -128,6 +128,7 @@ class LoRAArguments(LMTrainingArguments):
     lora_r: int = Field(default=16, ge=1, le=256, description="LoRA rank")
     lora_alpha: float = Field(default=32.0, gt=0, description="LoRA alpha (scale = alpha / r)")
     lora_dropout: float = Field(default=0.0, ge=0.0, lt=1.0, description="Dropout on the adapter input")
+    use_rslora: bool = Field(default=False, description="Rank-stabilised LoRA scale alpha / sqrt(r)")
     lora_targets: str = Field(default="q_proj,k_proj,v_proj,o_proj,gate_proj,up_proj,down_proj",
                               description="Comma-separated target modules")
     lr: float = Field(default=2e-4, gt=0, description="Peak learning rate")

@@ -34,15 +34,17 @@ class LoRAConfig:
     alpha: float = 32.0
     dropout: float = 0.0
     target_modules: list[str] = field(default_factory=lambda: list(ALL_LINEAR))
+    use_rslora: bool = False  # rank-stabilised scaling alpha / sqrt(r) (PEFT ``use_rslora``)
 
     @property
     def scale(self) -> float:
-        return self.alpha / self.r
+        return self.alpha / (self.r ** 0.5 if self.use_rslora else self.r)
 
     def to_peft(self, base_model: str) -> dict:
         return {"peft_type": "LORA", "task_type": "CAUSAL_LM", "r": self.r, "lora_alpha": self.alpha,
                 "lora_dropout": self.dropout, "target_modules": list(self.target_modules), "bias": "none",
-                "base_model_name_or_path": base_model, "fan_in_fan_out": False, "inference_mode": False}
+                "base_model_name_or_path": base_model, "fan_in_fan_out": False, "inference_mode": False,
+                "use_rslora": self.use_rslora}
 
     def to_dict(self):
         return asdict(self)

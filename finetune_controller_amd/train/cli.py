@@ -23,6 +23,7 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--lora-r", type=int, default=16)
     ap.add_argument("--lora-alpha", type=float, default=32.0)
     ap.add_argument("--lora-dropout", type=float, default=0.0)
+    ap.add_argument("--use-rslora", action="store_true", help="LoRA scale alpha / sqrt(r)")
     ap.add_argument("--lora-targets", default="q_proj,k_proj,v_proj,o_proj,gate_proj,up_proj,down_proj")
     ap.add_argument("--batch-size", type=int, default=4)
     ap.add_argument("--seq-len", type=int, default=4096)
@@ -66,7 +67,7 @@ def build_parser() -> argparse.ArgumentParser:
 
 def config_from_args(a) -> TrainConfig:
     return TrainConfig(model=a.model, method=a.method, lora_r=a.lora_r, lora_alpha=a.lora_alpha,
-                       lora_dropout=a.lora_dropout,
+                       lora_dropout=a.lora_dropout, use_rslora=a.use_rslora,
                        lora_targets=[t.strip() for t in a.lora_targets.split(",") if t.strip()],
                        batch_size=a.batch_size, seq_len=a.seq_len, grad_accum=a.grad_accum, epochs=a.epochs,
                        max_steps=a.max_steps, lr=a.lr, warmup_steps=a.warmup_steps, schedule=a.schedule,

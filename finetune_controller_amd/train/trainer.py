@@ -45,6 +45,7 @@ class TrainConfig:
     lora_r: int = 16
     lora_alpha: float = 32.0
     lora_dropout: float = 0.0
+    use_rslora: bool = False  # LoRA scale alpha / sqrt(r) instead of alpha / r
     lora_targets: list[str] = field(default_factory=lambda: ["q_proj", "k_proj", "v_proj", "o_proj", "gate_proj",
                                                               "up_proj", "down_proj"])
     batch_size: int = 4  # micro-batch per GPU
@@ -87,7 +88,7 @@ class TrainConfig:
     def lora_config(self) -> LoRAConfig | None:
         if self.method not in ("lora", "qlora"):
             return None
-        return LoRAConfig(r=self.lora_r, alpha=self.lora_alpha, dropout=self.lora_dropout,
+        return LoRAConfig(r=self.lora_r, alpha=self.lora_alpha, dropout=self.lora_dropout, use_rslora=self.use_rslora,
                           target_modules=list(self.lora_targets))
 
 

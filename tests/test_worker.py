@@ -576,3 +576,17 @@ def test_llama_family_presets(name):
     loss = m(ids, torch.roll(ids, -1, 1))
     loss.backward()
     assert torch.isfinite(loss) and all(p.grad is not None for p in m.parameters() if p.requires_grad)
+
+
+def test_rslora_scale_and_adapter_config(tmp_path):
+    from finetune_controller_amd.models import LoRAConfig
+
+    lc = LoRAConfig(r=16, alpha=32, use_rslora=True)
+    assert lc.scale == pytest.approx(32 / 4.0) and LoRAConfig(r=16, alpha=32).scale == 2.0
+    tr = Trainer(TrainConfig(model="llama-tiny", method="lora", use_rslora=True, lora_r=8, lora_alpha=16,
+                             batch_size=1, seq_len=16, synthetic=True, max_steps=1, checkpoint_path=str(tmp_path),
+                             resume=False, device="cpu"))
+    assert all(p.scale == pytest.approx(16 / 8 ** 0.5) for layer in tr.model.layers for p in layer.lora.values())
+    tr.run()
+    tr.close()
+    assert json.load(open(tmp_path / "adapter_config.json"))["use_rslora"] is True
