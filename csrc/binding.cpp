@@ -16,7 +16,7 @@ int ftc_rmsnorm_bwd(const void* dy, const void* h, const void* w, const float* r
                     float* dw_part, float* dw, int rows, int d, long long dres_rs, long long dx_rs,
                     hipStream_t stream);
 int ftc_rope(void* qkv, const float* cosT, const float* sinT, const int* positions, long long rows, int ld,
-             int n_rot_heads, int head_dim, int seq_len, int inverse, hipStream_t stream);
+             int n_rot_heads, int head_dim, int seq_len, int inverse, int max_pos, hipStream_t stream);
 int ftc_swiglu_fwd(const void* gu, void* a, long long rows, int F, long long a_rs, hipStream_t stream);
 int ftc_swiglu_bwd(const void* da, const void* gu, void* dgu, long long rows, int F, long long dgu_rs,
                    hipStream_t stream);
@@ -45,6 +45,11 @@ int ftc_flash_fwd(const void* q, const void* k, const void* v, void* o, float* l
                   long long q_row_stride, long long kv_row_stride, long long o_row_stride, float scale, int causal,
                   int window, const int* doc_start, hipStream_t stream);
 int ftc_flash_bwd_workspace(int B, int S, int H, int D, long long* bytes);
+long long ftc_decode_workspace_floats(int B, int H, int KV, int D, int max_len);
+int ftc_decode_attention(const void* q, void* kc, void* vc, const void* knew, const void* vnew, long long new_rs,
+                         const int* lens, void* out, float* workspace, int B, int H, int KV, int D, int max_len,
+                         long long q_rs, long long kv_rs, long long b_rs, long long o_rs, float scale, int window,
+                         hipStream_t stream);
 int ftc_flash_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
                   void* dq, void* dk, void* dv, void* workspace, int B, int S, int H, int KV, int D,
                   long long q_row_stride, long long kv_row_stride, long long o_row_stride, long long do_row_stride,
@@ -172,15 +177,13 @@ void rope_(at::Tensor& qkv, const at::Tensor& cos, const at::Tensor& sin, const 
   const long long rows = qkv.size(0);
   if (positions.has_value()) {
     need(*positions, at::kInt, "positions");
-    TORCH_CHECK(positions->numel() == rows, "positions length");
-    auto mx = positions->max().item<int>();
-    TORCH_CHECK(mx < cos.size(0), "rope: position beyond table");
-    pp = positions->data_ptr<int>();
+    TORCH_CHECK(positions->numel() == rows && positions->is_contiguous(), "positions length");
+    pp = positions->data_ptr<int>();  // clamped to the table in the kernel (no host read)
   } else {
     TORCH_CHECK(seq_len <= cos.size(0), "rope: seq_len beyond table");
   }
   check(ftc_rope(qkv.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(), pp, rows, (int)qkv.stride(0),
-                 (int)n_rot_heads, (int)head_dim, (int)seq_len, inverse ? 1 : 0, cur_stream()),
+                 (int)n_rot_heads, (int)head_dim, (int)seq_len, inverse ? 1 : 0, (int)cos.size(0), cur_stream()),
         "rope");
 }
 
@@ -472,6 +475,39 @@ void flash_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, co
         "flash_bwd");
 }
 
+// ---------------- decode attention (generation) ----------------
+// qkv: [B, >=(H+2KV)*D] row view of the current token's packed projection (q | k | v); k_cache /
+// v_cache: [B, Lmax, KV*D] contiguous; lens: int32 [B] valid keys (current token included, <= max_len
+// <= Lmax).  The current token's K/V rows are appended at position lens-1 by the kernel itself.
+at::Tensor decode_attention(const at::Tensor& q, at::Tensor& k_cache, at::Tensor& v_cache,
+                            const at::Tensor& lens, int64_t H, int64_t KV, int64_t D, int64_t max_len, double scale,
+                            int64_t window) {
+  need(q, at::kBFloat16, "q");
+  need(k_cache, at::kBFloat16, "k_cache");
+  need(v_cache, at::kBFloat16, "v_cache");
+  TORCH_CHECK(lens.is_cuda() && lens.scalar_type() == at::kInt && lens.is_contiguous(), "lens: int32 device tensor");
+  TORCH_CHECK(k_cache.dim() == 3 && k_cache.is_contiguous() && v_cache.sizes() == k_cache.sizes() &&
+                  v_cache.is_contiguous(), "decode_attention: caches [B, Lmax, KV*D] contiguous");
+  const int64_t B = k_cache.size(0), Lmax = k_cache.size(1);
+  TORCH_CHECK(D == 64 || D == 128, "decode_attention: head_dim 64 or 128");
+  TORCH_CHECK(H % KV == 0 && H / KV <= 8 && k_cache.size(2) == KV * D, "decode_attention: heads / cache width");
+  TORCH_CHECK(q.dim() == 2 && q.size(0) == B && q.size(1) >= (H + 2 * KV) * D && q.stride(1) == 1 &&
+                  q.stride(0) % 8 == 0,
+              "decode_attention: qkv [B, >=(H+2KV)*D] row view with 16-byte rows");
+  TORCH_CHECK(lens.numel() == B && max_len >= 1 && max_len <= Lmax, "decode_attention: lens / max_len");
+  auto out = at::empty({B, H * D}, q.options());
+  auto ws = at::empty({ftc_decode_workspace_floats((int)B, (int)H, (int)KV, (int)D, (int)max_len)},
+                      q.options().dtype(at::kFloat));
+  const auto* qp = static_cast<const uint16_t*>(q.data_ptr());
+  check(ftc_decode_attention(qp, k_cache.data_ptr(), v_cache.data_ptr(), qp + H * D, qp + (H + KV) * D, q.stride(0),
+                             lens.data_ptr<int>(), out.data_ptr(), ws.data_ptr<float>(), (int)B, (int)H, (int)KV,
+                             (int)D, (int)max_len,
+                             q.stride(0), KV * D, Lmax * KV * D, out.stride(0), (float)scale, (int)window,
+                             cur_stream()),
+        "decode_attention");
+  return out;
+}
+
 // ---------------- NF4 (QLoRA) ----------------
 std::vector<at::Tensor> nf4_quantize(const at::Tensor& w, int64_t block) {
   need(w, at::kBFloat16, "w");
@@ -627,6 +663,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("B"), py::arg("S"), py::arg("H"),
         py::arg("KV"), py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("window"),
         py::arg("doc_start") = py::none(), py::arg("doc_end") = py::none());
+  m.def("decode_attention", &decode_attention);
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequantize", &nf4_dequantize);
   m.def("nf4_linear", &nf4_linear);

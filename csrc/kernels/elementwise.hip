@@ -7,11 +7,14 @@ using namespace ftc;
 
 // qkv: [rows, ld] bf16; the first (n_rot_heads * head_dim) columns are rotated in place, half-split
 // (rotate_half) convention: (x1, x2) -> (x1 c - x2 s, x2 c + x1 s) with x1 = x[:D/2], x2 = x[D/2:].
-// pos = positions ? positions[row] : row % seq_len.  cos/sin tables: [max_pos, D/2] fp32.
+// pos = positions ? positions[row] : row % seq_len, clamped to the table (positions are device data:
+// no host read of them, so a step with explicit positions stays sync-free and graph-capturable).
+// cos/sin tables: [max_pos, D/2] fp32.
 __global__ __launch_bounds__(256) void rope_kernel(uint16_t* __restrict__ qkv, const float* __restrict__ cosT,
                                                    const float* __restrict__ sinT,
                                                    const int* __restrict__ positions, long long rows, int ld,
-                                                   int n_rot_heads, int head_dim, int seq_len, float sign) {
+                                                   int n_rot_heads, int head_dim, int seq_len, float sign,
+                                                   int max_pos) {
   const int half = head_dim >> 1;
   const int chunks = half >> 3;  // 8 pairs per work item
   const long long per_row = (long long)n_rot_heads * chunks;
@@ -21,7 +24,7 @@ __global__ __launch_bounds__(256) void rope_kernel(uint16_t* __restrict__ qkv, c
     const int rem = (int)(it - row * per_row);
     const int head = rem / chunks;
     const int c = rem - head * chunks;
-    const int pos = positions ? positions[row] : (int)(row % seq_len);
+    const int pos = positions ? min(max(positions[row], 0), max_pos - 1) : (int)(row % seq_len);
     uint16_t* base = qkv + row * ld + (long long)head * head_dim + c * 8;
     uint4* p1 = reinterpret_cast<uint4*>(base);
     uint4* p2 = reinterpret_cast<uint4*>(base + half);
@@ -46,12 +49,13 @@ __global__ __launch_bounds__(256) void rope_kernel(uint16_t* __restrict__ qkv, c
 }
 
 extern "C" int ftc_rope(void* qkv, const float* cosT, const float* sinT, const int* positions, long long rows,
-                        int ld, int n_rot_heads, int head_dim, int seq_len, int inverse, hipStream_t stream) {
+                        int ld, int n_rot_heads, int head_dim, int seq_len, int inverse, int max_pos,
+                        hipStream_t stream) {
   if (head_dim % 16 != 0 || ld % 8 != 0) return -1;
   const long long total = rows * n_rot_heads * (head_dim / 16);
   const int grid = ftc::stream_grid(total, 256);
   hipLaunchKernelGGL(rope_kernel, dim3(grid), dim3(256), 0, stream, (uint16_t*)qkv, cosT, sinT, positions, rows, ld,
-                     n_rot_heads, head_dim, seq_len, inverse ? -1.0f : 1.0f);
+                     n_rot_heads, head_dim, seq_len, inverse ? -1.0f : 1.0f, max_pos);
   return (int)hipGetLastError();
 }
 

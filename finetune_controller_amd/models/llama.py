@@ -135,7 +135,7 @@ class LlamaLayer(nn.Module):
         return ops.lora_linear(x, W, pair.A, pair.B, pair.scale, blocks=pair.blocks, aug=self.aug.get(name),
                                dropout=pair.dropout if self.training else 0.0)
 
-    def forward(self, h, delta, rope: ops.RotaryTable, B: int, S: int, positions=None, docs=None):
+    def forward(self, h, delta, rope: ops.RotaryTable, B: int, S: int, positions=None, docs=None, kv=None):
         cfg = self.cfg
         p_qkv, p_o, p_gu, p_down = (self.pad(n) for n in ("qkv", "o", "gu", "down"))
         # grad_pad: delta came from the previous layer's down projection (same LoRA shape in every layer;
@@ -143,8 +143,15 @@ class LlamaLayer(nn.Module):
         h, x = ops.add_rms_norm(h, delta, self.attn_norm, cfg.norm_eps, pad=p_qkv, grad_pad=p_down)
         qkv = self.proj("qkv", x)
         qkv = ops.apply_rope_packed(qkv, rope, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, S, positions)
-        a = ops.attention_packed(qkv, B, S, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, True, cfg.sliding_window,
-                                 out_pad=p_o, grad_pad=p_qkv, docs=docs)
+        if kv is not None and kv[0].decoding:  # generation: one new token per sequence vs its cache
+            cache, li = kv
+            a = ops.decode_attention(qkv, cache.k[li], cache.v[li], cache.lens_next, cache.attend_len(),
+                                     cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, window=cfg.sliding_window)
+        else:
+            if kv is not None:  # prefill: keep this prompt's K/V rows
+                kv[0].store(kv[1], qkv, cfg.n_heads, S)
+            a = ops.attention_packed(qkv, B, S, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, True, cfg.sliding_window,
+                                     out_pad=p_o, grad_pad=p_qkv, docs=docs)
         o = self.proj("o", a)
         h, x = ops.add_rms_norm(h, o, self.mlp_norm, cfg.norm_eps, pad=p_gu, grad_pad=p_o)
         mlp = self.mlp_projs(p_gu, p_down)
@@ -205,7 +212,7 @@ class LlamaForCausalLM(nn.Module):
         for name, p in self.named_parameters():
             p.requires_grad_(".lora." in name)
 
-    def hidden(self, input_ids: torch.Tensor, positions=None, segments=None) -> torch.Tensor:
+    def hidden(self, input_ids: torch.Tensor, positions=None, segments=None, kv_cache=None) -> torch.Tensor:
         """``segments`` (``ops.Segments``): packed documents -- RoPE positions restart and attention
         stays inside each document."""
         B, S = input_ids.shape
@@ -213,11 +220,12 @@ class LlamaForCausalLM(nn.Module):
             positions = segments.positions
         h = F.embedding(input_ids.reshape(-1), self.embed)
         delta = None
-        for layer in self.layers:
+        for li, layer in enumerate(self.layers):
             if self.checkpoint_layers and self.training and torch.is_grad_enabled():
                 h, delta = checkpoint(layer, h, delta, self.rope, B, S, positions, segments, use_reentrant=False)
             else:
-                h, delta = layer(h, delta, self.rope, B, S, positions, segments)
+                h, delta = layer(h, delta, self.rope, B, S, positions, segments,
+                                 (kv_cache, li) if kv_cache is not None else None)
         gp = self.layers[-1].pad("down") if len(self.layers) else 0
         _, x = ops.add_rms_norm(h, delta, self.final_norm, self.cfg.norm_eps, grad_pad=gp)
         return x

@@ -6,6 +6,7 @@ See ``_backend`` for the dispatch policy (HIP on GPU, loud failure if the extens
 from ._backend import ext_available, kernel_mode, load_ext, use_hip  # noqa: F401
 from .activation import gelu_tanh, swiglu  # noqa: F401
 from .attention import Segments, attention_packed, attention_reference, segments_from_eos  # noqa: F401
+from .decode import KVCache, decode_attention  # noqa: F401
 from .cross_entropy import cross_entropy_reference, fused_linear_cross_entropy  # noqa: F401
 from .linear import lora_linear  # noqa: F401
 from .norm import add_rms_norm, layer_norm, rms_norm  # noqa: F401
