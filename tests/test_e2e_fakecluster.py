@@ -63,9 +63,13 @@ def test_gpt2_full_ft_job_runs_on_cpu_worker(tmp_path, model):
         try:
             def done():
                 run_monitor(ctx)
-                return c.get(f"/api/v1/jobs/{jid}").json()["status"] in ("completed", "failed")
+                r = c.get(f"/api/v1/jobs/{jid}")
+                assert r.status_code == 200, r.text
+                return r.json()["status"] in ("completed", "failed")
 
-            wait_for(done, timeout=240)
+            # the GET route is rate-limited to 50/min per client (reference app/main.py), so poll
+            # below that rate: a slow CPU worker would otherwise see 429s.
+            wait_for(done, timeout=240, step=1.5)
         finally:
             ctx.kube.stop()
         j = c.get(f"/api/v1/jobs/{jid}").json()

@@ -76,7 +76,7 @@ def _wait_for(pred, timeout=240.0):
     while time.time() - t0 < timeout:
         if pred():
             return
-        time.sleep(0.2)
+        time.sleep(1.5)  # under the 50/min rate limit of GET /api/v1/jobs/{id}
     raise TimeoutError("condition not reached")
 
 
@@ -110,7 +110,9 @@ def test_mnist_job_through_api_on_fakecluster(tmp_path):
         try:
             def done():
                 asyncio.run(JobMonitor(ctx, interval=0).reconcile_once())
-                return c.get(f"/api/v1/jobs/{jid}").json()["status"] in ("completed", "failed")
+                r = c.get(f"/api/v1/jobs/{jid}")
+                assert r.status_code == 200, r.text
+                return r.json()["status"] in ("completed", "failed")
 
             _wait_for(done)
         finally:
