@@ -59,7 +59,9 @@ def init_distributed(device_type: str = "auto", timeout_s: int = 1800) -> DistIn
             kw = {}
             if backend == "nccl":
                 kw["device_id"] = device
+            # FTC_INIT_METHOD (e.g. file://...) overrides the env:// TCPStore rendezvous; tests use it
             dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                    init_method=os.environ.get("FTC_INIT_METHOD") or None,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
     return DistInfo(rank, world, local, backend, device)
 

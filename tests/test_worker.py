@@ -414,7 +414,23 @@ def test_trainer_eval_synthetic(tmp_path):
     assert a == b and a == pytest.approx(np.log(512), rel=0.1)
 
 
+def _hold_until_released(tmp, port, timeout=120.0):
+    """Keep a spawned rank alive until the parent has read its queued tensors: torch shares them by
+    file descriptor through the sender, so a sender that exits first resets the parent's read."""
+    import time
+
+    t0 = time.time()
+    while not os.path.exists(os.path.join(tmp, f"release_{port}")) and time.time() - t0 < timeout:
+        time.sleep(0.05)
+
+
+def _release(tmp, port):
+    open(os.path.join(tmp, f"release_{port}"), "w").close()
+
+
 def _ddp_worker(rank, world, port, tmp, q):
+    # file rendezvous in the test dir: a picked-then-released TCP port can be taken by a parallel test
+    os.environ["FTC_INIT_METHOD"] = f"file://{tmp}/rdv_{port}"
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
@@ -425,6 +441,7 @@ def _ddp_worker(rank, world, port, tmp, q):
     tr.train_step(0.0)
     q.put((rank, tr.opt.grad_flat.detach().clone(), [b for b in tr.ddp.buckets]))
     tr.close()
+    _hold_until_released(tmp, port)
 
 
 def test_ddp_gloo_two_ranks_matches_single_process(tmp_path):
@@ -440,6 +457,7 @@ def test_ddp_gloo_two_ranks_matches_single_process(tmp_path):
     for p in procs:
         p.start()
     res = dict((r, (g, b)) for r, g, b in (q.get(timeout=120) for _ in range(2)))
+    _release(str(tmp_path), port)
     for p in procs:
         p.join(timeout=60)
     g0, buckets = res[0]
@@ -488,6 +506,8 @@ def test_lora_dropout_matches_autograd_reference():
 
 
 def _zero_worker(rank, world, port, tmp, zero, q):
+    # file rendezvous in the test dir: a picked-then-released TCP port can be taken by a parallel test
+    os.environ["FTC_INIT_METHOD"] = f"file://{tmp}/rdv_{port}"
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
@@ -511,6 +531,7 @@ def _zero_worker(rank, world, port, tmp, zero, q):
         out["reload_ok"] = bool(torch.equal(opt2.exp_avg, tr.opt.exp_avg) and torch.equal(opt2.master, tr.opt.master))
     q.put((rank, out))
     tr.close()
+    _hold_until_released(tmp, port)
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -531,6 +552,7 @@ def test_zero1_sharded_optimizer_matches_ddp(tmp_path, world):
         for p in procs:
             p.start()
         res = dict(q.get(timeout=180) for _ in range(world))
+        _release(str(tmp_path), port)
         for p in procs:
             p.join(timeout=60)
         runs[zero] = res
