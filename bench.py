@@ -11,8 +11,17 @@ linear projections of every layer -- forward, backward, bucketed gradient all-re
 with backward, global grad-norm clip and the AdamW update are all inside the timed region.
 Weak scaling: the per-GPU micro-batch is fixed, so global batch = micro_batch x N.
 
+Launch modes:
+* under torchrun (``WORLD_SIZE`` set): this process is one rank; ``--gpus`` must equal ``WORLD_SIZE``;
+* ``--gpus N > 1`` with no ``WORLD_SIZE``: this process is a pure launcher -- it never imports torch
+  or touches HIP, starts N rank processes (``RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR=127.0.0.1/
+  MASTER_PORT``) as children, forwards rank 0's JSON line and exits with the first failing rank's
+  code (terminating the rest).
+
 W untimed warmup steps, then K steps bracketed by barrier + device synchronize on both sides; the
-elapsed time is the MAX over ranks; rank 0 prints one JSON line.
+elapsed time is the MAX over ranks; rank 0 prints one JSON line.  After the timed region (never
+inside it) the ranks measure the all-reduce bus bandwidth of one DDP-sized bucket on the process
+group's transport, and report the world size the process group saw and the RCCL version.
 """
 from __future__ import annotations
 
@@ -37,7 +46,88 @@ def _mark(op: str):
         pass
 
 
-def main(argv=None) -> int:
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv: list[str], timeout_s: float | None = None) -> int:
+    """Launcher mode: start ``n`` rank processes of this script and supervise them.
+
+    The parent imports nothing that initialises HIP (not even torch) and never exec()s: each rank
+    is a child ``python bench.py <same args>`` with the torchrun-style env.  Rank 0's JSON line is
+    relayed to stdout; every other line any rank prints goes to stderr.
+    If any rank exits non-zero the others are terminated and that code is returned."""
+    import signal
+    import subprocess
+    import threading
+
+    port = int(os.environ.get("FTC_BENCH_PORT") or _free_port())
+    procs = []
+    relay_done = threading.Event()
+    seen_json = []
+
+    def relay(stream):
+        for line in iter(stream.readline, ""):
+            # the result line goes to stdout; anything else rank 0's libraries print there (gloo's
+            # connection banner, ...) is diagnostics
+            out = sys.stdout if line.lstrip().startswith("{") else sys.stderr
+            out.write(line)
+            out.flush()
+            if out is sys.stdout:
+                seen_json.append(line)
+        relay_done.set()
+
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        p = subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                             stdout=subprocess.PIPE if r == 0 else sys.stderr, text=True)
+        procs.append(p)
+    t = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+    t.start()
+    t0 = time.monotonic()
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            if timeout_s and time.monotonic() - t0 > timeout_s:
+                print(f"[bench] launcher timeout after {timeout_s:.0f}s", file=sys.stderr)
+                rc = 124
+                break
+            time.sleep(0.2)
+    except KeyboardInterrupt:
+        rc = 130
+    if rc != 0:
+        for p in procs:  # the exact children we started
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        deadline = time.monotonic() + 15
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, deadline - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        print(f"[bench] a rank failed (exit {rc}); ranks' codes: {[p.returncode for p in procs]}", file=sys.stderr)
+    relay_done.wait(timeout=10)
+    if rc == 0 and not seen_json:
+        print("[bench] rank 0 printed no JSON line", file=sys.stderr)
+        rc = 1
+    return rc if rc >= 0 else 128 - rc  # a signal-killed child (-N) -> 128+N
+
+
+def _parse(argv):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -48,7 +138,12 @@ def main(argv=None) -> int:
     ap.add_argument("--seq-len", type=int, default=int(os.environ.get("FTC_BENCH_SEQ", "4096")))
     ap.add_argument("--lora-r", type=int, default=16)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
-    ap.add_argument("--comm-engine", default="torch", choices=["torch", "native"])
+    ap.add_argument("--comm-engine", default=os.environ.get("FTC_COMM_ENGINE", "torch"), choices=["torch", "native"])
+    ap.add_argument("--comm-ab", action="store_true", default=os.environ.get("FTC_BENCH_COMM_AB") == "1",
+                    help="after the timed region, also time the native RCCL engine's bucket all-reduce")
+    ap.add_argument("--grad-dtype", default="auto", choices=["auto", "fp32", "bf16"],
+                    help="gradient buffer / reduction dtype (full FT; auto: fp32 when accumulating)")
+    ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--zero-stage", type=int, default=0, choices=[0, 1],
                     help="1: ZeRO-1 -- AdamW state sharded over the data-parallel ranks (reduce-scatter + all-gather)")
     ap.add_argument("--checkpoint-layers", action="store_true")
@@ -56,42 +151,99 @@ def main(argv=None) -> int:
                     help="rows per lm_head + cross-entropy chunk (the only vocab-sized buffer)")
     ap.add_argument("--kernels", default=None, choices=["hip", "torch"],
                     help="torch = stock PyTorch-ROCm ops (the 'before' row)")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: plumbing rehearsal over gloo (tests); the metric is only meaningful on cuda")
     ap.add_argument("--graph", action="store_true", help="whole training step captured in a hipGraph (1 GPU)")
     ap.add_argument("--doc-len", type=int, default=0,
                     help="packed documents of this many tokens (document-masked attention; 0: one per row)")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (not timed)")
-    a = ap.parse_args(argv)
+    ap.add_argument("--launcher-timeout", type=float, default=float(os.environ.get("FTC_BENCH_TIMEOUT", "0")),
+                    help="launcher mode: give up after this many seconds (0: never)")
+    return ap.parse_args(argv)
+
+
+def _bucket_busbw(info, mb: float, native=None, iters: int = 10) -> dict:
+    """Bus bandwidth (GB/s) of one ``mb``-MB bf16 SUM all-reduce, the DDP bucket size: algbw x
+    2(n-1)/n, the per-link rate a ring moves (nccl-tests convention)."""
+    import torch
+    import torch.distributed as dist
+
+    from finetune_controller_amd.parallel import dist as pdist
+
+    n = info.world_size
+    numel = int(mb * 2 ** 20 / 2)
+    t = torch.ones(numel, device=info.device, dtype=torch.bfloat16)
+    cuda = info.device.type == "cuda"
+
+    def run():
+        if native is not None:
+            native.all_reduce_async(t).wait()
+        else:
+            dist.all_reduce(t)
+
+    for _ in range(3):
+        run()
+    if native is not None:
+        native.reset()
+    if cuda:
+        torch.cuda.synchronize(info.device)
+    pdist.barrier(info)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        run()
+    if cuda:
+        torch.cuda.synchronize(info.device)
+    sec = (time.perf_counter() - t0) / iters
+    if native is not None:
+        native.reset()
+    sec = max(sec, 1e-9)
+    return {"bucket_mb": mb, "ms": round(sec * 1e3, 3),
+            "busbw_GBps": round(numel * 2 / sec / 1e9 * 2 * (n - 1) / n, 1)}
+
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    a = _parse(argv)
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and a.gpus > 1:
+        return spawn_ranks(a.gpus, argv, a.launcher_timeout or None)
+    if world_env is not None and int(world_env) != a.gpus:
+        print(f"[bench] --gpus {a.gpus} but WORLD_SIZE={world_env}: refusing to report a mislabelled number",
+              file=sys.stderr)
+        return 2
     if a.kernels:
         os.environ["FTC_KERNELS"] = a.kernels
 
     import torch
+    import torch.distributed as dist
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from finetune_controller_amd.parallel import dist as pdist
     from finetune_controller_amd.train.trainer import TrainConfig, Trainer
 
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    if world_env != a.gpus:
-        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world_env}; using WORLD_SIZE", file=sys.stderr)
-
+    cuda = a.device == "cuda"
     tc = TrainConfig(model=a.model, method=a.method, lora_r=a.lora_r, lora_alpha=2.0 * a.lora_r,
                      batch_size=a.batch_size, seq_len=a.seq_len, synthetic=True, max_steps=a.warmup + a.steps,
-                     warmup_steps=0, schedule="constant", lr=1e-4, bucket_mb=a.bucket_mb, comm_engine=a.comm_engine, zero_stage=a.zero_stage,
-                     checkpoint_layers=a.checkpoint_layers, ce_chunk_rows=a.ce_chunk_rows, save_model=False, resume=False, device="cuda",
-                     pack_documents=a.doc_len > 0, eos_id=2, synthetic_doc_len=a.doc_len, graph=a.graph)
+                     warmup_steps=0, schedule="constant", lr=1e-4, bucket_mb=a.bucket_mb, comm_engine=a.comm_engine,
+                     zero_stage=a.zero_stage, grad_accum=a.grad_accum, grad_dtype=a.grad_dtype,
+                     checkpoint_layers=a.checkpoint_layers, ce_chunk_rows=a.ce_chunk_rows, save_model=False,
+                     resume=False, device=a.device, pack_documents=a.doc_len > 0, eos_id=2,
+                     synthetic_doc_len=a.doc_len, graph=a.graph)
     tr = Trainer(tc)
     info = tr.info
     dev = tr.device
 
     def sync():
-        torch.cuda.synchronize(dev)
+        if cuda:
+            torch.cuda.synchronize(dev)
 
     for _ in range(a.warmup):
         tr.train_step(tc.lr)
     sync()
     pdist.barrier(info)
     sync()
-    _mark("push")  # roctx range "ftc_timed" (rocprofv3 --marker-trace; tools/kstats_md.py filters on it)
+    if cuda:
+        _mark("push")  # roctx range "ftc_timed" (rocprofv3 --marker-trace; tools/kstats_md.py filters on it)
     t0 = time.perf_counter()
     last = None
     for _ in range(a.steps):
@@ -99,27 +251,55 @@ def main(argv=None) -> int:
     sync()
     pdist.barrier(info)
     sync()
-    elapsed = time.perf_counter() - t0
-    _mark("pop")
-    elapsed = pdist.all_reduce_max(elapsed, info)
+    elapsed_rank = time.perf_counter() - t0
+    if cuda:
+        _mark("pop")
+    elapsed = pdist.all_reduce_max(elapsed_rank, info)
+    fastest = -pdist.all_reduce_max(-elapsed_rank, info)
     loss = float(last.float().item()) if last is not None else float("nan")
 
     n = info.world_size
-    tokens = a.batch_size * a.seq_len * n * a.steps
+    pg_world = dist.get_world_size() if dist.is_initialized() else 1
+    tokens = a.batch_size * a.seq_len * a.grad_accum * n * a.steps
     value = tokens / elapsed
     ms = elapsed / a.steps * 1000
     flops_tok = tr.cfg.flops_per_token(a.seq_len, lora=a.method != "full")
+
+    # ---- after the timed region: transport diagnostics (never part of the metric)
+    comm = {}
+    if n > 1:
+        comm["torch"] = _bucket_busbw(info, a.bucket_mb)
+        if cuda and (a.comm_ab or a.comm_engine == "native"):
+            try:
+                native = tr.ddp._native
+                if native is None:
+                    from finetune_controller_amd.parallel.comm import NativeComm
+
+                    native = NativeComm(device=dev)
+                comm["native"] = _bucket_busbw(info, a.bucket_mb, native=native)
+            except Exception as e:  # report, never fail the headline on the diagnostic
+                comm["native"] = {"error": f"{type(e).__name__}: {e}"[:200]}
+    rccl = None
+    if cuda:
+        try:
+            v = torch.cuda.nccl.version()
+            rccl = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+        except Exception:
+            rccl = None
+
     if a.profile_steps:
         from torch.profiler import ProfilerActivity, profile
 
-        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if cuda else [])
+        with profile(activities=acts) as prof:
             for _ in range(a.profile_steps):
                 tr.train_step(tc.lr)
             sync()
         if info.is_main:
             os.makedirs("gpurun_out", exist_ok=True)
             with open("gpurun_out/torch_profile.txt", "w") as f:
-                f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
+                f.write(prof.key_averages().table(sort_by="cuda_time_total" if cuda else "cpu_time_total",
+                                                  row_limit=60))
     if info.is_main:
         from finetune_controller_amd.ops import _backend
 
@@ -134,26 +314,34 @@ def main(argv=None) -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if cuda else "fp32",
             "data": "synthetic (uniform random token ids; random-init weights)",
             "config": {
-                "model": "llama3-8b" if a.model == "llama3-8b" else a.model,
+                "model": a.model,
                 "method": a.method,
                 "lora": {"r": a.lora_r, "alpha": 2 * a.lora_r, "targets": "all-linear"} if a.method != "full" else None,
-                "global_batch": a.batch_size * n,
+                "global_batch": a.batch_size * a.grad_accum * n,
                 "micro_batch_per_gpu": a.batch_size,
+                "grad_accum": a.grad_accum,
                 "seq_len": a.seq_len,
-                "tokens_per_step": a.batch_size * a.seq_len * n,
+                "tokens_per_step": a.batch_size * a.seq_len * a.grad_accum * n,
                 "parallelism": f"dp{n}" + ("-zero1" if a.zero_stage and n > 1 else ""),
                 "kernels": _backend.kernel_mode(),
                 "comm_engine": a.comm_engine,
                 "zero_stage": a.zero_stage,
+                "grad_dtype": str(tr.opt.grad_flat.dtype).replace("torch.", ""),
+                "device": a.device,
                 **({"packed_doc_len": a.doc_len} if a.doc_len else {}),
                 **({"hipgraph": True} if tr.graph_ok() else {}),
             },
+            "world_size_pg": pg_world,
+            "dist_backend": info.backend,
+            "rccl_version": rccl,
+            "rank_ms_per_step": {"max": round(ms, 2), "min": round(fastest / a.steps * 1000, 2)},
+            **({"allreduce_bucket": comm} if comm else {}),
             "loss": round(loss, 4),
             "model_tflops_per_gpu": round(value * flops_tok / n / 1e12, 1),
-            "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1),
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1) if cuda else None,
         }
         print(json.dumps(out), flush=True)
     tr.close()

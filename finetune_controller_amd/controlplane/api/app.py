@@ -157,6 +157,17 @@ def create_app(ctx: AppContext, run_monitor: bool | None = None, validator_facto
             logger.warning("user %s tried to access restricted resource %s", jwt.user_id, record.job_id)
             raise HTTPException(status_code=400, detail="Cannot access resource")
 
+    def is_admin(jwt) -> bool:
+        return bool(jwt) and (s.ADMIN_SCOPE in (jwt.available_models or []) or jwt.user_id in (s.ADMIN_USERS or []))
+
+    def require_admin(jwt, action: str, owner: str | None = None):
+        """Admin routes: with auth on, only an admin (scope / user list) -- or, for per-user routes,
+        that user -- may act.  Without auth (dev / local) the reference's open behaviour is kept."""
+        if not jwt or is_admin(jwt) or (owner is not None and jwt.user_id == owner):
+            return
+        logger.warning("user %s denied admin action %s", jwt.user_id, action)
+        raise HTTPException(status_code=403, detail="Admin privileges required")
+
     def available_models(jwt=None) -> list[str]:
         return ctx.registry.available_for(jwt.available_models if jwt else None)
 
@@ -300,7 +311,10 @@ def create_app(ctx: AppContext, run_monitor: bool | None = None, validator_facto
         if fields.get("dataset_id"):
             ds = DatasetInput(dataset_id=fields["dataset_id"])
         elif fields.get("dataset_url"):
-            ds = DatasetInput(dataset_url=fields["dataset_url"])
+            try:
+                ds = DatasetInput(dataset_url=fields["dataset_url"])
+            except ValidationError as e:
+                raise HTTPException(status_code=422, detail="dataset_url: must be an absolute http(s) URL") from e
         elif files.get("dataset"):
             ds = DatasetInput(dataset_file=files["dataset"])
         else:
@@ -585,7 +599,11 @@ def create_app(ctx: AppContext, run_monitor: bool | None = None, validator_facto
             raise HTTPException(status_code=404, detail=str(e)) from e
 
     @api.get("/admin/job/poll/{job_id}", tags=["Admin"])
-    async def poll_admin_job(job_id: str):
+    async def poll_admin_job(request: Request, job_id: str):
+        jwt_data, jwt = decode_request(request)
+        if jwt and not is_admin(jwt):
+            info = await ctx.store.get_job(job_id)
+            require_admin(jwt, f"poll {job_id}", owner=info.user_id if info else None)
         try:
             job = await asyncio.to_thread(ctx.kube.get_pytorchjob, ctx.namespace, job_id)
             st = job.get("status") or {}
@@ -606,7 +624,8 @@ def create_app(ctx: AppContext, run_monitor: bool | None = None, validator_facto
             raise HTTPException(status_code=404, detail=str(e)) from e
 
     @api.get("/admin/jobs/list", tags=["Admin"])
-    async def list_jobs():
+    async def list_jobs(request: Request):
+        require_admin(decode_request(request)[1], "list cluster jobs")
         try:
             jobs = await asyncio.to_thread(ctx.kube.list_pytorchjobs, ctx.namespace)
             return {"jobs": [j["metadata"]["name"] for j in jobs]}
@@ -614,7 +633,10 @@ def create_app(ctx: AppContext, run_monitor: bool | None = None, validator_facto
             raise HTTPException(status_code=500, detail=f"Failed to list jobs: {e}") from e
 
     @api.delete("/admin/jobs/{user_id}", tags=["Admin"])
-    async def clean_user_jobs(user_id: str):
+    async def clean_user_jobs(request: Request, user_id: str):
+        # fixed route (the reference calls delete_job with the wrong signature and never deletes):
+        # with auth on, only that user or an admin may wipe a user's jobs
+        require_admin(decode_request(request)[1], f"delete jobs of {user_id}", owner=user_id)
         jobs = await ctx.store.get_all_user_jobs(user_id)
         deleted, skipped = [], []
         for j in jobs:

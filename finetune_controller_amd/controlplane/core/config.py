@@ -66,6 +66,10 @@ class Settings(BaseModel):
     JWT_SECRET_KEY: str = ""
     JWT_ALGORITHM: str = "HS256"
     DEV_DISABLE_INTROSPECTION: bool = False
+    # admin routes (/api/v1/admin/jobs/*, /admin/job/poll): with auth on, a caller is an admin when its
+    # token's scp carries ADMIN_SCOPE or its subject is listed in ADMIN_USERS (comma-separated)
+    ADMIN_SCOPE: str = "finetune:admin"
+    ADMIN_USERS: list[str] = Field(default_factory=list)
     # worker config
     CONFIGURATION_FILE: str = "config.json"
     # database

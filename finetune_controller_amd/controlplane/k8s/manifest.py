@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import copy
 import re
+import shlex
 
 from ..core.device_config import AMD_GPU, Worker
 from ..schemas.jobs import JobInput
@@ -35,17 +36,20 @@ def label_value(v) -> str:
 def wrap_command(cmd: list[str], ckpt: str) -> list[str]:
     out = list(cmd)
     body = out[-1]
-    out[-1] = (f"rm -f {ckpt}/failed.txt; {body}; rc=$?; "
-               f"if [ $rc -eq 0 ]; then touch {ckpt}/done.txt; else echo $rc > {ckpt}/failed.txt; fi; exit $rc")
+    q = shlex.quote
+    out[-1] = (f"rm -f {q(ckpt + '/failed.txt')}; {body}; rc=$?; "
+               f"if [ $rc -eq 0 ]; then touch {q(ckpt + '/done.txt')}; else echo $rc > {q(ckpt + '/failed.txt')}; fi; "
+               f"exit $rc")
     return out
 
 
 def sync_command(ckpt: str, dest: str, patterns: list[str], interval: int) -> str:
-    inc = " ".join(f"--include '{p}'" for p in patterns)
-    s = f"aws s3 sync {ckpt} {dest} --exclude '*' {inc} --exclude 'done.txt' --exclude 'failed.txt'"
-    return (f"f=0; while [ ! -f {ckpt}/done.txt ]; do {s}; sleep {interval}; "
-            f"if [ -f {ckpt}/failed.txt ]; then f=$((f+1)); [ $f -ge 3 ] && break; else f=0; fi; done; "
-            f"{s}; ls -la {ckpt}; echo 'Training finished. Exiting sidecar.'")
+    q = shlex.quote  # every path / URI / pattern is quoted: none of them may be shell syntax
+    inc = " ".join(f"--include {q(p)}" for p in patterns)
+    s = f"aws s3 sync {q(ckpt)} {q(dest)} --exclude '*' {inc} --exclude 'done.txt' --exclude 'failed.txt'"
+    return (f"f=0; while [ ! -f {q(ckpt + '/done.txt')} ]; do {s}; sleep {int(interval)}; "
+            f"if [ -f {q(ckpt + '/failed.txt')} ]; then f=$((f+1)); [ $f -ge 3 ] && break; else f=0; fi; done; "
+            f"{s}; ls -la {q(ckpt)}; echo 'Training finished. Exiting sidecar.'")
 
 
 def merged_resources(job: JobInput, worker: Worker) -> dict:
@@ -92,8 +96,9 @@ def build_pytorchjob_manifest(job: JobInput, worker: Worker, settings, namespace
             "image": AWS_CLI_IMAGE,
             "imagePullPolicy": "IfNotPresent",
             "command": ["/bin/sh", "-c"],
-            "args": [f"aws s3 cp {job.s3_uri} {model.dataset_mount}/ ; echo 'done'; "
-                     f"find {model.dataset_mount} -type f | wc -l; ls -la {model.dataset_mount}"],
+            # s3_uri ends in a user-supplied file name: quoted (the container holds the AWS secret)
+            "args": [f"aws s3 cp {shlex.quote(job.s3_uri)} {shlex.quote(model.dataset_mount + '/')} ; echo 'done'; "
+                     f"find {shlex.quote(model.dataset_mount)} -type f | wc -l; ls -la {shlex.quote(model.dataset_mount)}"],
             "volumeMounts": [{"name": "aws-credentials", "mountPath": "/root/.aws"},
                              {"name": "dataset-volume", "mountPath": model.dataset_mount}],
             "envFrom": aws_from,

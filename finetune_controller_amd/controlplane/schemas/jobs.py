@@ -8,7 +8,9 @@ from __future__ import annotations
 from datetime import datetime
 from typing import Any
 
-from pydantic import BaseModel, ConfigDict
+from urllib.parse import urlparse
+
+from pydantic import BaseModel, ConfigDict, field_validator
 
 from ..spec.finetuning import BaseFineTuneModel
 
@@ -23,11 +25,26 @@ class UploadedFile(BaseModel):
     size: int = 0
 
 
+def validate_http_url(v: str | None) -> str | None:
+    """An absolute http(s) URL with a host (the reference types the field ``HttpUrl``,
+    ``/root/reference/app/schemas/jobs_schemas.py:13``): anything else is a 422, not a 500 in the
+    streaming download."""
+    if v is None:
+        return v
+    v = v.strip()
+    u = urlparse(v)
+    if u.scheme not in ("http", "https") or not u.hostname or any(c in v for c in " \t\r\n"):
+        raise ValueError("dataset_url must be an absolute http(s) URL")
+    return v
+
+
 class DatasetInput(BaseModel):
     dataset_id: str | None = None
     dataset_url: str | None = None
     dataset_file: UploadedFile | None = None
     dataset_description: str = ""
+
+    _url = field_validator("dataset_url")(classmethod(lambda cls, v: validate_http_url(v)))
 
 
 class JobInput(BaseModel):

@@ -20,7 +20,7 @@ per GPU, RCCL over xGMI inside each node).
 """
 from __future__ import annotations
 
-from typing import ClassVar
+from typing import ClassVar, Literal
 
 from pydantic import Field
 
@@ -117,6 +117,8 @@ class LMTrainingArguments(TrainingArguments):
     checkpoint_layers: bool = Field(default=False, description="Activation checkpointing per decoder layer")
     zero_stage: int = Field(default=0, ge=0, le=1,
                             description="1: ZeRO-1 -- AdamW state sharded over the data-parallel ranks")
+    grad_dtype: Literal["auto", "fp32", "bf16"] = Field(
+        default="auto", description="Gradient buffer / all-reduce dtype (auto: fp32 for full FT with accumulation or DP)")
     eval_every: int = Field(default=0, ge=0, description="Held-out loss every N steps (0 = off)")
     eval_batches: int = Field(default=4, ge=1, description="Micro-batches per GPU per evaluation")
     eval_holdout: float = Field(default=0.01, gt=0, description="Held-out share of the dataset (>= 1: windows)")

@@ -19,7 +19,7 @@ from urllib.parse import urlparse
 import httpx
 
 from ..context import AppContext
-from ..core.naming import generate_short_uuid
+from ..core.naming import generate_short_uuid, safe_filename
 from ..k8s.manifest import build_pytorchjob_manifest
 from ..schemas.db import DatasetModel, DatasetTypes, PromotionStatus
 from ..schemas.jobs import DatasetInput, JobInput
@@ -38,9 +38,9 @@ def _http_client() -> httpx.Client:
 
 async def upload_dataset_file(ctx: AppContext, job: JobInput, upload, description: str) -> DatasetModel:
     try:
-        s3_uri = await ctx.s3.upload_dataset(upload.path, job.user_id, job.job_id, name=upload.filename)
-        doc = await ctx.store.insert_dataset(job.user_id, job.job_id, DatasetTypes(s3_uri=s3_uri), upload.filename,
-                                             description)
+        name = safe_filename(upload.filename)
+        s3_uri = await ctx.s3.upload_dataset(upload.path, job.user_id, job.job_id, name=name)
+        doc = await ctx.store.insert_dataset(job.user_id, job.job_id, DatasetTypes(s3_uri=s3_uri), name, description)
         job.s3_uri = doc.dataset.s3_uri
         job.model.dataset_info.dataset_name = doc.dataset_name
         return doc
@@ -50,10 +50,12 @@ async def upload_dataset_file(ctx: AppContext, job: JobInput, upload, descriptio
 
 
 def filename_from_response(headers, url: str) -> str:
+    """Dataset name from ``Content-Disposition`` or the URL path, sanitised (both are untrusted and
+    end up in the worker pod's shell command: ``k8s.manifest``)."""
     cd = headers.get("Content-Disposition") or headers.get("content-disposition")
     if cd and "filename=" in cd:
-        return cd.split("filename=")[-1].strip().strip('"')
-    return os.path.basename(urlparse(url).path) or "default_filename-" + generate_short_uuid()
+        return safe_filename(cd.split("filename=")[-1].strip().strip('"'))
+    return safe_filename(os.path.basename(urlparse(url).path) or "default_filename-" + generate_short_uuid())
 
 
 async def stream_dataset_url(ctx: AppContext, job: JobInput, url: str, description: str,

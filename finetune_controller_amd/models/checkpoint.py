@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import glob
 import json
+import logging
 import os
 import re
 
@@ -24,6 +25,8 @@ import torch
 from safetensors.torch import load_file, save_file
 
 from .lora import LoRAConfig
+
+_log = logging.getLogger("ftc.checkpoint")
 
 PEFT_PREFIX = "base_model.model."
 
@@ -189,31 +192,60 @@ def save_full(model, out_dir: str, shard_bytes: int = 5 * 1024**3, merge_lora: b
 
 
 @torch.no_grad()
-def load_hf_checkpoint(model, path: str) -> int:
-    """Load HF safetensors (sharded or single) into the packed layout; returns tensors loaded."""
+def load_hf_checkpoint(model, path: str, strict: bool = True) -> int:
+    """Load HF safetensors (sharded or single) into the packed layout; returns tensors loaded.
+
+    Every target tensor must be filled exactly once with a matching shape: a missing tensor (wrong
+    ``init_from``, a naming scheme this loader does not know, a partial shard set) or a shape
+    mismatch raises instead of silently fine-tuning random-init weights.  Checkpoint tensors the
+    model has no slot for (rotary ``inv_freq`` buffers, a tied ``lm_head``) are reported and skipped.
+    ``strict=False`` only downgrades *missing* tensors to a warning."""
     files = sorted(glob.glob(os.path.join(path, "*.safetensors"))) if os.path.isdir(path) else [path]
     files = [f for f in files if "adapter" not in os.path.basename(f)]
+    if not files:
+        raise FileNotFoundError(f"no *.safetensors weights under {path}")
     targets = dict(hf_tensors(model))
-    n = 0
+    loaded: set[str] = set()
+    unexpected: list[str] = []
     for fp in files:
         sd = load_file(fp)
         for k, v in sd.items():
-            if k not in targets:
+            if k not in targets and "transformer." + k in targets:
+                k = "transformer." + k  # GPT-2 hub checkpoints saved from GPT2Model (no LM-head prefix)
+            dst = targets.get(k)
+            if dst is None:
+                unexpected.append(k)
                 continue
-            dst = targets[k]
+            if tuple(v.shape) != tuple(dst.shape):
+                raise ValueError(f"{os.path.basename(fp)}: {k} has shape {tuple(v.shape)}, the model expects "
+                                 f"{tuple(dst.shape)} (different architecture / config?)")
+            if k in loaded:
+                raise ValueError(f"{k} appears in more than one checkpoint shard")
             dst.copy_(v.to(dst.dtype))
-            n += 1
+            loaded.add(k)
+    missing = sorted(set(targets) - loaded)
+    if unexpected:
+        _log.warning("load_hf_checkpoint: %d checkpoint tensors not used (e.g. %s)", len(unexpected),
+                     ", ".join(unexpected[:3]))
+    if missing:
+        msg = (f"load_hf_checkpoint: {len(missing)} of {len(targets)} model tensors not found in {path} "
+               f"(e.g. {', '.join(missing[:3])})")
+        if strict:
+            raise ValueError(msg)
+        _log.warning(msg)
     if hasattr(model, "invalidate_transposed"):
         model.invalidate_transposed()
-    return n
+    return len(loaded)
 
 
 # ---------------- resume checkpoints ----------------
 
 def save_resume(path: str, step: int, opt, data_state: dict, extra: dict | None = None, opt_state: dict | None = None):
     opt_state = opt.state_dict() if opt_state is None else opt_state
-    st = {"step": step, "param_flat": opt.param_flat.detach().cpu(), "opt": {k: (v.detach().cpu() if torch.is_tensor(v) else v)
-                                                                            for k, v in opt_state.items()},
+    # trainable parameters in the compact per-parameter layout (no bucket padding): loadable at any
+    # world size, with or without ZeRO-1
+    st = {"step": step, "params": opt.export_params(),
+          "opt": {k: (v.detach().cpu() if torch.is_tensor(v) else v) for k, v in opt_state.items()},
           "data": data_state, "extra": extra or {}}
     tmp = path + ".tmp"
     torch.save(st, tmp)
@@ -230,8 +262,10 @@ def latest_resume(ckpt_dir: str) -> str | None:
 @torch.no_grad()
 def load_resume(path: str, opt) -> dict:
     st = torch.load(path, map_location="cpu", weights_only=True)
-    opt.param_flat.copy_(st["param_flat"])
-    # full-layout state; a sharded (ZeRO-1) optimizer slices out its own part
-    dev = "cpu" if hasattr(opt, "shard_ranges") else opt.device
-    opt.load_state_dict({k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in st["opt"].items()})
+    if "params" not in st:
+        raise ValueError(f"{os.path.basename(path)}: resume checkpoint predates the compact layout; "
+                         "resume it with the build, world size and ZeRO setting that wrote it")
+    opt.import_params(st["params"])
+    # compact state: the optimizer scatters it into its own layout (a sharded one keeps its part)
+    opt.load_state_dict(st["opt"])
     return st

@@ -57,7 +57,7 @@ class _FusedLinearCE(torch.autograd.Function):
         buf = None
         # dh = dlogits . W through a cached W^T (TN GEMM layout, ~15 % faster): frozen heads keep one
         # copy, a trainable head (full FT) is re-transposed once per optimizer step
-        from .linear import _TN_DW, transpose2d, transposed_weight
+        from .linear import _TN_DW, accum_mm, transpose2d, transposed_weight
 
         WT = transposed_weight(W) if (need_dh and hip) else None
         for r0 in range(0, T, chunk_rows):
@@ -79,7 +79,7 @@ class _FusedLinearCE(torch.autograd.Function):
                 torch.mm(dlog, W if WT is None else WT.t(), out=dh[r0:r1])
             if need_dw:
                 if mg is not None:
-                    mg.addmm_(dlog.t(), transpose2d(hc).t() if (hip and _TN_DW) else hc)
+                    accum_mm(mg, dlog.t(), transpose2d(hc).t() if (hip and _TN_DW) else hc)
                 else:
                     dW.addmm_(dlog.t().float(), hc.float())
         loss = losses.sum() * gscale

@@ -162,6 +162,17 @@ def transposed_weight(W: torch.Tensor) -> torch.Tensor | None:
     return (param_t if W.requires_grad else frozen_t).get(W)
 
 
+def accum_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, alpha: float = 1.0) -> torch.Tensor:
+    """``out += alpha * a @ b``.  ``out`` may be wider than the operands (fp32 gradient buffer with
+    bf16 activations): on the GPU one GEMM with bf16 A/B and an fp32 C/D (beta = 1, in place), so
+    the accumulation never rounds to bf16."""
+    if out.dtype == a.dtype:
+        return out.addmm_(a, b, alpha=alpha)
+    if a.is_cuda:
+        return torch.addmm(out, a, b, alpha=alpha, out_dtype=out.dtype, out=out)
+    return out.addmm_(a.to(out.dtype), b.to(out.dtype), alpha=alpha)
+
+
 def _mm_into(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor):
     if _TUNABLEOP:
         out.copy_(torch.mm(a, b))
@@ -356,12 +367,12 @@ def _accum_xty(out: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, alpha: float
     (csrc/kernels/lora_wgrad.hip: split-T MFMA + deterministic split reduction) where supported,
     else beta=1 GEMMs.  ``blocks`` (r0, r1, c0, c1): only those diagonal blocks of out are formed
     (block-diagonal B of a packed projection) -- one launch for all of them."""
-    hip = _HIP_WGRAD and use_hip(X)
+    hip = _HIP_WGRAD and use_hip(X) and out.dtype == X.dtype
     if blocks is None:
         if hip and ext().lora_wgrad_ok(X, Y, Y.shape[1]):
             ext().lora_wgrad_(out, X, Y, Y.shape[1], float(alpha), 1.0)
         else:
-            out.addmm_(X.t(), Y, alpha=alpha)
+            accum_mm(out, X.t(), Y, alpha)
         return
     R = blocks[0][3] - blocks[0][2]
     segs_ok = (len(blocks) <= 4 and blocks[0][0] == 0 and blocks[-1][1] == X.shape[1]
@@ -495,9 +506,9 @@ class _LoRALinearFn(torch.autograd.Function):
                 if _TN_DW and use_hip(x2):
                     # hipBLASLt runs dW += dy^T x 14-24 % faster with x handed over transposed (K-major
                     # reduction operand, tools/bench_dw_gemm.py); the transpose streams at HBM rate
-                    mg.addmm_(dy2.t(), transpose2d(x2).t())
+                    accum_mm(mg, dy2.t(), transpose2d(x2).t())
                 else:
-                    mg.addmm_(dy2.t(), x2)
+                    accum_mm(mg, dy2.t(), x2)
                 _grad_ready(W)
             else:
                 dW = dy2.t() @ x2

@@ -113,7 +113,8 @@ def fused_mlp_supported(x2: torch.Tensor, gu, dn, pair_gu, pair_down, p_gu: int,
             and tuple(blocks[1]) == (F, 2 * F, 16, 32)):
         return False
     for p in (pair_gu.A, pair_gu.B, pair_down.A, pair_down.B):
-        if getattr(p, "main_grad", None) is None:
+        mg = getattr(p, "main_grad", None)
+        if mg is None or mg.dtype != torch.bfloat16:  # the fused weight-gradient kernel writes bf16
             return False
     if not _spare_cols(x2, gu.K, gu.Rp):
         return False

@@ -43,6 +43,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--comm-engine", default="torch", choices=["torch", "native"])
     ap.add_argument("--zero-stage", type=int, default=0, choices=[0, 1],
                     help="1: ZeRO-1 -- AdamW state sharded over the data-parallel ranks (reduce-scatter + all-gather)")
+    ap.add_argument("--grad-dtype", default="auto", choices=["auto", "fp32", "bf16"],
+                    help="gradient buffer / all-reduce dtype (auto: fp32 for full FT with accumulation or DP)")
     ap.add_argument("--init-from", default="", help="HF safetensors checkpoint dir to fine-tune from")
     ap.add_argument("--synthetic", action="store_true", help="ignore the dataset; synthetic tokens")
     ap.add_argument("--no-resume", action="store_true")
@@ -74,7 +76,8 @@ def config_from_args(a) -> TrainConfig:
                        weight_decay=a.weight_decay, max_grad_norm=a.max_grad_norm, seed=a.seed,
                        dataset_path=a.dataset_path, checkpoint_path=a.checkpoint_path, log_interval=a.log_interval,
                        save_every=a.save_every, resume=not a.no_resume, synthetic=a.synthetic, bucket_mb=a.bucket_mb,
-                       comm_engine=a.comm_engine, zero_stage=a.zero_stage, checkpoint_layers=a.checkpoint_layers, init_from=a.init_from,
+                       comm_engine=a.comm_engine, zero_stage=a.zero_stage, grad_dtype=a.grad_dtype,
+                       checkpoint_layers=a.checkpoint_layers, init_from=a.init_from,
                        dtype=a.dtype, device=a.device, timers=a.timers, profile_steps=a.profile_steps,
                        eval_every=a.eval_every, eval_batches=a.eval_batches, eval_holdout=a.eval_holdout,
                        pack_documents=a.pack_documents, eos_id=a.eos_id,

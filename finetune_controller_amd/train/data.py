@@ -26,30 +26,42 @@ import torch
 
 
 class SyntheticTokens:
-    """Uniform random token ids of the configured shape (the benchmark contract's synthetic data)."""
+    """Uniform random token ids of the configured shape (the benchmark contract's synthetic data).
+
+    Every step draws a FRESH batch on the device from a generator re-seeded with (seed, step): no
+    host->device copy in the timed loop, nothing the model could memorise (a small cycled pool lets
+    the loss fall below ln(vocab)), and a resumed run sees the same stream.  Packed-document mode
+    (``doc_len``) keeps a 4-batch pool whose label masks are precomputed."""
 
     def __init__(self, vocab: int, batch: int, seq_len: int, device, seed: int = 0, doc_len: int = 0,
                  eos_id: int = 2):
         self.vocab, self.batch, self.seq_len, self.device = vocab, batch, seq_len, device
+        self.seed = int(seed)
         self.gen = torch.Generator(device="cpu").manual_seed(seed)
-        # a small pool of pre-generated batches on device: no host->device copy in the timed loop
-        pool = [torch.randint(0, vocab, (batch, seq_len + 1), generator=self.gen) for _ in range(4)]
-        self.last_n_valid, self.labels = None, None
+        self.last_n_valid, self.labels, self.pool = None, None, None
         if doc_len:  # packed documents of doc_len tokens: EOS at the end of each (its label ignored)
+            pool = [torch.randint(0, vocab, (batch, seq_len + 1), generator=self.gen) for _ in range(4)]
             for t in pool:
                 t[t == eos_id] = (eos_id + 1) % vocab
                 t[:, doc_len - 1::doc_len] = eos_id
             self.labels = [t[:, 1:].masked_fill(t[:, :-1] == eos_id, -100).to(device) for t in pool]
             self.last_n_valid = int((self.labels[0] != -100).sum().item())
-        self.pool = [t.to(device) for t in pool]
+            self.pool = [t.to(device) for t in pool]
+        else:
+            self._dgen = torch.Generator(device=device)
         self.i = 0
 
     def __iter__(self):
         return self
 
     def __next__(self):
-        t = self.pool[self.i % len(self.pool)]
-        y = t[:, 1:] if self.labels is None else self.labels[self.i % len(self.pool)]
+        if self.pool is not None:
+            t = self.pool[self.i % len(self.pool)]
+            y = self.labels[self.i % len(self.pool)]
+        else:
+            self._dgen.manual_seed(self.seed * 1_000_003 + self.i)
+            t = torch.randint(0, self.vocab, (self.batch, self.seq_len + 1), device=self.device, generator=self._dgen)
+            y = t[:, 1:]
         self.i += 1
         return t[:, :-1], y
 

@@ -13,6 +13,17 @@ their gradients into ONE flat grad buffer (``grad_flat``); each ``p.data`` / ``p
   buffer, with the clip coefficient and the 1/world averaging read from device memory -- no host
   synchronisation inside ``step()``.
 
+Gradient precision (``grad_dtype``): by default the grad buffer has the model dtype.  With
+``grad_dtype=torch.float32`` (full fine-tuning with gradient accumulation or data parallelism) the
+buffer is fp32: the GEMM weight gradients accumulate into it with bf16 operands and an fp32 C
+(``ops.linear.accum_mm``), gradients that autograd produces in the model dtype (norm weights,
+embeddings) are folded in by a post-accumulate hook, and the data-parallel reduction sums fp32 --
+no mantissa is lost across micro-batches or ranks.
+
+Checkpoint format: ``state_dict`` holds the state per parameter with no padding ("compact"), so a
+resume works across world sizes and with ZeRO-1 switched on or off (the flat layout pads buckets
+to a multiple of the world size).
+
 Layout: parameters are placed in REVERSE registration order (last layer first), i.e. in the order
 backward produces their gradients, so the first DDP buckets become ready first.
 """
@@ -34,7 +45,8 @@ def _align(n: int) -> int:
 
 class FlatAdamW:
     def __init__(self, params, lr: float = 2e-4, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-                 max_grad_norm: float = 1.0, grad_scale: float = 1.0, bucket_elems: int = 0, pad_multiple: int = 1):
+                 max_grad_norm: float = 1.0, grad_scale: float = 1.0, bucket_elems: int = 0, pad_multiple: int = 1,
+                 grad_dtype: torch.dtype | None = None):
         seen, plist = set(), []
         for p in params:
             if p.requires_grad and id(p) not in seen:
@@ -72,14 +84,22 @@ class FlatAdamW:
             self.bucket_params.append(members)
         self.numel = off
         self.param_flat = torch.zeros(off, dtype=self.dtype, device=self.device)
-        self.grad_flat = torch.zeros(off, dtype=self.dtype, device=self.device)
+        self.grad_dtype = grad_dtype or self.dtype
+        self.grad_flat = torch.zeros(off, dtype=self.grad_dtype, device=self.device)
+        self._fold_hooks = []
         with torch.no_grad():
             for p, (o, n) in zip(self.params, self.offsets):
                 self.param_flat[o:o + n].copy_(p.detach().reshape(-1))
                 p.data = self.param_flat[o:o + n].view_as(p)
                 g = self.grad_flat[o:o + n].view_as(p)
-                p.grad = g
                 p.main_grad = g
+                if self.grad_dtype == self.dtype:
+                    p.grad = g  # autograd accumulates in place into the flat buffer
+                else:
+                    # autograd's gradient has the parameter's dtype: fold it into the wider buffer and
+                    # drop it (registered before any data-parallel hook, so it runs first)
+                    p.grad = None
+                    self._fold_hooks.append(p.register_post_accumulate_grad_hook(_fold_grad))
         self._init_state()
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.max_grad_norm = max_grad_norm
@@ -116,6 +136,39 @@ class FlatAdamW:
 
     def zero_grad(self):
         self.grad_flat.zero_()
+        if self._fold_hooks:
+            for p in self.params:
+                p.grad = None
+
+    # ---- layout-independent (compact) views of flat-layout tensors
+    def compact(self, flat: torch.Tensor, dtype: torch.dtype | None = None) -> torch.Tensor:
+        """CPU copy of the live elements of a full-layout tensor, parameter after parameter."""
+        out = torch.empty(self.num_params(), dtype=dtype or flat.dtype)
+        i = 0
+        for o, n in self.offsets:
+            out[i:i + n].copy_(flat[o:o + n])
+            i += n
+        return out
+
+    def expand_(self, compact: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """Scatter a compact tensor into the full layout ``out`` (padding untouched)."""
+        if compact.numel() != self.num_params():
+            raise ValueError(f"checkpoint holds {compact.numel()} elements, this parameter set has {self.num_params()}")
+        i = 0
+        for o, n in self.offsets:
+            out[o:o + n].copy_(compact[i:i + n])
+            i += n
+        return out
+
+    def layout(self) -> list[int]:
+        return [n for _, n in self.offsets]
+
+    def export_params(self) -> torch.Tensor:
+        return self.compact(self.param_flat)
+
+    @torch.no_grad()
+    def import_params(self, compact: torch.Tensor):
+        self.expand_(compact.to(self.param_flat.dtype), self.param_flat)
 
     @torch.no_grad()
     def step(self, lr: float | None = None):
@@ -153,16 +206,25 @@ class FlatAdamW:
         return float(self.last_grad_norm.float().sqrt().item()) * (self.grad_scale if use_hip(self.grad_flat) else 1.0)
 
     def state_dict(self) -> dict:
-        return {"master": self.master, "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq,
-                "step": self.step_count, "lr": self.lr, "numel": self.numel}
+        """Compact (unpadded, per-parameter) CPU state: loadable at any world size, ZeRO on or off."""
+        return {"format": "compact", "layout": self.layout(), "master": self.compact(self.master, torch.float32),
+                "exp_avg": self.compact(self.exp_avg), "exp_avg_sq": self.compact(self.exp_avg_sq),
+                "step": self.step_count, "lr": self.lr}
+
+    def _check_layout(self, sd: dict):
+        if sd.get("format") != "compact":
+            raise ValueError("optimizer checkpoint predates the compact format (resume it with the world size and "
+                             "ZeRO setting that wrote it)")
+        if list(sd["layout"]) != self.layout():
+            raise ValueError("optimizer checkpoint does not match this model's trainable parameters "
+                             f"({len(sd['layout'])} vs {len(self.offsets)} tensors)")
 
     @torch.no_grad()
     def load_state_dict(self, sd: dict):
-        if int(sd["numel"]) != self.numel:
-            raise ValueError("optimizer state does not match the parameter layout")
-        self.master.copy_(sd["master"])
-        self.exp_avg.copy_(sd["exp_avg"])
-        self.exp_avg_sq.copy_(sd["exp_avg_sq"])
+        self._check_layout(sd)
+        self.expand_(sd["master"], self.master)
+        self.expand_(sd["exp_avg"], self.exp_avg)
+        self.expand_(sd["exp_avg_sq"], self.exp_avg_sq)
         self.step_count = int(sd["step"])
         bump_param_generation()
         if self.master is not self.param_flat:
@@ -181,8 +243,8 @@ class ShardedFlatAdamW(FlatAdamW):
     per bucket, writing bf16 straight into ``param_flat``) after an all-reduced global grad norm, and
     the updated slices are all-gathered in place into every rank's ``param_flat``.
 
-    Checkpoints (``state_dict``) hold the gathered full-size state, so a run can resume on any world
-    size; ``state_dict`` / ``load_state_dict`` are collective calls."""
+    Checkpoints (``state_dict``) hold the gathered state in the compact per-parameter format, so a
+    run can resume on any world size or without ZeRO; ``state_dict`` is a collective call."""
 
     def __init__(self, params, world: int, rank: int, group=None, bucket_elems: int = 16 << 20, **kw):
         self.world, self.rank, self.group = world, rank, group
@@ -205,7 +267,7 @@ class ShardedFlatAdamW(FlatAdamW):
                 self.master[o:o + hi - lo].copy_(self.param_flat[lo:hi])
         self.exp_avg = torch.zeros(n, dtype=torch.float32, device=self.device)
         self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=self.device)
-        self.grad_shard = torch.zeros(n, dtype=self.dtype, device=self.device)
+        self.grad_shard = torch.zeros(n, dtype=self.grad_dtype, device=self.device)
 
     @torch.no_grad()
     def sync_master(self):
@@ -292,21 +354,29 @@ class ShardedFlatAdamW(FlatAdamW):
         return out
 
     def state_dict(self) -> dict:
-        return {"master": self._gather_full(self.master), "exp_avg": self._gather_full(self.exp_avg),
-                "exp_avg_sq": self._gather_full(self.exp_avg_sq), "step": self.step_count, "lr": self.lr,
-                "numel": self.numel}
+        return {"format": "compact", "layout": self.layout(),
+                **{k: self.compact(self._gather_full(getattr(self, k))) for k in ("master", "exp_avg", "exp_avg_sq")},
+                "step": self.step_count, "lr": self.lr}
 
     @torch.no_grad()
     def load_state_dict(self, sd: dict):
-        if int(sd["numel"]) != self.numel:
-            raise ValueError("optimizer state does not match the parameter layout")
+        self._check_layout(sd)
         for name in ("master", "exp_avg", "exp_avg_sq"):
-            full, dst = sd[name], getattr(self, name)
+            full = self.expand_(sd[name], torch.zeros(self.numel, dtype=torch.float32))
+            dst = getattr(self, name)
             for b in range(len(self.buckets)):
                 lo, hi = self.shard_ranges[b]
                 self.shard_view(b, dst).copy_(full[lo:hi])
         self.step_count = int(sd["step"])
         bump_param_generation()
+
+
+def _fold_grad(p: torch.Tensor):
+    """post-accumulate hook (fp32 grad buffer): main_grad += p.grad, then free p.grad.  Weights whose
+    custom backward wrote main_grad itself return no gradient: the hook still fires, with p.grad None."""
+    if p.grad is not None:
+        p.main_grad.add_(p.grad)
+        p.grad = None
 
 
 def lr_at(step: int, base_lr: float, warmup: int, total: int, schedule: str = "cosine", min_ratio: float = 0.1) -> float:

