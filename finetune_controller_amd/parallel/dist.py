@@ -55,6 +55,13 @@ def init_distributed(device_type: str = "auto", timeout_s: int = 1800) -> DistIn
         # nccl (= RCCL over xGMI) for GPU ranks; FTC_DIST_BACKEND=gloo forces host collectives (CPU
         # tests, shared-card rehearsals where RCCL refuses two ranks on one device)
         backend = os.environ.get("FTC_DIST_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
+        if backend == "nccl" and os.environ.get("FTC_SHARE_GPU") == "1":
+            # rehearsal of the multi-GPU RCCL path on ONE card: RCCL refuses two ranks on one device of
+            # one host ("Duplicate GPU detected"), so every rank claims its own host id -- RCCL then
+            # connects them through its socket transport over loopback.  Never set on a real node.
+            os.environ.setdefault("NCCL_HOSTID", f"ftc-rehearsal-rank{rank}")
+            os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+            os.environ.setdefault("NCCL_IB_DISABLE", "1")
         if not dist.is_initialized():
             kw = {}
             if backend == "nccl":

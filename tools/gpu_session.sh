@@ -50,6 +50,28 @@ for s in "${STEPS[@]}"; do
     flash)
       timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py -m gpu -x -q -k flash > gpurun_out/pytest_flash.log 2>&1
       fatal $? flash; tail -5 gpurun_out/pytest_flash.log ;;
+    rccl2)  # 2 ranks on the ONE card through the bench launcher, RCCL over loopback sockets (NCCL_HOSTID per rank)
+      FTC_SHARE_GPU=1 timeout -k 10 500 python bench.py --gpus 2 --model llama3-8b-1l --steps 5 --warmup 2 --comm-ab \
+        --launcher-timeout 450 > gpurun_out/rccl2.log 2>&1
+      fatal $? rccl2; grep '^{' gpurun_out/rccl2.log | cut -c1-2000 ;;
+    rccl2_native)  # same, DDP buckets through the native engine (csrc/comm/rccl_engine.cpp)
+      FTC_SHARE_GPU=1 timeout -k 10 500 python bench.py --gpus 2 --model llama3-8b-1l --steps 5 --warmup 2 \
+        --comm-engine native --launcher-timeout 450 > gpurun_out/rccl2_native.log 2>&1
+      fatal $? rccl2_native; grep '^{' gpurun_out/rccl2_native.log | cut -c1-2000 ;;
+    rccl2_full)  # full FT, fp32 grads, ZeRO-1 reduce-scatter/all-gather over RCCL, 2 ranks on one card
+      FTC_SHARE_GPU=1 timeout -k 10 500 python bench.py --gpus 2 --model llama3-8b-1l --method full --zero-stage 1 \
+        --steps 4 --warmup 2 --comm-ab --launcher-timeout 450 > gpurun_out/rccl2_full.log 2>&1
+      fatal $? rccl2_full; grep '^{' gpurun_out/rccl2_full.log | cut -c1-2000 ;;
+    full_fp32)  # full FT, grad accumulation 2: fp32 vs bf16 gradient buffer (cost of the precise mode)
+      timeout -k 10 600 python bench.py --method full --steps 4 --warmup 2 --grad-accum 2 --grad-dtype fp32 \
+        > gpurun_out/full_fp32.log 2>&1
+      fatal $? full_fp32; grep '^{' gpurun_out/full_fp32.log | cut -c1-600
+      timeout -k 10 600 python bench.py --method full --steps 4 --warmup 2 --grad-accum 2 --grad-dtype bf16 \
+        > gpurun_out/full_bf16.log 2>&1
+      fatal $? full_bf16; grep '^{' gpurun_out/full_bf16.log | cut -c1-600 ;;
+    gemms)
+      timeout -k 10 300 python tools/bench_gemms.py > gpurun_out/bench_gemms.log 2>&1
+      fatal $? gemms; tail -3 gpurun_out/bench_gemms.log ;;
     bench_b8)
       timeout -k 10 600 python bench.py --steps 8 --warmup 3 --batch-size 8 > gpurun_out/bench_b8.log 2>&1
       fatal $? bench_b8; tail -2 gpurun_out/bench_b8.log ;;
