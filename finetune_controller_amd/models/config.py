@@ -87,6 +87,8 @@ class ModelConfig:
             cfg["sliding_window"] = self.sliding_window
         if self.rope_scaling:
             cfg["rope_scaling"] = self.rope_scaling
+        # transformers >= 5 reads RoPE only from "rope_parameters" (the top-level keys above serve 4.x)
+        cfg["rope_parameters"] = {"rope_type": "default", **(self.rope_scaling or {}), "rope_theta": self.rope_theta}
         return cfg
 
     @classmethod
@@ -97,9 +99,22 @@ class ModelConfig:
             return cls("gpt2", cfg["vocab_size"], d, cfg["n_layer"], cfg["n_head"], cfg["n_head"],
                        cfg.get("n_inner") or 4 * d, cfg.get("n_positions", 1024), norm_eps=cfg.get("layer_norm_epsilon", 1e-5),
                        tie_embeddings=True, name=name or "gpt2")
+        # transformers >= 5 writes RoPE settings as one "rope_parameters" dict (theta + scaling);
+        # older configs carry top-level "rope_theta" / "rope_scaling"
+        rp = dict(cfg.get("rope_parameters") or {})
+        theta = float(rp.pop("rope_theta", cfg.get("rope_theta", 10000.0)))
+        scaling = cfg.get("rope_scaling")
+        if scaling is None and rp.get("rope_type", "default") != "default":
+            scaling = rp
+        if scaling and scaling.get("rope_type", scaling.get("type", "default")) == "default":
+            scaling = None
+        hd = cfg.get("head_dim")
+        if hd and hd * cfg["num_attention_heads"] != cfg["hidden_size"]:
+            raise ValueError(f"head_dim {hd} x {cfg['num_attention_heads']} heads != hidden_size {cfg['hidden_size']}: "
+                             "decoupled head_dim is not supported")
         return cls("llama", cfg["vocab_size"], cfg["hidden_size"], cfg["num_hidden_layers"], cfg["num_attention_heads"],
                    cfg.get("num_key_value_heads", cfg["num_attention_heads"]), cfg["intermediate_size"],
-                   cfg.get("max_position_embeddings", 8192), cfg.get("rope_theta", 10000.0), cfg.get("rope_scaling"),
+                   cfg.get("max_position_embeddings", 8192), theta, scaling,
                    cfg.get("rms_norm_eps", 1e-5), cfg.get("sliding_window") or 0,
                    cfg.get("tie_word_embeddings", False), name=name or mt)
 

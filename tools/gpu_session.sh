@@ -96,6 +96,19 @@ for s in "${STEPS[@]}"; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench \
         -- python3 bench.py --steps 3 --warmup 2 > gpurun_out/prof.log 2>&1
       fatal $? prof; ls -R gpurun_out/prof | head -20 ;;
+    gemm_shapes)  # plain timing of the step's hipBLASLt shapes (random operands)
+      timeout -k 10 300 python tools/pmc_gemms.py --iters 10 > gpurun_out/gemm_shapes.log 2>&1
+      fatal $? gemm_shapes; cat gpurun_out/gemm_shapes.log | grep '^{' ;;
+    pmc_gemm)
+      timeout -k 10 600 bash tools/pmc_run.sh gemm --labels gpurun_out/pmc_gemm_labels.json --match Cijk \
+        -- python3 tools/pmc_gemms.py --iters 4 --labels "$PWD/gpurun_out/pmc_gemm_labels.json"
+      fatal $? pmc_gemm ;;
+    pmc_attn)
+      timeout -k 10 600 bash tools/pmc_run.sh attn -- python3 tools/bench_attention.py --rounds 1 --iters 2
+      fatal $? pmc_attn ;;
+    pmc_step)  # every kernel of a 1-layer Llama-3-8B LoRA step (real shapes), grouped by kernel name
+      timeout -k 10 600 bash tools/pmc_run.sh step -- python3 bench.py --model llama3-8b-1l --steps 2 --warmup 1
+      fatal $? pmc_step ;;
     *) echo "unknown step $s" ;;
   esac
 done
