@@ -76,11 +76,12 @@ def _check_claims(claims: dict, audience: str | None, verify_exp: bool, leeway: 
             raise JWTError("Invalid audience")
 
 
-def decode_hs256(token: str, secret: str, audience: str | None = None, verify_exp: bool = True) -> dict:
+def decode_hs256(token: str, secret: str | bytes, audience: str | None = None, verify_exp: bool = True) -> dict:
     parts, header, claims = _split(token)
     if header.get("alg") != "HS256":
         raise JWTError("The specified alg value is not allowed")
-    want = hmac.new(secret.encode(), f"{parts[0]}.{parts[1]}".encode(), hashlib.sha256).digest()
+    key = secret if isinstance(secret, bytes) else secret.encode()
+    want = hmac.new(key, f"{parts[0]}.{parts[1]}".encode(), hashlib.sha256).digest()
     if not hmac.compare_digest(want, b64url_decode(parts[2])):
         raise JWTError("Signature verification failed")
     _check_claims(claims, audience, verify_exp)
@@ -166,7 +167,8 @@ def ecdsa_p256_verify(pub: tuple[int, int], msg: bytes, sig: bytes) -> bool:
     if len(sig) != 64:
         return False
     r, s = int.from_bytes(sig[:32], "big"), int.from_bytes(sig[32:], "big")
-    if not (1 <= r < _N and 1 <= s < _N) or not _on_curve(*pub):
+    x, y = pub
+    if not (1 <= r < _N and 1 <= s < _N) or not (0 <= x < _P and 0 <= y < _P) or not _on_curve(x, y):
         return False
     z = int.from_bytes(hashlib.sha256(msg).digest(), "big")
     w = pow(s, -1, _N)
