@@ -16,6 +16,7 @@ from __future__ import annotations
 import datetime as _dt
 import hashlib
 import hmac
+import logging
 import os
 import shutil
 import threading
@@ -158,50 +159,97 @@ def _sign(key: bytes, msg: str) -> bytes:
     return hmac.new(key, msg.encode(), hashlib.sha256).digest()
 
 
+def _uri_encode(s: str, keep_slash: bool) -> str:
+    return urllib.parse.quote(s, safe="/-_.~" if keep_slash else "-_.~")
+
+
+def _canonical_query(query: dict) -> str:
+    return "&".join(f"{_uri_encode(str(k), False)}={_uri_encode(str(v), False)}"
+                    for k, v in sorted((str(k), str(v)) for k, v in query.items()))
+
+
+def sigv4_signature(secret_key: str, region: str, amz_date: str, method: str, path: str, query: dict,
+                    headers: dict, payload_hash: str, service: str = "s3") -> tuple[str, str]:
+    """AWS Signature Version 4 over one request: returns (signed_headers, hex signature).
+
+    ``headers`` are the headers to sign (names lower-cased here, values trimmed); ``path`` is the
+    un-encoded absolute path; ``amz_date`` is ``YYYYMMDDTHHMMSSZ``.  Pure function of its inputs, so
+    AWS's published examples are known answers for it (tests/test_adapters_transport.py)."""
+    h = {k.lower(): " ".join(str(v).strip().split()) for k, v in headers.items()}
+    signed = ";".join(sorted(h))
+    canon_h = "".join(f"{k}:{h[k]}\n" for k in sorted(h))
+    creq = "\n".join([method, _uri_encode(path, True), _canonical_query(query), canon_h, signed, payload_hash])
+    date = amz_date[:8]
+    scope = f"{date}/{region}/{service}/aws4_request"
+    sts = "\n".join(["AWS4-HMAC-SHA256", amz_date, scope, _sha256(creq.encode())])
+    k = _sign(_sign(_sign(_sign(("AWS4" + secret_key).encode(), date), region), service), "aws4_request")
+    return signed, hmac.new(k, sts.encode(), hashlib.sha256).hexdigest()
+
+
+def sigv4_presign_query(access_key: str, secret_key: str, region: str, amz_date: str, host: str, path: str,
+                        expires: int, session_token: str | None = None, method: str = "GET") -> dict:
+    """Query-string authentication (presigned URL): the X-Amz-* parameters including the signature."""
+    scope = f"{amz_date[:8]}/{region}/s3/aws4_request"
+    q = {"X-Amz-Algorithm": "AWS4-HMAC-SHA256", "X-Amz-Credential": f"{access_key}/{scope}", "X-Amz-Date": amz_date,
+         "X-Amz-Expires": str(int(expires)), "X-Amz-SignedHeaders": "host"}
+    if session_token:
+        q["X-Amz-Security-Token"] = session_token
+    _, sig = sigv4_signature(secret_key, region, amz_date, method, path, q, {"host": host}, "UNSIGNED-PAYLOAD")
+    q["X-Amz-Signature"] = sig
+    return q
+
+
 class S3ObjectStore(ObjectStore):
-    """Minimal S3 client: AWS Signature Version 4, path-style addressing."""
+    """Minimal S3 client: AWS Signature Version 4; path-style (``/{bucket}/{key}`` on the endpoint,
+    the default: works with MinIO / Ceph / any custom ``S3_ENDPOINT_URL``) or virtual-hosted
+    (``{bucket}.{endpoint host}/{key}``, what AWS recommends for new buckets)."""
 
     MULTIPART_THRESHOLD = 64 * 1024 * 1024
     PART_SIZE = 32 * 1024 * 1024
 
     def __init__(self, access_key: str | None, secret_key: str | None, region: str = "us-east-1",
-                 endpoint: str | None = None, session_token: str | None = None, timeout: float = 120.0):
+                 endpoint: str | None = None, session_token: str | None = None, timeout: float = 120.0,
+                 addressing: str = "path", transport: httpx.BaseTransport | None = None, clock=None):
+        if addressing not in ("path", "virtual"):
+            raise ValueError("addressing must be 'path' or 'virtual'")
         self.ak, self.sk, self.region, self.token = access_key, secret_key, region, session_token
         self.endpoint = (endpoint or f"https://s3.{region}.amazonaws.com").rstrip("/")
-        self.host = urllib.parse.urlparse(self.endpoint).netloc
-        self.http = httpx.Client(timeout=timeout)
+        u = urllib.parse.urlparse(self.endpoint)
+        self.scheme, self.host = u.scheme, u.netloc
+        self.addressing = addressing
+        self.http = httpx.Client(timeout=timeout, transport=transport)
+        self._clock = clock or (lambda: _dt.datetime.now(_dt.timezone.utc))
+
+    def _target(self, bucket: str, key: str = "") -> tuple[str, str]:
+        """(host, un-encoded path) of an object or bucket request."""
+        if self.addressing == "virtual":
+            return f"{bucket}.{self.host}", "/" + key
+        return self.host, f"/{bucket}" + (f"/{key}" if key else "")
 
     # ---- signing ----
-    def _headers(self, method, path, query: dict, payload_hash: str, extra: dict | None = None):
-        now = _dt.datetime.now(_dt.timezone.utc)
-        amz = now.strftime("%Y%m%dT%H%M%SZ")
-        date = now.strftime("%Y%m%d")
-        h = {"host": self.host, "x-amz-date": amz, "x-amz-content-sha256": payload_hash}
+    def _headers(self, method, host, path, query: dict, payload_hash: str, extra: dict | None = None):
+        amz = self._clock().strftime("%Y%m%dT%H%M%SZ")
+        h = {"host": host, "x-amz-date": amz, "x-amz-content-sha256": payload_hash}
         if self.token:
             h["x-amz-security-token"] = self.token
         if extra:
             h.update({k.lower(): v for k, v in extra.items()})
         if not (self.ak and self.sk):
             return h
-        canon_q = "&".join(f"{urllib.parse.quote(k, safe='-_.~')}={urllib.parse.quote(str(v), safe='-_.~')}"
-                           for k, v in sorted(query.items()))
-        signed = ";".join(sorted(h))
-        canon_h = "".join(f"{k}:{str(h[k]).strip()}\n" for k in sorted(h))
-        creq = "\n".join([method, urllib.parse.quote(path, safe="/-_.~"), canon_q, canon_h, signed, payload_hash])
-        scope = f"{date}/{self.region}/s3/aws4_request"
-        sts = "\n".join(["AWS4-HMAC-SHA256", amz, scope, _sha256(creq.encode())])
-        k = _sign(_sign(_sign(_sign(("AWS4" + self.sk).encode(), date), self.region), "s3"), "aws4_request")
-        sig = hmac.new(k, sts.encode(), hashlib.sha256).hexdigest()
+        signed, sig = sigv4_signature(self.sk, self.region, amz, method, path, query, h, payload_hash)
+        scope = f"{amz[:8]}/{self.region}/s3/aws4_request"
         h["authorization"] = f"AWS4-HMAC-SHA256 Credential={self.ak}/{scope}, SignedHeaders={signed}, Signature={sig}"
         return h
 
     def _req(self, method, bucket, key="", query=None, body: bytes = b"", extra=None, ok=(200, 204, 206)):
-        path = f"/{bucket}" + (f"/{key}" if key else "")
+        host, path = self._target(bucket, key)
         query = query or {}
-        h = self._headers(method, path, query, _sha256(body), extra)
-        url = self.endpoint + urllib.parse.quote(path, safe="/-_.~")
-        r = self.http.request(method, url, params=query or None, content=body or None, headers=h)
-        if r.status_code == 404:
+        h = self._headers(method, host, path, query, _sha256(body), extra)
+        # the query string is sent exactly as it was signed (httpx's own encoding could differ)
+        qs = _canonical_query(query)
+        url = f"{self.scheme}://{host}{_uri_encode(path, True)}" + (f"?{qs}" if qs else "")
+        r = self.http.request(method, url, content=body or None, headers=h)
+        if r.status_code == 404 and 404 not in ok:
             raise ObjectNotFound(f"s3://{bucket}/{key}")
         if r.status_code not in ok:
             raise RuntimeError(f"S3 {method} {path} failed: {r.status_code} {r.text[:300]}")
@@ -240,7 +288,10 @@ class S3ObjectStore(ObjectStore):
                 "</CompleteMultipartUpload>"
             self._req("POST", bucket, key, query={"uploadId": upload_id}, body=xml.encode())
         except Exception:
-            self._req("DELETE", bucket, key, query={"uploadId": upload_id}, ok=(200, 204, 404))
+            try:  # AbortMultipartUpload; never let a failing abort mask the original error
+                self._req("DELETE", bucket, key, query={"uploadId": upload_id}, ok=(200, 204, 404))
+            except Exception as abort_err:  # noqa: BLE001
+                logging.getLogger("ftc.s3").warning("abort of multipart upload %s failed: %s", upload_id, abort_err)
             raise
 
     def get_bytes(self, bucket, key):
@@ -289,23 +340,10 @@ class S3ObjectStore(ObjectStore):
                   extra={"x-amz-copy-source": urllib.parse.quote(f"/{src_bucket}/{src_key}", safe="/-_.~")})
 
     def presign(self, bucket, key, expires=3600):
-        now = _dt.datetime.now(_dt.timezone.utc)
-        amz = now.strftime("%Y%m%dT%H%M%SZ")
-        date = now.strftime("%Y%m%d")
-        scope = f"{date}/{self.region}/s3/aws4_request"
-        path = f"/{bucket}/{key}"
-        q = {"X-Amz-Algorithm": "AWS4-HMAC-SHA256", "X-Amz-Credential": f"{self.ak}/{scope}", "X-Amz-Date": amz,
-             "X-Amz-Expires": str(int(expires)), "X-Amz-SignedHeaders": "host"}
-        if self.token:
-            q["X-Amz-Security-Token"] = self.token
-        canon_q = "&".join(f"{urllib.parse.quote(k, safe='-_.~')}={urllib.parse.quote(v, safe='-_.~')}"
-                           for k, v in sorted(q.items()))
-        creq = "\n".join(["GET", urllib.parse.quote(path, safe="/-_.~"), canon_q, f"host:{self.host}\n", "host",
-                          "UNSIGNED-PAYLOAD"])
-        sts = "\n".join(["AWS4-HMAC-SHA256", amz, scope, _sha256(creq.encode())])
-        k = _sign(_sign(_sign(_sign(("AWS4" + (self.sk or "")).encode(), date), self.region), "s3"), "aws4_request")
-        sig = hmac.new(k, sts.encode(), hashlib.sha256).hexdigest()
-        return f"{self.endpoint}{urllib.parse.quote(path, safe='/-_.~')}?{canon_q}&X-Amz-Signature={sig}"
+        host, path = self._target(bucket, key)
+        q = sigv4_presign_query(self.ak or "", self.sk or "", self.region, self._clock().strftime("%Y%m%dT%H%M%SZ"),
+                                host, path, expires, self.token)
+        return f"{self.scheme}://{host}{_uri_encode(path, True)}?{_canonical_query(q)}"
 
 
 def _xml_escape(s: str) -> str:

@@ -75,12 +75,16 @@ class HttpKubeClient(KubeClient):
     SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
 
     def __init__(self, server: str | None = None, token: str | None = None, verify=True, cert=None,
-                 kubeconfig: str | None = None, timeout: float = 30.0):
+                 kubeconfig: str | None = None, timeout: float = 30.0, transport: httpx.BaseTransport | None = None):
         if server is None:
             server, token, verify, cert = self._discover(kubeconfig)
         self.server = server.rstrip("/")
+        self.verify, self.cert = verify, cert
         headers = {"Authorization": f"Bearer {token}"} if token else {}
-        self.http = httpx.Client(base_url=self.server, headers=headers, verify=verify, cert=cert, timeout=timeout)
+        if transport is not None:  # injected transport (tests replay API-server responses): no TLS setup
+            self.http = httpx.Client(base_url=self.server, headers=headers, timeout=timeout, transport=transport)
+        else:
+            self.http = httpx.Client(base_url=self.server, headers=headers, verify=verify, cert=cert, timeout=timeout)
 
     # ---- configuration discovery (in-cluster first, then kubeconfig) ----
     @classmethod
