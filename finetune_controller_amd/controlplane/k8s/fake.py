@@ -90,6 +90,27 @@ class _Pod:
                 "status": {"phase": self.phase, "startTime": self.start_time, "containerStatuses": cs}}
 
 
+def kueue_quotas_from_manifests(docs) -> tuple[dict, dict]:
+    """(cluster_queues, local_queues) for FakeCluster from Kueue ClusterQueue / LocalQueue manifests.
+
+    The fake admits by per-ClusterQueue totals: each resource's nominalQuota is summed over the
+    queue's flavors (flavor placement, cohort borrowing and preemption are not simulated)."""
+    cqs, lqs = {}, {}
+    for d in docs:
+        if not d:
+            continue
+        if d.get("kind") == "ClusterQueue":
+            tot: dict = {}
+            for group in d["spec"].get("resourceGroups", []):
+                for fl in group.get("flavors", []):
+                    for r in fl.get("resources", []):
+                        tot[r["name"]] = tot.get(r["name"], 0.0) + parse_quantity(r["nominalQuota"])
+            cqs[d["metadata"]["name"]] = tot
+        elif d.get("kind") == "LocalQueue":
+            lqs[d["metadata"]["name"]] = d["spec"]["clusterQueue"]
+    return cqs, lqs
+
+
 class FakeCluster(KubeClient):
     def __init__(self, object_store=None, run_processes: bool | str = "cpu", workdir: str | None = None,
                  cluster_queues: dict | None = None, local_queues: dict | None = None, sim_ticks: int = 3,
@@ -118,6 +139,11 @@ class FakeCluster(KubeClient):
         self.deleted_pod_logs: dict[str, list[str]] = {}  # logs of pods removed with their job
 
     # ------------------------------------------------------------------ KubeClient API
+
+    def set_kueue(self, cluster_queues: dict, local_queues: dict):
+        """Replace the queue topology (e.g. from ``kueue_quotas_from_manifests``) before any admission."""
+        self.cluster_queues, self.local_queues = cluster_queues, local_queues
+        self.usage = {cq: {} for cq in cluster_queues}
     def create_custom(self, group, version, namespace, plural, body):
         with self.lock:
             name = body["metadata"]["name"]

@@ -214,6 +214,15 @@ class Llama3_8B_LoRA(_WorkerSpec):
     training_arguments: LoRAArguments = LoRAArguments()
 
 
+class Llama3_8B_LoRA_2GPU(Llama3_8B_LoRA):
+    """Llama-3-8B LoRA data parallel over 2 x MI355X of one node (the Kueue multi-tenant config:
+    four of these share an 8-GPU node; BASELINE.json configs[4])."""
+
+    name: str = "Llama3-8B-LoRA-2GPU"
+    description: str = "Llama-3-8B LoRA fine-tune, 2 x MI355X data parallel (RCCL all-reduce of the adapter grads)"
+    accelerator_count: int = Field(default=2, ge=1, description="MI355X GPUs per worker")
+
+
 class Llama3_8B_Full(_WorkerSpec):
     """Llama-3-8B full fine-tune, DDP over 8 x MI355X (RCCL all-reduce over xGMI)."""
 
@@ -324,5 +333,5 @@ class Mistral7B_v03_LoRA(Llama3_8B_LoRA):
     model_preset: ClassVar[str] = "mistral-7b-v0.3"
 
 
-BUILTIN_MODELS = [MNIST, MNIST_MI355X, GPT2SmallFT, Llama3_8B_LoRA, Llama3_8B_Full, Mistral7B_QLoRA, Llama31_8B_LoRA,
+BUILTIN_MODELS = [MNIST, MNIST_MI355X, GPT2SmallFT, Llama3_8B_LoRA, Llama3_8B_LoRA_2GPU, Llama3_8B_Full, Mistral7B_QLoRA, Llama31_8B_LoRA,
                   Llama32_3B_LoRA, Llama32_1B_LoRA, Llama3_70B_QLoRA, Llama3_70B_LoRA, Mistral7B_v03_LoRA]

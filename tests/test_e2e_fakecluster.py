@@ -9,6 +9,7 @@
 """
 import asyncio
 import json
+import os
 import time
 
 import pytest
@@ -93,16 +94,16 @@ def test_kueue_multi_tenant_gpu_quota(tmp_path):
     with TestClient(app) as c:
         ids = []
         for i in range(5):
-            r = c.post("/api/v1/jobs", data={"job_name": f"tenant{i}", "model": "Llama3-8B-LoRA", "device": "mi355x",
-                                            "task": "causal_lm", "user_id": f"user{i}",
-                                            "accelerator_count": "2"})
+            r = c.post("/api/v1/jobs", data={"job_name": f"tenant{i}", "model": "Llama3-8B-LoRA-2GPU",
+                                            "device": "mi355x", "task": "causal_lm", "user_id": f"user{i}"})
+            assert r.status_code == 200, r.text
             ids.append(r.json()["job_id"])
-        # accelerator_count is a spec field (not a training argument): use a 2-GPU spec instance
+        # the 2-GPU spec alone yields the 2-GPU request and the 2-rank launch (no manifest edits)
         for jid in ids:
             job = ctx.kube.objects[("kubeflow.org", "pytorchjobs", ctx.namespace, jid)]
-            for cont in job["spec"]["pytorchReplicaSpecs"]["Master"]["template"]["spec"]["containers"][:1]:
-                cont["resources"]["requests"]["amd.com/gpu"] = 2
-                cont["resources"]["limits"]["amd.com/gpu"] = 2
+            cont = job["spec"]["pytorchReplicaSpecs"]["Master"]["template"]["spec"]["containers"][0]
+            assert cont["resources"]["requests"]["amd.com/gpu"] == 2 and cont["resources"]["limits"]["amd.com/gpu"] == 2
+            assert "--nproc-per-node=2" in cont["command"][-1]
         for _ in range(4):
             ctx.kube.reconcile()
         run_monitor(ctx)
@@ -151,3 +152,50 @@ def test_failure_restart_then_failed(tmp_path):
         assert c.get(f"/api/v1/jobs/{jid}").json()["updated_at"] == j["updated_at"]
         poll = c.get(f"/api/v1/admin/job/poll/{jid}").json()["status"]
         assert poll["type"] == "Failed" and poll["restart_count"] >= 2
+
+
+def test_mixed_pool_kueue_example_through_the_api(tmp_path):
+    """deploy/kueue/examples (cohort "finetune": adapters + ddp ClusterQueues, cpu / mi355x-pool /
+    mi355x-node flavors) with its device catalogue: 2-GPU LoRA jobs share the 8-GPU adapters pool,
+    8-GPU full fine-tunes take whole nodes from the ddp queue, and each queue admits and queues
+    independently."""
+    import yaml
+
+    from finetune_controller_amd.controlplane.k8s.fake import kueue_quotas_from_manifests
+
+    ex = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "deploy", "kueue", "examples")
+    docs = []
+    for f in ("flavors.yaml", "cluster-queues.yaml", "local-queues.yaml"):
+        docs += list(yaml.safe_load_all(open(os.path.join(ex, f))))
+    flavors = {d["metadata"]["name"] for d in docs if d["kind"] == "ResourceFlavor"}
+    for d in docs:
+        if d["kind"] == "ClusterQueue":
+            assert d["spec"]["cohort"] == "finetune"
+            assert {f["name"] for g in d["spec"]["resourceGroups"] for f in g["flavors"]} <= flavors
+    cqs, lqs = kueue_quotas_from_manifests(docs)
+    assert cqs["adapters"]["amd.com/gpu"] == 8 and cqs["ddp"]["amd.com/gpu"] == 16
+    ctx = AppContext.local(workdir=str(tmp_path), run_processes=False,
+                           config_json=open(os.path.join(ex, "config.mixed.json")).read())
+    ctx.kube.set_kueue(cqs, lqs)
+    assert {ctx.devices.get_worker(n).local_queue for n in ctx.devices.list_workers()} <= set(lqs)
+    ctx.kube.sim_ticks = 50
+    app = create_app(ctx, run_monitor=False, force_auth=False)
+    with TestClient(app) as c:
+        def submit(model, device, i):
+            r = c.post("/api/v1/jobs", data={"job_name": f"j{i}", "model": model, "device": device,
+                                            "task": "causal_lm", "user_id": f"user{i}"})
+            assert r.status_code == 200, r.text
+            return r.json()["job_id"]
+
+        lora = [submit("Llama3-8B-LoRA-2GPU", "mi355x", i) for i in range(5)]
+        full = [submit("Llama3-8B-Full", "mi355x-node", 10 + i) for i in range(3)]
+        for _ in range(4):
+            ctx.kube.reconcile()
+        run_monitor(ctx)
+        st = {j: c.get(f"/api/v1/jobs/{j}").json()["status"] for j in lora + full}
+        assert all(st[j] in ("starting", "running") for j in lora[:4])
+        assert st[lora[4]] == "queued"
+        assert all(st[j] in ("starting", "running") for j in full[:2]) and st[full[2]] == "queued"
+        assert ctx.kube.usage["adapters"]["amd.com/gpu"] == 8 and ctx.kube.usage["ddp"]["amd.com/gpu"] == 16
+        job = ctx.kube.objects[("kubeflow.org", "pytorchjobs", ctx.namespace, full[0])]
+        assert job["metadata"]["labels"]["kueue.x-k8s.io/queue-name"] == "finetune-ddp-queue"
