@@ -1,0 +1,91 @@
+"""Tail padding for sequence lengths that are not a multiple of the flash kernels' 256-row tile
+(ops/attention.py:_FlashPaddedTail).
+
+On the CPU the HIP kernels are replaced by an exact torch implementation with the kernels' calling
+convention (``flash_fwd`` -> (o, lse), ``flash_bwd`` writing dq/dk/dv in place, per-token
+``doc_start`` / ``doc_end`` bounds), so what is tested here is the padding wrapper itself: forward
+and gradients against the unpadded fp64 reference, with windows and packed documents.  The same
+shapes against the real kernels are in tests/test_kernels_gpu.py (``test_flash_tail_lengths``).
+"""
+import math
+
+import pytest
+import torch
+
+from finetune_controller_amd.ops import attention as A
+
+
+class _TorchFlash:
+    """The kernels' contract in torch (fp64 math)."""
+
+    @staticmethod
+    def _mask(B, S, causal, window, doc_start, device):
+        i = torch.arange(S, device=device)
+        allowed = torch.ones(S, S, dtype=torch.bool, device=device)
+        if causal:
+            allowed &= i[None, :] <= i[:, None]
+        if window:
+            allowed &= (i[:, None] - i[None, :]) < window
+        allowed = allowed.expand(B, 1, S, S)
+        if doc_start is not None:
+            ds = doc_start.view(B, S).long()
+            allowed = allowed & (i[None, None, None, :] >= ds[:, None, :, None])
+        return allowed
+
+    def _fwd(self, q, k, v, B, S, H, KV, D, scale, causal, window, doc_start):
+        qh = q.double().reshape(B, S, H, D).transpose(1, 2)
+        kh = k.double().reshape(B, S, KV, D).transpose(1, 2).repeat_interleave(H // KV, 1)
+        vh = v.double().reshape(B, S, KV, D).transpose(1, 2).repeat_interleave(H // KV, 1)
+        s = (qh @ kh.transpose(-1, -2)) * scale
+        s = s.masked_fill(~self._mask(B, S, causal, window, doc_start, q.device), float("-inf"))
+        lse = torch.logsumexp(s, -1)
+        o = (s - lse[..., None]).exp() @ vh
+        return o.transpose(1, 2).reshape(B * S, H * D), lse
+
+    def flash_fwd(self, q, k, v, B, S, H, KV, D, scale, causal, window, out_pad, doc_start):
+        o, lse = self._fwd(q, k, v, B, S, H, KV, D, scale, causal, window, doc_start)
+        buf = torch.empty(B * S, H * D + out_pad, dtype=q.dtype)[:, :H * D]
+        buf.copy_(o)
+        return buf, lse.float()
+
+    def flash_bwd(self, q, k, v, o, do, lse, dq, dk, dv, B, S, H, KV, D, scale, causal, window, doc_start, doc_end):
+        with torch.enable_grad():  # called from inside autograd's backward
+            qq, kk, vv = (t.detach().double().requires_grad_(True) for t in (q, k, v))
+            out, _ = self._fwd(qq, kk, vv, B, S, H, KV, D, scale, causal, window, doc_start)
+            gq, gk, gv = torch.autograd.grad(out, (qq, kk, vv), do.double())
+        dq.copy_(gq)
+        dk.copy_(gk)
+        dv.copy_(gv)
+
+
+@pytest.mark.parametrize("S,window,docs", [(300, 0, False), (1000, 0, False), (300, 64, False), (520, 0, True)])
+def test_padded_tail_matches_reference(monkeypatch, S, window, docs):
+    monkeypatch.setattr(A, "ext", lambda: _TorchFlash())
+    B, H, KV, D = 2, 4, 2, 64
+    torch.manual_seed(0)
+    W = (H + 2 * KV) * D
+    qkv = torch.randn(B * S, W, dtype=torch.float64)
+    seg = None
+    if docs:
+        ids = torch.randint(3, 50, (B, S))
+        ids[0, 100] = ids[0, 333] = ids[1, 17] = 2  # documents end at EOS
+        seg = A.segments_from_eos(ids, 2)
+    scale = 1 / math.sqrt(D)
+    x1 = qkv.clone().requires_grad_(True)
+    out_pad, grad_pad = 64, 32
+    o = A._FlashPaddedTail.apply(x1, B, S, H, KV, D, window, scale, out_pad, grad_pad, seg)
+    assert o.shape == (B * S, H * D) and o.stride(0) == H * D + out_pad  # spare columns for the LoRA GEMM
+    x2 = qkv.clone().requires_grad_(True)
+    ref = A.attention_reference(x2, B, S, H, KV, D, True, window, scale, seg)
+    assert torch.allclose(o, ref.double(), atol=2e-5, rtol=1e-4)  # the reference computes in fp32
+    g = torch.randn_like(ref)
+    o.backward(g.double())
+    ref.backward(g)
+    assert torch.allclose(x1.grad, x2.grad, atol=2e-4, rtol=1e-3)
+
+
+def test_flash_usable_policy():
+    assert A.flash_supported(128, 4096) and not A.flash_supported(128, 4000)
+    assert A.flash_usable(128, 4000, causal=True) and A.flash_usable(64, 77, causal=True)
+    assert not A.flash_usable(128, 4000, causal=False)  # non-causal pads would be attended
+    assert not A.flash_usable(96, 4096, causal=True)

@@ -286,6 +286,45 @@ def test_flash_attention_fwd_bwd(C, B, S, H, KV, D, causal, window):
         assert err <= 2e-2 * mag + 2e-2, (lo, err, mag)
 
 
+@pytest.mark.parametrize("B,S,H,KV,D,window,docs", [
+    (1, 1000, 8, 2, 128, 0, False),
+    (1, 3000, 8, 2, 128, 0, False),
+    (2, 1000, 8, 4, 64, 0, False),
+    (1, 3000, 8, 2, 64, 512, False),
+    (1, 1000, 8, 2, 128, 300, False),
+    (2, 700, 4, 2, 128, 0, True),
+])
+def test_flash_tail_lengths(C, B, S, H, KV, D, window, docs):
+    """S not a multiple of the 256-row tile: attention_packed takes the tail-padded flash path (not
+    SDPA) and matches the fp32 reference, forward and backward."""
+    from finetune_controller_amd.ops import attention as A
+
+    assert not A.flash_supported(D, S) and A.flash_usable(D, S, True)
+    torch.manual_seed(0)
+    W = (H + 2 * KV) * D
+    qkv = bf(torch.randn(B * S, W, device=DEV))
+    seg = None
+    if docs:
+        ids = torch.randint(3, 100, (B, S), device=DEV)
+        ids[0, 211] = ids[0, 650] = ids[1, 300] = 2
+        seg = A.segments_from_eos(ids, 2)
+    scale = 1.0 / math.sqrt(D)
+    ref_in = qkv.float().clone().requires_grad_(True)
+    ref = A.attention_reference(ref_in, B, S, H, KV, D, True, window, scale, docs=seg)
+    x = qkv.clone().requires_grad_(True)
+    out = A.attention_packed(x, B, S, H, KV, D, True, window, scale, out_pad=64, grad_pad=64, docs=seg)
+    assert out.grad_fn is not None and "PaddedTail" in type(out.grad_fn).__name__
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+    dout = bf(torch.randn(B * S, H * D, device=DEV))
+    ref.backward(dout.float())
+    out.backward(dout)
+    g, gr = x.grad.float(), ref_in.grad
+    for lo, hi in ((0, H * D), (H * D, (H + KV) * D), ((H + KV) * D, W)):
+        err = (g[:, lo:hi] - gr[:, lo:hi]).abs().max().item()
+        mag = gr[:, lo:hi].abs().max().item()
+        assert err <= 2e-2 * mag + 2e-2, (lo, err, mag)
+
+
 def test_flash_lse(C):
     torch.manual_seed(1)
     B, S, H, KV, D = 1, 256, 4, 2, 128
