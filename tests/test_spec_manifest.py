@@ -43,7 +43,7 @@ def test_registry_builtins_and_scopes():
     r = ModelRegistry()
     assert {"MNIST", "GPT2-small-FT", "Llama3-8B-LoRA", "Llama3-8B-Full", "Mistral-7B-QLoRA"} <= set(r.names())
     assert r.available_for(None) == r.names()
-    assert r.available_for(["Llama3-8B"]) == ["Llama3-8B-LoRA", "Llama3-8B-Full"]
+    assert r.available_for(["Llama3-8B"]) == ["Llama3-8B-LoRA", "Llama3-8B-LoRA-2GPU", "Llama3-8B-Full"]
     assert r.available_for([]) == []
 
 
