@@ -332,6 +332,10 @@ def create_app(ctx: AppContext, run_monitor: bool | None = None, validator_facto
             model_arguments = inst.training_arguments.model_dump()
             if task != inst.task:
                 raise HTTPException(status_code=400, detail=f"Invalid task ({task.name}) for model ({inst.task.name})")
+            # a spec that declares dataset_required is refused without one here, not as a failed pod later
+            if inst.dataset_info.dataset_required and not (ds.dataset_id or ds.dataset_url or ds.dataset_file):
+                raise HTTPException(status_code=400, detail=f"Model '{model}': dataset is required "
+                                                            "(dataset, dataset_url or dataset_id)")
         except ValidationError as e:
             msgs = [f"{(err['loc'][-1] if err['loc'] else 'unknown field')}: {err['msg']}" for err in e.errors()]
             raise HTTPException(status_code=400, detail="<b class='regular'>Invalid model parameters:</b><br>• "
