@@ -491,7 +491,57 @@ class MemoryDatabase:
             return out
         if op == "$count":
             return [{arg: len(docs)}]
+        if op == "$group":
+            return _group(docs, arg)
         raise NotImplementedError(f"aggregation stage {op}")
+
+
+def _group(docs, spec: dict):
+    """``$group`` with accumulators $sum / $avg / $min / $max / $first / $last / $push (what
+    pymongo's ``count_documents`` sends is ``{"_id": 1, "n": {"$sum": 1}}``)."""
+    groups: dict = {}
+    order = []
+    for d in docs:
+        key = evaluate(spec["_id"], d) if spec["_id"] is not None else None
+        hk = repr(key)
+        if hk not in groups:
+            groups[hk] = {"_id": key, "_acc": {f: [] for f in spec if f != "_id"}}
+            order.append(hk)
+        for f, acc in spec.items():
+            if f == "_id":
+                continue
+            (aop, expr), = acc.items()
+            v = evaluate(expr, d)
+            groups[hk]["_acc"][f].append(None if v is _MISSING else v)
+    out = []
+    for hk in order:
+        g = groups[hk]
+        row = {"_id": g["_id"]}
+        for f, acc in spec.items():
+            if f == "_id":
+                continue
+            (aop, _), = acc.items()
+            vals = g["_acc"][f]
+            nums = [v for v in vals if isinstance(v, (int, float)) and not isinstance(v, bool)]
+            present = [v for v in vals if v is not None]
+            if aop == "$sum":
+                row[f] = sum(nums)
+            elif aop == "$avg":
+                row[f] = sum(nums) / len(nums) if nums else None
+            elif aop == "$min":
+                row[f] = min(present, key=_cmp_key) if present else None
+            elif aop == "$max":
+                row[f] = max(present, key=_cmp_key) if present else None
+            elif aop == "$first":
+                row[f] = vals[0] if vals else None
+            elif aop == "$last":
+                row[f] = vals[-1] if vals else None
+            elif aop == "$push":
+                row[f] = present
+            else:
+                raise NotImplementedError(f"$group accumulator {aop}")
+        out.append(row)
+    return out
 
 
 def _sorted(docs, spec: dict):
