@@ -60,6 +60,7 @@ from ..k8s.client import KubeError
 from ..k8s.queue import pod_events, pod_status
 from ..logs.stream import LogStreamManager
 from ..monitor.reconciler import JobMonitor
+from ..observability import PrometheusMiddleware, get_metrics
 from ..schemas.db import DatabaseStatusEnum, PromotionStatus
 from ..schemas.jobs import (Dataset, DatasetInput, DatasetMeta, Job, JobIdsRequest, JobInput, JobMetaData,
                             PaginatedTableResponse)
@@ -117,6 +118,7 @@ def create_app(ctx: AppContext, run_monitor: bool | None = None, validator_facto
         await ctx.store.close()
 
     app = FastAPI(lifespan=lifespan, title="Finetune Controller (MI355X)")
+    metrics = get_metrics(ctx)
     app.state.ctx = ctx
     app.state.limiter = limiter
     app.state.monitor = monitor
@@ -130,10 +132,18 @@ def create_app(ctx: AppContext, run_monitor: bool | None = None, validator_facto
         app.add_middleware(OpenBridgeAuthMiddleware, settings=s, validator_factory=factory)
     app.add_middleware(CORSMiddleware, allow_origins=s.FRONTEND_URL_CORS, allow_credentials=True,
                        allow_methods=["*"], allow_headers=["*"])
+    app.add_middleware(PrometheusMiddleware, metrics=metrics)  # outermost: sees auth rejections too
+
+    @app.get("/metrics", include_in_schema=False)
+    async def prometheus_metrics():
+        body, ctype = metrics.exposition()
+        return Response(content=body, media_type=ctype)
     app.openapi = custom_openapi_jwt_auth(app, s.API_V1_STR)
 
     @app.exception_handler(HTTPException)
     async def http_exc(request: Request, exc: HTTPException):
+        if request.method == "POST" and request.url.path == f"{s.API_V1_STR}/jobs":
+            metrics.submit_failures.labels(str(exc.status_code)).inc()
         return JSONResponse(status_code=exc.status_code, content={"detail": exc.detail, "status_code": exc.status_code})
 
     @app.exception_handler(RateLimitExceeded)
@@ -345,6 +355,7 @@ def create_app(ctx: AppContext, run_monitor: bool | None = None, validator_facto
         try:
             await task_builder(ctx, job, ds)
             logger.info("job started successfully: %s", job_id)
+            metrics.jobs_submitted.labels(model, str(getattr(device, "value", device))).inc()
             return {"message": "Job started successfully", "job_id": job_id}
         except NotFound as e:
             raise HTTPException(status_code=404, detail=str(e)) from e

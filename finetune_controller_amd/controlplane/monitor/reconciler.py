@@ -22,10 +22,12 @@ import logging
 import os
 import signal
 import socket
+import time
 import uuid
 
 from ..context import AppContext
 from ..k8s.queue import queue_positions
+from ..observability import get_metrics
 from ..schemas.db import DatabaseStatusEnum
 from ..schemas.kubeflow import KubeflowStatusEnum, TrainingJobStatus
 
@@ -56,9 +58,11 @@ class JobMonitor:
     async def reconcile_once(self) -> int:
         ctx = self.ctx
         ns = ctx.namespace
+        t0 = time.perf_counter()
         jobs = await asyncio.to_thread(ctx.kube.list_pytorchjobs, ns)
         queue = await asyncio.to_thread(queue_positions, ctx.kube, ns)
         n = 0
+        by_status: dict[str, int] = {}
         for job in jobs:
             job_id = job["metadata"]["name"]
             st = job.get("status") or {}
@@ -71,6 +75,7 @@ class JobMonitor:
                     not any(c.get("type") == "Running" for c in conds):
                 status = KubeflowStatusEnum.created.value
             mapped = TrainingJobStatus.map_status(status)
+            by_status[mapped.value] = by_status.get(mapped.value, 0) + 1
             prev = await ctx.store.get_job(job_id)
             if prev is None:
                 continue  # not ours (another controller / DB)
@@ -99,6 +104,7 @@ class JobMonitor:
                 await self.delete_job(job_id)
             elif status == KubeflowStatusEnum.failed.value:
                 logger.error("job %s failed: %s", job_id, cond.get("message"))
+        get_metrics(ctx).observe_pass(t0, by_status, len(queue), n)
         return n
 
     async def _process_metrics(self, job_id, info, st, completed: bool):
@@ -127,11 +133,13 @@ class JobMonitor:
         while not self.stop_monitoring:
             try:
                 self.is_leader = await self.ctx.store.acquire_lock(LEASE, self.owner, self.lease_ttl)
+                get_metrics(self.ctx).is_leader.set(1 if self.is_leader else 0)
                 if self.is_leader:
                     await self.reconcile_once()
             except asyncio.CancelledError:
                 raise
             except Exception as e:
+                get_metrics(self.ctx).reconcile_errors.inc()
                 logger.error("error in job monitoring loop: %s", e, exc_info=True)
                 await asyncio.sleep(5)
                 continue
@@ -170,6 +178,12 @@ async def run_service(ctx: AppContext) -> None:
     loop.set_exception_handler(lambda lp, c: (logger.error("caught exception: %s", c.get("exception", c["message"])),
                                               stop.set()))
     await ctx.store.connect()
+    port = int(os.environ.get("MONITOR_METRICS_PORT", "0") or 0)
+    if port:  # Prometheus scrape endpoint of the standalone monitor
+        from prometheus_client import start_http_server
+
+        start_http_server(port, registry=get_metrics(ctx).registry)
+        logger.info("monitor metrics on :%d/metrics", port)
     mon = JobMonitor(ctx)
     await mon.start()
     try:

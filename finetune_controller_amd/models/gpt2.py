@@ -110,9 +110,14 @@ class GPT2ForCausalLM(nn.Module):
         return ops.layer_norm(h, self.lnf_w, self.lnf_b, self.cfg.norm_eps)
 
     def forward(self, input_ids, labels=None, positions=None, n_valid=None, segments=None):
+        B, S = input_ids.shape
+        Sp = ops.model_tile_len(S, self.cfg.head_dim, ops.use_hip(self.wte), self.wte.dtype, self.cfg.max_seq_len)
+        if Sp != S:  # GPU, S off the flash tile: run tile-aligned (ops.attention.model_tile_len)
+            input_ids, labels, positions, segments = ops.pad_batch_to(Sp, input_ids, labels, positions, segments)
         x = self.hidden(input_ids, positions, segments)
         if labels is None:
-            return x @ self.wte.t()
+            logits = x @ self.wte.t()
+            return logits if Sp == S else logits.view(B, Sp, -1)[:, :S].reshape(B * S, -1)
         return ops.fused_linear_cross_entropy(x, self.wte, labels, self.ce_chunk_rows, -100, n_valid)
 
 

@@ -232,7 +232,12 @@ class LlamaForCausalLM(nn.Module):
 
     def forward(self, input_ids: torch.Tensor, labels: torch.Tensor | None = None, positions=None,
                 n_valid: int | None = None, segments=None):
+        B, S = input_ids.shape
+        Sp = ops.model_tile_len(S, self.cfg.head_dim, ops.use_hip(self.embed), self.embed.dtype, self.cfg.max_seq_len)
+        if Sp != S:  # GPU, S off the flash tile: run the whole model tile-aligned (ops.attention.model_tile_len)
+            input_ids, labels, positions, segments = ops.pad_batch_to(Sp, input_ids, labels, positions, segments)
         x = self.hidden(input_ids, positions, segments)
         if labels is None:
-            return x @ self.lm_head.t()
+            logits = x @ self.lm_head.t()
+            return logits if Sp == S else logits.view(B, Sp, -1)[:, :S].reshape(B * S, -1)
         return ops.fused_linear_cross_entropy(x, self.lm_head, labels, self.ce_chunk_rows, -100, n_valid)

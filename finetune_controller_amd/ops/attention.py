@@ -47,6 +47,39 @@ def flash_usable(D: int, S: int, causal: bool) -> bool:
     return FLASH_READY and D in (64, 128) and (S % FLASH_TILE == 0 or causal)
 
 
+def model_tile_len(S: int, D: int, hip: bool, dtype: torch.dtype, max_len: int) -> int:
+    """Sequence length a whole causal LM should run at on the GPU: S rounded up to the flash tile
+    when S is not a multiple of it (and the rounded length stays within the position range).
+
+    Padding at the MODEL input instead of inside attention keeps every kernel on its tile-aligned
+    fast path (T = B*Sp rows for hipBLASLt, the split-T LoRA weight-gradient kernels, native flash):
+    measured at 4 x 4000 tokens, attention-only tail padding ran the step 12 % slower than 4 x 4096
+    (profiles/r2/prof_tail4000_attention_only.md), model-level padding costs the padded tokens'
+    compute only.  Exact for causal models: pads sit at the END of each row, so no real position
+    attends to them, and their labels are ignored."""
+    if not hip or dtype != torch.bfloat16 or D not in (64, 128) or S % FLASH_TILE == 0:
+        return S
+    Sp = -(-S // FLASH_TILE) * FLASH_TILE
+    return Sp if Sp <= max_len else S
+
+
+def pad_batch_to(Sp: int, input_ids: torch.Tensor, labels: torch.Tensor | None = None, positions=None,
+                 segments: "Segments | None" = None, pad_id: int = 0):
+    """Right-pad a [B, S] batch to Sp positions: pad tokens ``pad_id``, labels -100 (ignored by the
+    loss), positions continue, and the pads form one extra document per row when packed."""
+    B, S = input_ids.shape
+    ids = F.pad(input_ids, (0, Sp - S), value=pad_id)
+    if labels is not None:
+        labels = F.pad(labels.reshape(B, S), (0, Sp - S), value=-100)
+    if positions is not None:
+        pos = positions.reshape(-1, S)
+        tail = torch.arange(S, Sp, device=pos.device, dtype=pos.dtype).expand(pos.shape[0], Sp - S)
+        positions = torch.cat([pos, tail], 1).reshape(-1) if positions.dim() == 1 else torch.cat([pos, tail], 1)
+    if segments is not None:
+        segments = _pad_segments(segments, B, S, Sp)
+    return ids, labels, positions, segments
+
+
 def _warn_fallback(reason: str):
     if reason not in _WARNED:
         _WARNED.add(reason)

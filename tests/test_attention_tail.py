@@ -89,3 +89,47 @@ def test_flash_usable_policy():
     assert A.flash_usable(128, 4000, causal=True) and A.flash_usable(64, 77, causal=True)
     assert not A.flash_usable(128, 4000, causal=False)  # non-causal pads would be attended
     assert not A.flash_usable(96, 4096, causal=True)
+
+
+@pytest.mark.parametrize("preset,S,docs", [("llama-tiny", 200, False), ("mistral-tiny", 300, False),
+                                           ("llama-tiny", 200, True), ("gpt2-tiny", 100, False)])
+def test_model_level_tile_padding_is_exact(monkeypatch, preset, S, docs):
+    """The GPU path right-pads whole batches to the 256-row tile (ops.attention.model_tile_len): the
+    loss, its gradients and the logits must equal the unpadded model's."""
+    from finetune_controller_amd import ops
+    from finetune_controller_amd.models import LoRAConfig, build_model
+    from finetune_controller_amd.models.config import get_config
+
+    cfg = get_config(preset)
+    torch.manual_seed(0)
+    B = 2
+    ids = torch.randint(3, cfg.vocab_size, (B, S))
+    if docs:
+        ids[0, 50] = ids[1, 120] = 2
+    labels = torch.roll(ids, -1, 1)
+    labels[:, -1] = -100
+
+    def run(pad: bool):
+        torch.manual_seed(1)  # adapters draw from the global RNG
+        m = build_model(cfg, LoRAConfig(r=4, alpha=8), device="cpu", dtype=torch.float32)
+        m.init_weights(seed=5)
+        for layer in getattr(m, "layers", []):
+            for pair in layer.lora.values():
+                torch.nn.init.normal_(pair.B, std=0.05)
+        if pad:
+            monkeypatch.setattr(ops, "model_tile_len", lambda S_, *a: -(-S_ // 256) * 256)
+        else:
+            monkeypatch.setattr(ops, "model_tile_len", lambda S_, *a: S_)
+        seg = A.segments_from_eos(ids, 2) if docs else None
+        loss = m(ids, labels, n_valid=int((labels != -100).sum()), segments=seg)
+        loss.backward()
+        grads = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+        with torch.no_grad():
+            logits = m(ids, segments=seg)
+        return float(loss), grads, logits
+
+    l0, g0, z0 = run(False)
+    l1, g1, z1 = run(True)
+    assert abs(l0 - l1) < 1e-5 and z0.shape == z1.shape == (B * S, cfg.vocab_size)
+    assert torch.allclose(z0, z1, atol=1e-4, rtol=1e-4)
+    assert g0.keys() == g1.keys() and all(torch.allclose(g0[k], g1[k], atol=1e-5, rtol=1e-4) for k in g0)

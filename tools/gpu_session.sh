@@ -62,6 +62,13 @@ for s in "${STEPS[@]}"; do
       FTC_SHARE_GPU=1 timeout -k 10 500 python bench.py --gpus 2 --model llama3-8b-1l --method full --zero-stage 1 \
         --steps 4 --warmup 2 --comm-ab --launcher-timeout 450 > gpurun_out/rccl2_full.log 2>&1
       fatal $? rccl2_full; grep '^{' gpurun_out/rccl2_full.log | cut -c1-2000 ;;
+    rccl4)  # 4 ranks on the one card (RCCL over loopback sockets), torch + native engines A/B, 1-layer
+      FTC_SHARE_GPU=1 timeout -k 10 500 python bench.py --gpus 4 --model llama3-8b-1l --steps 4 --warmup 2 --comm-ab \
+        --batch-size 2 --launcher-timeout 450 > gpurun_out/rccl4.log 2>&1
+      fatal $? rccl4; grep '^{' gpurun_out/rccl4.log | cut -c1-2000 ;;
+    bench_tail)  # seq_len not a multiple of the 256-row flash tile: tail-padded flash path vs 4096
+      timeout -k 10 600 python bench.py --steps 6 --warmup 2 --seq-len 4000 > gpurun_out/bench_tail.log 2>&1
+      fatal $? bench_tail; grep '^{' gpurun_out/bench_tail.log | cut -c1-400 ;;
     full_fp32)  # full FT, grad accumulation 2: fp32 vs bf16 gradient buffer (cost of the precise mode)
       timeout -k 10 600 python bench.py --method full --steps 4 --warmup 2 --grad-accum 2 --grad-dtype fp32 \
         > gpurun_out/full_fp32.log 2>&1

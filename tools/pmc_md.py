@@ -54,6 +54,21 @@ def load_pass(d):
     return out
 
 
+def _short(name: str) -> str:
+    """Kernel name without namespaces, return type and argument list (templates kept)."""
+    n = name.replace("(anonymous namespace)::", "")
+    if n.startswith("void "):
+        n = n[5:]
+    depth = 0
+    for i, ch in enumerate(n):
+        depth += ch == "<"
+        depth -= ch == ">"
+        if ch == "(" and depth == 0:
+            n = n[:i]
+            break
+    return n[:100]
+
+
 def group(disp, labels, match):
     """Aggregate dispatches per key: the labelled shape (sentinel-split) or the kernel name."""
     agg = defaultdict(lambda: {"n": 0, "ns": 0.0, "c": defaultdict(float)})
@@ -72,7 +87,7 @@ def group(disp, labels, match):
                 continue
             key = shapes[cur]["label"]
         else:
-            key = name.split("(")[0][:90]
+            key = _short(name)
         a = agg[key]
         a["n"] += 1
         a["ns"] += e["ns"] or 0.0
