@@ -749,6 +749,34 @@ extern "C" int ftc_flash_bwd_workspace(int B, int S, int H, int D, long long* by
   return 0;
 }
 
+// Second stream of the calling process's current device for the dQ kernel (FTC_FLASH_BWD_CONCURRENT=1):
+// dK/dV and dQ only share read-only inputs and the delta workspace, so dQ could fill the CUs that
+// dK/dV's causal tail leaves idle.  Measured at the Llama-3-8B layer shape: 2.017 vs 2.016 ms for the
+// backward and 35.3k vs 35.4k tok/s end to end (profiles/r2/s8_*conc*.log) -- dK/dV holds every CU's
+// registers until its last workgroups retire, so the dQ workgroups find no room earlier; off by default.  Fork / join by events keeps the pair one unit on the caller's
+// stream (and capturable in a hipGraph).  One process drives one GPU here; a per-device table
+// still keeps a multi-device caller correct.
+namespace {
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+SideStream& side_stream() {
+  static SideStream per_dev[64];
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  SideStream& ss = per_dev[dev & 63];
+  if (ss.s == nullptr) {
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    (void)hipStreamCreateWithPriority(&ss.s, hipStreamNonBlocking, lo);
+    (void)hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&ss.join, hipEventDisableTiming);
+  }
+  return ss;
+}
+}  // namespace
+
 extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
                              const float* lse, void* dq, void* dk, void* dv, void* workspace, int B, int S, int H,
                              int KV, int D, long long q_rs, long long kv_rs, long long o_rs, long long do_rs,
@@ -793,18 +821,35 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
     const char* e = getenv("FTC_FLASH_DKDV_DIST");
     return !(e && e[0] == '2');
   }();
+  static const bool concurrent = [] {
+    const char* e = getenv("FTC_FLASH_BWD_CONCURRENT");
+    return e && e[0] == '1';
+  }();
+  hipStream_t qs = stream;
+  SideStream* ss = nullptr;
   if (D == 128) {
     hipLaunchKernelGGL(bwd_delta_kernel<128>, dim3(grid_d), dim3(256), 0, stream, a);
-    launch_dkdv<128>(a, g_kv, dkdv_waves, pp, dist3, stream);
-    if (occ == 1) {
-      hipLaunchKernelGGL((bwd_dq_kernel<128, 1>), dim3(g_q), dim3(256), 0, stream, a);
-    } else {
-      hipLaunchKernelGGL((bwd_dq_kernel<128, 2>), dim3(g_q), dim3(256), 0, stream, a);
-    }
   } else {
     hipLaunchKernelGGL(bwd_delta_kernel<64>, dim3(grid_d), dim3(256), 0, stream, a);
+  }
+  if (concurrent) {  // dK/dV first on the caller's stream, dQ on the side stream after the delta pass
+    ss = &side_stream();
+    qs = ss->s;
+    if (hipEventRecord(ss->fork, stream) != hipSuccess || hipStreamWaitEvent(qs, ss->fork, 0) != hipSuccess) return -2;
+  }
+  if (D == 128) {
+    launch_dkdv<128>(a, g_kv, dkdv_waves, pp, dist3, stream);
+    if (occ == 1) {
+      hipLaunchKernelGGL((bwd_dq_kernel<128, 1>), dim3(g_q), dim3(256), 0, qs, a);
+    } else {
+      hipLaunchKernelGGL((bwd_dq_kernel<128, 2>), dim3(g_q), dim3(256), 0, qs, a);
+    }
+  } else {
     launch_dkdv<64>(a, g_kv, dkdv_waves, pp, dist3, stream);
-    hipLaunchKernelGGL((bwd_dq_kernel<64, 2>), dim3(g_q), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((bwd_dq_kernel<64, 2>), dim3(g_q), dim3(256), 0, qs, a);
+  }
+  if (ss) {
+    if (hipEventRecord(ss->join, qs) != hipSuccess || hipStreamWaitEvent(stream, ss->join, 0) != hipSuccess) return -2;
   }
   return (int)hipGetLastError();
 }

@@ -62,6 +62,18 @@ for s in "${STEPS[@]}"; do
       FTC_SHARE_GPU=1 timeout -k 10 500 python bench.py --gpus 2 --model llama3-8b-1l --method full --zero-stage 1 \
         --steps 4 --warmup 2 --comm-ab --launcher-timeout 450 > gpurun_out/rccl2_full.log 2>&1
       fatal $? rccl2_full; grep '^{' gpurun_out/rccl2_full.log | cut -c1-2000 ;;
+    conc_ab)  # flash backward: dQ on a side stream concurrent with dK/dV (FTC_FLASH_BWD_CONCURRENT) -- A/B
+      timeout -k 10 300 python tools/bench_attention.py > gpurun_out/attn_conc0.log 2>&1
+      fatal $? attn_conc0; grep -v amdgpu gpurun_out/attn_conc0.log | tail -3
+      FTC_FLASH_BWD_CONCURRENT=1 timeout -k 10 300 python tools/bench_attention.py > gpurun_out/attn_conc1.log 2>&1
+      fatal $? attn_conc1; grep -v amdgpu gpurun_out/attn_conc1.log | tail -3
+      FTC_FLASH_BWD_CONCURRENT=1 timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py -m gpu -x -q -k "flash or llama_lora or graph" \
+        > gpurun_out/pytest_conc1.log 2>&1
+      fatal $? pytest_conc1; tail -2 gpurun_out/pytest_conc1.log
+      FTC_FLASH_BWD_CONCURRENT=1 timeout -k 10 600 python bench.py --steps 10 --warmup 3 > gpurun_out/bench_conc1.log 2>&1
+      fatal $? bench_conc1; grep '^{' gpurun_out/bench_conc1.log | cut -c1-200
+      timeout -k 10 600 python bench.py --steps 10 --warmup 3 > gpurun_out/bench_conc0.log 2>&1
+      fatal $? bench_conc0; grep '^{' gpurun_out/bench_conc0.log | cut -c1-200 ;;
     rccl4)  # 4 ranks on the one card (RCCL over loopback sockets), torch + native engines A/B, 1-layer
       FTC_SHARE_GPU=1 timeout -k 10 500 python bench.py --gpus 4 --model llama3-8b-1l --steps 4 --warmup 2 --comm-ab \
         --batch-size 2 --launcher-timeout 450 > gpurun_out/rccl4.log 2>&1
