@@ -62,6 +62,16 @@ for s in "${STEPS[@]}"; do
       FTC_SHARE_GPU=1 timeout -k 10 500 python bench.py --gpus 2 --model llama3-8b-1l --method full --zero-stage 1 \
         --steps 4 --warmup 2 --comm-ab --launcher-timeout 450 > gpurun_out/rccl2_full.log 2>&1
       fatal $? rccl2_full; grep '^{' gpurun_out/rccl2_full.log | cut -c1-2000 ;;
+    pipe_ab)  # flash forward in-wave software pipeline (FTC_FLASH_FWD_PIPE=1|2) -- numerics, then A/B
+      for p in 1 2; do
+        FTC_FLASH_FWD_PIPE=$p timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py -m gpu -x -q \
+          -k "flash or llama_lora or packed or tail or family" > gpurun_out/pytest_pipe$p.log 2>&1
+        fatal $? pytest_pipe$p; tail -2 gpurun_out/pytest_pipe$p.log
+      done
+      for p in 0 1 2 0 1 2; do
+        FTC_FLASH_FWD_PIPE=$p timeout -k 10 300 python tools/bench_attention.py --rounds 3 > gpurun_out/attn_pipe$p.log 2>&1
+        fatal $? attn_pipe$p; grep -v amdgpu gpurun_out/attn_pipe$p.log | tail -1 | cut -c1-240
+      done ;;
     conc_ab)  # flash backward: dQ on a side stream concurrent with dK/dV (FTC_FLASH_BWD_CONCURRENT) -- A/B
       timeout -k 10 300 python tools/bench_attention.py > gpurun_out/attn_conc0.log 2>&1
       fatal $? attn_conc0; grep -v amdgpu gpurun_out/attn_conc0.log | tail -3
