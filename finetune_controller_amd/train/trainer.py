@@ -448,8 +448,13 @@ class Trainer:
             files = ckpt.save_adapter(self.model, out, self.cfg.name, self.lora)
         else:
             files = ckpt.save_full(self.model, out)
+        runtime = {"kernels": ops.kernel_mode(), "device": str(self.device), "world_size": self.info.world_size,
+                   "dist_backend": self.info.backend, "torch": torch.__version__,
+                   "hip": getattr(torch.version, "hip", None),
+                   "gpu": torch.cuda.get_device_name(self.device) if self.device.type == "cuda" else None}
         with open(os.path.join(out, "training_config.json"), "w") as f:
-            json.dump({"train": asdict(self.tc), "model": self.cfg.to_dict()}, f, indent=2, default=str)
+            json.dump({"train": asdict(self.tc), "model": self.cfg.to_dict(), "runtime": runtime}, f, indent=2,
+                      default=str)
         return files
 
     def close(self):
