@@ -269,6 +269,9 @@ def main(argv=None) -> int:
     comm = {}
     if n > 1:
         comm["torch"] = _bucket_busbw(info, a.bucket_mb)
+        if cuda:  # bucket-size sweep on the same process group: xGMI data for tuning bucket_mb
+            comm["sweep_busbw_GBps"] = {str(mb): _bucket_busbw(info, mb, iters=5)["busbw_GBps"]
+                                        for mb in (4, 16, 64, 256)}
         if cuda and (a.comm_ab or a.comm_engine == "native"):
             try:
                 native = tr.ddp._native
