@@ -199,3 +199,45 @@ def test_mixed_pool_kueue_example_through_the_api(tmp_path):
         assert ctx.kube.usage["adapters"]["amd.com/gpu"] == 8 and ctx.kube.usage["ddp"]["amd.com/gpu"] == 16
         job = ctx.kube.objects[("kubeflow.org", "pytorchjobs", ctx.namespace, full[0])]
         assert job["metadata"]["labels"]["kueue.x-k8s.io/queue-name"] == "finetune-ddp-queue"
+
+
+class GPT2TinyFT2Node(GPT2TinyFT):
+    """Two replicas (Master + 1 Worker): the operator-injected PET_* rendezvous, torchrun per pod."""
+
+    name: str = "GPT2-tiny-FT-2node"
+    cluster_nodes: int = Field(default=2, ge=1, description="Total number of workers for training")
+
+
+@pytest.mark.slow
+def test_multi_node_job_trains_data_parallel_across_pods(tmp_path):
+    """cluster_nodes=2 through the API: the FakeCluster starts Master and Worker pods with the
+    training-operator's PET_NNODES / PET_NODE_RANK / PET_MASTER_* env, each pod's torchrun joins one
+    2-rank gloo group, and the job completes with metrics reporting world size 2."""
+    ctx = AppContext.local(workdir=str(tmp_path), run_processes="cpu")
+    ctx.registry.register(GPT2TinyFT2Node)
+    ctx.kube.sync_interval = 0.2
+    app = create_app(ctx, run_monitor=False, force_auth=False)
+    with TestClient(app) as c:
+        files = {"dataset": ("corpus.txt", ("pack my box with five dozen liquor jugs\n" * 300).encode(), "text/plain")}
+        r = c.post("/api/v1/jobs", data={"job_name": "2node", "model": "GPT2-tiny-FT-2node", "device": "cpu",
+                                        "task": "causal_lm"}, files=files)
+        assert r.status_code == 200, r.text
+        jid = r.json()["job_id"]
+        job = ctx.kube.objects[("kubeflow.org", "pytorchjobs", ctx.namespace, jid)]
+        assert job["spec"]["pytorchReplicaSpecs"]["Worker"]["replicas"] == 1
+        cmd = job["spec"]["pytorchReplicaSpecs"]["Master"]["template"]["spec"]["containers"][0]["command"][-1]
+        assert "--nnodes=${PET_NNODES:-1}" in cmd and "--node-rank=${PET_NODE_RANK:-0}" in cmd
+        ctx.kube.start(tick=0.1)
+        try:
+            def done():
+                run_monitor(ctx)
+                return c.get(f"/api/v1/jobs/{jid}").json()["status"] in ("completed", "failed")
+
+            wait_for(done, timeout=300, step=1.5)
+        finally:
+            ctx.kube.stop()
+        logs = "\n".join("\n".join(p.logs) for p in ctx.kube.pods.values()) + \
+            "\n".join("\n".join(v) for v in ctx.kube.deleted_pod_logs.values())
+        assert c.get(f"/api/v1/jobs/{jid}").json()["status"] == "completed", logs[-3000:]
+        m = c.get(f"/api/v1/jobs/{jid}/metrics").json()["metrics"]
+        assert m and all(int(row["world_size"]) == 2 for row in m), m[:2]
