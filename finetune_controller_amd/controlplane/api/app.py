@@ -39,7 +39,6 @@ from __future__ import annotations
 import asyncio
 import json
 import logging
-import os
 import shutil
 from contextlib import asynccontextmanager
 from datetime import datetime, timezone

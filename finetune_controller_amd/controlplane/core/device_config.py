@@ -16,7 +16,6 @@ from __future__ import annotations
 
 import json
 import logging
-import re
 from enum import Enum
 
 from pydantic import BaseModel

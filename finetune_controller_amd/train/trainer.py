@@ -19,7 +19,6 @@ from __future__ import annotations
 
 import json
 import logging
-import math
 import os
 import time
 from dataclasses import asdict, dataclass, field

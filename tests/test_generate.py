@@ -1,8 +1,6 @@
 """KV-cache generation (models.generate): greedy decoding with the cache equals greedy decoding by
 re-running the whole sequence, for several prompts of different lengths at once (sliding window
 included); decode attention reference vs a direct softmax."""
-import math
-
 import pytest
 import torch
 

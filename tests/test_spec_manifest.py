@@ -1,7 +1,6 @@
 """Job-spec layer: model registry, spec type guard, run_cmd rendering, PyTorchJob manifest golden checks,
 Kubeflow -> DB status mapping (SURVEY.md §4 "[new] Unit")."""
 import pytest
-from pydantic import Field
 
 from finetune_controller_amd.controlplane.context import AppContext
 from finetune_controller_amd.controlplane.core.config import Settings
@@ -11,8 +10,8 @@ from finetune_controller_amd.controlplane.k8s.manifest import build_pytorchjob_m
 from finetune_controller_amd.controlplane.schemas.db import DatabaseStatusEnum
 from finetune_controller_amd.controlplane.schemas.jobs import JobInput
 from finetune_controller_amd.controlplane.schemas.kubeflow import KubeflowStatusEnum, TrainingJobStatus
-from finetune_controller_amd.controlplane.spec.finetuning import (BaseFineTuneModel, TrainingArguments,
-                                                                  TrainingFramework, TrainingTask)
+from finetune_controller_amd.controlplane.spec.finetuning import (  # noqa: F401 (used by exec'd spec sources)
+    BaseFineTuneModel, TrainingArguments, TrainingFramework, TrainingTask)
 from finetune_controller_amd.controlplane.spec.registry import ModelRegistry
 
 CFG = """{
