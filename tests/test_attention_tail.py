@@ -126,7 +126,7 @@ def test_model_level_tile_padding_is_exact(monkeypatch, preset, S, docs):
         grads = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
         with torch.no_grad():
             logits = m(ids, segments=seg)
-        return float(loss), grads, logits
+        return loss.detach().item(), grads, logits
 
     l0, g0, z0 = run(False)
     l1, g1, z1 = run(True)
