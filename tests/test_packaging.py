@@ -41,3 +41,19 @@ def test_packages_cover_the_code():
         if rel.endswith("spec.custom"):  # user model specs: data files, imported by path
             continue
         assert rel in pkgs, f"{rel} has .py files but no __init__.py (not packaged)"
+
+
+def test_dockerfile_copy_sources_survive_dockerignore():
+    """Every COPY source of deploy/docker/* exists and is not excluded from the build context."""
+    import fnmatch
+    import glob
+
+    ignore = [ln.strip().rstrip("/") for ln in open(os.path.join(ROOT, ".dockerignore"))
+              if ln.strip() and not ln.startswith("#")]
+    for df in glob.glob(os.path.join(ROOT, "deploy", "docker", "Dockerfile.*")):
+        for ln in open(df):
+            if not ln.startswith("COPY "):
+                continue
+            for src in ln.split()[1:-1]:
+                assert os.path.exists(os.path.join(ROOT, src)), (df, src)
+                assert not any(fnmatch.fnmatch(src, pat) or src.split("/")[0] == pat for pat in ignore), (df, src)
