@@ -331,3 +331,54 @@ def test_kubeconfig_discovery(tmp_path, monkeypatch):
     monkeypatch.setenv("KUBERNETES_SERVICE_HOST", "10.96.0.1")
     monkeypatch.setenv("KUBERNETES_SERVICE_PORT", "443")
     assert kc.HttpKubeClient._discover(None) == ("https://10.96.0.1:443", "sa-token", str(sa / "ca.crt"), None)
+
+
+def _rbac_allows(rules, group, resource, verb, name=None) -> bool:
+    for r in rules:
+        if group in r["apiGroups"] and resource in r["resources"] and verb in r["verbs"]:
+            if "resourceNames" not in r or name in r["resourceNames"]:
+                return True
+    return False
+
+
+def test_rbac_role_covers_every_request_the_control_plane_makes():
+    """deploy/k8s/rbac.yaml is least-privilege (namespaced Role, not the reference's cluster-admin):
+    every request HttpKubeClient issues -- mapped to (apiGroup, resource[/subresource], verb,
+    resourceName) by the Kubernetes REST conventions -- must be allowed by it."""
+    import os
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    role = next(d for d in yaml.safe_load_all(open(os.path.join(root, "deploy", "k8s", "rbac.yaml")))
+                if d and d["kind"] == "Role")
+    env = dict(ln.split("#")[0].strip().split("=", 1) for ln in open(os.path.join(root, "deploy", ".env.example"))
+               if "=" in ln.split("#")[0])
+    seen = []
+
+    def handler(req: httpx.Request):
+        seen.append((req.method, req.url.path, req.url.params.get("follow")))
+        if req.url.path.endswith("/log"):
+            return httpx.Response(200, text="x\n")
+        return httpx.Response(200, json={"items": [], "data": {}, "metadata": {"name": "n"}})
+
+    k = kc.HttpKubeClient("https://api:6443", token="t", transport=httpx.MockTransport(handler))
+    ns = "finetune"
+    k.list_pytorchjobs(ns), k.get_pytorchjob(ns, "j"), k.create_pytorchjob(ns, {"metadata": {"name": "j"}})
+    k.delete_pytorchjob(ns, "j"), k.list_workloads(ns), k.list_pods(ns, "a=b"), k.read_pod(ns, "p")
+    k.read_pod_log(ns, "p", container="pytorch"), list(k.stream_pod_log(ns, "p", container="pytorch"))
+    k.list_events(ns), k.read_secret(env["AWS_SECRET_NAME"], ns)
+    verbs = {"GET": "get", "POST": "create", "DELETE": "delete", "PATCH": "patch", "PUT": "update"}
+    for method, path, follow in seen:
+        parts = path.strip("/").split("/")
+        if parts[0] == "api":  # /api/v1/namespaces/{ns}/{resource}[/{name}[/{sub}]]
+            group, rest = "", parts[4:]
+        else:  # /apis/{group}/{version}/namespaces/{ns}/{resource}[/{name}[/{sub}]]
+            group, rest = parts[1], parts[5:]
+        resource = rest[0] + (f"/{rest[2]}" if len(rest) > 2 else "")
+        name = rest[1] if len(rest) > 1 else None
+        verb = verbs[method]
+        if method == "GET" and name is None:
+            verb = "list"
+        if follow == "true":
+            verb = "get"  # a followed log is still a get on pods/log
+        assert _rbac_allows(role["rules"], group, resource, verb, name), (method, path, group, resource, verb, name)
+    assert len(seen) == 11
