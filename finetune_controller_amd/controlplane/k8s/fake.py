@@ -135,6 +135,7 @@ class FakeCluster(KubeClient):
         self._thread = None
         self._stop = threading.Event()
         self._fail_next: set[str] = set()
+        self._fault_env: dict[str, dict[str, str]] = {}
         self.history: list[tuple[str, str]] = []  # (job, condition) transitions, for tests
         self.deleted_pod_logs: dict[str, list[str]] = {}  # logs of pods removed with their job
 
@@ -258,6 +259,20 @@ class FakeCluster(KubeClient):
 
     def fail_next(self, job_name: str):
         self._fail_next.add(job_name)
+
+    def inject_fault(self, job_name: str, fault: str | None = None, collective_timeout_s: float | None = None,
+                     step_timeout_s: float | None = None):
+        """Worker-side faults for a job's processes (``utils.faults``): ``fault`` is an ``FTC_FAULT``
+        spec -- ``crash@3``, ``oom@2:rank=1``, ``hang@2:rank=1`` (a lost RCCL peer) -- fired once per
+        job; the timeouts are the worker's failure detectors (``FTC_COLLECTIVE_TIMEOUT_S``,
+        ``FTC_STEP_TIMEOUT_S``).  Applies to every pod (re)started after the call."""
+        env = self._fault_env.setdefault(job_name, {})
+        if fault:
+            env["FTC_FAULT"] = fault
+        if collective_timeout_s is not None:
+            env["FTC_COLLECTIVE_TIMEOUT_S"] = str(collective_timeout_s)
+        if step_timeout_s is not None:
+            env["FTC_STEP_TIMEOUT_S"] = str(step_timeout_s)
 
     # ------------------------------------------------------------------ reconciliation
     def start(self, tick: float = 0.2):
@@ -509,6 +524,7 @@ class FakeCluster(KubeClient):
         for e in main.get("env", []):
             env[e["name"]] = str(e.get("value", ""))
         env.update(getattr(p, "env_extra", {}))
+        env.update(self._fault_env.get(p.job, {}))
         env["PYTHONPATH"] = REPO_ROOT + os.pathsep + env.get("PYTHONPATH", "")
         env["PYTHONUNBUFFERED"] = "1"
         env.pop("NCCL_DEBUG", None)

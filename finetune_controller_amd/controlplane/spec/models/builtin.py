@@ -124,6 +124,9 @@ class LMTrainingArguments(TrainingArguments):
     eval_holdout: float = Field(default=0.01, gt=0, description="Held-out share of the dataset (>= 1: windows)")
     pack_documents: bool = Field(default=False, description="Packed documents attend only within themselves")
     completion_only: bool = Field(default=False, description="prompt/completion data: loss on completions only")
+    step_timeout: float = Field(default=0.0, ge=0,
+                                description="Fail the worker (exit 124) when no step finishes for this many seconds "
+                                            "(0 = off); the job then restarts from its last checkpoint")
 
 
 class LoRAArguments(LMTrainingArguments):

@@ -256,15 +256,28 @@ def latest_resume(ckpt_dir: str) -> str | None:
     c = glob.glob(os.path.join(ckpt_dir, "checkpoint_step*.pt"))
     if not c:
         return None
-    return max(c, key=lambda p: int(re.search(r"checkpoint_step(\d+)\.pt$", p).group(1)))
+    return max(c, key=resume_step)
 
 
-@torch.no_grad()
-def load_resume(path: str, opt) -> dict:
+def resume_step(path: str) -> int:
+    return int(re.search(r"checkpoint_step(\d+)\.pt$", path).group(1))
+
+
+def read_resume(path: str) -> dict:
     st = torch.load(path, map_location="cpu", weights_only=True)
     if "params" not in st:
         raise ValueError(f"{os.path.basename(path)}: resume checkpoint predates the compact layout; "
                          "resume it with the build, world size and ZeRO setting that wrote it")
+    return st
+
+
+@torch.no_grad()
+def load_resume(path: str, opt) -> dict:
+    return apply_resume(read_resume(path), opt)
+
+
+@torch.no_grad()
+def apply_resume(st: dict, opt) -> dict:
     opt.import_params(st["params"])
     # compact state: the optimizer scatters it into its own layout (a sharded one keeps its part)
     opt.load_state_dict(st["opt"])

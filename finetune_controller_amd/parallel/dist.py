@@ -34,7 +34,12 @@ class DistInfo:
 
 
 def init_distributed(device_type: str = "auto", timeout_s: int = 1800) -> DistInfo:
-    """Initialise torch.distributed when WORLD_SIZE > 1; bind this rank to its GPU."""
+    """Initialise torch.distributed when WORLD_SIZE > 1; bind this rank to its GPU.
+
+    ``FTC_COLLECTIVE_TIMEOUT_S`` overrides ``timeout_s``: a collective a lost peer never joins aborts
+    the rank (RCCL watchdog) or raises (gloo) after that long, so the job fails over to its restart
+    path instead of holding its GPUs (``utils.faults``)."""
+    timeout_s = int(float(os.environ.get("FTC_COLLECTIVE_TIMEOUT_S") or timeout_s))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -102,6 +107,53 @@ def broadcast_params_(params, info: DistInfo, src: int = 0):
         return
     for p in params:
         dist.broadcast(p.data, src=src)
+
+
+_TENSOR = "__ftc_tensor__"
+
+
+def broadcast_state(obj, info: DistInfo, src: int = 0):
+    """Broadcast a nested dict / list of CPU tensors and plain values from rank ``src``; every rank
+    returns the same structure with CPU tensors.
+
+    The resume path of ranks that cannot read ``src``'s checkpoint file (pod-local volumes of a
+    multi-node job).  The structure travels pickled once (``broadcast_object_list`` -- our own state,
+    rank to rank); each tensor is one broadcast on the group's device, so a full fine-tune's
+    optimizer state never has to exist as a single pickled blob."""
+    if not info.distributed:
+        return obj
+    tensors = []
+
+    def skel(o):
+        if torch.is_tensor(o):
+            tensors.append(o)
+            return (_TENSOR, len(tensors) - 1, tuple(o.shape), o.dtype)
+        if isinstance(o, dict):
+            return {k: skel(v) for k, v in o.items()}
+        if isinstance(o, (list, tuple)):
+            return type(o)(skel(v) for v in o)
+        return o
+
+    box = [skel(obj) if info.rank == src else None]
+    dist.broadcast_object_list(box, src=src, device=info.device if info.backend == "nccl" else None)
+    dev = info.device if info.backend == "nccl" else torch.device("cpu")
+
+    def fill(o):
+        if isinstance(o, tuple) and len(o) == 4 and o[0] == _TENSOR:
+            _, i, shape, dtype = o
+            if info.rank == src:
+                t = tensors[i].detach().to(dev).contiguous()
+            else:
+                t = torch.empty(shape, dtype=dtype, device=dev)
+            dist.broadcast(t, src=src)
+            return t.cpu()
+        if isinstance(o, dict):
+            return {k: fill(v) for k, v in o.items()}
+        if isinstance(o, (list, tuple)):
+            return type(o)(fill(v) for v in o)
+        return o
+
+    return fill(box[0])
 
 
 def destroy(info: DistInfo):

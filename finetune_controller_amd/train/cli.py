@@ -64,6 +64,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--eval-batches", type=int, default=4, help="micro-batches per rank per evaluation")
     ap.add_argument("--eval-holdout", type=float, default=0.01,
                     help="held-out share of the dataset windows (>= 1: a window count)")
+    ap.add_argument("--step-timeout", type=float, default=0.0,
+                    help="exit 124 when no step / eval / checkpoint finishes for this many seconds (0: off; "
+                         "FTC_STEP_TIMEOUT_S overrides)")
     return ap
 
 
@@ -81,7 +84,8 @@ def config_from_args(a) -> TrainConfig:
                        dtype=a.dtype, device=a.device, timers=a.timers, profile_steps=a.profile_steps,
                        eval_every=a.eval_every, eval_batches=a.eval_batches, eval_holdout=a.eval_holdout,
                        pack_documents=a.pack_documents, eos_id=a.eos_id,
-                       completion_only=a.completion_only, graph=a.graph)
+                       completion_only=a.completion_only, graph=a.graph,
+                       step_timeout_s=a.step_timeout)
 
 
 def main(argv=None) -> int:

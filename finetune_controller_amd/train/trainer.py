@@ -10,7 +10,9 @@ honours that image's contract with the controller:
   ``/root/reference/app/utils/stream_logger.py:404-418``);
 * flat, uniquely named artifacts matching the model's ``store_asset_patterns``;
 * restart-safe: resumes from the newest ``checkpoint_step*.pt`` (backoffLimit restarts,
-  ``/root/reference/app/jobs/kubeflow/PyTorchJobDeployer.py:183``).
+  ``/root/reference/app/jobs/kubeflow/PyTorchJobDeployer.py:183``) -- rank 0's choice, broadcast to
+  ranks whose volume does not hold it (multi-node pods each have their own);
+* failure detection: collective timeout, step watchdog, injectable faults (``utils.faults``).
 
 Distributed: one process per GPU; gradients of the flat buffer are all-reduced in buckets
 overlapped with backward (``parallel.ddp``); the optimizer averages via its device-side scale.
@@ -30,6 +32,7 @@ from ..models import LoRAConfig, build_model, get_config
 from ..models import checkpoint as ckpt
 from ..parallel import dist as pdist
 from ..parallel.ddp import GradBucketer
+from ..utils.faults import FaultInjector, StepWatchdog
 from ..utils.metrics import MetricsCSV
 from .data import EvalWindows, PackedTokenDataset, SyntheticTokens, Tokenizer
 from .optim import FlatAdamW, ShardedFlatAdamW, lr_at
@@ -86,6 +89,7 @@ class TrainConfig:
     eos_id: int = -1  # -1: the dataset tokenizer's EOS (tokenizer.json, or the byte-level fallback's 2)
     completion_only: bool = False  # prompt/completion records: loss on the completion tokens only
     synthetic_doc_len: int = 0  # synthetic data: EOS every that many tokens (packed-document benchmarks)
+    step_timeout_s: float = 0.0  # >0: exit 124 when no step / eval / save finishes for that long (FTC_STEP_TIMEOUT_S)
 
     def lora_config(self) -> LoRAConfig | None:
         if self.method not in ("lora", "qlora"):
@@ -350,12 +354,15 @@ class Trainer:
         os.makedirs(tc.checkpoint_path, exist_ok=True)
         total = self.total_steps()
         start = 0
-        if tc.resume and (rp := ckpt.latest_resume(tc.checkpoint_path)):
-            st = ckpt.load_resume(rp, self.opt)
+        st = self._resume_state() if tc.resume else None
+        if st is not None:
+            ckpt.apply_resume(st, self.opt)
             start = int(st["step"])
             self.data().load_state(st.get("data", {}))
             if self.is_main:
-                log.info("resumed from %s at step %d", os.path.basename(rp), start)
+                log.info("resumed from checkpoint_step%d.pt", start)
+        faults = FaultInjector.from_env(self.info.rank, tc.checkpoint_path)
+        self.watchdog = watchdog = StepWatchdog.from_env(tc.step_timeout_s, self.info.rank)
         metrics = MetricsCSV(os.path.join(tc.checkpoint_path, "metrics.csv"), enabled=self.is_main,
                              resume=start > 0)
         tok_per_step = tc.batch_size * tc.seq_len * tc.grad_accum * self.info.world_size
@@ -372,6 +379,7 @@ class Trainer:
         losses = []
         prof = None
         for step in range(start, total):
+            faults.maybe_fire(step)
             lr = lr_at(step, tc.lr, tc.warmup_steps, total, tc.schedule)
             if tc.profile_steps and step == start + 2 and prof is None:
                 from torch.profiler import ProfilerActivity, profile
@@ -387,6 +395,7 @@ class Trainer:
                 prof.export_chrome_trace(os.path.join(tc.checkpoint_path, f"trace_rank{self.info.rank}.json"))
                 prof = False
             self.step = step + 1
+            watchdog.beat(f"step {self.step}")
             if self.step % tc.log_interval == 0 or self.step == total:
                 sync()
                 dt = time.perf_counter() - t0
@@ -412,6 +421,7 @@ class Trainer:
                 t0 = time.perf_counter()
             if tc.eval_every and (self.step % tc.eval_every == 0 or self.step == total):
                 ev_loss = self.evaluate()
+                watchdog.beat(f"eval after step {self.step}")
                 if ev_loss is not None:
                     last["eval_loss"] = round(ev_loss, 6)
                     if self.is_main:
@@ -421,11 +431,37 @@ class Trainer:
                               f"eval_loss {ev_loss:.4f}", flush=True)
             if tc.save_every and self.step % tc.save_every == 0 and self.step < total:
                 self.save_resume()
+                watchdog.beat(f"checkpoint at step {self.step}")
         metrics.close()
         if tc.save_model:
             self.save_artifacts()
         pdist.barrier(self.info)
+        watchdog.close()
         return last
+
+    def _resume_state(self) -> dict | None:
+        """The resume state every rank starts from: rank 0's newest ``checkpoint_step*.pt`` (only rank
+        0 writes them).  Ranks that see the same file read it; when any rank cannot (pod-local volumes
+        of a multi-node job) rank 0 broadcasts the state instead."""
+        rp = ckpt.latest_resume(self.tc.checkpoint_path)
+        if not self.info.distributed:
+            return ckpt.read_resume(rp) if rp else None
+        import torch.distributed as dist
+
+        dev = self.info.device if self.info.backend == "nccl" else torch.device("cpu")
+        k = torch.tensor([ckpt.resume_step(rp) if rp else -1], dtype=torch.int64, device=dev)
+        dist.broadcast(k, src=0)
+        k = int(k.item())
+        if k < 0:
+            return None
+        mine = os.path.join(self.tc.checkpoint_path, f"checkpoint_step{k}.pt")
+        have = torch.tensor([int(os.path.exists(mine))], dtype=torch.int64, device=dev)
+        dist.all_reduce(have, op=dist.ReduceOp.MIN)
+        if int(have.item()):
+            return ckpt.read_resume(mine)
+        if self.is_main:
+            log.info("checkpoint_step%d.pt is not on every rank's volume: broadcasting it", k)
+        return pdist.broadcast_state(ckpt.read_resume(mine) if self.is_main else None, self.info)
 
     def save_resume(self):
         opt_state = self.opt.state_dict()  # collective under ZeRO-1 (gathers the sharded state)
@@ -457,5 +493,8 @@ class Trainer:
         return files
 
     def close(self):
+        wd = getattr(self, "watchdog", None)
+        if wd is not None:
+            wd.close()
         self.ddp.close()
         pdist.destroy(self.info)
