@@ -33,6 +33,7 @@ int ftc_swiglu_bwd_wgrad(const void* da, long long da_rs, const void* gu, void* 
 int ftc_tail_gemm(void* x, long long ldx, long long rows, int K, const void* Bm, long long ldb, int nct, int Rp,
                   hipStream_t stream);
 int ftc_transpose(const void* x, long long ldx, void* y, long long ldy, int R, int C, hipStream_t stream);
+int ftc_copy2d_batched(const void* jobs, int njobs, long long max_elems, hipStream_t stream);
 int ftc_ce_fwd_bwd(void* logits, const long long* labels, float* loss, float* lse, long long rows, int V, long long ld,
                    float gscale, long long ignore_index, hipStream_t stream);
 int ftc_adamw(void* param_bf16, float* master, float* m, float* v, const void* grad, int grad_is_fp32, long long n,
@@ -325,6 +326,15 @@ void tail_gemm_(at::Tensor& x, const at::Tensor& bm, int64_t nct, int64_t Rp) {
   check(ftc_tail_gemm(x.data_ptr(), x.stride(0), x.size(0), (int)x.size(1), bm.data_ptr(), bm.stride(0), (int)nct,
                       (int)Rp, cur_stream()),
         "tail_gemm_");
+}
+
+// ---------------- batched strided copy / scale (LoRA operand refresh) ----------------
+// jobs: device table of njobs 64-byte records built by ops/linear.py from live bf16 tensor views (so
+// every address and stride it holds is inside its tensor); checked here for size and placement only.
+void copy2d_batched_(const at::Tensor& jobs, int64_t njobs, int64_t max_elems) {
+  TORCH_CHECK(jobs.is_cuda() && jobs.is_contiguous() && jobs.scalar_type() == at::kLong, "copy2d_batched: jobs");
+  TORCH_CHECK(jobs.numel() * 8 == njobs * 64 && njobs > 0 && njobs <= 65535, "copy2d_batched: job table size");
+  check(ftc_copy2d_batched(jobs.data_ptr(), (int)njobs, (long long)max_elems, cur_stream()), "copy2d_batched");
 }
 
 // ---------------- transpose ----------------
@@ -641,6 +651,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("rmsnorm_bwd", &rmsnorm_bwd, py::arg("dy"), py::arg("h"), py::arg("w"), py::arg("rstd"), py::arg("dres"),
         py::arg("need_dw"), py::arg("pad") = 0);
   m.def("rope_", &rope_);
+  m.def("copy2d_batched_", &copy2d_batched_);
   m.def("swiglu_fwd", &swiglu_fwd, py::arg("gu"), py::arg("pad") = 0);
   m.def("swiglu_bwd", &swiglu_bwd, py::arg("da"), py::arg("gu"), py::arg("pad") = 0);
   m.def("swiglu_fwd_lora", &swiglu_fwd_lora, py::arg("gu"), py::arg("pad"), py::arg("am"), py::arg("nct"));

@@ -3,6 +3,8 @@
 // (no on-device trig: guide Appendix B "Element-wise"), grid-stride capped at 2048 blocks.
 #include "common.h"
 
+#include <algorithm>
+
 using namespace ftc;
 
 // qkv: [rows, ld] bf16; the first (n_rot_heads * head_dim) columns are rotated in place, half-split
@@ -120,5 +122,40 @@ extern "C" int ftc_swiglu_bwd(const void* da, const void* gu, void* dgu, long lo
   const int grid = ftc::stream_grid(rows * (F / 8), 256);
   hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid), dim3(256), 0, stream, (const uint16_t*)da, (const uint16_t*)gu,
                      (uint16_t*)dgu, rows, F, dgu_rs);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------- batched strided 2-D copy / scale
+// dst[r, c] = bf16(scale * src[r, c]) for a table of small strided jobs in ONE launch: the LoRA operand
+// refresh after each optimizer step (A, B, s A^T, B^T into the augmented GEMM buffers of every layer)
+// was ~400 separate ~5 us copy / mul launches per Llama-3-8B step.  blockIdx.y = job; the job record
+// is read by scalar loads; columns are the fast index (the host orients every job so the destination
+// row is contiguous, dcs == 1).  Rounding = torch's bf16 mul (fp32 product, round-to-nearest-even).
+struct Copy2DJob {
+  long long src, dst;            // byte addresses of element (0, 0)
+  long long srs, scs, drs, dcs;  // element strides
+  int rows, cols;
+  float scale;
+  int pad;
+};
+static_assert(sizeof(Copy2DJob) == 64, "job record layout (mirrored in ops/linear.py)");
+
+__global__ __launch_bounds__(256) void copy2d_batched_kernel(const Copy2DJob* __restrict__ jobs) {
+  const Copy2DJob j = jobs[blockIdx.y];
+  const uint16_t* src = reinterpret_cast<const uint16_t*>(j.src);
+  uint16_t* dst = reinterpret_cast<uint16_t*>(j.dst);
+  const long long n = (long long)j.rows * j.cols;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+    const int r = (int)(e / j.cols), c = (int)(e - (long long)r * j.cols);
+    const float v = bf2f(src[r * j.srs + c * j.scs]);
+    dst[r * j.drs + c * j.dcs] = j.scale == 1.0f ? src[r * j.srs + c * j.scs] : f2bf(v * j.scale);
+  }
+}
+
+extern "C" int ftc_copy2d_batched(const void* jobs, int njobs, long long max_elems, hipStream_t stream) {
+  if (njobs <= 0) return 0;
+  if (njobs > 65535) return -1;
+  const int gx = (int)std::min<long long>(256, std::max<long long>(1, (max_elems + 2047) / 2048));
+  hipLaunchKernelGGL(copy2d_batched_kernel, dim3(gx, njobs), dim3(256), 0, stream, (const Copy2DJob*)jobs);
   return (int)hipGetLastError();
 }

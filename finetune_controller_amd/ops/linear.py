@@ -34,6 +34,8 @@ columns the two-GEMM path runs instead.
 from __future__ import annotations
 
 import os
+import struct
+import weakref
 
 import torch
 
@@ -48,6 +50,100 @@ _PARAM_GENERATION = [0]
 
 def bump_param_generation():
     _PARAM_GENERATION[0] += 1
+
+
+def _refresh_key(A: torch.Tensor, B: torch.Tensor, scale: float) -> tuple:
+    return (_PARAM_GENERATION[0], A._version, B._version, A.data_ptr(), B.data_ptr(), float(scale))
+
+
+# ---- batched operand refresh.  After an optimizer step every augmented projection needs its A / B
+# copies (s A, B, and the transposed s A^T / B^T where kept) refreshed: ~16 small copy / scale launches
+# per layer.  The first refresh of a parameter generation refreshes EVERY bound operand set in one
+# launch (csrc/kernels/elementwise.hip ``copy2d_batched``); the later calls find their key current.
+_BATCH_REFRESH = os.environ.get("FTC_BATCH_REFRESH", "1") != "0"
+_BOUND: list = []  # weakrefs to AugWeight / TailOperands bound to their (A, B, scale)
+_JOB_TABLES: dict = {}  # packed job table bytes -> device int64 tensor (addresses are stable per model)
+
+
+class _Refreshable:
+    _key = None
+    _bind = None
+
+    def refresh(self, A: torch.Tensor, B: torch.Tensor, scale: float):
+        key = _refresh_key(A, B, scale)
+        if key == self._key:
+            return
+        if self._bind is None:
+            self._bind = (A, B, float(scale))
+            _BOUND.append(weakref.ref(self))
+        bound = self._bind[0] is A and self._bind[1] is B and self._bind[2] == float(scale)
+        if not (_BATCH_REFRESH and bound and refresh_bound()):
+            self._refresh_now(A, B, scale)
+            self._key = key
+
+    def _refresh_now(self, A, B, scale):
+        for dst, src, sc in self._copy_jobs(A, B, float(scale)):
+            if sc == 1.0:
+                dst.copy_(src)
+            else:
+                torch.mul(src, sc, out=dst)
+
+    def _copy_jobs(self, A, B, scale) -> list:
+        raise NotImplementedError
+
+
+def _pack_job(dst: torch.Tensor, src: torch.Tensor, scale: float) -> bytes:
+    if dst.stride(1) != 1:  # orient so the destination row is contiguous (coalesced stores)
+        dst, src = dst.t(), src.t()
+    rows, cols = dst.shape
+    return struct.pack("<qqqqqqiifi", src.data_ptr(), dst.data_ptr(), src.stride(0), src.stride(1), dst.stride(0),
+                       dst.stride(1), rows, cols, float(scale), 0)
+
+
+def refresh_bound() -> bool:
+    """Refresh every bound operand set whose key is stale in one launch.  False (nothing done) when
+    any of them cannot take the HIP path; the caller then refreshes itself the plain way."""
+    stale, alive = [], []
+    for r in _BOUND:
+        o = r()
+        if o is None:
+            continue
+        alive.append(r)
+        A, B, sc = o._bind
+        k = _refresh_key(A, B, sc)
+        if k != o._key:
+            stale.append((o, k))
+    _BOUND[:] = alive
+    jobs = []
+    for o, _ in stale:
+        A, B, sc = o._bind
+        for dst, src, js in o._copy_jobs(A, B, sc):
+            if not (use_hip(dst) and dst.dtype == src.dtype == torch.bfloat16 and dst.device == src.device
+                    and dst.dim() == 2 and dst.shape == src.shape and 1 in dst.stride() and dst.numel() > 0):
+                return False
+            jobs.append((dst, src, js))
+    if not jobs:
+        return True
+    if not hasattr(ext(), "copy2d_batched_"):
+        return False
+    dev = jobs[0][0].device
+    if any(d.device != dev for d, _, _ in jobs):
+        return False
+    blob = b"".join(_pack_job(*j) for j in jobs)
+    table = _JOB_TABLES.get(blob)
+    if table is None:
+        if len(_JOB_TABLES) > 8:
+            _JOB_TABLES.clear()
+        import numpy as np
+
+        table = torch.from_numpy(np.frombuffer(blob, dtype=np.int64).copy()).to(dev)
+        _JOB_TABLES[blob] = table
+    for i in range(0, len(jobs), 65535):
+        n = min(65535, len(jobs) - i)
+        ext().copy2d_batched_(table[i * 8:(i + n) * 8], n, max(d.numel() for d, _, _ in jobs[i:i + n]))
+    for o, k in stale:
+        o._key = k
+    return True
 
 
 def set_grad_ready_hook(fn):
@@ -199,7 +295,7 @@ def take_prefilled(direction: str, t: torch.Tensor, aug) -> bool:
     return v is not None and v == _operand_key(t, aug)
 
 
-class TailOperands:
+class TailOperands(_Refreshable):
     """Stand-alone tail operands for a projection whose weight is not an ``AugWeight`` (QLoRA: the NF4
     weight is dequantised per call into a shared scratch): ``[s A ; 0]`` as [Rp, K] and ``B^T`` as
     [Rp, N], refreshed once per optimizer generation -- the same interface as AugWeight's
@@ -215,13 +311,8 @@ class TailOperands:
     def nct(self) -> int:
         return -(-self.R // 16)
 
-    def refresh(self, A: torch.Tensor, B: torch.Tensor, scale: float):
-        key = (_PARAM_GENERATION[0], A._version, B._version, A.data_ptr(), B.data_ptr(), float(scale))
-        if key == self._key:
-            return
-        torch.mul(A, scale, out=self.fwd[:self.R])
-        self.bt[:self.R].copy_(B.t())
-        self._key = key
+    def _copy_jobs(self, A, B, scale) -> list:
+        return [(self.fwd[:self.R], A, scale), (self.bt[:self.R], B.t(), 1.0)]
 
     def fwd_tail_operand(self, A, B, scale):
         self.refresh(A, B, scale)
@@ -270,7 +361,7 @@ def _wide(t: torch.Tensor, width: int) -> torch.Tensor:
     return t.as_strided((t.shape[0], width), (t.stride(0), 1), t.storage_offset())
 
 
-class AugWeight:
+class AugWeight(_Refreshable):
     """``big [N+Rp, K+Rp]`` bf16 buffer whose ``[:N, :K]`` block is the frozen base weight."""
 
     TILE = 64
@@ -287,25 +378,19 @@ class AugWeight:
     def owns(self, W: torch.Tensor) -> bool:
         return W.data_ptr() == self.big.data_ptr() and W.shape == (self.N, self.K) and W.stride(0) == self.K + self.Rp
 
-    _key = None
+    def _copy_jobs(self, A, B, scale) -> list:
+        """big[:N, K:K+R] = B ; big[N:N+R, :K] = s A (pad rows / columns stay zero); bigT / bt follow.
 
-    def refresh(self, A: torch.Tensor, B: torch.Tensor, scale: float):
-        """big[:N, K:K+R] = B ; big[N:N+R, :K] = s A (pad rows / columns stay zero); bigT follows.
-
-        Runs once per parameter update, not per call: forward and backward of every micro-batch
-        between two optimizer steps see the same A/B (key = optimizer generation + the tensors'
-        version counters and storage)."""
-        key = (_PARAM_GENERATION[0], A._version, B._version, A.data_ptr(), B.data_ptr(), float(scale))
-        if key == self._key:
-            return
+        ``refresh`` runs them once per parameter update, not per call: forward and backward of every
+        micro-batch between two optimizer steps see the same A/B (key = optimizer generation + the
+        tensors' version counters and storage)."""
         N, K, R = self.N, self.K, self.R
-        self.big[:N, K:K + R].copy_(B)
-        torch.mul(A, scale, out=self.big[N:N + R, :K])
+        jobs = [(self.big[:N, K:K + R], B, 1.0), (self.big[N:N + R, :K], A, scale)]
         if self.bigT is not None:
-            self.bigT[:, N:N + R].copy_(self.big[N:N + R, :K].t())
+            jobs.append((self.bigT[:, N:N + R], A.t(), scale))
         if self.bt is not None:
-            self.bt[:R].copy_(B.t())
-        self._key = key
+            jobs.append((self.bt[:R], B.t(), 1.0))
+        return jobs
 
     # ---- producer-side tail products (csrc/kernels/swiglu_lora.hip): the kernel that produces this
     # projection's input (forward) or output gradient (backward) forms s x A^T / dy B itself.

@@ -138,6 +138,9 @@ for s in "${STEPS[@]}"; do
     pmc_step)  # every kernel of a 1-layer Llama-3-8B LoRA step (real shapes), grouped by kernel name
       timeout -k 10 600 bash tools/pmc_run.sh step -- python3 bench.py --model llama3-8b-1l --steps 2 --warmup 1
       fatal $? pmc_step ;;
+    op_kernels)  # kernel -> launching op attribution, 1-layer LoRA step (torch.profiler)
+      timeout -k 10 300 python tools/op_kernels.py --top 60 > gpurun_out/op_kernels.md 2> gpurun_out/op_kernels.err
+      fatal $? op_kernels; head -30 gpurun_out/op_kernels.md ;;
     *) echo "unknown step $s" ;;
   esac
 done
