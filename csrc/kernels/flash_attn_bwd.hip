@@ -32,6 +32,20 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr float LOG2E = 1.4426950408889634f;
 
+// Diagnostic build only (tools/stamp_dkdv.hip defines FTC_STAMPS; the extension never does): per-wave
+// cycle sums of the dK/dV loop's segments for one workgroup, read through g_stamps (guide "In-kernel
+// stamps": shares, not lengths -- the stamps' waits forbid some overlap).
+#ifdef FTC_STAMPS
+__device__ unsigned long long g_stamps[8][6];  // [wave][sync, A, B1, B2, loop total, slices]
+__device__ int g_stamp_block;
+#define FTC_STAMP(t)                                                                          \
+  do {                                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");                 \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+  } while (0)
+#endif
+
 FTC_DEV int swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
 template <int D>
 FTC_DEV int lds_off(int r, int chunk) {
@@ -171,7 +185,13 @@ FTC_DEV void dkdv_dma(__amdgpu_buffer_rsrc_t qr, __amdgpu_buffer_rsrc_t dr, __am
 // SIMD").  Slice j is read by half 1 one barrier interval later, so the Q/dO ring has 4 slots.
 // QR = 32-row query blocks per slice: QR = 2 (D = 64) doubles the MFMA work between two barriers,
 // which at D = 64 is otherwise half of D = 128's (the per-slice barrier / DMA cost stays the same).
-template <int D, int HW, bool PP = false, int DIST = 2, int QR = 1>
+// PP2 (with PP, DIST = 3): half 1 runs B1(j - 1) B2(j - 1) A(j) instead of B2(j - 1) A(j) B1(j), carrying
+// the raw S / dP' accumulators of slice j - 1 across the barrier (not the packed P / dS): both halves
+// then end each interval on MFMAs and each half's softmax VALU issues beside the other half's MFMAs
+// (tools/stamp_dkdv.hip: with PP alone half 1's B1 ran alone at the end of every interval).  Measured:
+// bwd 2.03 vs 1.96 ms, 36.1k vs 36.5k tok/s (profiles/r2/stamp_dkdv.md) -- the MFMA phases wait on the
+// 8 waves' LDS reads, not on the partner's VALU; opt-in (FTC_FLASH_DKDV_PP2=1).
+template <int D, int HW, bool PP = false, int DIST = 2, int QR = 1, bool PP2 = false>
 __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
   static_assert(DIST == 2 || (PP && DIST == 3), "DMA distance 3 needs the ping-pong 5-slot ring");
   static_assert(QR == 1 || QR == 2, "one or two 32-row query blocks per slice");
@@ -458,13 +478,42 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
     // the halves run separate straight-line loops (one branch outside the loop, not one per slice:
     // the register allocator then sees two independent paths) with the same barrier count
     if constexpr (DIST == 3) {
+#ifdef FTC_STAMPS
+      const bool stamping = blockIdx.x == g_stamp_block;
+      unsigned long long st_acc[4] = {0, 0, 0, 0}, st_prev = 0, st_now = 0, st_t0 = 0, st_t1 = 0;
+#define SEG_START()            \
+  do {                         \
+    if (stamping) FTC_STAMP(st_prev); \
+  } while (0)
+#define SEG_END(i)                                                  \
+  do {                                                              \
+    if (stamping) {                                                 \
+      FTC_STAMP(st_now);                                            \
+      st_acc[i] += st_now - st_prev;                                \
+      st_prev = st_now;                                             \
+    }                                                               \
+  } while (0)
+      if (stamping) FTC_STAMP(st_t0);
+#else
+#define SEG_START() \
+  do {              \
+  } while (0)
+#define SEG_END(i) \
+  do {             \
+  } while (0)
+#endif
       // 5-slot ring, DMA three slices ahead: slice it + 3 reuses the slot of slice it - 2
       if (wave < 4) {
         auto body = [&](const int it, const char* Qs, char* dma_slot) __attribute__((always_inline)) {
+          SEG_START();
           sync_slice(it, dma_slot);
+          SEG_END(0);
           phaseA(Qs);
+          SEG_END(1);
           phaseB1(it);
+          SEG_END(2);
           phaseB2(Qs);
+          SEG_END(3);
         };
         for (int it = 0; it < total; it += 5) {
           body(it, slot0, slot3);
@@ -473,12 +522,43 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
           if (it + 3 < total) body(it + 3, slot3, slot1);
           if (it + 4 < total) body(it + 4, slot4, slot2);
         }
+      } else if constexpr (PP2) {
+        auto body = [&](const int it, const char* Qs, const char* Qprev, char* dma_slot) __attribute__((always_inline)) {
+          SEG_START();
+          sync_slice(it, dma_slot);
+          SEG_END(0);
+          if (it > 0) {
+            phaseB1(it - 1);
+            SEG_END(2);
+            phaseB2(Qprev);
+            SEG_END(3);
+          }
+          phaseA(Qs);
+          SEG_END(1);
+        };
+        for (int it = 0; it < total; it += 5) {
+          body(it, slot0, slot4, slot3);
+          if (it + 1 < total) body(it + 1, slot1, slot0, slot4);
+          if (it + 2 < total) body(it + 2, slot2, slot1, slot0);
+          if (it + 3 < total) body(it + 3, slot3, slot2, slot1);
+          if (it + 4 < total) body(it + 4, slot4, slot3, slot2);
+        }
+        if (total > 0) {
+          const int r = (total - 1) % 5;
+          phaseB1(total - 1);
+          phaseB2(r == 0 ? slot0 : r == 1 ? slot1 : r == 2 ? slot2 : r == 3 ? slot3 : slot4);
+        }
       } else {
         auto body = [&](const int it, const char* Qs, const char* Qprev, char* dma_slot) __attribute__((always_inline)) {
+          SEG_START();
           sync_slice(it, dma_slot);
+          SEG_END(0);
           if (it > 0) phaseB2(Qprev);
+          SEG_END(3);
           phaseA(Qs);
+          SEG_END(1);
           phaseB1(it);
+          SEG_END(2);
         };
         for (int it = 0; it < total; it += 5) {
           body(it, slot0, slot4, slot3);
@@ -492,6 +572,19 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
           phaseB2(r == 0 ? slot0 : r == 1 ? slot1 : r == 2 ? slot2 : r == 3 ? slot3 : slot4);
         }
       }
+#ifdef FTC_STAMPS
+      if (stamping) {
+        FTC_STAMP(st_t1);
+        if (lane == 0) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) g_stamps[wave][i] = st_acc[i];
+          g_stamps[wave][4] = st_t1 - st_t0;
+          g_stamps[wave][5] = (unsigned long long)total;
+        }
+      }
+#endif
+#undef SEG_START
+#undef SEG_END
     } else if (wave < 4) {  // waves w and w + 4 share a SIMD
       auto body = [&](const int it, const char* Qs, char* dma_slot) __attribute__((always_inline)) {
         sync_slice(it, dma_slot);
@@ -729,8 +822,17 @@ void launch_dkdv(const BwdArgs& a, int grid, int waves, bool pp, bool dist3, hip
     const char* e = getenv("FTC_FLASH_DKDV_QR");
     return !(e && e[0] == '1');
   }();
-  if (D == 64 && qr2 && waves == 8 && pp && dist3)
+  // FTC_FLASH_DKDV_PP2=1: half 1 in B1 B2 A order (see bwd_dkdv_kernel)
+  static const bool pp2 = [] {
+    const char* e = getenv("FTC_FLASH_DKDV_PP2");
+    return e && e[0] == '1';
+  }();
+  if (D == 64 && qr2 && waves == 8 && pp && dist3 && pp2)
+    hipLaunchKernelGGL((bwd_dkdv_kernel<64, 1, true, 3, 2, true>), dim3(grid), dim3(512), 0, stream, a);
+  else if (D == 64 && qr2 && waves == 8 && pp && dist3)
     hipLaunchKernelGGL((bwd_dkdv_kernel<64, 1, true, 3, 2>), dim3(grid), dim3(512), 0, stream, a);
+  else if (waves == 8 && pp && dist3 && pp2)
+    hipLaunchKernelGGL((bwd_dkdv_kernel<D, 1, true, 3, 1, true>), dim3(grid), dim3(512), 0, stream, a);
   else if (waves == 8 && pp && dist3)
     hipLaunchKernelGGL((bwd_dkdv_kernel<D, 1, true, 3>), dim3(grid), dim3(512), 0, stream, a);
   else if (waves == 8 && pp)

@@ -141,6 +141,18 @@ for s in "${STEPS[@]}"; do
     op_kernels)  # kernel -> launching op attribution, 1-layer LoRA step (torch.profiler)
       timeout -k 10 300 python tools/op_kernels.py --top 60 > gpurun_out/op_kernels.md 2> gpurun_out/op_kernels.err
       fatal $? op_kernels; head -30 gpurun_out/op_kernels.md ;;
+    pp2_ab)  # dK/dV half-1 order B1 B2 A (FTC_FLASH_DKDV_PP2) -- stamps, numerics, interleaved A/B, bench
+      FTC_FLASH_DKDV_PP2=1 timeout -k 10 120 ./tools/stamp_dkdv 0 256 > gpurun_out/stamp_dkdv_pp2.md 2>&1
+      fatal $? stamp_pp2; head -12 gpurun_out/stamp_dkdv_pp2.md
+      FTC_FLASH_DKDV_PP2=1 timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py -m gpu -x -q \
+        -k "flash or llama_lora or packed or tail or family" > gpurun_out/pytest_pp2.log 2>&1
+      fatal $? pytest_pp2; tail -2 gpurun_out/pytest_pp2.log
+      for p in 0 1 0 1; do
+        FTC_FLASH_DKDV_PP2=$p timeout -k 10 300 python tools/bench_attention.py --rounds 3 > gpurun_out/attn_pp2_$p.log 2>&1
+        fatal $? attn_pp2_$p; grep -v amdgpu gpurun_out/attn_pp2_$p.log | tail -1 | cut -c1-300
+      done
+      FTC_FLASH_DKDV_PP2=1 timeout -k 10 600 python bench.py --steps 10 --warmup 3 > gpurun_out/bench_pp2.log 2>&1
+      fatal $? bench_pp2; grep '^{' gpurun_out/bench_pp2.log | cut -c1-200 ;;
     *) echo "unknown step $s" ;;
   esac
 done
