@@ -223,6 +223,18 @@ def test_adamw_flat(C, gdtype):
     torch.testing.assert_close(param.float(), bf(ref.detach()).float(), atol=1e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("gdtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("n,offset", [(7, 0), (4_000_037, 0), (4_000_037, 1), (40_000_000, 0)])
+def test_grad_sumsq_paths(C, gdtype, n, offset):
+    """16-byte vector path (aligned), element path (offset view), tails, multi-iteration grids vs fp64."""
+    torch.manual_seed(1)
+    base = torch.randn(n + offset, device=DEV).to(gdtype)
+    g = base[offset:]
+    stats = C.grad_sumsq(g, 0.0, 1.0)
+    ref = (g.double() ** 2).sum()
+    assert abs(stats[0].item() - ref.item()) <= 1e-5 * ref.item() + 1e-3
+
+
 def test_grad_clip_coef(C):
     g = torch.full((4096,), 0.5, device=DEV)
     stats = C.grad_sumsq(g, 1.0, 1.0)
