@@ -33,6 +33,10 @@ int ftc_swiglu_bwd_wgrad(const void* da, long long da_rs, const void* gu, void* 
 int ftc_tail_gemm(void* x, long long ldx, long long rows, int K, const void* Bm, long long ldb, int nct, int Rp,
                   hipStream_t stream);
 int ftc_transpose(const void* x, long long ldx, void* y, long long ldy, int R, int C, hipStream_t stream);
+int ftc_gemm_tn_ok(const void* a, long long lda, const void* b, long long ldb, const void* c, long long ldc, int M, int N,
+                   int K);
+int ftc_gemm_tn(const void* a, long long lda, const void* b, long long ldb, void* c, long long ldc, int c_fp32, int M,
+                int N, int K, float alpha, float beta, hipStream_t stream);
 int ftc_copy2d_batched(const void* jobs, int njobs, long long max_elems, hipStream_t stream);
 int ftc_ce_fwd_bwd(void* logits, const long long* labels, float* loss, float* lse, long long rows, int V, long long ld,
                    float gscale, long long ignore_index, hipStream_t stream);
@@ -360,6 +364,28 @@ at::Tensor transpose2d(const at::Tensor& x, const c10::optional<at::Tensor>& out
   return y;
 }
 
+// ---------------- weight-gradient GEMM: c = beta c + alpha a^T b ----------------
+// a [K, M], b [K, N] bf16 row views (unit column stride); c [M, N] bf16 or fp32 row view.
+bool gemm_tn_ok(const at::Tensor& c, const at::Tensor& a, const at::Tensor& b) {
+  if (!a.is_cuda() || !b.is_cuda() || !c.is_cuda() || a.dim() != 2 || b.dim() != 2 || c.dim() != 2) return false;
+  if (a.scalar_type() != at::kBFloat16 || b.scalar_type() != at::kBFloat16) return false;
+  if (c.scalar_type() != at::kBFloat16 && c.scalar_type() != at::kFloat) return false;
+  if (a.stride(1) != 1 || b.stride(1) != 1 || c.stride(1) != 1) return false;
+  if (a.size(0) != b.size(0) || c.size(0) != a.size(1) || c.size(1) != b.size(1)) return false;
+  if (a.size(0) > INT32_MAX || a.size(1) > INT32_MAX || b.size(1) > INT32_MAX) return false;
+  return ftc_gemm_tn_ok(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
+                        (int)a.size(1), (int)b.size(1), (int)a.size(0)) != 0;
+}
+
+void gemm_tn_(at::Tensor& c, const at::Tensor& a, const at::Tensor& b, double alpha, double beta) {
+  TORCH_CHECK(gemm_tn_ok(c, a, b), "gemm_tn_: shapes / layouts outside the kernel contract (M, N % 256, K % 64, "
+              "bf16 row views a [K, M], b [K, N], c [M, N] bf16/fp32)");
+  check(ftc_gemm_tn(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
+                    c.scalar_type() == at::kFloat, (int)a.size(1), (int)b.size(1), (int)a.size(0), (float)alpha,
+                    (float)beta, cur_stream()),
+        "gemm_tn_");
+}
+
 // ---------------- cross entropy (in place on logits) ----------------
 at::Tensor ce_fwd_bwd_(at::Tensor& logits, const at::Tensor& labels, double gscale, int64_t ignore_index) {
   need(logits, at::kBFloat16, "logits");
@@ -662,6 +688,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("tail_gemm_ok", &tail_gemm_ok);
   m.def("tail_gemm_", &tail_gemm_);
   m.def("transpose2d", &transpose2d, py::arg("x"), py::arg("out") = py::none());
+  m.def("gemm_tn_ok", &gemm_tn_ok);
+  m.def("gemm_tn_", &gemm_tn_);
   m.def("ce_fwd_bwd_", &ce_fwd_bwd_);
   m.def("adamw_", &adamw_, py::arg("param"), py::arg("master"), py::arg("m"), py::arg("v"), py::arg("grad"),
         py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("step"),

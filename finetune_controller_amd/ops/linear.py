@@ -251,6 +251,22 @@ def transpose2d(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tenso
     return x.t().contiguous()
 
 
+def own_wgrad(mg: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> bool:
+    """Whether ``mg += dy2^T x2`` runs on the hand-written gfx950 TN GEMM (csrc/kernels/gemm_tn.hip)
+    instead of hipBLASLt on a transposed copy of x.  ``FTC_GEMM_TN``: ``0`` (default) -- never;
+    ``auto`` -- only for wide activations (in-features >= 8192: the down projection's [T, 14336]
+    input, whose transposed copy alone costs 0.2 ms); ``1`` -- whenever the shape fits the kernel.
+    Measured (profiles/r2/gemm_tn.md): the kernel beats hipBLASLt on these "TT" operands as stored
+    (down 1.76 vs 1.94 ms) but not the library on a transposed x, and the full-FT step A/B gave
+    auto -0.5 % -- so the library path stays the default."""
+    mode = os.environ.get("FTC_GEMM_TN", "0")
+    if mode == "0" or not use_hip(x2):
+        return False
+    if mode == "auto" and x2.shape[1] < 8192:
+        return False
+    return bool(ext().gemm_tn_ok(mg, dy2, x2))
+
+
 def transposed_weight(W: torch.Tensor) -> torch.Tensor | None:
     """W^T for the TN backward GEMM dx = dy W (None when the TN path is off or not on the HIP backend)."""
     if not (_TN_BWD and use_hip(W) and W.dim() == 2):
@@ -588,7 +604,9 @@ class _LoRALinearFn(torch.autograd.Function):
         if need_w:
             mg = getattr(W, "main_grad", None)
             if mg is not None:
-                if _TN_DW and use_hip(x2):
+                if own_wgrad(mg, dy2, x2):
+                    ext().gemm_tn_(mg, dy2, x2, 1.0, 1.0)  # both operands as stored, no copies
+                elif _TN_DW and use_hip(x2):
                     # hipBLASLt runs dW += dy^T x 14-24 % faster with x handed over transposed (K-major
                     # reduction operand, tools/bench_dw_gemm.py); the transpose streams at HBM rate
                     accum_mm(mg, dy2.t(), transpose2d(x2).t())

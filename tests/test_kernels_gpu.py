@@ -235,6 +235,33 @@ def test_grad_sumsq_paths(C, gdtype, n, offset):
     assert abs(stats[0].item() - ref.item()) <= 1e-5 * ref.item() + 1e-3
 
 
+@pytest.mark.parametrize("cdtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("M,N,K,lda_pad,beta", [(256, 256, 64, 0, 0.0), (512, 768, 1024, 0, 1.0),
+                                                (768, 256, 4096, 64, 1.0), (2048, 1024, 192, 0, 0.5)])
+def test_gemm_tn(C, cdtype, M, N, K, lda_pad, beta):
+    """Weight-gradient GEMM c = beta c + alpha a^T b (a [K, M], b [K, N] as stored) vs an fp32 reference;
+    lda_pad: a is a column view of a wider buffer (the LoRA-padded activation rows)."""
+    torch.manual_seed(2)
+    abuf = (torch.rand(K, M + lda_pad, device=DEV) * 2 - 1).to(torch.bfloat16)
+    a = abuf[:, :M]
+    b = (torch.rand(K, N, device=DEV) * 2 - 1).to(torch.bfloat16)
+    c = torch.randn(M, N, device=DEV).to(cdtype)
+    ref = beta * c.float() + 0.5 * (a.float().t() @ b.float())
+    assert C.gemm_tn_ok(c, a, b)
+    C.gemm_tn_(c, a, b, 0.5, beta)
+    tol = 2e-2 * (K ** 0.5) / 8 if cdtype == torch.bfloat16 else 1e-3 * (K ** 0.5) / 8
+    torch.testing.assert_close(c.float(), ref, atol=tol, rtol=1e-2 if cdtype == torch.bfloat16 else 1e-4)
+
+
+def test_gemm_tn_rejects(C):
+    a = torch.zeros(64, 200, device=DEV, dtype=torch.bfloat16)  # M not a multiple of 256
+    b = torch.zeros(64, 256, device=DEV, dtype=torch.bfloat16)
+    c = torch.zeros(200, 256, device=DEV, dtype=torch.bfloat16)
+    assert not C.gemm_tn_ok(c, a, b)
+    with pytest.raises(RuntimeError):
+        C.gemm_tn_(c, a, b, 1.0, 0.0)
+
+
 def test_grad_clip_coef(C):
     g = torch.full((4096,), 0.5, device=DEV)
     stats = C.grad_sumsq(g, 1.0, 1.0)
@@ -563,10 +590,13 @@ def test_transpose2d(C, rows, cols, pad):
     assert C.transpose2d(x, out).data_ptr() == out.data_ptr() and torch.equal(out, x.t())
 
 
-def test_full_ft_steps_hip_match_torch_path(C, monkeypatch):
+@pytest.mark.parametrize("gemm_tn", ["0", "1"])
+def test_full_ft_steps_hip_match_torch_path(C, monkeypatch, gemm_tn):
     """Full fine-tuning on the HIP path -- TN input-gradient GEMMs through per-step W^T copies, weight
-    gradients with the activation transposed (csrc/kernels/transpose.hip), flat AdamW -- against the
+    gradients with the activation transposed (csrc/kernels/transpose.hip) or, gemm_tn = 1, on the
+    hand-written TN GEMM (csrc/kernels/gemm_tn.hip) for every projection, flat AdamW -- against the
     stock-PyTorch path over two optimizer steps (the W^T cache must follow the in-place updates)."""
+    monkeypatch.setenv("FTC_GEMM_TN", gemm_tn)
     from finetune_controller_amd.models import build_model
     from finetune_controller_amd.models.config import ModelConfig
     from finetune_controller_amd.train.optim import FlatAdamW
@@ -958,9 +988,12 @@ def test_accum_mm_fp32_out_bf16_operands(C):
     assert err < 1e-5, err
 
 
-def test_full_ft_fp32_grads_hip_match_torch_path(C, monkeypatch):
+@pytest.mark.parametrize("gemm_tn", ["0", "1"])
+def test_full_ft_fp32_grads_hip_match_torch_path(C, monkeypatch, gemm_tn):
     """Full fine-tuning with the fp32 gradient buffer and 2 accumulated micro-batches: HIP path vs the
-    stock-PyTorch path (same fp32 accumulation semantics), losses and the summed gradient."""
+    stock-PyTorch path (same fp32 accumulation semantics), losses and the summed gradient; gemm_tn = 1
+    accumulates every weight gradient with the hand-written TN GEMM straight into the fp32 buffer."""
+    monkeypatch.setenv("FTC_GEMM_TN", gemm_tn)
     from finetune_controller_amd.models import build_model
     from finetune_controller_amd.models.config import ModelConfig
     from finetune_controller_amd.train.optim import FlatAdamW
