@@ -178,6 +178,17 @@ class LlamaForCausalLM(nn.Module):
         self.rope = ops.RotaryTable(cfg.head_dim, cfg.max_seq_len, cfg.rope_theta, cfg.rope_scaling)
         self.checkpoint_layers = checkpoint_layers
         self.ce_chunk_rows = 4096
+        # set by the trainer when the optimizer update overlaps the next forward (FlatAdamW.enable_overlap):
+        # called with the stage index before the stage's parameters are read
+        self.param_gate = None
+
+    def param_stages(self) -> list[list[nn.Parameter]]:
+        """Parameters in forward order of first use: [embed], [layer 0], ..., [layer L-1], [final norm,
+        lm_head] -- the stages of ``param_gate``."""
+        stages = [[self.embed]] + [list(layer.parameters()) for layer in self.layers] + [[self.final_norm]]
+        if self.lm_head is not self.embed:
+            stages[-1].append(self.lm_head)
+        return stages
 
     @torch.no_grad()
     def init_weights(self, seed: int = 0, std: float = 0.02):
@@ -218,15 +229,22 @@ class LlamaForCausalLM(nn.Module):
         B, S = input_ids.shape
         if segments is not None:
             positions = segments.positions
+        gate = self.param_gate
+        if gate is not None:
+            gate(0)
         h = F.embedding(input_ids.reshape(-1), self.embed)
         delta = None
         for li, layer in enumerate(self.layers):
+            if gate is not None:
+                gate(li + 1)
             if self.checkpoint_layers and self.training and torch.is_grad_enabled():
                 h, delta = checkpoint(layer, h, delta, self.rope, B, S, positions, segments, use_reentrant=False)
             else:
                 h, delta = layer(h, delta, self.rope, B, S, positions, segments,
                                  (kv_cache, li) if kv_cache is not None else None)
         gp = self.layers[-1].pad("down") if len(self.layers) else 0
+        if gate is not None:
+            gate(len(self.layers) + 1)
         _, x = ops.add_rms_norm(h, delta, self.final_norm, self.cfg.norm_eps, grad_pad=gp)
         return x
 

@@ -108,6 +108,9 @@ class FlatAdamW:
         self.last_grad_norm: torch.Tensor | None = None
         self._hp_table: torch.Tensor | None = None  # device schedule (graph-captured steps)
         self._hp_idx: torch.Tensor | None = None
+        self._stages: list[tuple[int, int]] | None = None  # overlapped update: flat ranges in forward order
+        self._side: torch.cuda.Stream | None = None
+        self._events: list | None = None  # per stage, recorded on the side stream by the last step
 
     def use_device_schedule(self, lrs: list[float]):
         """Read lr and the bias corrections from a device table, one row per coming step, indexed by a
@@ -134,8 +137,50 @@ class FlatAdamW:
     def num_params(self) -> int:
         return sum(n for _, n in self.offsets)
 
+    # ---- update overlapped with the next forward (full fine-tuning)
+    def enable_overlap(self, stages: list[list[torch.Tensor]]) -> bool:
+        """Run the AdamW update stage by stage on a side stream so that the next step's forward can start
+        on stage 0 (embeddings, then layer 0, ...) while later stages are still being updated; the model
+        calls ``wait_stage(i)`` before it reads stage i's parameters.  ``stages``: the trainable
+        parameters grouped in forward order; every parameter in exactly one stage, each stage a
+        contiguous range of the flat layout.  The AdamW kernel is HBM-bound (28 B per parameter: 39 ms
+        for Llama-3-8B) and the forward GEMMs are matrix-bound, so the two share the chip.  Each stage's
+        gradient slice is zeroed on the side stream right after its update (the next ``zero_grad`` has
+        nothing left to do: gradients are next written by the backward, after the forward has waited
+        for every stage).  Returns False (nothing changed) when the layout does not allow it."""
+        if not (use_hip(self.grad_flat) and self.dtype in (torch.bfloat16, torch.float32)):
+            return False
+        where = {id(p): (o, _align(n)) for p, (o, n) in zip(self.params, self.offsets)}
+        ranges = []
+        seen = 0
+        for group in stages:
+            spans = [where[id(p)] for p in group if id(p) in where]
+            if not spans:
+                continue
+            lo, hi = min(o for o, _ in spans), max(o + n for o, n in spans)
+            if sum(n for _, n in spans) != hi - lo:
+                return False  # not contiguous in the flat layout
+            ranges.append((lo, hi))
+            seen += len(spans)
+        if seen != len(self.params):
+            return False
+        self._stages = ranges
+        self._side = torch.cuda.Stream(device=self.device)
+        return True
+
+    def wait_stage(self, i: int):
+        """Make the current stream wait for the last update of stage i (no-op when none is pending)."""
+        if self._events is not None and i < len(self._events):
+            torch.cuda.current_stream(self.device).wait_event(self._events[i])
+
+    def join(self):
+        """Every pending stage update is ordered before the current stream's next work."""
+        if self._events is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._events[-1])
+
     def zero_grad(self):
-        self.grad_flat.zero_()
+        if self._events is None:
+            self.grad_flat.zero_()
         if self._fold_hooks:
             for p in self.params:
                 p.grad = None
@@ -184,8 +229,27 @@ class FlatAdamW:
             if self._hp_table is not None:
                 hp = self._hp_table.index_select(0, self._hp_idx.clamp(max=self._hp_table.shape[0] - 1)).reshape(3)
                 self._hp_idx += 1
-            ext().adamw_(param, self.master, self.exp_avg, self.exp_avg_sq, self.grad_flat, lr, b1, b2, self.eps,
-                         self.wd, self.step_count, stats[1:2], hp)
+            if self._stages is None:
+                ext().adamw_(param, self.master, self.exp_avg, self.exp_avg_sq, self.grad_flat, lr, b1, b2, self.eps,
+                             self.wd, self.step_count, stats[1:2], hp)
+                return
+            main = torch.cuda.current_stream(self.device)
+            side = self._side
+            side.wait_stream(main)  # grads final, norm / clip coefficient computed
+            stats.record_stream(side)
+            if hp is not None:
+                hp.record_stream(side)
+            events = []
+            with torch.cuda.stream(side):
+                for lo, hi in self._stages:
+                    ext().adamw_(param[lo:hi] if param is not None else None, self.master[lo:hi], self.exp_avg[lo:hi],
+                                 self.exp_avg_sq[lo:hi], self.grad_flat[lo:hi], lr, b1, b2, self.eps, self.wd,
+                                 self.step_count, stats[1:2], hp)
+                    self.grad_flat[lo:hi].zero_()
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    events.append(ev)
+            self._events = events
             return
         g = self.grad_flat.float() * self.grad_scale
         norm = g.norm()

@@ -1064,3 +1064,30 @@ def test_batched_refresh_trainer_steps_match_per_projection(C, tmp_path, monkeyp
         tr.close()
     assert res[True][0] == res[False][0]
     assert torch.equal(res[True][1], res[False][1])
+
+
+def test_full_ft_overlapped_update_matches_serial(C, monkeypatch, tmp_path):
+    """Full fine-tuning through the Trainer with the AdamW update overlapped with the next forward
+    (stage-wise on a side stream, FlatAdamW.enable_overlap) vs the serial update: identical losses and
+    bitwise-identical parameters / optimizer state after three steps (same kernels, same math)."""
+    from finetune_controller_amd.train.trainer import TrainConfig, Trainer
+
+    res = {}
+    for ov in ("1", "0"):
+        monkeypatch.setenv("FTC_OPT_OVERLAP", ov)
+        tc = TrainConfig(model="llama-smoke", method="full", batch_size=2, seq_len=256, synthetic=True, max_steps=3,
+                         warmup_steps=0, schedule="constant", lr=1e-3, save_model=False, resume=False, device="cuda",
+                         checkpoint_path=str(tmp_path / ov))
+        tr = Trainer(tc)
+        assert (tr.opt._stages is not None) == (ov == "1")
+        losses = [tr.train_step(1e-3).float().item() for _ in range(3)]
+        tr.opt.join()
+        torch.cuda.synchronize()
+        res[ov] = (losses, tr.opt.param_flat.clone(), tr.opt.exp_avg_sq.clone(), tr.opt.grad_flat.clone())
+        tr.close()
+    (l1, p1, v1, g1), (l0, p0, v0, g0) = res["1"], res["0"]
+    assert l1 == l0, (l1, l0)
+    assert torch.equal(p1, p0) and torch.equal(v1, v0)
+    # the overlapped path zeroes each stage's gradient right after its update; the serial one keeps
+    # the last gradients until the next zero_grad
+    assert torch.count_nonzero(g1) == 0 and torch.count_nonzero(g0) > 0
