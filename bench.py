@@ -146,6 +146,9 @@ def _parse(argv):
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--zero-stage", type=int, default=0, choices=[0, 1],
                     help="1: ZeRO-1 -- AdamW state sharded over the data-parallel ranks (reduce-scatter + all-gather)")
+    ap.add_argument("--sp", type=int, default=1,
+                    help="Ulysses sequence parallelism: groups of SP ranks share each sequence (1/SP of the tokens "
+                         "per rank); --seq-len is the FULL sequence length")
     ap.add_argument("--checkpoint-layers", action="store_true")
     ap.add_argument("--ce-chunk-rows", type=int, default=int(os.environ.get("FTC_CE_CHUNK", "4096")),
                     help="rows per lm_head + cross-entropy chunk (the only vocab-sized buffer)")
@@ -225,7 +228,7 @@ def main(argv=None) -> int:
     tc = TrainConfig(model=a.model, method=a.method, lora_r=a.lora_r, lora_alpha=2.0 * a.lora_r,
                      batch_size=a.batch_size, seq_len=a.seq_len, synthetic=True, max_steps=a.warmup + a.steps,
                      warmup_steps=0, schedule="constant", lr=1e-4, bucket_mb=a.bucket_mb, comm_engine=a.comm_engine,
-                     zero_stage=a.zero_stage, grad_accum=a.grad_accum, grad_dtype=a.grad_dtype,
+                     zero_stage=a.zero_stage, grad_accum=a.grad_accum, grad_dtype=a.grad_dtype, sp=a.sp,
                      checkpoint_layers=a.checkpoint_layers, ce_chunk_rows=a.ce_chunk_rows, save_model=False,
                      resume=False, device=a.device, pack_documents=a.doc_len > 0, eos_id=2,
                      synthetic_doc_len=a.doc_len, graph=a.graph)
@@ -260,7 +263,8 @@ def main(argv=None) -> int:
 
     n = info.world_size
     pg_world = dist.get_world_size() if dist.is_initialized() else 1
-    tokens = a.batch_size * a.seq_len * a.grad_accum * n * a.steps
+    ngroups = n // max(1, a.sp)  # data-parallel replicas; an SP group trains B full sequences together
+    tokens = a.batch_size * a.seq_len * a.grad_accum * ngroups * a.steps
     value = tokens / elapsed
     ms = elapsed / a.steps * 1000
     flops_tok = tr.cfg.flops_per_token(a.seq_len, lora=a.method != "full")
@@ -323,12 +327,13 @@ def main(argv=None) -> int:
                 "model": a.model,
                 "method": a.method,
                 "lora": {"r": a.lora_r, "alpha": 2 * a.lora_r, "targets": "all-linear"} if a.method != "full" else None,
-                "global_batch": a.batch_size * a.grad_accum * n,
+                "global_batch": a.batch_size * a.grad_accum * ngroups,
                 "micro_batch_per_gpu": a.batch_size,
                 "grad_accum": a.grad_accum,
                 "seq_len": a.seq_len,
-                "tokens_per_step": a.batch_size * a.seq_len * a.grad_accum * n,
-                "parallelism": f"dp{n}" + ("-zero1" if a.zero_stage and n > 1 else ""),
+                "tokens_per_step": a.batch_size * a.seq_len * a.grad_accum * ngroups,
+                "parallelism": f"dp{ngroups}" + (f"-sp{a.sp}" if a.sp > 1 else "")
+                               + ("-zero1" if a.zero_stage and n > 1 else ""),
                 "kernels": _backend.kernel_mode(),
                 "comm_engine": a.comm_engine,
                 "zero_stage": a.zero_stage,

@@ -150,8 +150,14 @@ class LlamaLayer(nn.Module):
         else:
             if kv is not None:  # prefill: keep this prompt's K/V rows
                 kv[0].store(kv[1], qkv, cfg.n_heads, S)
-            a = ops.attention_packed(qkv, B, S, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, True, cfg.sliding_window,
-                                     out_pad=p_o, grad_pad=p_qkv, docs=docs)
+            sp = getattr(self, "sp", None)
+            if sp is not None and kv is None:  # Ulysses: heads <-> tokens all-to-all around full-sequence attention
+                from ..parallel.sequence import sp_attention
+
+                a = sp_attention(qkv, B, S, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, cfg.sliding_window, sp)
+            else:
+                a = ops.attention_packed(qkv, B, S, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, True,
+                                         cfg.sliding_window, out_pad=p_o, grad_pad=p_qkv, docs=docs)
         o = self.proj("o", a)
         h, x = ops.add_rms_norm(h, o, self.mlp_norm, cfg.norm_eps, pad=p_gu, grad_pad=p_o)
         mlp = self.mlp_projs(p_gu, p_down)
@@ -181,6 +187,14 @@ class LlamaForCausalLM(nn.Module):
         # set by the trainer when the optimizer update overlaps the next forward (FlatAdamW.enable_overlap):
         # called with the stage index before the stage's parameters are read
         self.param_gate = None
+        self.sp = None  # parallel.sequence.SeqGroup: this rank holds 1/P of every sequence (set_sequence_parallel)
+
+    def set_sequence_parallel(self, sp):
+        """Ulysses sequence parallelism (parallel/sequence.py): inputs are this rank's contiguous 1/P of
+        each sequence, RoPE uses global positions, attention runs over the whole sequence on H/P heads."""
+        self.sp = sp
+        for layer in self.layers:
+            layer.sp = sp
 
     def param_stages(self) -> list[list[nn.Parameter]]:
         """Parameters in forward order of first use: [embed], [layer 0], ..., [layer L-1], [final norm,
@@ -251,6 +265,15 @@ class LlamaForCausalLM(nn.Module):
     def forward(self, input_ids: torch.Tensor, labels: torch.Tensor | None = None, positions=None,
                 n_valid: int | None = None, segments=None):
         B, S = input_ids.shape
+        if self.sp is not None:  # S = this rank's 1/P of each sequence (attention pads the full one itself)
+            if segments is not None:
+                raise ValueError("packed documents are not supported with sequence parallelism")
+            if positions is None:
+                positions = self.sp.positions(B, S, input_ids.device)
+            x = self.hidden(input_ids, positions, None)
+            if labels is None:
+                return x @ self.lm_head.t()
+            return ops.fused_linear_cross_entropy(x, self.lm_head, labels, self.ce_chunk_rows, -100, n_valid)
         Sp = ops.model_tile_len(S, self.cfg.head_dim, ops.use_hip(self.embed), self.embed.dtype, self.cfg.max_seq_len)
         if Sp != S:  # GPU, S off the flash tile: run the whole model tile-aligned (ops.attention.model_tile_len)
             input_ids, labels, positions, segments = ops.pad_batch_to(Sp, input_ids, labels, positions, segments)

@@ -41,6 +41,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--checkpoint-layers", action="store_true")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--comm-engine", default="torch", choices=["torch", "native"])
+    ap.add_argument("--sp", type=int, default=1,
+                    help="Ulysses sequence parallelism degree: groups of SP ranks share each sequence")
     ap.add_argument("--zero-stage", type=int, default=0, choices=[0, 1],
                     help="1: ZeRO-1 -- AdamW state sharded over the data-parallel ranks (reduce-scatter + all-gather)")
     ap.add_argument("--grad-dtype", default="auto", choices=["auto", "fp32", "bf16"],
@@ -79,7 +81,7 @@ def config_from_args(a) -> TrainConfig:
                        weight_decay=a.weight_decay, max_grad_norm=a.max_grad_norm, seed=a.seed,
                        dataset_path=a.dataset_path, checkpoint_path=a.checkpoint_path, log_interval=a.log_interval,
                        save_every=a.save_every, resume=not a.no_resume, synthetic=a.synthetic, bucket_mb=a.bucket_mb,
-                       comm_engine=a.comm_engine, zero_stage=a.zero_stage, grad_dtype=a.grad_dtype,
+                       comm_engine=a.comm_engine, zero_stage=a.zero_stage, grad_dtype=a.grad_dtype, sp=a.sp,
                        checkpoint_layers=a.checkpoint_layers, init_from=a.init_from,
                        dtype=a.dtype, device=a.device, timers=a.timers, profile_steps=a.profile_steps,
                        eval_every=a.eval_every, eval_batches=a.eval_batches, eval_holdout=a.eval_holdout,

@@ -70,6 +70,9 @@ class TrainConfig:
     bucket_mb: float = 64.0
     comm_engine: str = "torch"  # torch | native
     zero_stage: int = 0  # 1: ZeRO-1 (optimizer state sharded over data-parallel ranks, reduce-scatter grads)
+    # Ulysses sequence parallelism: groups of `sp` consecutive ranks share the same sequences, each
+    # holding 1/sp of every sequence's tokens (attention all-to-alls heads <-> tokens; parallel/sequence.py)
+    sp: int = 1
     # gradient buffer / reduction dtype: fp32 | bf16 | auto (fp32 for full fine-tuning with gradient
     # accumulation or data parallelism -- summing 4+ bf16 micro-batch / rank gradients loses mantissa)
     grad_dtype: str = "auto"
@@ -116,6 +119,20 @@ class Trainer:
         self.model = build_model(self.cfg, self.lora, device=self.device, dtype=self.dtype,
                                  checkpoint_layers=tc.checkpoint_layers)
         self.model.ce_chunk_rows = tc.ce_chunk_rows
+        # sequence-parallel groups (collective: every rank creates every group); data-parallel index /
+        # size = which sequences this rank's group trains on
+        self.sp, self.dp_rank, self.dp_world = None, self.info.rank, self.info.world_size
+        if tc.sp > 1:
+            from ..parallel.sequence import make_seq_groups
+
+            if not self.info.distributed:
+                raise ValueError(f"sequence parallelism (sp={tc.sp}) needs WORLD_SIZE >= sp ranks")
+            self.sp, self.dp_rank, self.dp_world = make_seq_groups(tc.sp, self.info.world_size, self.info.rank)
+            if not hasattr(self.model, "set_sequence_parallel"):
+                raise ValueError(f"model {tc.model} has no sequence-parallel attention")
+            if tc.pack_documents:
+                raise ValueError("packed documents are not supported with sequence parallelism")
+            self.model.set_sequence_parallel(self.sp)
         self.model.init_weights(seed=tc.seed)
         if tc.init_from:
             n = ckpt.load_hf_checkpoint(self.model, tc.init_from)
@@ -205,15 +222,19 @@ class Trainer:
             if tc.synthetic or not tc.dataset_path or not os.path.exists(tc.dataset_path) or not os.listdir(
                     tc.dataset_path if os.path.isdir(tc.dataset_path) else os.path.dirname(tc.dataset_path)):
                 self._data = SyntheticTokens(self.cfg.vocab_size, tc.batch_size, tc.seq_len, self.device,
-                                             seed=tc.seed + self.info.rank, doc_len=tc.synthetic_doc_len,
+                                             seed=tc.seed + self.dp_rank, doc_len=tc.synthetic_doc_len,
                                              eos_id=self.eos_id() if tc.pack_documents else 2)
                 self.steps_per_epoch = 100
             else:
                 self._data = PackedTokenDataset(tc.dataset_path, self.cfg.vocab_size, tc.batch_size, tc.seq_len,
-                                                self.device, self.info.rank, self.info.world_size, tc.seed,
+                                                self.device, self.dp_rank, self.dp_world, tc.seed,
                                                 holdout=tc.eval_holdout if tc.eval_every > 0 else 0,
                                                 eos_id=self.eos_id(), completion_only=tc.completion_only)
                 self.steps_per_epoch = max(1, self._data.steps_per_epoch // tc.grad_accum)
+            if self.sp is not None:  # this rank's contiguous 1/sp of every sequence of its group's batch
+                from ..parallel.sequence import SeqShard
+
+                self._data = SeqShard(self._data, self.sp)
         return self._data
 
     def eos_id(self) -> int | None:

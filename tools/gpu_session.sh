@@ -84,6 +84,15 @@ for s in "${STEPS[@]}"; do
       fatal $? bench_conc1; grep '^{' gpurun_out/bench_conc1.log | cut -c1-200
       timeout -k 10 600 python bench.py --steps 10 --warmup 3 > gpurun_out/bench_conc0.log 2>&1
       fatal $? bench_conc0; grep '^{' gpurun_out/bench_conc0.log | cut -c1-200 ;;
+    sp2)  # Ulysses sequence parallelism, 2 ranks on the one card (RCCL over loopback): Llama-3-8B, 1 x 32k
+      # tokens split 2 x 16k, heads <-> tokens all-to-all around full-sequence flash attention
+      FTC_SHARE_GPU=1 timeout -k 10 600 python bench.py --gpus 2 --sp 2 --batch-size 1 --seq-len 32768 --steps 3 \
+        --warmup 1 --launcher-timeout 550 > gpurun_out/sp2.log 2>&1
+      fatal $? sp2; grep '^{' gpurun_out/sp2.log | cut -c1-900 ;;
+    sp2_1l)  # same on the 1-layer model, 4 x 8k
+      FTC_SHARE_GPU=1 timeout -k 10 400 python bench.py --gpus 2 --sp 2 --model llama3-8b-1l --batch-size 4 \
+        --seq-len 8192 --steps 4 --warmup 2 --launcher-timeout 350 > gpurun_out/sp2_1l.log 2>&1
+      fatal $? sp2_1l; grep '^{' gpurun_out/sp2_1l.log | cut -c1-900 ;;
     rccl4)  # 4 ranks on the one card (RCCL over loopback sockets), torch + native engines A/B, 1-layer
       FTC_SHARE_GPU=1 timeout -k 10 500 python bench.py --gpus 4 --model llama3-8b-1l --steps 4 --warmup 2 --comm-ab \
         --batch-size 2 --launcher-timeout 450 > gpurun_out/rccl4.log 2>&1
