@@ -49,6 +49,20 @@ FTC_DEV int lds_off(int r, int chunk) {  // byte offset of 16-byte chunk `chunk`
 
 FTC_DEV bf16x8 as_bf8(const uint4& v) { return __builtin_bit_cast(bf16x8, v); }
 
+// max over lanes l and l ^ 32: v_permlane32_swap (gfx950 VALU, one instruction) instead of
+// ds_bpermute -- the row max sits on the softmax's dependency chain every tile, and the LDS permute's
+// round trip was part of it.  PL = false: the ds_bpermute form (FTC_FLASH_FWD_XHALF=0, A/B).
+template <bool PL>
+FTC_DEV float xhalf_max(float v) {
+  if constexpr (PL) {
+    const auto pr = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    const float a = __uint_as_float(pr[0]), b = __uint_as_float(pr[1]);
+    return a > b ? a : b;  // lane l holds {v_l, v_(l^32)} in some order
+  } else {
+    return fmaxf(v, __shfl_xor(v, 32, 64));
+  }
+}
+
 FTC_DEV bf16x8 pack_p(const f32x16& p, int base) {
   f32x4 lo = {p[base + 0], p[base + 1], p[base + 2], p[base + 3]};
   f32x4 hi = {p[base + 4], p[base + 5], p[base + 6], p[base + 7]};
@@ -119,7 +133,7 @@ FTC_DEV void fwd_dma(__amdgpu_buffer_rsrc_t kr, __amdgpu_buffer_rsrc_t vr, const
 // at the Llama-3-8B layer shape: 0.64 ms vs 0.617 (8 waves) and 0.604 (4 waves, the default) -- unlike
 // the dK/dV kernel, the forward's softmax already overlaps across the two co-resident 4-wave
 // workgroups, so PP stays opt-in (FTC_FLASH_FWD_WAVES=8 FTC_FLASH_FWD_PP=1; profiles/r1_attn_fwd_pp.log).
-template <int D, int WAVES, bool PP = false>
+template <int D, int WAVES, bool PP = false, bool PL = true>
 __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArgs a) {
   constexpr int BQ = 32 * WAVES;
   constexpr int NCH = D / 8;           // 16-byte chunks per row
@@ -266,8 +280,8 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[kt][i]);
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * c;  // c > 0: max commutes with the scale
+      for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[kt][i]);  // (a depth-5 fmaxf tree measured 3-4 % slower)
+    mt = xhalf_max<PL>(mt) * c;  // c > 0: max commutes with the scale
     // deferred rescale (guide T13): the running reference m moves -- and O, l are rescaled -- only
     // when some row's max grew by more than 2^8; otherwise P <= 256 (exact in bf16's exponent range,
     // fp32 accumulation) and the 64 multiplies of O are skipped.  Wave-uniform branch.
@@ -669,6 +683,12 @@ extern "C" int ftc_flash_fwd(const void* q, const void* k, const void* v, void* 
     const char* e = getenv("FTC_FLASH_FWD_PIPE");
     return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
   }();
+  // FTC_FLASH_FWD_XHALF=0: the row max's lane l <-> l ^ 32 exchange by ds_bpermute instead of
+  // v_permlane32_swap (A/B of xhalf_max)
+  static const bool xhalf_pl = [] {
+    const char* e = getenv("FTC_FLASH_FWD_XHALF");
+    return !(e && e[0] == '0');
+  }();
   if (pipe && waves == 4) {
     if (D == 128 && pipe == 1)
       hipLaunchKernelGGL((flash_fwd_pipe_kernel<128, 2>), dim3(nblocks), dim3(256), lds, stream, a);
@@ -687,7 +707,10 @@ extern "C" int ftc_flash_fwd(const void* q, const void* k, const void* v, void* 
       hipLaunchKernelGGL((flash_fwd_kernel<64, 8>), dim3(nblocks), dim3(512), lds, stream, a);
   } else {
     if (D == 128)
-      hipLaunchKernelGGL((flash_fwd_kernel<128, 4>), dim3(nblocks), dim3(256), lds, stream, a);
+      if (xhalf_pl)
+        hipLaunchKernelGGL((flash_fwd_kernel<128, 4>), dim3(nblocks), dim3(256), lds, stream, a);
+      else
+        hipLaunchKernelGGL((flash_fwd_kernel<128, 4, false, false>), dim3(nblocks), dim3(256), lds, stream, a);
     else
       hipLaunchKernelGGL((flash_fwd_kernel<64, 4>), dim3(nblocks), dim3(256), lds, stream, a);
   }
