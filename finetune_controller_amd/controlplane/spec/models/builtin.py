@@ -117,6 +117,9 @@ class LMTrainingArguments(TrainingArguments):
     checkpoint_layers: bool = Field(default=False, description="Activation checkpointing per decoder layer")
     zero_stage: int = Field(default=0, ge=0, le=1,
                             description="1: ZeRO-1 -- AdamW state sharded over the data-parallel ranks")
+    sp: int = Field(default=1, ge=1, le=64,
+                    description="Ulysses sequence parallelism: groups of this many GPUs share each sequence "
+                                "(long context; must divide the GPU count and the model's head counts)")
     grad_dtype: Literal["auto", "fp32", "bf16"] = Field(
         default="auto", description="Gradient buffer / all-reduce dtype (auto: fp32 for full FT with accumulation or DP)")
     eval_every: int = Field(default=0, ge=0, description="Held-out loss every N steps (0 = off)")

@@ -277,7 +277,14 @@ def test_family_specs_render_worker_commands(name, preset, method, gpus):
     argv = cmd.split(" -m finetune_controller_amd.train.cli ", 1)[-1].split() if gpus > 1 else \
         cmd.split("python -m finetune_controller_amd.train.cli ", 1)[-1].split()
     a = cli.build_parser().parse_args(argv)
-    assert a.model == preset and a.method == method and a.zero_stage == 0
+    assert a.model == preset and a.method == method and a.zero_stage == 0 and a.sp == 1
+    # a long-context job: sequence parallelism over the job's GPUs flows from the form to the trainer
+    long = cls(training_arguments=cls().training_arguments.model_copy(update={"sp": gpus, "seq_len": 65536}))
+    cmd = long.run_cmd()[-1]
+    argv = cmd.split(" -m finetune_controller_amd.train.cli ", 1)[-1].split() if gpus > 1 else \
+        cmd.split("python -m finetune_controller_amd.train.cli ", 1)[-1].split()
+    a = cli.build_parser().parse_args(argv)
+    assert a.sp == gpus and a.seq_len == 65536
 
 
 def test_untrusted_dataset_names_cannot_inject_shell():
