@@ -11,8 +11,9 @@ using ftc_rt::TokenLoader;
 PYBIND11_MODULE(_rt, m) {
   m.doc() = "finetune_controller_amd native runtime: prefetching memory-mapped token loader";
   py::class_<TokenLoader>(m, "TokenLoader")
-      .def(py::init<const std::string&, int, int64_t, int64_t, int, int, int>(), py::arg("path"), py::arg("itemsize"),
-           py::arg("seq_len"), py::arg("batch"), py::arg("rank"), py::arg("world"), py::arg("threads") = 2)
+      .def(py::init<const std::string&, int, int64_t, int64_t, int, int, int, int64_t, int64_t>(), py::arg("path"),
+           py::arg("itemsize"), py::arg("seq_len"), py::arg("batch"), py::arg("rank"), py::arg("world"),
+           py::arg("threads") = 2, py::arg("offset") = 0, py::arg("vocab") = 0)
       .def_property_readonly("n_windows", &TokenLoader::n_windows)
       .def_property_readonly("n_tokens", &TokenLoader::n_tokens)
       .def("set_buffers", &TokenLoader::set_buffers)

@@ -31,15 +31,21 @@ namespace ftc_rt {
 
 class TokenLoader {
  public:
-  TokenLoader(const std::string& path, int itemsize, int64_t seq_len, int64_t batch, int rank, int world, int threads)
-      : itemsize_(itemsize), seq_(seq_len), batch_(batch), rank_(rank), world_(world) {
+  // offset: bytes before the first token (a .npy header); vocab > 0: every gathered id is checked
+  // against it and a batch holding an id >= vocab fails with an error instead of reaching the GPU
+  // (an out-of-range id would make the embedding gather fault the device)
+  TokenLoader(const std::string& path, int itemsize, int64_t seq_len, int64_t batch, int rank, int world, int threads,
+              int64_t offset = 0, int64_t vocab = 0)
+      : itemsize_(itemsize), seq_(seq_len), batch_(batch), rank_(rank), world_(world), offset_(offset), vocab_(vocab) {
     if (itemsize != 2 && itemsize != 4) throw std::runtime_error("token_loader: itemsize must be 2 or 4");
+    if (offset < 0 || offset % itemsize) throw std::runtime_error("token_loader: offset must be a multiple of itemsize");
     fd_ = ::open(path.c_str(), O_RDONLY);
     if (fd_ < 0) throw std::runtime_error("token_loader: cannot open " + path);
     struct stat st;
     if (fstat(fd_, &st) != 0) throw std::runtime_error("token_loader: fstat failed");
     bytes_ = (size_t)st.st_size;
-    ntok_ = (int64_t)(bytes_ / itemsize);
+    if ((int64_t)bytes_ <= offset) throw std::runtime_error("token_loader: file shorter than its header");
+    ntok_ = (int64_t)((bytes_ - (size_t)offset) / itemsize);
     if (ntok_ <= seq_) throw std::runtime_error("token_loader: file shorter than one window");
     map_ = ::mmap(nullptr, bytes_, PROT_READ, MAP_SHARED, fd_, 0);
     if (map_ == MAP_FAILED) throw std::runtime_error("token_loader: mmap failed");
@@ -148,23 +154,35 @@ class TokenLoader {
 
   void fill(int64_t b, int64_t* out) const {
     const int64_t w = seq_ + 1;
+    const char* base = static_cast<const char*>(map_) + offset_;
     for (int64_t i = 0; i < batch_; ++i) {
       const int64_t j = order_[(size_t)(((b * world_ + rank_) * batch_ + i) % n_windows_)];
       const int64_t t0 = j * seq_;
       int64_t* dst = out + i * w;
+      uint32_t hi = 0;
       if (itemsize_ == 2) {
-        const uint16_t* src = static_cast<const uint16_t*>(map_) + t0;
-        for (int64_t k = 0; k < w; ++k) dst[k] = src[k];
+        const uint16_t* src = reinterpret_cast<const uint16_t*>(base) + t0;
+        for (int64_t k = 0; k < w; ++k) {
+          dst[k] = src[k];
+          hi = src[k] > hi ? src[k] : hi;
+        }
       } else {
-        const uint32_t* src = static_cast<const uint32_t*>(map_) + t0;
-        for (int64_t k = 0; k < w; ++k) dst[k] = src[k];
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(base) + t0;
+        for (int64_t k = 0; k < w; ++k) {
+          dst[k] = src[k];
+          hi = src[k] > hi ? src[k] : hi;
+        }
       }
+      if (vocab_ > 0 && (int64_t)hi >= vocab_)  // (int32 ids read as uint32: negatives land here too)
+        throw std::runtime_error("token_loader: token id " + std::to_string(hi) + " >= vocab " +
+                                 std::to_string(vocab_) + " in window " + std::to_string(j));
     }
   }
 
   int itemsize_;
   int64_t seq_, batch_;
   int rank_, world_;
+  int64_t offset_ = 0, vocab_ = 0;
   int fd_ = -1;
   void* map_ = nullptr;
   size_t bytes_ = 0;

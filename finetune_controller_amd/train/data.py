@@ -147,6 +147,16 @@ class Tokenizer:
         return [b + 3 for b in text.encode("utf-8")]
 
 
+def check_token_ids(w: np.ndarray, vocab: int) -> np.ndarray:
+    """A host batch of ids must lie in [0, vocab): an out-of-range id would make the embedding gather
+    read outside the table -- a GPU memory fault, not an exception (the native loader checks the same
+    per batch)."""
+    if w.size and (int(w.max()) >= vocab or int(w.min()) < 0):
+        raise ValueError(f"dataset token ids must lie in [0, {vocab}) for this model; found "
+                         f"[{int(w.min())}, {int(w.max())}] (wrong tokenizer / vocabulary?)")
+    return w
+
+
 def load_token_array(path: str, vocab: int) -> np.ndarray:
     """Return a 1-D int array of token ids for a dataset path (memory-mapped when binary)."""
     return load_tokens_and_mask(path, vocab)[0]
@@ -215,10 +225,13 @@ class PackedTokenDataset:
         try:
             from ..utils.native import NativeTokenLoader
 
-            if (isinstance(self.tokens, np.memmap) and self.loss_mask is None
+            dt = self.tokens.dtype
+            if (isinstance(self.tokens, np.memmap) and self.loss_mask is None and dt.itemsize in (2, 4)
+                    and dt.kind in "ui" and dt.byteorder in "=<|" and self.tokens.ndim == 1
                     and os.environ.get("FTC_NATIVE_LOADER", "1") != "0"):
-                self._native = NativeTokenLoader(self.tokens.filename, self.tokens.dtype.itemsize, seq_len, batch,
-                                                 rank, world, seed, n_use=self.n_use)
+                # offset: a .npy file's header precedes the tokens; vocab: ids are range-checked per batch
+                self._native = NativeTokenLoader(self.tokens.filename, dt.itemsize, seq_len, batch, rank, world, seed,
+                                                 n_use=self.n_use, offset=int(self.tokens.offset), vocab=vocab)
         except ImportError:  # _rt.so not built: numpy path
             self._native = None
         self._perm()
@@ -263,7 +276,8 @@ class PackedTokenDataset:
 
     def _windows(self, idx) -> torch.Tensor:
         S = self.seq_len
-        return torch.from_numpy(np.stack([np.asarray(self.tokens[j * S: j * S + S + 1], dtype=np.int64) for j in idx]))
+        w = np.stack([np.asarray(self.tokens[j * S: j * S + S + 1], dtype=np.int64) for j in idx])
+        return torch.from_numpy(check_token_ids(w, self.vocab))
 
     def _labels(self, arr: torch.Tensor, idx) -> torch.Tensor | None:
         """Masked labels of a [batch, S+1] host window batch (None: no masking configured)."""

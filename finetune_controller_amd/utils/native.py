@@ -22,10 +22,12 @@ def load_rt():
 
 class NativeTokenLoader:
     def __init__(self, filename: str, itemsize: int, seq_len: int, batch: int, rank: int = 0, world: int = 1,
-                 seed: int = 0, depth: int = 4, threads: int = 2, pin: bool | None = None, n_use: int | None = None):
+                 seed: int = 0, depth: int = 4, threads: int = 2, pin: bool | None = None, n_use: int | None = None,
+                 offset: int = 0, vocab: int = 0):
         rt = load_rt()
+        # offset: header bytes before the first token (.npy); vocab: ids >= vocab fail the batch on the host
         self.L = rt.TokenLoader(str(filename), int(itemsize), int(seq_len), int(batch), int(rank), int(world),
-                                int(threads))
+                                int(threads), int(offset), int(vocab))
         self.seq_len, self.batch, self.world, self.seed = seq_len, batch, world, seed
         self.n_windows = int(self.L.n_windows)
         # train on the first n_use windows only (the tail is a held-out evaluation split)

@@ -324,14 +324,20 @@ def test_dataset_formats(tmp_path):
     assert len(load_token_array(str(tmp_path / "c.csv"), vocab=512)) > 4
 
 
-@pytest.mark.parametrize("dtype,vocab", [(np.uint16, 512), (np.uint32, 100000)])
-def test_native_token_loader_matches_numpy_path(tmp_path, monkeypatch, dtype, vocab):
+@pytest.mark.parametrize("dtype,vocab,ext", [(np.uint16, 512, "bin"), (np.uint32, 100000, "bin"),
+                                             (np.int32, 128256, "npy"), (np.uint16, 512, "npy")])
+def test_native_token_loader_matches_numpy_path(tmp_path, monkeypatch, dtype, vocab, ext):
     """csrc/runtime token loader (mmap + prefetch threads) yields exactly the numpy path's batches,
-    across epoch boundaries, per rank, and after a resume seek."""
+    across epoch boundaries, per rank, and after a resume seek -- raw .bin files and .npy files (whose
+    header the native loader must skip: reading it as tokens produced ids far past the vocabulary)."""
     pytest.importorskip("finetune_controller_amd._rt")
     toks = (np.arange(5000, dtype=np.int64) * 7919 % vocab).astype(dtype)
-    name = "t.u32.bin" if dtype == np.uint32 else "t.bin"
-    toks.tofile(tmp_path / name)
+    if ext == "npy":
+        name = "t.npy"
+        np.save(tmp_path / name, toks, allow_pickle=False)
+    else:
+        name = "t.u32.bin" if dtype == np.uint32 else "t.bin"
+        toks.tofile(tmp_path / name)
     for rank in (0, 1):
         monkeypatch.setenv("FTC_NATIVE_LOADER", "1")
         nat = PackedTokenDataset(str(tmp_path / name), vocab=vocab, batch=3, seq_len=32, device="cpu", rank=rank,
@@ -350,6 +356,25 @@ def test_native_token_loader_matches_numpy_path(tmp_path, monkeypatch, dtype, vo
         for _ in range(3):
             assert torch.equal(next(nat)[0], next(ref)[0])
         nat._native.close()
+
+
+@pytest.mark.parametrize("native", ["0", "1"])
+def test_out_of_vocab_token_ids_fail_on_the_host(tmp_path, monkeypatch, native):
+    """A dataset id >= the model's vocabulary (wrong tokenizer) must raise a clear error on the host --
+    on the GPU it would make the embedding gather fault the device."""
+    if native == "1":
+        pytest.importorskip("finetune_controller_amd._rt")
+    monkeypatch.setenv("FTC_NATIVE_LOADER", native)
+    toks = (np.arange(4000, dtype=np.int64) % 500).astype(np.int32)
+    toks[1234] = 700  # one bad id
+    np.save(tmp_path / "t.npy", toks, allow_pickle=False)
+    ds = PackedTokenDataset(str(tmp_path / "t.npy"), vocab=512, batch=4, seq_len=64, device="cpu", seed=1)
+    assert (ds._native is not None) == (native == "1")
+    with pytest.raises((ValueError, RuntimeError), match="512"):
+        for _ in range(2 * ds.steps_per_epoch):
+            next(ds)
+    if ds._native is not None:
+        ds._native.close()
 
 
 @pytest.mark.parametrize("native", ["0", "1"])
