@@ -1091,3 +1091,40 @@ def test_full_ft_overlapped_update_matches_serial(C, monkeypatch, tmp_path):
     # the overlapped path zeroes each stage's gradient right after its update; the serial one keeps
     # the last gradients until the next zero_grad
     assert torch.count_nonzero(g1) == 0 and torch.count_nonzero(g0) > 0
+
+
+@pytest.mark.parametrize("method", ["full", "lora"])
+def test_gpt2_steps_hip_match_torch_path(C, monkeypatch, method):
+    """GPT-2 geometry (d 768, 12 heads of 64, odd vocab 50257, tied lm_head, LayerNorm/GELU, learned
+    positions) on the HIP path -- D=64 flash attention, chunked CE over the odd vocabulary, flat AdamW
+    (+ LoRA on the packed projections) -- against the stock-PyTorch path over three steps."""
+    from finetune_controller_amd.models import LoRAConfig, build_model
+    from finetune_controller_amd.models.config import ModelConfig
+    from finetune_controller_amd.train.optim import FlatAdamW
+
+    cfg = ModelConfig("gpt2", 50257, 768, 2, 12, 12, 3072, 1024, tie_embeddings=True, name="gpt2-2l")
+    lc = LoRAConfig(r=16, alpha=32) if method == "lora" else None
+    ids = torch.randint(0, cfg.vocab_size, (2, 512), device=DEV)
+    labels = torch.roll(ids, -1, 1)
+    res = {}
+    for mode in ("hip", "torch"):
+        monkeypatch.setenv("FTC_KERNELS", mode)
+        torch.manual_seed(0)
+        m = build_model(cfg, lc, device=DEV, dtype=torch.bfloat16)
+        m.init_weights(seed=5)
+        if lc is not None:
+            m.freeze_base()
+        opt = FlatAdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3 if lc else 1e-4, max_grad_norm=1.0)
+        losses = []
+        for _ in range(3):
+            opt.zero_grad()
+            loss = m(ids, labels)
+            loss.backward()
+            opt.step()
+            losses.append(loss.float().item())
+        res[mode] = (losses, opt.param_flat.float().clone())
+    (lh, ph), (lt, pt) = res["hip"], res["torch"]
+    for a, b in zip(lh, lt):
+        assert abs(a - b) < 2e-2 * abs(b), (lh, lt)
+    assert lh[2] < lh[0]
+    assert (ph - pt).abs().max().item() < 1e-2
