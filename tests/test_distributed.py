@@ -314,3 +314,51 @@ def test_sequence_parallel_rccl_matches_single_gpu(tmp_path, method):
           f"{ref_norm:.6g}")
     assert cos > 0.9999, cos  # measured 0.999995-0.999997
     assert abs(res[0]["norm"] / 2 - ref_norm) < 1e-3 * ref_norm, (res[0]["norm"] / 2, ref_norm)
+
+
+# --------------------------------------------------------------------------- DDP over RCCL on the GPU
+_DDP_GPU = dict(model="llama3-8b-1l", batch_size=2, seq_len=512, synthetic=True, max_steps=1, resume=False,
+                device="cuda", dtype="bf16", lr=0.0, max_grad_norm=0.0, save_model=False, grad_dtype="fp32")
+
+
+def _ddp_gpu_worker(rank, world, port, tmp, q, method, engine):
+    os.environ["FTC_SHARE_GPU"] = "1"
+    _rank_env(rank, world, port, tmp)
+    tr = Trainer(TrainConfig(method=method, checkpoint_path=tmp, comm_engine=engine,
+                             bucket_mb=0.25 if method == "lora" else 64.0, **_DDP_GPU))
+    tr.train_step(0.0)
+    sample, norm = _grad_digest(tr)
+    q.put((rank, {"sample": sample, "norm": norm, "buckets": len(tr.ddp.buckets)}))
+    tr.close()
+    _hold(tmp, port)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method,engine", [("lora", "torch"), ("lora", "native"), ("full", "torch")])
+def test_ddp_rccl_matches_per_rank_sum(tmp_path, method, engine):
+    """DDP with 2 ranks over RCCL (sharing the card; torch.distributed or the native engine): the bucketed
+    all-reduce -- launched from grad hooks mid-backward, including the grad-ready hook of weights whose
+    gradient a beta=1 GEMM writes in place -- leaves on both ranks the sum of the gradients one process
+    computes on each rank's batch alone (same kernels, same data seeds; fp32 buffer)."""
+    res = _run_ranks(_ddp_gpu_worker, 2, tmp_path, method, engine, timeout=100)
+    total, norm_ref = None, None
+    for rank in range(2):
+        tr = Trainer(TrainConfig(method=method, checkpoint_path=str(tmp_path), **_DDP_GPU))
+        tr._data = SyntheticTokens(tr.cfg.vocab_size, 2, 512, tr.device, seed=tr.tc.seed + rank)
+        tr.train_step(0.0)
+        if total is None:
+            total = tr.opt.grad_flat.detach().clone()
+        else:
+            total += tr.opt.grad_flat.detach()
+        tr.close()
+    gen = torch.Generator().manual_seed(1234)
+    idx = torch.randint(0, total.numel(), (1 << 20,), generator=gen)
+    ref, norm_ref = total[idx.to(total.device)].float().cpu(), float(total.double().norm())
+    assert res[0]["buckets"] > 1
+    torch.testing.assert_close(res[1]["sample"], res[0]["sample"], atol=0, rtol=0)
+    scale = ref.abs().max().item()
+    assert scale > 0
+    err = (res[0]["sample"] - ref).abs().max().item() / scale
+    print(f"ddp2 {method}/{engine}: max rel err {err:.3g}, norm {res[0]['norm']:.6g} vs {norm_ref:.6g}, "
+          f"{res[0]['buckets']} buckets")
+    assert err < 1e-5, err  # measured: bitwise equal (0) for all three
