@@ -362,3 +362,37 @@ def test_ddp_rccl_matches_per_rank_sum(tmp_path, method, engine):
     print(f"ddp2 {method}/{engine}: max rel err {err:.3g}, norm {res[0]['norm']:.6g} vs {norm_ref:.6g}, "
           f"{res[0]['buckets']} buckets")
     assert err < 1e-5, err  # measured: bitwise equal (0) for all three
+
+
+def _zero_gpu_worker(rank, world, port, tmp, q, zero):
+    os.environ["FTC_SHARE_GPU"] = "1"
+    _rank_env(rank, world, port, tmp)
+    tr = Trainer(TrainConfig(method="full", checkpoint_path=tmp, zero_stage=zero,
+                             **{**_DDP_GPU, "lr": 1e-3, "max_grad_norm": 1.0}))
+    params = [p for p in tr.model.parameters() if p.requires_grad]
+
+    def digest():
+        return torch.cat([p.detach().reshape(-1)[:: max(1, p.numel() // 4096)].float().cpu() for p in params])
+
+    before = digest()
+    tr.train_step(1e-3)
+    torch.cuda.synchronize()
+    q.put((rank, {"before": before, "after": digest()}))
+    tr.close()
+    _hold(tmp, port)
+
+
+@pytest.mark.gpu
+def test_zero1_rccl_update_matches_ddp(tmp_path):
+    """ZeRO-1 on 2 RCCL ranks (gradient reduce-scatter, AdamW on each rank's shard, parameter all-gather;
+    grad clipping on the sharded norm) updates every parameter exactly as replicated DDP + AdamW does."""
+    z = _run_ranks(_zero_gpu_worker, 2, tmp_path, 1, timeout=100)
+    d = _run_ranks(_zero_gpu_worker, 2, tmp_path, 0, timeout=100)
+    for r in (0, 1):
+        torch.testing.assert_close(z[r]["before"], d[r]["before"], atol=0, rtol=0)
+        torch.testing.assert_close(z[r]["after"], z[0]["after"], atol=0, rtol=0)  # the all-gather
+    moved = (d[0]["after"] != d[0]["before"]).float().mean().item()
+    diff = (z[0]["after"] - d[0]["after"]).abs().max().item()
+    print(f"zero1 vs ddp: {moved:.3f} of sampled weights moved, max |diff| {diff:.3g}")
+    assert moved > 0.5
+    torch.testing.assert_close(z[0]["after"], d[0]["after"], atol=1e-6, rtol=0)
