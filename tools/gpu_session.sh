@@ -24,7 +24,7 @@ fatal() {  # rc -> 0 if the session may continue
 for s in "${STEPS[@]}"; do
   case "$s" in
     tests)
-      timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
       fatal $? tests; tail -5 gpurun_out/pytest_gpu.log ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
