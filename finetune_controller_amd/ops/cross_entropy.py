@@ -41,8 +41,9 @@ class _FusedLinearCE(torch.autograd.Function):
         h2 = h.reshape(-1, d)
         lab = labels.reshape(-1)
         T = h2.shape[0]
-        n_valid = int(n_valid_override) if n_valid_override else int((lab != ignore_index).sum().item())
-        gscale = 1.0 / max(n_valid, 1)
+        # the normaliser may be fractional: a sequence-parallel shard divides by the whole batch's count / P
+        n_valid = float(n_valid_override) if n_valid_override else float((lab != ignore_index).sum().item())
+        gscale = 1.0 / n_valid if n_valid > 0 else 1.0
         hip = use_hip(h2) and h2.dtype == torch.bfloat16
         # gradients are produced in this pass: only when the caller runs with autograd on (an eval
         # forward under no_grad must neither compute dh nor touch W.main_grad)
@@ -103,8 +104,9 @@ class _FusedLinearCE(torch.autograd.Function):
 
 
 def fused_linear_cross_entropy(h: torch.Tensor, W: torch.Tensor, labels: torch.Tensor, chunk_rows: int = 4096,
-                               ignore_index: int = -100, n_valid: int | None = None) -> torch.Tensor:
-    """Mean CE over non-ignored labels. ``n_valid`` (optional) avoids a host sync per step."""
+                               ignore_index: int = -100, n_valid: float | None = None) -> torch.Tensor:
+    """Mean CE over non-ignored labels. ``n_valid`` (optional) avoids a host sync per step; it is the
+    normaliser (the loss is the sum over valid labels / n_valid) and may be fractional."""
     return _FusedLinearCE.apply(h, W, labels, chunk_rows, ignore_index, n_valid or 0, torch.is_grad_enabled())
 
 

@@ -151,27 +151,42 @@ def sp_attention(qkv: torch.Tensor, B: int, S_local: int, H: int, KV: int, D: in
     return _OutToTokens.apply(a, B, S_local, H, D, sp)
 
 
+def shard_batch(x: torch.Tensor, y: torch.Tensor, sp: SeqGroup) -> tuple[torch.Tensor, torch.Tensor]:
+    """This rank's contiguous 1/P of every row of a [B, S] batch (inputs and labels alike: the label of
+    a chunk's last token is the next chunk's first input, already in ``y``)."""
+    S = x.shape[-1]
+    if S % sp.size:
+        raise ValueError(f"seq_len {S} is not divisible by the sequence parallel degree {sp.size}")
+    Sl = S // sp.size
+    lo = sp.rank * Sl
+    y = y.reshape(x.shape)
+    return x[:, lo:lo + Sl].contiguous(), y[:, lo:lo + Sl].contiguous()
+
+
 class SeqShard:
     """Data wrapper: every rank of an SP group draws the same [B, S] batch and keeps its contiguous
-    1/P of each row (inputs and labels alike: the label of a chunk's last token is the next chunk's
-    first input, already in ``y``)."""
+    1/P of each row (``shard_batch``).
+
+    Loss normaliser: a masked batch (document boundaries, completion-only prompts) leaves the P shards
+    different valid-token counts, so each rank divides its local loss sum by the WHOLE batch's count
+    over P (``last_n_valid``, counted host-side by the source on the full batch): the mean over the
+    group's ranks is then the batch's mean loss exactly, and so is the all-reduced gradient."""
 
     def __init__(self, inner, sp: SeqGroup):
         self.inner, self.sp = inner, sp
-        self.last_n_valid = None
+
+    @property
+    def last_n_valid(self):
+        n = getattr(self.inner, "last_n_valid", None)
+        return None if n is None else n / self.sp.size
 
     def __iter__(self):
         return self
 
     def __next__(self):
-        x, y = next(self.inner)
-        S = x.shape[-1]
-        if S % self.sp.size:
-            raise ValueError(f"seq_len {S} is not divisible by the sequence parallel degree {self.sp.size}")
-        Sl = S // self.sp.size
-        lo = self.sp.rank * Sl
-        y = y.reshape(x.shape)
-        return x[:, lo:lo + Sl].contiguous(), y[:, lo:lo + Sl].contiguous()
+        return shard_batch(*next(self.inner), self.sp)
 
     def __getattr__(self, name):  # state(), load_state(), steps_per_epoch, ... of the wrapped source
+        if name in ("inner", "sp"):
+            raise AttributeError(name)
         return getattr(self.inner, name)

@@ -349,11 +349,18 @@ class Trainer:
         """Fixed held-out batches of this rank: the dataset's tail windows, or (synthetic data) a
         separate pool drawn from another seed."""
         data = self.data()
+        if self.sp is not None:  # the group's ranks evaluate the same sequences, each its 1/P of them
+            from ..parallel.sequence import shard_batch
+
+            return (shard_batch(x, y, self.sp) for x, y in self._eval_full(data.inner))
+        return self._eval_full(data)
+
+    def _eval_full(self, data):
         if isinstance(data, PackedTokenDataset):
             return EvalWindows(data, self.tc.eval_batches).batches()
-        if self._eval_synth is None:
+        if self._eval_synth is None:  # one pool per data-parallel replica (shared by an SP group)
             self._eval_synth = SyntheticTokens(self.cfg.vocab_size, self.tc.batch_size, self.tc.seq_len, self.device,
-                                               seed=self.tc.seed + 7919 + self.info.rank)
+                                               seed=self.tc.seed + 7919 + self.dp_rank)
         self._eval_synth.i = 0  # the same batches every evaluation
         return (next(self._eval_synth) for _ in range(self.tc.eval_batches))
 

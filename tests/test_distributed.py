@@ -231,35 +231,41 @@ def test_resume_rejects_foreign_parameter_set(tmp_path):
 
 
 # --------------------------------------------------------------------------- Ulysses sequence parallelism
-def _sp_worker(rank, world, port, tmp, q, method, window_model):
+def _sp_worker(rank, world, port, tmp, q, method, window_model, doc_len):
     _rank_env(rank, world, port, tmp)
     tc = TrainConfig(model=window_model, method=method, batch_size=2, seq_len=64, synthetic=True, max_steps=1,
                      checkpoint_path=tmp, resume=False, device="cpu", dtype="fp32", lr=0.0, max_grad_norm=0.0,
-                     save_model=False, sp=world, bucket_mb=0.05)
+                     save_model=False, sp=world, bucket_mb=0.05, synthetic_doc_len=doc_len, eval_batches=2)
     tr = Trainer(tc)
     loss = tr.train_step(0.0)
     q.put((rank, {"loss": float(loss), "grad": tr.opt.grad_flat.detach().double().clone(),
-                  "layout": [(o, n) for o, n in tr.opt.offsets]}))
+                  "layout": [(o, n) for o, n in tr.opt.offsets], "eval": tr.evaluate()}))
     tr.close()
     _hold(tmp, port)
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("method,model", [("full", "llama-tiny"), ("lora", "llama-tiny"), ("full", "mistral-tiny")])
-def test_sequence_parallel_matches_single_process(tmp_path, method, model):
+@pytest.mark.parametrize("method,model,doc_len", [("full", "llama-tiny", 0), ("lora", "llama-tiny", 0),
+                                                  ("full", "mistral-tiny", 0), ("full", "llama-tiny", 40)])
+def test_sequence_parallel_matches_single_process(tmp_path, method, model, doc_len):
     """Ulysses SP over 2 gloo ranks (each holds half of every sequence; attention all-to-alls heads <->
     tokens) against one process training the same full sequences: the mean of the ranks' losses and the
-    all-reduced gradient equal the single-process loss / gradient (fp32, sliding window included)."""
+    all-reduced gradient equal the single-process loss / gradient (fp32, sliding window included), also
+    when masked labels leave the two halves different valid-token counts (doc_len 40: the document
+    boundary's masked label falls in the second half only), and the held-out loss matches."""
     world = 2
-    res = _run_ranks(_sp_worker, world, tmp_path, method, model)
+    res = _run_ranks(_sp_worker, world, tmp_path, method, model, doc_len)
     tc = TrainConfig(model=model, method=method, batch_size=2, seq_len=64, synthetic=True, max_steps=1,
                      checkpoint_path=str(tmp_path), resume=False, device="cpu", dtype="fp32", lr=0.0,
-                     max_grad_norm=0.0, save_model=False)
+                     max_grad_norm=0.0, save_model=False, synthetic_doc_len=doc_len, eval_batches=2)
     tr = Trainer(tc)
     ref_loss = float(tr.train_step(0.0))
     ref = tr.opt.grad_flat.detach().double().clone()
+    ref_eval = tr.evaluate()
     tr.close()
     assert abs(sum(res[r]["loss"] for r in range(world)) / world - ref_loss) < 1e-5 * abs(ref_loss)
+    assert res[0]["eval"] == res[1]["eval"]
+    assert abs(res[0]["eval"] - ref_eval) < 1e-5 * abs(ref_eval), (res[0]["eval"], ref_eval)
     g = res[0]["grad"]
     torch.testing.assert_close(res[1]["grad"], g, atol=0, rtol=0)  # one all-reduced gradient
     # the buffer holds the SUM of the ranks' half-sequence mean gradients; the optimizer applies
