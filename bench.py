@@ -216,6 +216,9 @@ def main(argv=None) -> int:
         return 2
     if a.kernels:
         os.environ["FTC_KERNELS"] = a.kernels
+    # RCCL's intra-node buffers travel by dmabuf IPC on these hosts; the legacy IPC handle path fails
+    # (hipIpcGetMemHandle: invalid argument).  Read by the HIP runtime at its first call, i.e. after here.
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
     import torch
     import torch.distributed as dist
