@@ -220,6 +220,18 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
   // of the 32-wide d tile and key rows [16ks + 4*hh (+8), +4)
   const int gi = lane >> 4, li = lane & 15;
   const int trq = li >> 2, trp = li & 3;
+  // lane byte offsets of the transposed V reads, hoisted out of the tile loop: row r1 = 16 ks + 4 hh
+  // + trq has swizzle (trq << 2) | hh for every ks (r1 + 8: | (hh + 2)), so ks only moves the row by
+  // a compile-time 16 * D * 2 bytes (the ds_read's immediate offset) and the 2 * DT lane offsets below
+  // are the only per-lane addressing left in phase B2 (was ~20 address adds per tile)
+  int vto[DT][2];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    const int col = dt * 32 + 16 * (gi & 1) + 4 * trp;
+    const int chunk = col >> 3, half8 = (col & 7) ? 8 : 0;
+    vto[dt][0] = lds_off<D>(4 * hh + trq, chunk) + half8;
+    vto[dt][1] = lds_off<D>(4 * hh + trq + 8, chunk) + half8;
+  }
 
   f32x16 s[2];   // S^T of the current tile, then its P (registers between the phases)
   bf16x8 pf[4];  // packed P^T operand of the PV MFMAs (carried across a barrier by PP's half 1)
@@ -313,14 +325,13 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
   auto phaseB2 = [&](const char* Vc) __attribute__((always_inline)) {
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
-      const int col = dt * 32 + 16 * (gi & 1) + 4 * trp;
-      const int chunk = col >> 3, half8 = (col & 7) ? 8 : 0;
       s16x4 vt[8];  // all 8 transposed reads of this 32-wide d tile in flight before the MFMA chain
+      const char* v0 = Vc + vto[dt][0];
+      const char* v8 = Vc + vto[dt][1];
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const int r1 = 16 * ks + 4 * hh + trq;
-        vt[2 * ks] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vc + lds_off<D>(r1, chunk) + half8));
-        vt[2 * ks + 1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vc + lds_off<D>(r1 + 8, chunk) + half8));
+        vt[2 * ks] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(v0 + ks * 16 * D * 2));
+        vt[2 * ks + 1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(v8 + ks * 16 * D * 2));
       }
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
