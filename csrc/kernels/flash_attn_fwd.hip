@@ -36,6 +36,14 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 // query rows per workgroup = 32 x waves (WAVES = 4: 256 threads, two workgroups per CU; WAVES = 8: 512
 // threads, one workgroup per CU sharing every K/V tile between twice the query rows)
 constexpr int BK = 64;   // keys per tile
+// build-time A/B knobs (tools/fwd_knobs_ab.sh): K-fragment reads issued ahead of the S MFMA chain, and a
+// raised wave priority over the S MFMA phase
+#ifndef FWD_KPRE
+#define FWD_KPRE 4
+#endif
+#ifndef FWD_PRIO
+#define FWD_PRIO 0
+#endif
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
@@ -260,13 +268,13 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
     }
     // software pipeline of the 2*DSTEPS K-fragment reads against the MFMA chain, 4 reads in flight
     // (the default scheduler serialises read -> wait -> mfma to save registers)
-    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, FWD_KPRE, 0);
 #pragma unroll
-    for (int i = 0; i < 2 * DSTEPS - 4; ++i) {
+    for (int i = 0; i < 2 * DSTEPS - FWD_KPRE; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, FWD_KPRE, 0);
   };
   // ---- phase B1: mask (wave-uniform branch, branch-free selects inside) + online softmax in the log2
   // domain; P packed as the bf16 B operand of the PV MFMAs
@@ -346,7 +354,9 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
     // wave passed this tile's barrier
     auto tile = [&](const int t, const char* Kc, const char* Vc, char* Kn, char* Vn) __attribute__((always_inline)) {
       sync_tile(t, Kn, Vn);
+      if constexpr (FWD_PRIO) __builtin_amdgcn_s_setprio(1);  // S MFMA phase ahead of the partner wave's VALU
       phaseA(Kc);
+      if constexpr (FWD_PRIO) __builtin_amdgcn_s_setprio(0);
       phaseB1(t);
       phaseB2(Vc);
     };
