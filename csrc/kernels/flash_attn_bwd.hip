@@ -641,6 +641,9 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
 }
 
 // ---------------------------------------------------------------- 3. dQ
+#ifndef DQ_CINIT
+#define DQ_CINIT 1
+#endif
 // One K/V tile by LDS-DMA: NGT 1 KiB pieces per matrix per wave (device-only: see dkdv_dma)
 template <int D, int NGT, int RPG>
 FTC_DEV void kv_dma(__amdgpu_buffer_rsrc_t kr, __amdgpu_buffer_rsrc_t vr, const int* voff, int toff, char* kdst,
@@ -728,6 +731,12 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
   for (int t = 0; t < DT; ++t)
 #pragma unroll
     for (int i = 0; i < 16; ++i) dq[t][i] = 0.f;
+  // DQ_CINIT: the dP^T chains start from -delta (the query is on the lane, so one loop-invariant
+  // accumulator image serves every tile as the first MFMA's C operand): dS^T = P (dP - delta) then
+  // needs no per-element add (32 VALU per tile)
+  f32x16 ndv;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) ndv[i] = DQ_CINIT ? ndlt : 0.f;
 
   __builtin_amdgcn_s_waitcnt(0x0F70);  // retire the Q/dO/lse loads before any DMA (vmcnt(0))
   if (ntiles > 0) issue(kv_begin, Kt0, Vt0);
@@ -741,7 +750,8 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) { s[kt][i] = 0.f; dp[kt][i] = 0.f; }
+      for (int i = 0; i < 16; ++i) s[kt][i] = 0.f;
+      dp[kt] = ndv;
       const int r = kt * 32 + lr;
 #pragma unroll
       for (int st = 0; st < DSTEPS; ++st) {
@@ -781,7 +791,7 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) dp[kt][i] = s[kt][i] * (dp[kt][i] + ndlt);  // dS^T
+      for (int i = 0; i < 16; ++i) dp[kt][i] = DQ_CINIT ? s[kt][i] * dp[kt][i] : s[kt][i] * (dp[kt][i] + ndlt);  // dS^T
     bf16x8 sb[4];
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) sb[ks] = pack8_bf(dp[ks >> 1], 8 * (ks & 1));
