@@ -44,6 +44,9 @@ constexpr int BK = 64;   // keys per tile
 #ifndef FWD_PRIO
 #define FWD_PRIO 0
 #endif
+#ifndef FWD_WIDE_STORE  // 16-byte O stores in the epilogue (tools/fwd_knobs_ab.sh)
+#define FWD_WIDE_STORE 1
+#endif
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
@@ -403,8 +406,32 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
   // ---- epilogue: normalise, store O (bf16) and LSE (natural log)
   const float ltot = l + __shfl_xor(l, 32, 64);
   const float inv = ltot > 0.f ? 1.0f / ltot : 0.f;
-  if (qvalid) {
-    uint16_t* op = a.o + ((long long)b * S + qrow) * a.o_rs + (long long)hq * D;
+  uint16_t* op = a.o + ((long long)b * S + (qvalid ? qrow : 0)) * a.o_rs + (long long)hq * D;
+  if (FWD_WIDE_STORE && (a.o_rs & 7) == 0) {
+    // 16-byte stores (guide T21: the store tail is issue-bound): lanes l and l ^ 32 hold the same
+    // query row, d runs {8 g4 + 4 hh + 0..3}; two v_permlane32_swap per dword pair give lane half hh
+    // the 16 contiguous d [16 hh, 16 hh + 16) of each 32-wide tile -> 2 x dwordx4 instead of 4 x dwordx2
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      uint32_t w[4][2];
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        w[g4][0] = pack_bf2(o[dt][4 * g4 + 0] * inv, o[dt][4 * g4 + 1] * inv);
+        w[g4][1] = pack_bf2(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
+      }
+      // swap(x, y): lanes 0-31 keep x and receive the upper half's x; lanes 32-63 receive the lower
+      // half's y and keep y -> (x_own | x_partner) below, (y_partner | y_own) above
+      const auto a0 = __builtin_amdgcn_permlane32_swap(w[0][0], w[2][0], false, false);
+      const auto a1 = __builtin_amdgcn_permlane32_swap(w[0][1], w[2][1], false, false);
+      const auto b0 = __builtin_amdgcn_permlane32_swap(w[1][0], w[3][0], false, false);
+      const auto b1 = __builtin_amdgcn_permlane32_swap(w[1][1], w[3][1], false, false);
+      if (qvalid) {
+        const int d = dt * 32 + 16 * hh;
+        *reinterpret_cast<uint4*>(op + d) = make_uint4(a0[0], a1[0], a0[1], a1[1]);
+        *reinterpret_cast<uint4*>(op + d + 8) = make_uint4(b0[0], b1[0], b0[1], b1[1]);
+      }
+    }
+  } else if (qvalid) {
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -415,6 +442,8 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
         w.y = pack_bf2(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
         *reinterpret_cast<uint2*>(op + d) = w;
       }
+  }
+  if (qvalid) {
     if (hh == 0) {
       const float lse2 = (m == -INFINITY) ? -INFINITY : m + __log2f(ltot);
       a.lse[((long long)b * a.H + hq) * S + qrow] = lse2 * LN2;

@@ -7,11 +7,14 @@
 # Result (profiles/r2/fwd_knobs/, one box): base 0.560 / 0.564 ms, prio 0.574 / 0.570 (slower: the
 # raised priority starves the partner wave's softmax), kpre8 0.564 / 0.567, kpre2 0.563 / 0.559 (noise)
 # -> the defaults (KPRE 4, no priority) stay.
+# narrow (8-byte O stores instead of the 16-byte epilogue, profiles/r2/fwd_wide_store/): 0.559-0.562 vs
+# 0.553-0.555 ms, headline 36,752 / 36,818 vs 36,918 / 36,822 tok/s -> wide stores are the default.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-declare -A FLAGS=([prio]="-DFWD_PRIO=1" [kpre8]="-DFWD_KPRE=8" [kpre2]="-DFWD_KPRE=2")
-NAMES=(prio kpre8 kpre2)
+declare -A FLAGS=([prio]="-DFWD_PRIO=1" [kpre8]="-DFWD_KPRE=8" [kpre2]="-DFWD_KPRE=2" [narrow]="-DFWD_WIDE_STORE=0")
+# variants to build / run (default: the latest question); e.g. FWD_AB_NAMES="prio kpre8 kpre2"
+read -r -a NAMES <<< "${FWD_AB_NAMES:-narrow}"
 if [ "$1" = "build" ]; then
   TL=$(python -c 'import torch,os;print(os.path.join(os.path.dirname(torch.__file__),"lib"))')
   for n in "${NAMES[@]}"; do
@@ -29,6 +32,10 @@ if [ "$1" = "build" ]; then
   exit 0
 fi
 O=gpurun_out/fwd_knobs; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread \
+  -k "flash or llama_lora or packed or tail or family or gpt2 or decode or generate" > $O/pytest_tree.log 2>&1 \
+  || { tail -5 $O/pytest_tree.log; exit 1; }
+echo "tree: $(tail -1 $O/pytest_tree.log)"
 for n in "${NAMES[@]}"; do
   (cd ab_fwd_$n && timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 120 \
     --timeout-method thread -k "flash or llama_lora or packed or tail" > ../$O/pytest_$n.log 2>&1) \
@@ -41,5 +48,13 @@ for r in 1 2; do
   for n in "${NAMES[@]}"; do
     (cd ab_fwd_$n && timeout -k 10 300 python tools/bench_attention.py --rounds 3 > ../$O/attn_$n$r.log 2>&1) || exit 1
     echo "$n $(grep -v amdgpu $O/attn_$n$r.log | tail -1 | grep -o "\"ours_fwd\": {[^}]*}")"
+  done
+done
+for r in 1 2; do
+  timeout -k 10 400 python bench.py --steps 10 --warmup 3 > $O/bench_base$r.log 2>&1 || exit 1
+  echo "base $(grep '^{' $O/bench_base$r.log | cut -c70-140)"
+  for n in "${NAMES[@]}"; do
+    (cd ab_fwd_$n && timeout -k 10 400 python bench.py --steps 10 --warmup 3 > ../$O/bench_$n$r.log 2>&1) || exit 1
+    echo "$n $(grep '^{' $O/bench_$n$r.log | cut -c70-140)"
   done
 done
