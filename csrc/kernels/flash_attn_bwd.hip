@@ -61,6 +61,43 @@ FTC_DEV bf16x8 pack8_bf(const f32x16& p, int base) {
   u.w = pack_bf2(p[base + 6], p[base + 7]);
   return as_bf8(u);
 }
+// Epilogue rows (lanes l and l ^ 32 hold the same row, d runs {8 g4 + 4 hh + 0..3} of each 32-wide tile):
+// WIDE swaps dword pairs across the lane halves (v_permlane32_swap) so each lane stores 16 contiguous
+// d as 2 x dwordx4 per tile instead of 4 x dwordx2 (the store tail is issue-bound; forward: -1 %).
+#ifndef BWD_WIDE_STORE
+#define BWD_WIDE_STORE 1
+#endif
+template <int DT>
+FTC_DEV void store_rows(uint16_t* p, const f32x16* acc, float sc, int hh, bool wide) {
+  if (BWD_WIDE_STORE && wide) {
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      uint32_t w[4][2];
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        w[g4][0] = pack_bf2(acc[dt][4 * g4 + 0] * sc, acc[dt][4 * g4 + 1] * sc);
+        w[g4][1] = pack_bf2(acc[dt][4 * g4 + 2] * sc, acc[dt][4 * g4 + 3] * sc);
+      }
+      const auto a0 = __builtin_amdgcn_permlane32_swap(w[0][0], w[2][0], false, false);
+      const auto a1 = __builtin_amdgcn_permlane32_swap(w[0][1], w[2][1], false, false);
+      const auto b0 = __builtin_amdgcn_permlane32_swap(w[1][0], w[3][0], false, false);
+      const auto b1 = __builtin_amdgcn_permlane32_swap(w[1][1], w[3][1], false, false);
+      const int d = dt * 32 + 16 * hh;
+      *reinterpret_cast<uint4*>(p + d) = make_uint4(a0[0], a1[0], a0[1], a1[1]);
+      *reinterpret_cast<uint4*>(p + d + 8) = make_uint4(b0[0], b1[0], b0[1], b1[1]);
+    }
+  } else {
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        uint2 w;
+        w.x = pack_bf2(acc[dt][4 * g4 + 0] * sc, acc[dt][4 * g4 + 1] * sc);
+        w.y = pack_bf2(acc[dt][4 * g4 + 2] * sc, acc[dt][4 * g4 + 3] * sc);
+        *reinterpret_cast<uint2*>(p + dt * 32 + 8 * g4 + 4 * hh) = w;
+      }
+  }
+}
 // A operand (32 rows x 16 k, permuted k) via two transposed reads of an LDS image whose rows are k
 // and columns are the A rows: elements 0..3 <- image rows kb+4h+0..3, elements 4..7 <- +8.
 // tr_offsets() gives the lane's two byte offsets for kb = 0; since the swizzle depends on r & 15 only,
@@ -624,19 +661,9 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
     const int key = wkey0 + 32 * j + lr;
     uint16_t* dkp = a.dk + ((long long)b * S + key) * a.dkv_rs + (long long)kvh * D;
     uint16_t* dvp = a.dv + ((long long)b * S + key) * a.dkv_rs + (long long)kvh * D;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = dt * 32 + 8 * g4 + 4 * hh;
-        uint2 wk, wv;
-        wk.x = pack_bf2(dk[j][dt][4 * g4 + 0] * a.scale, dk[j][dt][4 * g4 + 1] * a.scale);
-        wk.y = pack_bf2(dk[j][dt][4 * g4 + 2] * a.scale, dk[j][dt][4 * g4 + 3] * a.scale);
-        wv.x = pack_bf2(dv[j][dt][4 * g4 + 0], dv[j][dt][4 * g4 + 1]);
-        wv.y = pack_bf2(dv[j][dt][4 * g4 + 2], dv[j][dt][4 * g4 + 3]);
-        *reinterpret_cast<uint2*>(dkp + d) = wk;
-        *reinterpret_cast<uint2*>(dvp + d) = wv;
-      }
+    const bool wide = (a.dkv_rs & 7) == 0;
+    store_rows<DT>(dkp, dk[j], a.scale, hh, wide);
+    store_rows<DT>(dvp, dv[j], 1.0f, hh, wide);
   }
 }
 
@@ -810,16 +837,7 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
     if (t + 1 < ntiles) tile(t + 1, Kt1, Vt1, Kt0, Vt0);
   }
   uint16_t* op = a.dq + ((long long)b * S + qrow) * a.dq_rs + (long long)hq * D;
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int d = dt * 32 + 8 * g4 + 4 * hh;
-      uint2 w;
-      w.x = pack_bf2(dq[dt][4 * g4 + 0] * a.scale, dq[dt][4 * g4 + 1] * a.scale);
-      w.y = pack_bf2(dq[dt][4 * g4 + 2] * a.scale, dq[dt][4 * g4 + 3] * a.scale);
-      *reinterpret_cast<uint2*>(op + d) = w;
-    }
+  store_rows<DT>(op, dq, a.scale, hh, (a.dq_rs & 7) == 0);
 }
 
 
