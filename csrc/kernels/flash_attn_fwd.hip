@@ -44,6 +44,9 @@ constexpr int BK = 64;   // keys per tile
 #ifndef FWD_PRIO
 #define FWD_PRIO 0
 #endif
+#ifndef FWD_EARLY_DMA  // tile 0's DMA issued before the Q loads (tools/fwd_knobs_ab.sh)
+#define FWD_EARLY_DMA 0
+#endif
 #ifndef FWD_WIDE_STORE  // 16-byte O stores in the epilogue (tools/fwd_knobs_ab.sh)
 #define FWD_WIDE_STORE 1
 #endif
@@ -174,16 +177,17 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
   const bool qvalid = qrow < S;
   static_assert(BQ == 32 * WAVES, "geometry");
 
-  // ---- Q^T fragments (B operand of S^T = K Q^T): lane holds Q[qrow][16s + 8hh .. +8)
   bf16x8 qf[DSTEPS];
-  {
+  auto load_q = [&]() __attribute__((always_inline)) {
+    // ---- Q^T fragments (B operand of S^T = K Q^T): lane holds Q[qrow][16s + 8hh .. +8)
     const uint16_t* qp = a.q + ((long long)b * S + (qvalid ? qrow : 0)) * a.q_rs + (long long)hq * D + 8 * hh;
 #pragma unroll
     for (int s = 0; s < DSTEPS; ++s) {
       uint4 v = qvalid ? *reinterpret_cast<const uint4*>(qp + 16 * s) : make_uint4(0, 0, 0, 0);
       qf[s] = as_bf8(v);
     }
-  }
+  };
+  if constexpr (!FWD_EARLY_DMA) load_q();
 
   // ---- key range
   const int q_last = min(S, q0 + BQ) - 1;
@@ -224,8 +228,15 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
   float m = -INFINITY, l = 0.f;
   const float c = a.scale_log2;
 
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // Q fragments (plain loads) retired before any DMA: vmcnt(0)
-  if (ntiles > 0) fwd_dma<D, NGT, RPG>(krs, vrs, voff, kv_begin * (int)a.kv_rs * 2, K0, V0, wave);
+  if constexpr (FWD_EARLY_DMA) {
+    // tile 0's K/V DMA first, then the Q loads: both latencies overlap (the first tile's vmcnt(0)
+    // covers the two) instead of Q retiring before the DMA is issued
+    if (ntiles > 0) fwd_dma<D, NGT, RPG>(krs, vrs, voff, kv_begin * (int)a.kv_rs * 2, K0, V0, wave);
+    load_q();
+  } else {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // Q fragments (plain loads) retired before any DMA: vmcnt(0)
+    if (ntiles > 0) fwd_dma<D, NGT, RPG>(krs, vrs, voff, kv_begin * (int)a.kv_rs * 2, K0, V0, wave);
+  }
 
   // tr-read addressing (V^T A operand): 16-lane group gi = lane>>4 covers d cols [16*(gi&1), +16)
   // of the 32-wide d tile and key rows [16ks + 4*hh (+8), +4)

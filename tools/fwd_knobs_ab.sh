@@ -9,12 +9,14 @@
 # -> the defaults (KPRE 4, no priority) stay.
 # narrow (8-byte O stores instead of the 16-byte epilogue, profiles/r2/fwd_wide_store/): 0.559-0.562 vs
 # 0.553-0.555 ms, headline 36,752 / 36,818 vs 36,918 / 36,822 tok/s -> wide stores are the default.
+# FWD_EARLY_DMA=1 (tile 0's DMA before the Q loads; profiles/r2/fwd_early_dma/, 'base' = early there):
+# 0.586 / 0.566 vs 0.581 / 0.571 ms, headline 36,307 / 36,322 vs 36,306 / 36,302 -> noise, stays off.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-declare -A FLAGS=([prio]="-DFWD_PRIO=1" [kpre8]="-DFWD_KPRE=8" [kpre2]="-DFWD_KPRE=2" [narrow]="-DFWD_WIDE_STORE=0")
+declare -A FLAGS=([prio]="-DFWD_PRIO=1" [kpre8]="-DFWD_KPRE=8" [kpre2]="-DFWD_KPRE=2" [narrow]="-DFWD_WIDE_STORE=0" [lateq]="-DFWD_EARLY_DMA=0")
 # variants to build / run (default: the latest question); e.g. FWD_AB_NAMES="prio kpre8 kpre2"
-read -r -a NAMES <<< "${FWD_AB_NAMES:-narrow}"
+read -r -a NAMES <<< "${FWD_AB_NAMES:-lateq}"
 if [ "$1" = "build" ]; then
   TL=$(python -c 'import torch,os;print(os.path.join(os.path.dirname(torch.__file__),"lib"))')
   for n in "${NAMES[@]}"; do
