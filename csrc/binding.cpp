@@ -37,6 +37,10 @@ int ftc_gemm_tn_ok(const void* a, long long lda, const void* b, long long ldb, c
                    int K);
 int ftc_gemm_tn(const void* a, long long lda, const void* b, long long ldb, void* c, long long ldc, int c_fp32, int M,
                 int N, int K, float alpha, float beta, hipStream_t stream);
+int ftc_gemm_nt_ok(const void* a, long long lda, const void* b, long long ldb, const void* c, long long ldc, int c_fp32,
+                   int M, int N, int K);
+int ftc_gemm_nt(const void* a, long long lda, const void* b, long long ldb, void* c, long long ldc, int c_fp32, int M,
+                int N, int K, float alpha, float beta, hipStream_t stream);
 int ftc_copy2d_batched(const void* jobs, int njobs, long long max_elems, hipStream_t stream);
 int ftc_ce_fwd_bwd(void* logits, const long long* labels, float* loss, float* lse, long long rows, int V, long long ld,
                    float gscale, long long ignore_index, hipStream_t stream);
@@ -386,6 +390,29 @@ void gemm_tn_(at::Tensor& c, const at::Tensor& a, const at::Tensor& b, double al
         "gemm_tn_");
 }
 
+// ---------------- projection GEMM: c = alpha a b^T + beta c ----------------
+// a [M, K], b [N, K] bf16 row views (unit column stride, K contiguous); c [M, N] bf16 or fp32 row view.
+bool gemm_nt_ok(const at::Tensor& c, const at::Tensor& a, const at::Tensor& b) {
+  if (!a.is_cuda() || !b.is_cuda() || !c.is_cuda() || a.dim() != 2 || b.dim() != 2 || c.dim() != 2) return false;
+  if (a.device() != b.device() || a.device() != c.device()) return false;
+  if (a.scalar_type() != at::kBFloat16 || b.scalar_type() != at::kBFloat16) return false;
+  if (c.scalar_type() != at::kBFloat16 && c.scalar_type() != at::kFloat) return false;
+  if (a.stride(1) != 1 || b.stride(1) != 1 || c.stride(1) != 1) return false;
+  if (a.size(1) != b.size(1) || c.size(0) != a.size(0) || c.size(1) != b.size(0)) return false;
+  if (a.size(0) > INT32_MAX || a.size(1) > INT32_MAX || b.size(0) > INT32_MAX) return false;
+  return ftc_gemm_nt_ok(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
+                        c.scalar_type() == at::kFloat, (int)a.size(0), (int)b.size(0), (int)a.size(1)) != 0;
+}
+
+void gemm_nt_(at::Tensor& c, const at::Tensor& a, const at::Tensor& b, double alpha, double beta) {
+  TORCH_CHECK(gemm_nt_ok(c, a, b), "gemm_nt_: shapes / layouts outside the kernel contract (M, N % 256, K % 32, "
+              "bf16 row views a [M, K], b [N, K], c [M, N] bf16/fp32, 16-byte aligned)");
+  check(ftc_gemm_nt(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
+                    c.scalar_type() == at::kFloat, (int)a.size(0), (int)b.size(0), (int)a.size(1), (float)alpha,
+                    (float)beta, cur_stream()),
+        "gemm_nt_");
+}
+
 // ---------------- cross entropy (in place on logits) ----------------
 at::Tensor ce_fwd_bwd_(at::Tensor& logits, const at::Tensor& labels, double gscale, int64_t ignore_index) {
   need(logits, at::kBFloat16, "logits");
@@ -690,6 +717,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("transpose2d", &transpose2d, py::arg("x"), py::arg("out") = py::none());
   m.def("gemm_tn_ok", &gemm_tn_ok);
   m.def("gemm_tn_", &gemm_tn_);
+  m.def("gemm_nt_ok", &gemm_nt_ok);
+  m.def("gemm_nt_", &gemm_nt_, py::arg("c"), py::arg("a"), py::arg("b"), py::arg("alpha") = 1.0, py::arg("beta") = 0.0);
   m.def("ce_fwd_bwd_", &ce_fwd_bwd_);
   m.def("adamw_", &adamw_, py::arg("param"), py::arg("master"), py::arg("m"), py::arg("v"), py::arg("grad"),
         py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("step"),

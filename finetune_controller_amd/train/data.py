@@ -227,7 +227,10 @@ class PackedTokenDataset:
 
             dt = self.tokens.dtype
             if (isinstance(self.tokens, np.memmap) and self.loss_mask is None and dt.itemsize in (2, 4)
-                    and dt.kind in "ui" and dt.byteorder in "=<|" and self.tokens.ndim == 1
+                    and (dt.kind == "u" or (dt.kind == "i" and dt.itemsize == 4))  # the loader reads unsigned:
+                    # a negative int32 id wraps past any vocabulary and is rejected, a negative int16 one
+                    # (-1 -> 65535) would pass a > 65535 vocabulary -- int16 files take the numpy path
+                    and dt.byteorder in "=<|" and self.tokens.ndim == 1
                     and os.environ.get("FTC_NATIVE_LOADER", "1") != "0"):
                 # offset: a .npy file's header precedes the tokens; vocab: ids are range-checked per batch
                 self._native = NativeTokenLoader(self.tokens.filename, dt.itemsize, seq_len, batch, rank, world, seed,

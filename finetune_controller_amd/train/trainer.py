@@ -370,13 +370,17 @@ class Trainer:
         tc = self.tc
         was = self.model.training
         self.model.eval()
+        # (sum of token losses, valid-token count) per rank, reduced over the world before dividing: the
+        # token-weighted mean over every held-out token.  Sequence-parallel shards of one batch hold
+        # unequal valid counts under label masking, so a mean of per-shard means would be biased.
         tot = torch.zeros(2, dtype=torch.float64, device=self.device)
         try:
             with torch.no_grad():
                 for x, y in self.eval_batches():
                     x, y, seg, _ = self._batch(x, y, None)
-                    tot[0] += self.model(x, y, segments=seg).double()
-                    tot[1] += 1
+                    lab = y.reshape(-1)
+                    tot[0] += self.model(x, y, n_valid=1.0, segments=seg).double()  # normaliser 1: the sum
+                    tot[1] += (lab != -100).sum().double()
         finally:
             self.model.train(was)
         pdist.all_reduce_mean_(tot, self.info)
@@ -413,7 +417,9 @@ class Trainer:
         self.watchdog = watchdog = StepWatchdog.from_env(tc.step_timeout_s, self.info.rank)
         metrics = MetricsCSV(os.path.join(tc.checkpoint_path, "metrics.csv"), enabled=self.is_main,
                              resume=start > 0)
-        tok_per_step = tc.batch_size * tc.seq_len * tc.grad_accum * self.info.world_size
+        # tokens trained per optimizer step: every data-parallel replica's micro-batches (the ranks of a
+        # sequence-parallel group share their sequences, so they count once)
+        tok_per_step = tc.batch_size * tc.seq_len * tc.grad_accum * self.dp_world
         flops_tok = self.cfg.flops_per_token(tc.seq_len, lora=tc.method != "full")
         if self.is_main:
             n_train = self.opt.num_params()
@@ -448,7 +454,10 @@ class Trainer:
                 sync()
                 dt = time.perf_counter() - t0
                 n = len(losses)
-                loss_v = float(torch.stack(losses).float().mean().item())
+                # the global batch mean: each rank's loss is its micro-batches' mean (a sequence-parallel
+                # rank's is its shard's sum over the batch's valid count / P), so the world mean is exact
+                loss_t = pdist.all_reduce_mean_(torch.stack(losses).float().mean().reshape(1), self.info)
+                loss_v = float(loss_t.item())
                 step_ms = dt / n * 1000
                 tps = tok_per_step * n / dt
                 mem = torch.cuda.max_memory_allocated(self.device) / 1e9 if self.device.type == "cuda" else 0.0
@@ -481,10 +490,12 @@ class Trainer:
                 self.save_resume()
                 watchdog.beat(f"checkpoint at step {self.step}")
         metrics.close()
+        # training is over: the final save (a full-FT model or merged adapter can take minutes on rank 0)
+        # and the barrier non-main ranks wait in must not trip the step watchdog
+        watchdog.close()
         if tc.save_model:
             self.save_artifacts()
         pdist.barrier(self.info)
-        watchdog.close()
         return last
 
     def _resume_state(self) -> dict | None:

@@ -98,8 +98,13 @@ class FaultInjector:
 class StepWatchdog:
     """Exit(124) when :meth:`beat` has not been called for ``timeout_s`` seconds (0 = disabled)."""
 
-    def __init__(self, timeout_s: float, rank: int = 0, exit_fn=None, poll_s: float | None = None):
+    def __init__(self, timeout_s: float, rank: int = 0, exit_fn=None, poll_s: float | None = None,
+                 first_timeout_s: float | None = None):
         self.timeout_s = float(timeout_s)
+        # the first step also builds kernels' heuristics / TunableOp tables and warms allocators: until
+        # the first beat the limit is max(3 x timeout, 300 s) unless given
+        self.first_timeout_s = float(first_timeout_s) if first_timeout_s is not None else max(3 * self.timeout_s, 300.0)
+        self._beats = 0
         self.rank = rank
         self._exit = exit_fn or os._exit
         self._last = time.monotonic()
@@ -116,6 +121,7 @@ class StepWatchdog:
         return cls(float(os.environ.get("FTC_STEP_TIMEOUT_S", default_s) or 0), rank)
 
     def beat(self, what: str = ""):
+        self._beats += 1
         self._last = time.monotonic()
         self._what = what or self._what
 
@@ -127,7 +133,7 @@ class StepWatchdog:
     def _run(self):
         while not self._stop.wait(self._poll):
             idle = time.monotonic() - self._last
-            if idle > self.timeout_s:
+            if idle > (self.timeout_s if self._beats else self.first_timeout_s):
                 print(f"[watchdog] rank {self.rank}: no progress for {idle:.0f} s (last: {self._what}); "
                       f"dumping stacks and exiting {WATCHDOG_EXIT}", file=sys.stderr, flush=True)
                 try:

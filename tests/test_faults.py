@@ -75,6 +75,44 @@ def test_step_watchdog_exits_124_with_stacks(capfd):
     assert StepWatchdog(0)._thread is None  # 0 = disabled
 
 
+def test_step_watchdog_first_step_grace():
+    codes = []
+    wd = StepWatchdog(0.1, exit_fn=codes.append, poll_s=0.02, first_timeout_s=0.6)
+    time.sleep(0.3)  # a slow first step (warm-up): past timeout_s, inside the first-step limit
+    assert codes == []
+    wd.beat("step 1")
+    time.sleep(0.4)  # from now on the plain limit applies
+    wd.close()
+    assert codes and codes[0] == WATCHDOG_EXIT
+
+
+def test_slow_final_save_does_not_trip_the_watchdog(tmp_path, monkeypatch):
+    """The watchdog covers steps, evaluations and checkpoints; the final artifact save (minutes for a
+    full-FT model on rank 0, with the other ranks waiting in the barrier) runs after it is closed."""
+    from finetune_controller_amd.train import trainer as trmod
+
+    codes = []
+    real = trmod.StepWatchdog
+
+    def make(default_s, rank=0):
+        return real(0.2, rank, exit_fn=codes.append, poll_s=0.02, first_timeout_s=30.0)
+
+    monkeypatch.setattr(trmod.StepWatchdog, "from_env", staticmethod(make))
+    tr = Trainer(TrainConfig(model="llama-tiny", method="lora", batch_size=1, seq_len=16, synthetic=True,
+                             max_steps=2, log_interval=1, checkpoint_path=str(tmp_path), device="cpu"))
+    orig = tr.save_artifacts
+
+    def slow_save():
+        time.sleep(0.6)  # 3x the step timeout
+        return orig()
+
+    tr.save_artifacts = slow_save
+    tr.run()
+    tr.close()
+    assert codes == []
+    assert (tmp_path / "adapter_config.json").exists()
+
+
 def _bcast_worker(rank, world, port, tmp, q):
     _rank_env(rank, world, port, tmp)
     info = pdist.init_distributed("cpu")

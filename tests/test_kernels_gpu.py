@@ -262,6 +262,42 @@ def test_gemm_tn_rejects(C):
         C.gemm_tn_(c, a, b, 1.0, 0.0)
 
 
+@pytest.mark.parametrize("cdtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("M,N,K,pad,beta", [(256, 256, 64, 0, 0.0), (512, 768, 4160, 64, 0.0), (768, 512, 128, 8, 1.0),
+                                            (256, 1024, 1088, 0, -0.5), (512, 256, 192, 0, 0.0)])
+def test_gemm_nt(C, cdtype, M, N, K, pad, beta):
+    """Projection GEMM c = alpha a b^T + beta c (a [M, K], b [N, K] K-contiguous, a a column view of a wider
+    row buffer when pad > 0) vs an fp32 reference; asymmetric integer-valued operands first (exact
+    in fp32: any fragment / output permutation error shows as a wrong integer), then random data."""
+    torch.manual_seed(3)
+    abuf = torch.randint(-3, 4, (M, K + pad), device=DEV).to(torch.bfloat16)
+    a = abuf[:, :K]
+    b = (torch.arange(N * K, device=DEV).reshape(N, K) % 7 - 3).to(torch.bfloat16)
+    c = torch.zeros(M, N, device=DEV, dtype=cdtype)
+    assert C.gemm_nt_ok(c, a, b)
+    C.gemm_nt_(c, a, b, 1.0, 0.0)
+    exact = a.double() @ b.double().t()  # integer sums < 2^24: exact in the fp32 accumulator, one rounding
+    assert torch.equal(c, exact.to(cdtype))
+    abuf = (torch.rand(M, K + pad, device=DEV) * 2 - 1).to(torch.bfloat16)
+    a = abuf[:, :K]
+    b = (torch.rand(N, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    c = torch.randn(M, N, device=DEV).to(cdtype)
+    ref = beta * c.float() + 0.5 * (a.float() @ b.float().t())
+    C.gemm_nt_(c, a, b, 0.5, beta)
+    tol = 2e-2 * (K ** 0.5) / 8 if cdtype == torch.bfloat16 else 1e-3 * (K ** 0.5) / 8
+    torch.testing.assert_close(c.float(), ref, atol=tol, rtol=1e-2 if cdtype == torch.bfloat16 else 1e-4)
+
+
+def test_gemm_nt_rejects(C):
+    a = torch.zeros(256, 40, device=DEV, dtype=torch.bfloat16)  # K not a multiple of 32
+    b = torch.zeros(256, 40, device=DEV, dtype=torch.bfloat16)
+    c = torch.zeros(256, 256, device=DEV, dtype=torch.bfloat16)
+    assert not C.gemm_nt_ok(c, a, b)
+    with pytest.raises(RuntimeError):
+        C.gemm_nt_(c, a, b, 1.0, 0.0)
+    assert not C.gemm_nt_ok(c[:, :200], a, b[:200])  # N not a multiple of 256
+
+
 def test_grad_clip_coef(C):
     g = torch.full((4096,), 0.5, device=DEV)
     stats = C.grad_sumsq(g, 1.0, 1.0)

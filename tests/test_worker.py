@@ -358,6 +358,20 @@ def test_native_token_loader_matches_numpy_path(tmp_path, monkeypatch, dtype, vo
         nat._native.close()
 
 
+def test_negative_int16_token_ids_fail_on_the_host(tmp_path, monkeypatch):
+    """A signed int16 file is never read as unsigned by the native loader (-1 would become 65535, a valid
+    id of a 128k vocabulary): it takes the numpy path, whose range check rejects the negative id."""
+    monkeypatch.setenv("FTC_NATIVE_LOADER", "1")
+    toks = (np.arange(4000, dtype=np.int64) % 500).astype(np.int16)
+    toks[777] = -1
+    np.save(tmp_path / "t.npy", toks, allow_pickle=False)
+    ds = PackedTokenDataset(str(tmp_path / "t.npy"), vocab=128256, batch=4, seq_len=64, device="cpu", seed=1)
+    assert ds._native is None
+    with pytest.raises((ValueError, RuntimeError)):
+        for _ in range(2 * ds.steps_per_epoch):
+            next(ds)
+
+
 @pytest.mark.parametrize("native", ["0", "1"])
 def test_out_of_vocab_token_ids_fail_on_the_host(tmp_path, monkeypatch, native):
     """A dataset id >= the model's vocabulary (wrong tokenizer) must raise a clear error on the host --
