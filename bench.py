@@ -144,8 +144,9 @@ def _parse(argv):
     ap.add_argument("--grad-dtype", default="auto", choices=["auto", "fp32", "bf16"],
                     help="gradient buffer / reduction dtype (full FT; auto: fp32 when accumulating)")
     ap.add_argument("--grad-accum", type=int, default=1)
-    ap.add_argument("--zero-stage", type=int, default=0, choices=[0, 1],
-                    help="1: ZeRO-1 -- AdamW state sharded over the data-parallel ranks (reduce-scatter + all-gather)")
+    ap.add_argument("--zero-stage", type=int, default=-1, choices=[-1, 0, 1],
+                    help="1: ZeRO-1 -- AdamW state sharded over the data-parallel ranks (reduce-scatter + all-gather); "
+                         "-1 (auto): ZeRO-1 for full fine-tuning on > 1 GPU")
     ap.add_argument("--sp", type=int, default=1,
                     help="Ulysses sequence parallelism: groups of SP ranks share each sequence (1/SP of the tokens "
                          "per rank); --seq-len is the FULL sequence length")
@@ -234,7 +235,7 @@ def main(argv=None) -> int:
                      zero_stage=a.zero_stage, grad_accum=a.grad_accum, grad_dtype=a.grad_dtype, sp=a.sp,
                      checkpoint_layers=a.checkpoint_layers, ce_chunk_rows=a.ce_chunk_rows, save_model=False,
                      resume=False, device=a.device, pack_documents=a.doc_len > 0, eos_id=2,
-                     synthetic_doc_len=a.doc_len, graph=a.graph)
+                     synthetic_doc_len=a.doc_len, graph=a.graph, comm_probe=a.gpus > 1)
     tr = Trainer(tc)
     info = tr.info
     dev = tr.device
@@ -248,6 +249,7 @@ def main(argv=None) -> int:
     sync()
     pdist.barrier(info)
     sync()
+    tr.comm_exposed_ms()  # drop the warm-up steps' probes (events only: nothing synchronises in the loop)
     if cuda:
         _mark("push")  # roctx range "ftc_timed" (rocprofv3 --marker-trace; tools/kstats_md.py filters on it)
     t0 = time.perf_counter()
@@ -262,6 +264,9 @@ def main(argv=None) -> int:
         _mark("pop")
     elapsed = pdist.all_reduce_max(elapsed_rank, info)
     fastest = -pdist.all_reduce_max(-elapsed_rank, info)
+    # gradient-reduction time backward did not hide, measured by device events inside the timed steps
+    exposed = tr.comm_exposed_ms()
+    exposed = pdist.all_reduce_max(exposed, info) if exposed is not None else None
     loss = float(last.float().item()) if last is not None else float("nan")
 
     n = info.world_size
@@ -338,10 +343,10 @@ def main(argv=None) -> int:
                 "seq_len": a.seq_len,
                 "tokens_per_step": a.batch_size * a.seq_len * a.grad_accum * ngroups,
                 "parallelism": f"dp{ngroups}" + (f"-sp{a.sp}" if a.sp > 1 else "")
-                               + ("-zero1" if a.zero_stage and n > 1 else ""),
+                               + ("-zero1" if tr.zero_stage and n > 1 else ""),
                 "kernels": _backend.kernel_mode(),
                 "comm_engine": a.comm_engine,
-                "zero_stage": a.zero_stage,
+                "zero_stage": tr.zero_stage,
                 "grad_dtype": str(tr.opt.grad_flat.dtype).replace("torch.", ""),
                 "device": a.device,
                 **({"packed_doc_len": a.doc_len} if a.doc_len else {}),
@@ -352,6 +357,14 @@ def main(argv=None) -> int:
             "rccl_version": rccl,
             "rank_ms_per_step": {"max": round(ms, 2), "min": round(fastest / a.steps * 1000, 2)},
             **({"allreduce_bucket": comm} if comm else {}),
+            "comm": {
+                "comm_exposed_ms": None if exposed is None else round(exposed, 3),
+                "wire_GB_per_step": round(tr.ddp.wire_bytes_per_step() / 1e9, 4),
+                "n_buckets": tr.ddp.n_collectives(),
+                "bucket_mb": a.bucket_mb,
+                "env": {k: v for k, v in sorted(os.environ.items())
+                        if k.startswith(("NCCL_", "RCCL_")) or k in ("HSA_ENABLE_IPC_MODE_LEGACY", "FTC_SHARE_GPU")},
+            },
             "loss": round(loss, 4),
             "model_tflops_per_gpu": round(value * flops_tok / n / 1e12, 1),
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1) if cuda else None,

@@ -39,12 +39,13 @@ FTC_DEV u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, int voff_bytes, int soff_byte
 // asm, so hipcc keeps it out of its own s_waitcnt bookkeeping (through the builtin, every ds_read of
 // ANOTHER stage gets a compiler vmcnt(0) in front of it and the prefetch drains).  The caller counts
 // completion with explicit vmcnt waits.  M0 is saved / restored inside the statement (compiler-
-// reserved); s_nop 4 covers an SGPR operand written by v_readfirstlane just before.
+// reserved).  The operands must come from SALU (kernel arguments, blockIdx / readfirstlane-derived
+// values computed well before): no VALU-written SGPR hazard is padded here.
 FTC_DEV void lds_dma16(__amdgpu_buffer_rsrc_t r, const void* lds, int voff, int soff) {
   const unsigned dst = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)lds;
   unsigned keep;
   asm volatile(
-      "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
       "buffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(voff), "s"(r), "s"(dst), "s"(soff)

@@ -193,8 +193,8 @@ FTC_DEV constexpr int b_nt(int nt) { return (32 * (nt >> 1) + 4 * (nt & 1)) * 64
 // t+1 into set Y, then vmcnt (tile t+2 landed: only tile t+3's 4 pieces may still fly) and ONE barrier
 // that publishes tile t+2.  The two waves of a SIMD interleave freely; the barrier costs only the
 // arrival skew once per 32 MFMAs per wave.  Two named register sets, loop unrolled by 2 (guide rule 20).
-// MODE (diagnostics only, tools/bench_gemm_nt.py --mode; results are garbage): bit 0 skips the DMA
-// wait, bit 1 the loop's DMA, bit 2 the loop's barrier.
+// MODE (diagnostics only, FTC_GEMM_NT_MODE; results are garbage): bit 0 skips the DMA wait, bit 1 the
+// loop's DMA, bit 2 the loop's barrier; bit 3 makes every DMA re-read K-tile 0 (L2-resident operands).
 template <bool F32C, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void gemm_nt_kernel(NTArgs p) {
   __shared__ __attribute__((aligned(16))) char S[NSTAGE * STAGE];
@@ -231,7 +231,15 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel(NTArgs p) {
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cb[nt], ca[mt], acc[mt][nt], 0, 0, 0);
       na[mt] = rd(st, a_off + mt * 1024);
       if (mt < 4) nb_[mt] = rd(st, b_off + b_nt(mt));
-      if ((mt & 1) == 0 && !(MODE & 2)) dma.piece(tdma, mt >> 1, sdma);
+      if (!(MODE & 2)) {
+        if constexpr (MODE & 16) {
+          // the two waves of a SIMD (wm 0 / 1) issue their DMA pieces after different MFMA groups, so
+          // one wave's DMA issue stall falls where its partner is issuing MFMAs
+          if ((mt & 1) == wm) dma.piece((MODE & 8) ? 0 : tdma, mt >> 1, sdma);
+        } else if ((mt & 1) == 0) {
+          dma.piece((MODE & 8) ? 0 : tdma, mt >> 1, sdma);
+        }
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
     if (!(MODE & 1)) __builtin_amdgcn_s_waitcnt(0x0F74);  // vmcnt(4): tile t+2 landed, only the 4 pieces just issued fly
@@ -465,6 +473,8 @@ extern "C" int ftc_gemm_nt(const void* a, long long lda, const void* b, long lon
       case 2: hipLaunchKernelGGL((gemm_nt_kernel<false, 2>), dim3(grid), dim3(512), 0, stream, p); break;
       case 3: hipLaunchKernelGGL((gemm_nt_kernel<false, 3>), dim3(grid), dim3(512), 0, stream, p); break;
       case 7: hipLaunchKernelGGL((gemm_nt_kernel<false, 7>), dim3(grid), dim3(512), 0, stream, p); break;
+      case 8: hipLaunchKernelGGL((gemm_nt_kernel<false, 8>), dim3(grid), dim3(512), 0, stream, p); break;
+      case 16: hipLaunchKernelGGL((gemm_nt_kernel<false, 16>), dim3(grid), dim3(512), 0, stream, p); break;
       default: hipLaunchKernelGGL((gemm_nt_kernel<false>), dim3(grid), dim3(512), 0, stream, p);
     }
   }

@@ -115,8 +115,9 @@ class LMTrainingArguments(TrainingArguments):
     log_interval: int = Field(default=10, ge=1, description="Steps between metrics.csv rows / Epoch log lines")
     save_every: int = Field(default=0, ge=0, description="Resume checkpoint every N steps (0 = only at the end)")
     checkpoint_layers: bool = Field(default=False, description="Activation checkpointing per decoder layer")
-    zero_stage: int = Field(default=0, ge=0, le=1,
-                            description="1: ZeRO-1 -- AdamW state sharded over the data-parallel ranks")
+    zero_stage: int = Field(default=-1, ge=-1, le=1,
+                            description="1: ZeRO-1 -- AdamW state sharded over the data-parallel ranks; "
+                                        "-1 (auto): ZeRO-1 for full fine-tuning on > 1 GPU")
     sp: int = Field(default=1, ge=1, le=64,
                     description="Ulysses sequence parallelism: groups of this many GPUs share each sequence "
                                 "(long context; must divide the GPU count and the model's head counts)")

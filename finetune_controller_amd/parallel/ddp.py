@@ -155,6 +155,27 @@ class GradBucketer:
             self._native.reset()
         self.reset()
 
+    def n_collectives(self) -> int:
+        """Gradient collectives per optimizer step (buckets + deferred multi-use parameters)."""
+        return len(self.buckets) + len(self.deferred) if self.enabled else 0
+
+    def wire_bytes_per_step(self) -> int:
+        """Bytes each rank sends per optimizer step for the gradient reduction (and, under ZeRO-1, the
+        parameter all-gather), ring-equivalent: an all-reduce of S bytes moves 2 (n-1)/n S, a
+        reduce-scatter or all-gather (n-1)/n S (nccl-tests bus-bandwidth convention)."""
+        if not self.enabled:
+            return 0
+        n = self.world
+        g = self.opt.grad_flat.element_size()
+        if self.sharded:
+            red = sum(e - s for s, e in self.buckets) * g * (n - 1) / n
+            gather = sum(e - s for s, e in self.buckets) * self.opt.param_flat.element_size() * (n - 1) / n
+        else:
+            red = sum(e - s for s, e in self.buckets) * g * 2 * (n - 1) / n
+            gather = 0
+        red += sum(k for _, k in self.deferred) * g * 2 * (n - 1) / n
+        return int(red + gather)
+
     def close(self):
         for h in self._hooks:
             h.remove()

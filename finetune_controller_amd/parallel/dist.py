@@ -46,9 +46,13 @@ def init_distributed(device_type: str = "auto", timeout_s: int = 1800) -> DistIn
     if device_type == "auto":
         # device_count() does not initialise the HIP runtime on this image; is_available() does
         device_type = "cuda" if torch.cuda.device_count() > 0 and torch.cuda.is_available() else "cpu"
+    share = os.environ.get("FTC_SHARE_GPU") == "1"
     if device_type == "cuda":
         # FTC_SHARE_GPU=1: several ranks on one card (rehearsing the multi-GPU path on a 1-GPU box)
-        idx = local % torch.cuda.device_count() if os.environ.get("FTC_SHARE_GPU") == "1" else local
+        count = torch.cuda.device_count()
+        if not share:
+            check_local_rank(local, count)
+        idx = local % count if share else local
         torch.cuda.set_device(idx)
         device = torch.device("cuda", idx)
     else:
@@ -75,7 +79,32 @@ def init_distributed(device_type: str = "auto", timeout_s: int = 1800) -> DistIn
             dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                     init_method=os.environ.get("FTC_INIT_METHOD") or None,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        if device.type == "cuda" and not share:
+            # one GPU per rank: a weak-scaling number from ranks sharing a card would be mislabelled
+            import socket
+
+            props = torch.cuda.get_device_properties(device)
+            me = (socket.gethostname(), str(getattr(props, "uuid", "") or f"index{device.index}"), rank)
+            allr: list = [None] * world
+            dist.all_gather_object(allr, me)
+            check_distinct_devices(allr)
     return DistInfo(rank, world, local, backend, device)
+
+
+def check_local_rank(local: int, count: int) -> None:
+    if local >= count:
+        raise RuntimeError(f"LOCAL_RANK {local} has no GPU of its own: {count} visible device(s) "
+                           "(set FTC_SHARE_GPU=1 only to rehearse several ranks on one card)")
+
+
+def check_distinct_devices(entries) -> None:
+    """``entries``: (host, device id, rank) of every rank.  Two ranks of one host on one device raise."""
+    seen: dict = {}
+    for host, dev, rank in entries:
+        other = seen.setdefault((host, dev), rank)
+        if other != rank:
+            raise RuntimeError(f"ranks {other} and {rank} are bound to the same GPU ({dev}) on {host}; "
+                               "each rank needs its own device (FTC_SHARE_GPU=1 to rehearse on one card)")
 
 
 def barrier(info: DistInfo):

@@ -43,8 +43,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--comm-engine", default="torch", choices=["torch", "native"])
     ap.add_argument("--sp", type=int, default=1,
                     help="Ulysses sequence parallelism degree: groups of SP ranks share each sequence")
-    ap.add_argument("--zero-stage", type=int, default=0, choices=[0, 1],
-                    help="1: ZeRO-1 -- AdamW state sharded over the data-parallel ranks (reduce-scatter + all-gather)")
+    ap.add_argument("--zero-stage", type=int, default=-1, choices=[-1, 0, 1],
+                    help="1: ZeRO-1 -- AdamW state sharded over the data-parallel ranks (reduce-scatter + all-gather); "
+                         "-1 (auto): ZeRO-1 for full fine-tuning on > 1 GPU")
     ap.add_argument("--grad-dtype", default="auto", choices=["auto", "fp32", "bf16"],
                     help="gradient buffer / all-reduce dtype (auto: fp32 for full FT with accumulation or DP)")
     ap.add_argument("--init-from", default="", help="HF safetensors checkpoint dir to fine-tune from")

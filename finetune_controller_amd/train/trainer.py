@@ -69,7 +69,10 @@ class TrainConfig:
     synthetic: bool = False
     bucket_mb: float = 64.0
     comm_engine: str = "torch"  # torch | native
-    zero_stage: int = 0  # 1: ZeRO-1 (optimizer state sharded over data-parallel ranks, reduce-scatter grads)
+    # 1: ZeRO-1 (optimizer state sharded over data-parallel ranks, reduce-scatter grads + bf16 all-gather);
+    # -1 (auto): ZeRO-1 for full fine-tuning on > 1 rank (exact fp32 reduction at 3/4 of an fp32
+    # all-reduce's wire volume and 1/world of the AdamW state; docs/parallelism.md), else 0
+    zero_stage: int = -1
     # Ulysses sequence parallelism: groups of `sp` consecutive ranks share the same sequences, each
     # holding 1/sp of every sequence's tokens (attention all-to-alls heads <-> tokens; parallel/sequence.py)
     sp: int = 1
@@ -93,12 +96,25 @@ class TrainConfig:
     completion_only: bool = False  # prompt/completion records: loss on the completion tokens only
     synthetic_doc_len: int = 0  # synthetic data: EOS every that many tokens (packed-document benchmarks)
     step_timeout_s: float = 0.0  # >0: exit 124 when no step / eval / save finishes for that long (FTC_STEP_TIMEOUT_S)
+    # device events around the gradient-reduction wait of every step: the comm time backward did not
+    # hide (``comm_exposed_ms``; bench.py turns it on for > 1 GPU)
+    comm_probe: bool = False
 
     def lora_config(self) -> LoRAConfig | None:
         if self.method not in ("lora", "qlora"):
             return None
         return LoRAConfig(r=self.lora_r, alpha=self.lora_alpha, dropout=self.lora_dropout, use_rslora=self.use_rslora,
                           target_modules=list(self.lora_targets))
+
+
+def resolve_zero_stage(zero_stage: int, method: str, world: int, sp: int = 1) -> int:
+    """``zero_stage`` -1 (auto): ZeRO-1 for full fine-tuning with data parallelism.  Per rank per step
+    it moves (n-1)/n (4 B + 2 B) per parameter -- an exact fp32 reduce-scatter plus a bf16 all-gather
+    -- against 2 (n-1)/n 4 B for the fp32 all-reduce (42 vs 56 GB on 8 ranks for Llama-3-8B), and
+    keeps 1/n of the 12 B/param AdamW state; adapters (MBs of gradients) keep the plain all-reduce."""
+    if zero_stage >= 0:
+        return zero_stage
+    return 1 if (method == "full" and world > 1 and sp <= 1) else 0
 
 
 class Trainer:
@@ -150,7 +166,8 @@ class Trainer:
         okw = dict(lr=tc.lr, weight_decay=tc.weight_decay, max_grad_norm=tc.max_grad_norm,
                    grad_scale=1.0 / (self.info.world_size * tc.grad_accum), grad_dtype=self._grad_dtype())
         trainable = [p for p in self.model.parameters() if p.requires_grad]
-        if tc.zero_stage >= 1 and self.info.distributed:
+        self.zero_stage = resolve_zero_stage(tc.zero_stage, tc.method, self.info.world_size, tc.sp)
+        if self.zero_stage >= 1 and self.info.distributed:
             esize = torch.finfo(self.dtype).bits // 8
             self.opt = ShardedFlatAdamW(trainable, self.info.world_size, self.info.rank,
                                         bucket_elems=max(1, int(tc.bucket_mb * 2 ** 20 / esize)), **okw)
@@ -169,6 +186,7 @@ class Trainer:
         self.step = 0
         self.is_main = self.info.is_main
         self._timing: list[tuple] = []  # per-step (start, fwd, bwd, comm, optim) device events
+        self._comm_ev: list[tuple] = []  # per-step (backward end, reduction complete) device events
 
     def _overlap_update(self):
         """Full fine-tuning: the AdamW update runs stage by stage on a side stream and the next forward
@@ -335,7 +353,14 @@ class Trainer:
             total = loss.detach() if total is None else total + loss.detach()
         if ev:
             ev[2].record()
+        probe = tc.comm_probe and self.device.type == "cuda" and self.ddp.enabled
+        if probe:
+            pe = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            pe[0].record()
         self.ddp.finish()  # device-side waits on the bucket all-reduces: the non-overlapped comm tail
+        if probe:
+            pe[1].record()
+            self._comm_ev.append(pe)
         if ev:
             ev[3].record()
         self.opt.step(lr)
@@ -387,6 +412,18 @@ class Trainer:
         if float(tot[1]) == 0:
             return None
         return float(tot[0] / tot[1])
+
+    def comm_exposed_ms(self, reset: bool = True) -> float | None:
+        """Mean device time per step from the end of backward's last kernel to the completion of the
+        gradient reduction (the part of the all-reduce / reduce-scatter backward did not hide), over
+        the steps since the last reset; None without probes.  Synchronises the device."""
+        if not self._comm_ev:
+            return None
+        torch.cuda.synchronize(self.device)
+        v = sum(a.elapsed_time(b) for a, b in self._comm_ev) / len(self._comm_ev)
+        if reset:
+            self._comm_ev = []
+        return v
 
     def _phase_ms(self) -> dict:
         """Mean fwd/bwd/comm/optim milliseconds of the steps since the last call (after a sync)."""

@@ -85,6 +85,39 @@ def test_bench_self_launches_ranks_on_cpu(tmp_path):
     assert out["value"] > 0 and out["steps"] == 2 and out["warmup"] == 1
     assert out["rank_ms_per_step"]["max"] >= out["rank_ms_per_step"]["min"] > 0
     assert out["allreduce_bucket"]["torch"]["busbw_GBps"] > 0
+    assert out["comm"]["n_buckets"] >= 1 and out["comm"]["wire_GB_per_step"] > 0
+    assert out["comm"]["comm_exposed_ms"] is None  # device events: GPU runs only
+
+
+@pytest.mark.slow
+def test_bench_eight_ranks_on_cpu(tmp_path):
+    """The driver's 8-GPU command shape, rehearsed with 8 gloo ranks: exactly one JSON line, n_gpus ==
+    the process group's world size == 8, global batch 8 x micro-batch."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "FTC_INIT_METHOD"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1", "--warmup", "1",
+                        "--device", "cpu", "--model", "llama-tiny", "--batch-size", "1", "--seq-len", "16",
+                        "--launcher-timeout", "400"],
+                       capture_output=True, text=True, timeout=480, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8 and out["world_size_pg"] == 8
+    assert out["config"]["parallelism"] == "dp8" and out["config"]["global_batch"] == 8
+    assert out["config"]["zero_stage"] == 0  # LoRA: plain bucketed all-reduce
+
+
+def test_distinct_device_binding_checks():
+    from finetune_controller_amd.parallel import dist as pdist
+
+    pdist.check_distinct_devices([("h0", "g0", 0), ("h0", "g1", 1), ("h1", "g0", 2)])  # per host: distinct
+    with pytest.raises(RuntimeError, match="ranks 0 and 2"):
+        pdist.check_distinct_devices([("h0", "g0", 0), ("h0", "g1", 1), ("h0", "g0", 2)])
+    pdist.check_local_rank(7, 8)
+    with pytest.raises(RuntimeError, match="LOCAL_RANK 8"):
+        pdist.check_local_rank(8, 8)
 
 
 def test_bench_refuses_mislabelled_world(tmp_path):
@@ -109,22 +142,30 @@ def test_bench_launcher_propagates_rank_failure(tmp_path):
 ACCUM = 4
 
 
-def _accum_worker(rank, world, port, tmp, q, grad_dtype):
+def _accum_worker(rank, world, port, tmp, q, grad_dtype, zero):
     _rank_env(rank, world, port, tmp)
     tc = TrainConfig(model="llama-tiny", method="full", batch_size=2, seq_len=16, synthetic=True, max_steps=1,
                      checkpoint_path=tmp, resume=False, device="cpu", dtype="bf16", lr=0.0, bucket_mb=0.05,
-                     max_grad_norm=0.0, save_model=False, grad_accum=ACCUM, grad_dtype=grad_dtype)
+                     max_grad_norm=0.0, save_model=False, grad_accum=ACCUM, grad_dtype=grad_dtype, zero_stage=zero)
     tr = Trainer(tc)
     tr.train_step(0.0)
-    q.put((rank, {"grad": tr.opt.grad_flat.detach().double().clone(), "dtype": str(tr.opt.grad_flat.dtype),
-                  "buckets": len(tr.ddp.buckets)}))
+    out = {"dtype": str(tr.opt.grad_flat.dtype), "buckets": len(tr.ddp.buckets), "zero": tr.zero_stage,
+           "offsets": [tuple(o) for o in tr.opt.offsets], "numel": tr.opt.numel,
+           "wire": tr.ddp.wire_bytes_per_step()}
+    if tr.zero_stage:  # this rank's owned slices of the summed gradient
+        out["shard"] = tr.opt.grad_shard.detach().double().clone()
+        out["ranges"] = list(tr.opt.shard_ranges)
+        out["shard_offsets"] = list(tr.opt.shard_offsets)
+    else:
+        out["grad"] = tr.opt.grad_flat.detach().double().clone()
+    q.put((rank, out))
     tr.close()
     _hold(tmp, port)
 
 
 def _reference_grads(tmp, world):
     """Single process: every (rank, micro-batch) gradient computed alone (bf16 model, same weights and
-    data as the ranks), summed in float64."""
+    data as the ranks), summed in float64; returned per parameter in layout order."""
     total = None
     for rank in range(world):
         tc = TrainConfig(model="llama-tiny", method="full", batch_size=2, seq_len=16, synthetic=True, max_steps=1,
@@ -139,31 +180,47 @@ def _reference_grads(tmp, world):
             total = g if total is None else total + g
         layout = [(o, n) for o, n in tr.opt.offsets]
         tr.close()
-    return total, layout
+    return torch.cat([total[o:o + n] for o, n in layout])
+
+
+def _summed_grads(res, world):
+    """The reduced gradient per parameter (layout order) as the ranks hold it: the all-reduced flat
+    buffer (identical on every rank), or the ZeRO-1 owned slices put back together."""
+    r0 = res[0]
+    if not r0["zero"]:
+        for r in range(1, world):
+            torch.testing.assert_close(res[r]["grad"], r0["grad"], atol=0, rtol=0)  # all ranks hold the same sum
+        flat = r0["grad"]
+    else:
+        flat = torch.zeros(r0["numel"], dtype=torch.float64)
+        for r in range(world):
+            sh = res[r]["shard"]
+            for (lo, hi), o in zip(res[r]["ranges"], res[r]["shard_offsets"]):
+                flat[lo:hi] = sh[o:o + hi - lo]
+    return torch.cat([flat[o:o + n] for o, n in r0["offsets"]])
 
 
 @pytest.mark.slow
 def test_fp32_grad_accumulation_three_ranks_matches_fp64_reference(tmp_path):
-    """3 gloo ranks x grad_accum 4 on a bf16 full fine-tune: the fp32 gradient buffer (accumulated
-    across micro-batches, summed across ranks) equals the float64 sum of the 12 per-micro-batch
-    gradients to fp32 rounding; the bf16 buffer is measurably worse."""
+    """3 gloo ranks x grad_accum 4 on a bf16 full fine-tune: the fp32 gradient (accumulated across
+    micro-batches, reduced across ranks) equals the float64 sum of the 12 per-micro-batch gradients to
+    fp32 rounding -- on the default path (auto = ZeRO-1: fp32 reduce-scatter into owned slices) and on
+    the plain fp32 all-reduce; the bf16 buffer is measurably worse.  ZeRO-1 moves 3/4 of the all-reduce's
+    bytes (fp32 reduce-scatter + bf16 all-gather vs fp32 all-reduce)."""
     world = 3
-    ref, layout = _reference_grads(tmp_path, world)
-    live = torch.zeros_like(ref, dtype=torch.bool)
-    for o, n in layout:
-        live[o:o + n] = True
-    errs = {}
-    for gd in ("fp32", "bf16"):
-        res = _run_ranks(_accum_worker, world, tmp_path, gd)
-        g0 = res[0]["grad"]
-        for r in range(1, world):
-            torch.testing.assert_close(res[r]["grad"], g0, atol=0, rtol=0)  # all ranks hold the same sum
-        assert res[0]["dtype"] == ("torch.float32" if gd == "fp32" else "torch.bfloat16")
+    ref = _reference_grads(tmp_path, world)
+    errs, wire = {}, {}
+    for gd, zero in (("auto", -1), ("fp32", 0), ("bf16", 0)):
+        res = _run_ranks(_accum_worker, world, tmp_path, gd, zero)
+        assert res[0]["zero"] == (1 if zero == -1 else 0)
+        g = _summed_grads(res, world)
+        assert res[0]["dtype"] == ("torch.bfloat16" if gd == "bf16" else "torch.float32")
         assert res[0]["buckets"] > 1
-        d = (g0[live] - ref[live]).abs()
-        errs[gd] = float(d.max() / ref[live].abs().max())
-    assert errs["fp32"] < 2e-6, errs
-    assert errs["bf16"] > 20 * errs["fp32"], errs
+        errs[(gd, zero)] = float((g - ref).abs().max() / ref.abs().max())
+        wire[(gd, zero)] = res[0]["wire"]
+    assert errs[("auto", -1)] < 2e-6 and errs[("fp32", 0)] < 2e-6, errs
+    assert errs[("bf16", 0)] > 20 * errs[("fp32", 0)], errs
+    assert abs(wire[("auto", -1)] / wire[("fp32", 0)] - 0.75) < 0.02, wire
 
 
 def test_grad_dtype_auto_policy():

@@ -271,13 +271,13 @@ def test_family_specs_render_worker_commands(name, preset, method, gpus):
     cls = ModelRegistry().get(name)
     spec = cls()
     cmd = spec.run_cmd()[-1]
-    assert f"--model={preset}" in cmd and f"--method={method}" in cmd and "--zero-stage=0" in cmd
+    assert f"--model={preset}" in cmd and f"--method={method}" in cmd and "--zero-stage=-1" in cmd
     if gpus > 1:
         assert cmd.startswith(f"torchrun --standalone --nproc-per-node={gpus} ")
     argv = cmd.split(" -m finetune_controller_amd.train.cli ", 1)[-1].split() if gpus > 1 else \
         cmd.split("python -m finetune_controller_amd.train.cli ", 1)[-1].split()
     a = cli.build_parser().parse_args(argv)
-    assert a.model == preset and a.method == method and a.zero_stage == 0 and a.sp == 1
+    assert a.model == preset and a.method == method and a.zero_stage == -1 and a.sp == 1
     # a long-context job: sequence parallelism over the job's GPUs flows from the form to the trainer
     long = cls(training_arguments=cls().training_arguments.model_copy(update={"sp": gpus, "seq_len": 65536}))
     cmd = long.run_cmd()[-1]
