@@ -37,6 +37,7 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 using namespace ftc;
 
@@ -126,17 +127,16 @@ FTC_DEV bf16x8 rd(const char* s, int off) { return *reinterpret_cast<const bf16x
 
 // Epilogue: lane holds C[m0 + wm 128 + 16 mt + li][n0 + wn 64 + 32 pr + 8 kc + 0..7] in acc[mt][2 pr]
 // (columns +0..3) and acc[mt][2 pr + 1] (+4..7): one 16-byte (bf16) / two 16-byte (fp32) stores.
-template <bool F32C>
-FTC_DEV void store_tile(const NTArgs& p, const f32x4 (&acc)[8][4], long long m0, long long n0, int wm, int wn,
-                        int lane) {
+template <bool F32C, int MT, int NT>
+FTC_DEV void store_wave(const NTArgs& p, const f32x4 (&acc)[MT][NT], long long row0, long long col0, int lane) {
   const int li = lane & 15, kc = lane >> 4;
-  const long long mrow = m0 + wm * 128 + li;
-  const long long ncol = n0 + wn * 64 + 8 * kc;
+  const long long mrow = row0 + li;
+  const long long ncol = col0 + 8 * kc;
   const bool accumulate = p.beta != 0.f;
 #pragma unroll
-  for (int mt = 0; mt < 8; ++mt)
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int pr = 0; pr < 2; ++pr) {
+    for (int pr = 0; pr < NT / 2; ++pr) {
       float v[8];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -164,6 +164,14 @@ FTC_DEV void store_tile(const NTArgs& p, const f32x4 (&acc)[8][4], long long m0,
         *cp = pack8(v);
       }
     }
+}
+
+// Epilogue of the 8-wave kernels: lane holds C[m0 + wm 128 + 16 mt + li][n0 + wn 64 + 32 pr + 8 kc + 0..7] in
+// acc[mt][2 pr] (columns +0..3) and acc[mt][2 pr + 1] (+4..7): one 16-byte (bf16) / two (fp32) stores.
+template <bool F32C>
+FTC_DEV void store_tile(const NTArgs& p, const f32x4 (&acc)[8][4], long long m0, long long n0, int wm, int wn,
+                        int lane) {
+  store_wave<F32C, 8, 4>(p, acc, m0 + wm * 128, n0 + wn * 64, lane);
 }
 
 FTC_DEV void barrier() {
@@ -236,7 +244,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel(NTArgs p) {
           // the two waves of a SIMD (wm 0 / 1) issue their DMA pieces after different MFMA groups, so
           // one wave's DMA issue stall falls where its partner is issuing MFMAs
           if ((mt & 1) == wm) dma.piece((MODE & 8) ? 0 : tdma, mt >> 1, sdma);
-        } else if ((mt & 1) == 0) {
+        } else if ((mt & 1) == 0 && (!(MODE & 32) || mt < 4)) {  // MODE 32: A pieces only
           dma.piece((MODE & 8) ? 0 : tdma, mt >> 1, sdma);
         }
       }
@@ -340,6 +348,347 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_rs_kernel(NTArgs p) {
     iter(t, xb, yb);
     iter(t + 1, yb, xb);
   }
+  store_tile<F32C>(p, acc, m0, n0, wm, wn, lane);
+}
+
+// ---- packed-B kernel: the weight operand never touches LDS ---------------------------------------------
+// Variant 1 with the loop's DMA switched off runs 1.60 PF against 1.27 with it: the LDS, not the matrix
+// pipe, is the limiter -- per 32-deep tile a CU writes 32 KiB (ds_write_b128 ~79 B/clk) and reads 96 KiB.
+// Here B (the frozen projection weight -- or its transposed copy for the input-gradient GEMM) is stored
+// once in MFMA fragment order ("packed", pack_b_nt in ops/gemm.py): [N/32][K/32][2][64 lanes][8], so a
+// wave's 16x32 B fragment is ONE coalesced 1 KiB buffer_load straight into VGPRs.  Only A goes through
+// LDS (register-staged: buffer_load -> ds_write_b128 two tiles ahead), halving the LDS write traffic and
+// cutting the reads by a third.  Every memory op is compiler-visible, so hipcc counts vmcnt exactly.
+//
+// Iteration t: the MFMAs of tile t (A fragments of tile t in fa, B fragments in cb) interleaved with
+//   the A fragment reads of tile t+1 (LDS) into fa (each after its last use), the B fragment loads of
+//   tile t+1 (global) into nb_, the ds_writes of A tile t+2 from the staging registers and their
+//   re-load with A tile t+3; lgkmcnt(0) and one barrier publish tile t+2.
+struct PBArgs {
+  const uint16_t* a;   // [M, lda]
+  const uint16_t* bp;  // packed [N/32][K/32][2][64][8]
+  void* c;             // [M, ldc]
+  long long lda, ldc;
+  int K, nm, nn, group_m;
+  float alpha, beta;
+};
+
+// MODE (diagnostics, FTC_GEMM_NT_MODE; garbage results): bit 0 -- B loads re-read K-tile 0; bit 1 -- no A
+// staging in the loop.
+template <bool F32C, int MODE = 0>
+__global__ __launch_bounds__(512, 1) void gemm_nt_pb_kernel(PBArgs p) {
+  __shared__ __attribute__((aligned(16))) char S[NSTAGE * IMG];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  int mb, nb;
+  {
+    NTArgs q{};
+    q.nm = p.nm;
+    q.nn = p.nn;
+    q.group_m = p.group_m;
+    tile_of(q, mb, nb);
+  }
+  const long long m0 = (long long)mb * BM, n0 = (long long)nb * BN;
+  const int nk = p.K / BK;  // even (host contract)
+
+  // A staging: wave w owns rows [32 w, 32 w + 32) of the A image, 2 pieces of 16 rows
+  int voa;
+  {
+    const int r = 32 * wave + (lane >> 2);
+    voa = (int)((r * p.lda + 8 * ((lane & 3) ^ swz(r))) * 2);
+  }
+  const int sa16 = (int)(16 * p.lda * 2);
+  const auto ra = make_rsrc(p.a + m0 * p.lda);
+  char* const wa = S + 32 * wave * 64 + lane * 16;
+  // B fragments: wave wn reads 32-column groups n0/32 + 2 wn + {0, 1}, 2 fragments each
+  const int grp_bytes = nk * 2048;
+  const auto rbp = make_rsrc(p.bp + (n0 >> 5) * (long long)nk * 1024);
+  const int vob = lane * 16 + 2 * wn * grp_bytes;
+  const int a_off = a_frag_off(wm, lane) - 0;  // A image at the stage base (no B image here)
+
+  auto ldA = [&](int kt, int j) __attribute__((always_inline)) { return buf_load16(ra, voa, kt * BK * 2 + j * sa16); };
+  auto stA = [&](int kt, int j, const u32x4& v) __attribute__((always_inline)) {
+    *reinterpret_cast<u32x4*>(wa + (kt & (NSTAGE - 1)) * IMG + j * 1024) = v;
+  };
+  auto ldB = [&](int kt, int nt) __attribute__((always_inline)) {
+    const bf16x8 v = __builtin_bit_cast(bf16x8, buf_load16(rbp, vob, kt * 2048 + (nt >> 1) * grp_bytes + (nt & 1) * 1024));
+    return v;
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 fa[8], xb[4], yb[4];
+  u32x4 rs[2];
+
+  auto iter = [&](int t, const bf16x8 (&cb)[4], bf16x8 (&nb_)[4]) __attribute__((always_inline)) {
+    const int tB = (MODE & 1) ? 0 : min(t + 1, nk - 1);
+    const int tA = min(t + 3, nk - 1);
+    const char* st = S + ((t + 1) & (NSTAGE - 1)) * IMG;
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cb[nt], fa[mt], acc[mt][nt], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);  // the MFMAs read fa[mt] before it is reloaded (same registers)
+      fa[mt] = rd(st, a_off + mt * 1024);
+      if (mt < 4) nb_[mt] = ldB(tB, mt);
+      if ((mt == 1 || mt == 5) && !(MODE & 2)) {
+        const int j = mt >> 2;
+        stA(t + 2, j, rs[j]);  // A tile t+2 (past the end: a dead stage)
+        rs[j] = ldA(tA, j);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's A writes of tile t+2 are in LDS
+    barrier();
+  };
+
+  // prologue: A tiles 0, 1 into stages 0, 1; A tile 2 into the staging registers; B tile 0 into xb
+#pragma unroll
+  for (int j = 0; j < 2; ++j) rs[j] = ldA(0, j);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) stA(0, j, rs[j]);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) rs[j] = ldA(1, j);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) stA(1, j, rs[j]);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) rs[j] = ldA(min(2, nk - 1), j);
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) xb[nt] = ldB(0, nt);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  barrier();
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt) fa[mt] = rd(S, a_off + mt * 1024);
+
+  for (int t = 0; t < nk; t += 2) {
+    iter(t, xb, yb);
+    iter(t + 1, yb, xb);
+  }
+  NTArgs q{};
+  q.c = p.c;
+  q.ldc = p.ldc;
+  q.alpha = p.alpha;
+  q.beta = p.beta;
+  store_tile<F32C>(q, acc, m0, n0, wm, wn, lane);
+}
+
+// ---- variant 4: one wave per SIMD, 128 x 128 per wave, register-staged loads -------------------------
+// The LDS is the shared resource of the 8-wave kernels (per 32-deep tile a CU reads 96 KiB of fragments
+// and writes 32 KiB): with 4 waves of 128 x 128 each fragment read feeds 8 MFMAs instead of 4 / 8, so
+// the reads drop to 64 KiB.  One wave per SIMD (512 registers: 256 accumulators + fragments + staging)
+// hides its own latencies: fragment reads of tile t+1 and the global loads of tile t+3 are issued
+// between the MFMAs of tile t (register staging: a global_load / ds_write pair issues in a few cycles
+// inside an MFMA's shadow, where an LDS-DMA piece would stall the wave ~60+ cycles with no partner wave
+// to fill the pipe).
+template <bool F32C>
+__global__ __launch_bounds__(256, 1) void gemm_nt_w4_kernel(NTArgs p) {
+  __shared__ __attribute__((aligned(16))) char S[NSTAGE * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  int mb, nb;
+  tile_of(p, mb, nb);
+  const long long m0 = (long long)mb * BM, n0 = (long long)nb * BN;
+  const int nk = p.K / BK;  // even (host contract)
+
+  // staging: wave w loads rows [64 w, 64 w + 64) of both images, 4 pieces of 16 rows each per operand
+  int voa, vob;
+  {
+    const int r = 64 * wave + (lane >> 2);
+    const int c = (lane & 3) ^ swz(r);
+    voa = (int)((r * p.lda + 8 * c) * 2);
+    vob = (int)((r * p.ldb + 8 * c) * 2);
+  }
+  const int sa16 = (int)(16 * p.lda * 2), sb16 = (int)(16 * p.ldb * 2);
+  const auto ra = make_rsrc(p.a + m0 * p.lda);
+  const auto rb = make_rsrc(p.b + n0 * p.ldb);
+  char* const wdst = S + 64 * wave * 64 + lane * 16;
+  // piece j: operand j >> 2, rows + 16 (j & 3)
+  auto ld = [&](int kt, int j) __attribute__((always_inline)) {
+    return buf_load16((j >> 2) ? rb : ra, (j >> 2) ? vob : voa, kt * BK * 2 + (j & 3) * ((j >> 2) ? sb16 : sa16));
+  };
+  auto st = [&](int kt, int j, const u32x4& v) __attribute__((always_inline)) {
+    *reinterpret_cast<u32x4*>(wdst + (kt & (NSTAGE - 1)) * STAGE + (j >> 2) * IMG + (j & 3) * 1024) = v;
+  };
+  const int li = lane & 15, kc = lane >> 4;
+  const int a_off = (wm * 128 + li) * 64 + 16 * (kc ^ swz(li));
+  const int brow = wn * 128 + 8 * (li >> 2) + (li & 3);
+  const int b_off = IMG + brow * 64 + 16 * (kc ^ swz(brow));
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 fa[8], xb[8], yb[8];
+  u32x4 rs[8];
+
+  auto iter = [&](int t, const bf16x8 (&cb)[8], bf16x8 (&nb_)[8]) __attribute__((always_inline)) {
+    const int tld = min(t + 3, nk - 1);
+    const char* sr = S + ((t + 1) & (NSTAGE - 1)) * STAGE;
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cb[nt], fa[mt], acc[mt][nt], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      fa[mt] = rd(sr, a_off + mt * 1024);
+      nb_[mt] = rd(sr, b_off + b_nt(mt));
+      st(t + 2, mt, rs[mt]);  // tile t+2 (past the end: a dead stage)
+      rs[mt] = ld(tld, mt);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's writes of tile t+2 are in LDS
+    barrier();
+  };
+
+#pragma unroll
+  for (int j = 0; j < 8; ++j) rs[j] = ld(0, j);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) st(0, j, rs[j]);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) rs[j] = ld(1, j);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) st(1, j, rs[j]);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) rs[j] = ld(min(2, nk - 1), j);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  barrier();
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt) fa[mt] = rd(S, a_off + mt * 1024);
+#pragma unroll
+  for (int nt = 0; nt < 8; ++nt) xb[nt] = rd(S, b_off + b_nt(nt));
+
+  for (int t = 0; t < nk; t += 2) {
+    iter(t, xb, yb);
+    iter(t + 1, yb, xb);
+  }
+  store_wave<F32C, 8, 8>(p, acc, m0 + wm * 128, n0 + wn * 128, lane);
+}
+
+// ---- variant 5 (default): 64-deep super-stages, full 128-byte lines per DMA row --------------------------
+// rocprofv3 on variants 1-4 (profiles/r3/gemm_nt.md): the texture addresser was 95 % busy (hipBLASLt:
+// 60 %) -- with 32-deep tiles every DMA row is a 64-byte HALF line, so a 1 KiB piece touches 16 cache
+// lines instead of 8.  Here the LDS ring holds two 64-deep "super-stages" (A [256][64] | B [256][64],
+// 64 KiB each, 128-byte rows), each DMA piece is 8 rows x 128 B, and the MFMA loop still walks 32-deep
+// tiles (tile t = half t & 1 of super-stage t >> 1).  The 128-byte-row image is swizzled by
+// f(R) = R0 | R1 << 1 | R3 << 2 on the 16-byte chunk (conflict-free for both fragment reads).
+//
+// Iteration t (32 MFMAs of tile t, fragment reads of tile t+1 into the other register set):
+//   odd t:  8 DMA pieces of super-stage (t+3)/2 (tiles t+3, t+4) into the stage tiles t-1 / t held --
+//           tile t's fragments are already in registers and every wave's reads of tile t-1 completed
+//           before the previous barrier;
+//   even t: vmcnt(0) (super-stage t/2+1 landed) + lgkmcnt(0) + barrier.
+FTC_DEV int f5(int r) { return (r & 1) | (r & 2) | ((r >> 1) & 4); }
+
+template <bool F32C>
+__global__ __launch_bounds__(512, 1) void gemm_nt_v5_kernel(NTArgs p) {
+  constexpr int IMG2 = 256 * 64 * 2;  // one operand image of a super-stage: 32 KiB
+  constexpr int SS = 2 * IMG2;        // super-stage: A | B
+  __shared__ __attribute__((aligned(16))) char S[2 * SS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  int mb, nb;
+  tile_of(p, mb, nb);
+  const long long m0 = (long long)mb * BM, n0 = (long long)nb * BN;
+  const int nk = p.K / BK;  // even (host contract)
+  const int ns = nk >> 1;   // super-stages
+
+  // DMA: wave w fills rows [32 w, 32 w + 32) of both images as 4 pieces of 8 rows x 128 B; lane i -> row
+  // +(i >> 3), physical chunk i & 7 = logical chunk (i & 7) ^ f5(row).  Piece sub's rows start at 8 sub,
+  // so row bit 3 = sub & 1: one per-lane source offset per parity.
+  int vo[2][2];  // [operand][parity]
+  {
+    const int rr = lane >> 3, pc = lane & 7;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int lc = pc ^ f5(rr + 8 * q);
+      vo[0][q] = (int)(((32 * wave + rr) * p.lda + 8 * lc) * 2);
+      vo[1][q] = (int)(((32 * wave + rr) * p.ldb + 8 * lc) * 2);
+    }
+  }
+  const int s8a = (int)(8 * p.lda * 2), s8b = (int)(8 * p.ldb * 2);
+  const auto ra = make_rsrc(p.a + m0 * p.lda);
+  const auto rb = make_rsrc(p.b + n0 * p.ldb);
+  char* const ddst = S + 32 * wave * 128;
+  // piece j (0..7) of super-stage ss: operand j >> 2, rows 32 w + 8 (j & 3)
+  auto piece = [&](int ss_src, int ss_dst, int j) __attribute__((always_inline)) {
+    const int op = j >> 2, sub = j & 3;
+    char* d = ddst + (ss_dst & 1) * SS + op * IMG2 + sub * 1024;
+    const int so = ss_src * 128 + sub * (op ? s8b : s8a);
+    lds_dma16(op ? rb : ra, d, vo[op][sub & 1], so);
+  };
+
+  const int li = lane & 15, kc = lane >> 4;
+  int a_off[2], b_off[2];
+  {
+    const int ra_ = wm * 128 + li;
+    const int rb_ = wn * 64 + 8 * (li >> 2) + (li & 3);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      a_off[h] = ra_ * 128 + 16 * ((4 * h + kc) ^ f5(li));
+      b_off[h] = IMG2 + rb_ * 128 + 16 * ((4 * h + kc) ^ f5(rb_));
+    }
+  }
+  auto bnt = [](int nt) { return (32 * (nt >> 1) + 4 * (nt & 1)) * 128; };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 fa[8], xb[4], yb[4];
+
+  // ODD: compile-time parity of t (the loop is unrolled by 2)
+  auto iter = [&](int t, auto odd_c, const bf16x8 (&cb)[4], bf16x8 (&nb_)[4]) __attribute__((always_inline)) {
+    constexpr bool ODD = decltype(odd_c)::value;
+    const int tn = t + 1;  // fragments of tile t+1 (past the end: a dead read)
+    const char* st = S + ((tn >> 1) & 1) * SS;
+    const int h = ODD ? 0 : 1;  // tn & 1
+    const int dsrc = min((t + 3) >> 1, ns - 1), ddst_ss = (t + 3) >> 1;
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cb[nt], fa[mt], acc[mt][nt], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);  // the MFMAs read fa[mt] before it is reloaded (same registers)
+      fa[mt] = rd(st, a_off[h] + mt * 2048);
+      if (mt < 4) nb_[mt] = rd(st, b_off[h] + bnt(mt));
+      if constexpr (ODD) piece(dsrc, ddst_ss, mt);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (!ODD) {
+      __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) + lgkmcnt(0): super-stage t/2+1 landed, reads done
+      barrier();
+    }
+  };
+
+  // prologue: super-stages 0 and 1 in flight, wait for 0
+#pragma unroll
+  for (int j = 0; j < 8; ++j) piece(0, 0, j);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) piece(min(1, ns - 1), 1, j);
+  __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8)
+  barrier();
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt) fa[mt] = rd(S, a_off[0] + mt * 2048);
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) xb[nt] = rd(S, b_off[0] + bnt(nt));
+
+  for (int t = 0; t < nk; t += 2) {
+    iter(t, std::false_type{}, xb, yb);
+    iter(t + 1, std::true_type{}, yb, xb);
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no DMA may land in LDS after the workgroup ends
   store_tile<F32C>(p, acc, m0, n0, wm, wn, lane);
 }
 
@@ -448,10 +797,20 @@ extern "C" int ftc_gemm_nt(const void* a, long long lda, const void* b, long lon
            alpha, beta};
   static const int variant = [] {
     const char* e = getenv("FTC_GEMM_NT_VARIANT");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 5;
   }();
   const int grid = p.nm * p.nn;
-  if (variant == 2) {
+  if (variant == 5) {
+    if (c_fp32)
+      hipLaunchKernelGGL((gemm_nt_v5_kernel<true>), dim3(grid), dim3(512), 0, stream, p);
+    else
+      hipLaunchKernelGGL((gemm_nt_v5_kernel<false>), dim3(grid), dim3(512), 0, stream, p);
+  } else if (variant == 4) {
+    if (c_fp32)
+      hipLaunchKernelGGL((gemm_nt_w4_kernel<true>), dim3(grid), dim3(256), 0, stream, p);
+    else
+      hipLaunchKernelGGL((gemm_nt_w4_kernel<false>), dim3(grid), dim3(256), 0, stream, p);
+  } else if (variant == 2) {
     if (c_fp32)
       hipLaunchKernelGGL((gemm_nt_rs_kernel<true>), dim3(grid), dim3(512), 0, stream, p);
     else
@@ -475,8 +834,47 @@ extern "C" int ftc_gemm_nt(const void* a, long long lda, const void* b, long lon
       case 7: hipLaunchKernelGGL((gemm_nt_kernel<false, 7>), dim3(grid), dim3(512), 0, stream, p); break;
       case 8: hipLaunchKernelGGL((gemm_nt_kernel<false, 8>), dim3(grid), dim3(512), 0, stream, p); break;
       case 16: hipLaunchKernelGGL((gemm_nt_kernel<false, 16>), dim3(grid), dim3(512), 0, stream, p); break;
+      case 32: hipLaunchKernelGGL((gemm_nt_kernel<false, 32>), dim3(grid), dim3(512), 0, stream, p); break;
       default: hipLaunchKernelGGL((gemm_nt_kernel<false>), dim3(grid), dim3(512), 0, stream, p);
     }
   }
+  return (int)hipGetLastError();
+}
+
+// C[M, N] (ldc) = alpha A Bp^T + beta C with Bp the packed [N/32][K/32][2][64][8] form of B [N, K].
+extern "C" int ftc_gemm_nt_pb_ok(const void* a, long long lda, const void* bp, const void* c, long long ldc, int M,
+                                 int N, int K) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || K % (2 * BK)) return 0;
+  if (lda % 8 || ldc % 8 || lda < K || ldc < N) return 0;
+  if ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(bp) | reinterpret_cast<uintptr_t>(c)) & 15) return 0;
+  if ((long long)(BM - 1) * lda * 2 + (long long)K * 2 + 64 >= (1LL << 31)) return 0;
+  if ((long long)8 * (K / BK) * 2048 >= (1LL << 31)) return 0;  // B offsets inside one block's panel
+  return 1;
+}
+
+extern "C" int ftc_gemm_nt_pb(const void* a, long long lda, const void* bp, void* c, long long ldc, int c_fp32, int M,
+                              int N, int K, float alpha, float beta, hipStream_t stream) {
+  if (!ftc_gemm_nt_pb_ok(a, lda, bp, c, ldc, M, N, K)) return -1;
+  static const int group_m = [] {
+    const char* e = getenv("FTC_GEMM_NT_GROUP");
+    return e ? atoi(e) : 4;
+  }();
+  PBArgs p{(const uint16_t*)a, (const uint16_t*)bp, c, lda, ldc, K, M / BM, N / BN, group_m > 0 ? group_m : 4, alpha,
+           beta};
+  const int grid = p.nm * p.nn;
+  static const int mode = [] {
+    const char* e = getenv("FTC_GEMM_NT_PB_MODE");
+    return e ? atoi(e) : 0;
+  }();
+  if (c_fp32)
+    hipLaunchKernelGGL((gemm_nt_pb_kernel<true>), dim3(grid), dim3(512), 0, stream, p);
+  else if (mode == 1)
+    hipLaunchKernelGGL((gemm_nt_pb_kernel<false, 1>), dim3(grid), dim3(512), 0, stream, p);
+  else if (mode == 2)
+    hipLaunchKernelGGL((gemm_nt_pb_kernel<false, 2>), dim3(grid), dim3(512), 0, stream, p);
+  else if (mode == 3)
+    hipLaunchKernelGGL((gemm_nt_pb_kernel<false, 3>), dim3(grid), dim3(512), 0, stream, p);
+  else
+    hipLaunchKernelGGL((gemm_nt_pb_kernel<false>), dim3(grid), dim3(512), 0, stream, p);
   return (int)hipGetLastError();
 }

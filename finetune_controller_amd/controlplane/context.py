@@ -48,7 +48,7 @@ class AppContext:
             kube = HttpKubeClient()
         settings.load_aws_credentials(kube)
         objects = make_object_store(settings.OBJECT_STORE, settings)
-        if isinstance(kube, object) and settings.KUBE_BACKEND == "fake":
+        if settings.KUBE_BACKEND == "fake":  # the fake cluster's pods sync artifacts into the object store
             kube.store = objects
         registry = ModelRegistry()
         registry.load_custom(settings.CUSTOM_MODELS_DIR)

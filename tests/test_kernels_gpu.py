@@ -288,6 +288,34 @@ def test_gemm_nt(C, cdtype, M, N, K, pad, beta):
     torch.testing.assert_close(c.float(), ref, atol=tol, rtol=1e-2 if cdtype == torch.bfloat16 else 1e-4)
 
 
+@pytest.mark.parametrize("cdtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("M,N,K,pad,beta", [(256, 256, 64, 0, 0.0), (512, 768, 4160, 64, 0.0), (768, 512, 128, 8, 1.0),
+                                            (256, 1024, 1088, 0, -0.5)])
+def test_gemm_nt_packed(C, cdtype, M, N, K, pad, beta):
+    """Packed-B projection GEMM (B in MFMA fragment order, ops/gemm.py) vs an exact integer product and
+    an fp32 reference."""
+    from finetune_controller_amd.ops.gemm import pack_b_nt
+
+    torch.manual_seed(4)
+    abuf = torch.randint(-3, 4, (M, K + pad), device=DEV).to(torch.bfloat16)
+    a = abuf[:, :K]
+    b = (torch.arange(N * K, device=DEV).reshape(N, K) % 7 - 3).to(torch.bfloat16)
+    bp = pack_b_nt(b)
+    c = torch.zeros(M, N, device=DEV, dtype=cdtype)
+    assert C.gemm_nt_pb_ok(c, a, bp, N, K)
+    C.gemm_nt_pb_(c, a, bp, N, K, 1.0, 0.0)
+    assert torch.equal(c, (a.double() @ b.double().t()).to(cdtype))
+    abuf = (torch.rand(M, K + pad, device=DEV) * 2 - 1).to(torch.bfloat16)
+    a = abuf[:, :K]
+    b = (torch.rand(N, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    bp = pack_b_nt(b)
+    c = torch.randn(M, N, device=DEV).to(cdtype)
+    ref = beta * c.float() + 0.5 * (a.float() @ b.float().t())
+    C.gemm_nt_pb_(c, a, bp, N, K, 0.5, beta)
+    tol = 2e-2 * (K ** 0.5) / 8 if cdtype == torch.bfloat16 else 1e-3 * (K ** 0.5) / 8
+    torch.testing.assert_close(c.float(), ref, atol=tol, rtol=1e-2 if cdtype == torch.bfloat16 else 1e-4)
+
+
 def test_gemm_nt_rejects(C):
     a = torch.zeros(256, 40, device=DEV, dtype=torch.bfloat16)  # K not a multiple of 32
     b = torch.zeros(256, 40, device=DEV, dtype=torch.bfloat16)
@@ -462,8 +490,8 @@ def test_llama_lora_step_hip_matches_torch_path(C, monkeypatch, window, aug, ckp
 
 def test_native_rccl_engine_world1(C):
     """csrc/comm engine on one rank: communicator bootstrap through c10d, every collective, event
-    ordering against the current stream (the multi-rank math is RCCL's; the 2-rank gradient
-    equivalence of the bucketer runs over gloo in test_worker.py)."""
+    ordering against the current stream.  The 2-rank gradient equivalence of the bucketer over real
+    RCCL (both engines) is tests/test_distributed.py::test_ddp_rccl_matches_per_rank_sum."""
     import os
 
     import torch.distributed as dist

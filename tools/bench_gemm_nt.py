@@ -18,6 +18,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from finetune_controller_amd.ops._backend import ext  # noqa: E402
+from finetune_controller_amd.ops.gemm import pack_b_nt  # noqa: E402
 
 T = 16384
 SHAPES = {  # name: (k, n)
@@ -51,22 +52,30 @@ def main():
         w = torch.empty(n, k, device="cuda", dtype=torch.bfloat16).uniform_(-1, 1)
         y0 = torch.empty(T, n, device="cuda", dtype=torch.bfloat16)
         y1 = torch.empty(T, n, device="cuda", dtype=torch.bfloat16)
-        assert C.gemm_nt_ok(y1, x, w), name
-        ours, lib = [], []
-        C.gemm_nt_(y1, x, w)
+        wp = pack_b_nt(w)  # the packed (fragment-order) weight: built once, like a frozen weight's
+        assert C.gemm_nt_ok(y1, x, w) and C.gemm_nt_pb_ok(y1, x, wp, n, k), name
+        ours, lib, pk = [], [], []
         torch.mm(x, w.t(), out=y0)
+        C.gemm_nt_pb_(y1, x, wp, n, k)
+        torch.cuda.synchronize()
+        err_pk = ((y1.float() - y0.float()).abs().max() / y0.float().abs().max()).item()
+        C.gemm_nt_(y1, x, w)
         torch.cuda.synchronize()
         err = ((y1.float() - y0.float()).abs().max() / y0.float().abs().max()).item()
         for _ in range(a.rounds):
             ours.append(timeit(lambda: C.gemm_nt_(y1, x, w), a.iters))
+            pk.append(timeit(lambda: C.gemm_nt_pb_(y1, x, wp, n, k), a.iters))
             lib.append(timeit(lambda: torch.mm(x, w.t(), out=y0), a.iters))
         fl = 2.0 * T * n * k
-        mo, ml = statistics.median(ours), statistics.median(lib)
+        mo, ml, mp = statistics.median(ours), statistics.median(lib), statistics.median(pk)
         print(json.dumps({"gemm": name, "M": T, "N": n, "K": k,
                           "ours_ms": [round(mo, 3), round(min(ours), 3)], "ours_tf": round(fl / mo / 1e9),
+                          "packed_ms": [round(mp, 3), round(min(pk), 3)], "packed_tf": round(fl / mp / 1e9),
                           "lib_ms": [round(ml, 3), round(min(lib), 3)], "lib_tf": round(fl / ml / 1e9),
-                          "speedup": round(ml / mo, 3), "max_rel_err_vs_lib": float(f"{err:.2e}")}), flush=True)
-        del x, w, y0, y1
+                          "speedup": round(ml / mo, 3), "speedup_packed": round(ml / mp, 3),
+                          "max_rel_err_vs_lib": float(f"{err:.2e}"),
+                          "max_rel_err_packed_vs_lib": float(f"{err_pk:.2e}")}), flush=True)
+        del x, w, wp, y0, y1
         torch.cuda.empty_cache()
 
 

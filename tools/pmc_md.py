@@ -102,6 +102,7 @@ def main():
     ap.add_argument("--labels", default=None)
     ap.add_argument("--match", default=None, help="only kernels whose name contains this")
     ap.add_argument("--title", default="rocprofv3 PMC summary")
+    ap.add_argument("--raw", action="store_true", help="every counter's mean per dispatch (custom passes)")
     a = ap.parse_args()
     labels = json.load(open(a.labels)) if a.labels else None
     merged = {}
@@ -113,6 +114,17 @@ def main():
                 m["c"].setdefault(k, x / max(v["n"], 1))
     flops = {s["label"]: s for s in labels["shapes"]} if labels else {}
     print(f"# {a.title}\n")
+    if a.raw:  # per kernel: us, clock, then every counter as a mean per dispatch (cycles counters also / wave cycles)
+        names = sorted({k for m in merged.values() for k in m["c"]})
+        print("| kernel | disp | us | clock GHz | " + " | ".join(names) + " |")
+        print("|" + "---|" * (4 + len(names)))
+        for key, m in sorted(merged.items(), key=lambda kv: -kv[1]["ns"] / max(kv[1]["n"], 1)):
+            us = m["ns"] / max(m["n"], 1) / 1e3
+            gui = m["c"].get("GRBM_GUI_ACTIVE")
+            clk = f"{gui / 8 / (us * 1e3):.2f}" if gui and us else ""
+            vals = " | ".join(f"{m['c'][k]:.4g}" if k in m["c"] else "" for k in names)
+            print(f"| `{key}` | {m['n']} | {us:.1f} | {clk} | {vals} |")
+        return
     hdr = ("| kernel / shape | disp | us | clock GHz | MFMA busy | FLOP/clk share | TF/s | WAIT_INST_ANY | WAIT_ANY |"
            " LDS confl/active | HBM GB |")
     print(hdr + "\n|" + "---|" * (hdr.count("|") - 1))

@@ -18,6 +18,9 @@ CMD=()
 for arg in "$@"; do if [ -e "$R/$arg" ]; then CMD+=("$R/$arg"); else CMD+=("$arg"); fi; done
 PASSES=("SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"
         "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE FETCH_SIZE")
+# PMC_PASSES="A B C;D E F": custom passes (each within the per-block slot limits), raw means per kernel
+# in gpurun_out/pmc_NAME.raw.md (tools/pmc_md.py --raw)
+if [ -n "$PMC_PASSES" ]; then IFS=';' read -r -a PASSES <<< "$PMC_PASSES"; MDARGS+=("--raw"); fi
 mkdir -p "gpurun_out/pmc_$NAME"
 DIRS=()
 i=0
