@@ -55,7 +55,7 @@ int ftc_sumsq(const void* x, int is_fp32, long long n, float* partial, float* ou
               float scale, hipStream_t stream);
 int ftc_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H, int KV, int D,
                   long long q_row_stride, long long kv_row_stride, long long o_row_stride, float scale, int causal,
-                  int window, const int* doc_start, hipStream_t stream);
+                  int window, const int* doc_start, int kv_valid, hipStream_t stream);
 int ftc_flash_bwd_workspace(int B, int S, int H, int D, long long* bytes);
 long long ftc_decode_workspace_floats(int B, int H, int KV, int D, int max_len);
 int ftc_decode_attention(const void* q, void* kc, void* vc, const void* knew, const void* vnew, long long new_rs,
@@ -67,7 +67,7 @@ int ftc_flash_bwd(const void* q, const void* k, const void* v, const void* o, co
                   long long q_row_stride, long long kv_row_stride, long long o_row_stride, long long do_row_stride,
                   long long dq_row_stride,
                   long long dkv_row_stride, float scale, int causal, int window, const int* doc_start,
-                  const int* doc_end, hipStream_t stream);
+                  const int* doc_end, int kv_valid, hipStream_t stream);
 int ftc_nf4_dequant(const uint8_t* packed, const uint8_t* absmax_q, const float* absmax_scale, float absmax_offset,
                     void* out, long long n, int block, int block2, hipStream_t stream);
 int ftc_nf4_quant(const void* w, uint8_t* packed, float* absmax, long long n, int block, hipStream_t stream);
@@ -514,7 +514,7 @@ static const int* doc_ptr(const c10::optional<at::Tensor>& t, int64_t n, const c
 // q: [B*S, >=H*D] view (row stride q_rs), k/v: [B*S, >=KV*D] views; all bf16 with unit column stride.
 std::vector<at::Tensor> flash_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, int64_t B, int64_t S,
                                   int64_t H, int64_t KV, int64_t D, double scale, bool causal, int64_t window,
-                                  int64_t pad, const c10::optional<at::Tensor>& doc_start) {
+                                  int64_t pad, const c10::optional<at::Tensor>& doc_start, int64_t kv_valid) {
   need(q, at::kBFloat16, "q");
   need(k, at::kBFloat16, "k");
   need(v, at::kBFloat16, "v");
@@ -533,7 +533,7 @@ std::vector<at::Tensor> flash_fwd(const at::Tensor& q, const at::Tensor& k, cons
   auto lse = at::empty({B, H, S}, q.options().dtype(at::kFloat));
   check(ftc_flash_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), (int)B, (int)S,
                       (int)H, (int)KV, (int)D, q.stride(0), k.stride(0), o.stride(0), (float)scale, causal ? 1 : 0,
-                      (int)window, doc_ptr(doc_start, B * S, "doc_start"), cur_stream()),
+                      (int)window, doc_ptr(doc_start, B * S, "doc_start"), (int)kv_valid, cur_stream()),
         "flash_fwd");
   return {o, lse};
 }
@@ -542,7 +542,8 @@ std::vector<at::Tensor> flash_fwd(const at::Tensor& q, const at::Tensor& k, cons
 void flash_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const at::Tensor& o,
                const at::Tensor& dout, const at::Tensor& lse, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv,
                int64_t B, int64_t S, int64_t H, int64_t KV, int64_t D, double scale, bool causal, int64_t window,
-               const c10::optional<at::Tensor>& doc_start, const c10::optional<at::Tensor>& doc_end) {
+               const c10::optional<at::Tensor>& doc_start, const c10::optional<at::Tensor>& doc_end,
+               int64_t kv_valid) {
   TORCH_CHECK(doc_start.has_value() == doc_end.has_value(), "flash_bwd: doc_start and doc_end go together");
   for (auto* t : {&q, &k, &v, &o, &dout}) need(*t, at::kBFloat16, "flash_bwd input");
   need(lse, at::kFloat, "lse");
@@ -560,7 +561,7 @@ void flash_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, co
                       (int)D, q.stride(0), k.stride(0), o.stride(0), dout.stride(0), dq.stride(0), dk.stride(0),
                       (float)scale,
                       causal ? 1 : 0, (int)window, doc_ptr(doc_start, B * S, "doc_start"),
-                      doc_ptr(doc_end, B * S, "doc_end"), cur_stream()),
+                      doc_ptr(doc_end, B * S, "doc_end"), (int)kv_valid, cur_stream()),
         "flash_bwd");
 }
 
@@ -755,11 +756,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("grad_sumsq", &grad_sumsq);
   m.def("flash_fwd", &flash_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("B"), py::arg("S"), py::arg("H"),
         py::arg("KV"), py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("pad") = 0,
-        py::arg("doc_start") = py::none());
+        py::arg("doc_start") = py::none(), py::arg("kv_valid") = -1);
   m.def("flash_bwd", &flash_bwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("dout"),
         py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("B"), py::arg("S"), py::arg("H"),
         py::arg("KV"), py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("window"),
-        py::arg("doc_start") = py::none(), py::arg("doc_end") = py::none());
+        py::arg("doc_start") = py::none(), py::arg("doc_end") = py::none(), py::arg("kv_valid") = -1);
   m.def("decode_attention", &decode_attention);
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequantize", &nf4_dequantize);

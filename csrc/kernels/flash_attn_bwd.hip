@@ -131,6 +131,10 @@ struct BwdArgs {
   int prio_young;
   const int* doc_start;  // [B*S] packed-sequence document bounds (null: one document per sequence):
   const int* doc_end;    //   key k visible to query q iff doc_start[q] <= k, i.e. q < doc_end[k]  // dK/dV, 8 waves: s_setprio 1 for the second-dispatched half (guide T5 static form)
+  // keys >= kv_valid are masked for every query (right-padded tail of non-causal attention).  Only
+  // the dQ pass masks them: dK / dV rows of those keys are discarded by the caller, and a masked key
+  // never reaches a valid key's dK / dV.
+  int kv_valid;
 };
 
 // ---------------------------------------------------------------- 1. delta
@@ -725,7 +729,7 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
   const float lse2 = a.lse[sidx] * LOG2E;
   const float ndlt = a.delta[sidx];  // -delta
 
-  int kv_end = a.causal ? q0 + BQ : S;
+  int kv_end = min(a.causal ? q0 + BQ : S, a.kv_valid);
   int kv_begin = 0;
   if (a.window > 0) kv_begin = (max(0, q0 - a.window + 1) / BK) * BK;
   int dlo = -0x3fffffff, wdmax = -0x3fffffff;  // packed documents: as in the forward
@@ -802,10 +806,11 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
       for (int i = 0; i < 16; ++i) s[kt][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(a.c, s[kt][i], -lse2));
     const int qmin_w = q0 + wave * 32;
     const bool need_mask = (a.causal && kv0 + BK - 1 > qmin_w) || (a.window > 0 && qmin_w + 31 - kv0 >= a.window) ||
+                           kv0 + BK > a.kv_valid ||
                            kv0 < wdmax;
     if (need_mask) {  // wave-uniform; selects inside
       const int base = kv0 + 4 * hh;
-      const int hi = (a.causal ? qrow : 0x3fffffff) - base;
+      const int hi = min(a.causal ? qrow : 0x3fffffff, a.kv_valid - 1) - base;
       const int lo = max(a.window > 0 ? qrow - a.window + 1 : -0x3fffffff, dlo) - base;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
@@ -911,14 +916,15 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
                              const float* lse, void* dq, void* dk, void* dv, void* workspace, int B, int S, int H,
                              int KV, int D, long long q_rs, long long kv_rs, long long o_rs, long long do_rs,
                              long long dq_rs, long long dkv_rs, float scale, int causal, int window,
-                             const int* doc_start, const int* doc_end, hipStream_t stream) {
+                             const int* doc_start, const int* doc_end, int kv_valid, hipStream_t stream) {
   if (S % 256 != 0 || H % KV != 0 || (D != 128 && D != 64)) return -1;
+  if (kv_valid <= 0 || kv_valid > S) kv_valid = S;
   // the dK/dV kernel addresses one batch's Q / dO rows and the workspace with 32-bit buffer offsets
   const long long max_rs = q_rs > do_rs ? (q_rs > kv_rs ? q_rs : kv_rs) : (do_rs > kv_rs ? do_rs : kv_rs);
   if ((long long)S * max_rs * 2 >= (1LL << 31) || 2LL * B * H * S * 4 >= (1LL << 31)) return -1;
   BwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)o, (const uint16_t*)dout,
             lse, (float*)workspace, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, q_rs, kv_rs, o_rs, dq_rs, dkv_rs, do_rs,
-            B, S, H, KV, scale, scale * LOG2E, causal, window, 0, doc_start, doc_end};
+            B, S, H, KV, scale, scale * LOG2E, causal, window, 0, doc_start, doc_end, kv_valid};
   static const int prio = [] {
     const char* e = getenv("FTC_FLASH_BWD_PRIO");
     return (e && e[0] == '1') ? 1 : 0;

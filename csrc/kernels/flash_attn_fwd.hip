@@ -99,6 +99,7 @@ struct FwdArgs {
   float scale_log2;
   int causal, window;
   const int* doc_start;  // [B*S] first position of each token's document (packed sequences), or null
+  int kv_valid;          // keys >= kv_valid are masked for every query (a right-padded tail; S: none)
 };
 
 // logical block -> (qb, b, kvh, g) with heavy-first order and GQA groups co-located on one XCD
@@ -191,7 +192,7 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
 
   // ---- key range
   const int q_last = min(S, q0 + BQ) - 1;
-  int kv_end = a.causal ? q_last + 1 : S;
+  int kv_end = min(a.causal ? q_last + 1 : S, a.kv_valid);
   int kv_begin = 0;
   if (a.window > 0) {
     kv_begin = max(0, q0 - a.window + 1);
@@ -296,11 +297,12 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
     const int kv0 = kv_begin + t * BK;
     const int qmin_w = q0 + wave * 32;
     const bool need_mask = (a.causal && kv0 + BK - 1 > qmin_w) || (a.window > 0 && qmin_w + 31 - kv0 >= a.window) ||
+                           kv0 + BK > a.kv_valid ||
                            kv0 < wdmax;
     if (need_mask) {
       // key k of element (kt, i) = kv0 + kt*32 + (i&3) + 8*(i>>2) + 4*hh; valid iff lo <= k <= hi
       const int base = kv0 + 4 * hh;
-      const int hi = (a.causal ? qrow : 0x3fffffff) - base;
+      const int hi = min(a.causal ? qrow : 0x3fffffff, a.kv_valid - 1) - base;
       const int lo = max(a.window > 0 ? qrow - a.window + 1 : -0x3fffffff, dlo) - base;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
@@ -517,7 +519,7 @@ __global__ __launch_bounds__(256, OCC) void flash_fwd_pipe_kernel(FwdArgs a) {
     }
   }
   const int q_last = min(S, q0 + BQ) - 1;
-  int kv_end = a.causal ? q_last + 1 : S;
+  int kv_end = min(a.causal ? q_last + 1 : S, a.kv_valid);
   int kv_begin = 0;
   if (a.window > 0) {
     kv_begin = max(0, q0 - a.window + 1);
@@ -581,10 +583,11 @@ __global__ __launch_bounds__(256, OCC) void flash_fwd_pipe_kernel(FwdArgs a) {
     const int kv0 = kv_begin + t * BK;
     const int qmin_w = q0 + wave * 32;
     const bool need_mask = (a.causal && kv0 + BK - 1 > qmin_w) || (a.window > 0 && qmin_w + 31 - kv0 >= a.window) ||
+                           kv0 + BK > a.kv_valid ||
                            kv0 < wdmax;
     if (need_mask) {
       const int base = kv0 + 4 * hh;
-      const int hi = (a.causal ? qrow : 0x3fffffff) - base;
+      const int hi = min(a.causal ? qrow : 0x3fffffff, a.kv_valid - 1) - base;
       const int lo = max(a.window > 0 ? qrow - a.window + 1 : -0x3fffffff, dlo) - base;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
@@ -724,15 +727,16 @@ __global__ __launch_bounds__(256, OCC) void flash_fwd_pipe_kernel(FwdArgs a) {
 
 extern "C" int ftc_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H,
                              int KV, int D, long long q_rs, long long kv_rs, long long o_rs, float scale, int causal,
-                             int window, const int* doc_start, hipStream_t stream) {
+                             int window, const int* doc_start, int kv_valid, hipStream_t stream) {
   if (S % BK != 0 || H % KV != 0 || (D != 128 && D != 64)) return -1;
+  if (kv_valid <= 0 || kv_valid > S) kv_valid = S;
   static const int waves = [] {
     const char* e = getenv("FTC_FLASH_FWD_WAVES");
     return (e && e[0] == '8') ? 8 : 4;
   }();
   const int BQ = 32 * waves;
   FwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, q_rs, kv_rs, o_rs,
-            B, S, H, KV, (S + BQ - 1) / BQ, scale * LOG2E, causal, window, doc_start};
+            B, S, H, KV, (S + BQ - 1) / BQ, scale * LOG2E, causal, window, doc_start, kv_valid};
   const int nblocks = a.nqb * B * H;
   const size_t lds = 0;  // static: K/V double buffers
   static const bool pp = [] {

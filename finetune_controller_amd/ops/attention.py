@@ -42,9 +42,10 @@ def flash_supported(D: int, S: int) -> bool:
 
 
 def flash_usable(D: int, S: int, causal: bool) -> bool:
-    """The flash path handles this shape: natively, or -- causal attention with S not a multiple of the
-    tile -- through tail padding (``_FlashPaddedTail``)."""
-    return FLASH_READY and D in (64, 128) and (S % FLASH_TILE == 0 or causal)
+    """The flash path handles this shape: natively, or -- S not a multiple of the tile -- through tail
+    padding (``_FlashPaddedTail``: causal attention never sees the pads; non-causal attention masks
+    keys past S in the kernels, ``kv_valid``)."""
+    return FLASH_READY and D in (64, 128)
 
 
 def model_tile_len(S: int, D: int, hip: bool, dtype: torch.dtype, max_len: int) -> int:
@@ -203,15 +204,16 @@ def _pad_segments(docs: Segments, B: int, S: int, Sp: int) -> Segments:
 
 
 class _FlashPaddedTail(torch.autograd.Function):
-    """Causal flash attention for S not a multiple of the 256-row tile: each row is padded to
+    """Flash attention for S not a multiple of the 256-row tile: each row is padded to
     Sp = ceil(S/256)*256 with zero q/k/v rows at the END.  Exact: under the causal mask no real
-    query (position < S) sees a pad key (position >= S); pad queries' outputs are dropped and their
-    output gradient is zero, so they add nothing to dK/dV; the pads of a packed-document batch form
-    a document of their own.  Costs one copy of qkv / o / do / dqkv per call (about a tenth of the
-    attention time at S ~ 4k) instead of the 3x slower SDPA fallback."""
+    query (position < S) sees a pad key (position >= S); without it the kernels mask every key >= S
+    (``kv_valid``: forward and dQ pass).  Pad queries' outputs are dropped and their output gradient
+    is zero, so they add nothing to dK/dV; the pads of a packed-document batch form a document of
+    their own.  Costs one copy of qkv / o / do / dqkv per call (about a tenth of the attention time at
+    S ~ 4k) instead of the 3x slower SDPA fallback."""
 
     @staticmethod
-    def forward(ctx, qkv, B, S, H, KV, D, window, scale, out_pad=0, grad_pad=0, docs=None):
+    def forward(ctx, qkv, B, S, H, KV, D, window, scale, out_pad=0, grad_pad=0, docs=None, causal=True):
         Sp = -(-S // FLASH_TILE) * FLASH_TILE
         W = qkv.shape[1]
         qkv_p = qkv.new_zeros(B, Sp, W)
@@ -219,20 +221,23 @@ class _FlashPaddedTail(torch.autograd.Function):
         qkv_p = qkv_p.view(B * Sp, W)
         docs_p = _pad_segments(docs, B, S, Sp) if docs is not None else None
         q, k, v = _split(qkv_p, B, Sp, H, KV, D)
-        o_p, lse = ext().flash_fwd(q, k, v, B, Sp, H, KV, D, scale, True, window, 0,
-                                   docs_p.doc_start if docs_p is not None else None)
+        # causal: the pads are invisible to every real query as they are (and masking them would leave
+        # late pad queries under a window with no key at all); non-causal: mask keys >= S in the kernels
+        kv_valid = -1 if causal else S
+        o_p, lse = ext().flash_fwd(q, k, v, B, Sp, H, KV, D, scale, causal, window, 0,
+                                   docs_p.doc_start if docs_p is not None else None, kv_valid)
         HD = H * D
         out = torch.empty(B * S, HD + out_pad, dtype=qkv.dtype, device=qkv.device)[:, :HD]
         out.unflatten(0, (B, S)).copy_(o_p.view(B, Sp, HD)[:, :S])
         ctx.save_for_backward(qkv_p, o_p, lse)
-        ctx.cfg = (B, S, Sp, H, KV, D, window, scale, grad_pad)
+        ctx.cfg = (B, S, Sp, H, KV, D, window, scale, grad_pad, causal)
         ctx.docs = docs_p
         return out
 
     @staticmethod
     def backward(ctx, do):
         qkv_p, o_p, lse = ctx.saved_tensors
-        B, S, Sp, H, KV, D, window, scale, grad_pad = ctx.cfg
+        B, S, Sp, H, KV, D, window, scale, grad_pad, causal = ctx.cfg
         HD, W = H * D, qkv_p.shape[1]
         do_p = do.new_zeros(B, Sp, HD)
         do_p[:, :S].copy_(do.unflatten(0, (B, S)))
@@ -241,11 +246,12 @@ class _FlashPaddedTail(torch.autograd.Function):
         q, k, v = _split(qkv_p, B, Sp, H, KV, D)
         dq, dk, dv = _split(dqkv_p, B, Sp, H, KV, D)
         docs = ctx.docs
-        ext().flash_bwd(q, k, v, o_p, do_p, lse, dq, dk, dv, B, Sp, H, KV, D, scale, True, window,
-                        docs.doc_start if docs is not None else None, docs.doc_end if docs is not None else None)
+        ext().flash_bwd(q, k, v, o_p, do_p, lse, dq, dk, dv, B, Sp, H, KV, D, scale, causal, window,
+                        docs.doc_start if docs is not None else None, docs.doc_end if docs is not None else None,
+                        -1 if causal else S)
         dqkv = torch.empty(B * S, W + grad_pad, dtype=qkv_p.dtype, device=qkv_p.device)[:, :W]
         dqkv.unflatten(0, (B, S)).copy_(dqkv_p.view(B, Sp, W)[:, :S])
-        return dqkv, None, None, None, None, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None, None, None, None, None
 
 
 def attention_packed(qkv: torch.Tensor, B: int, S: int, H: int, KV: int, D: int, causal: bool = True,
@@ -263,7 +269,8 @@ def attention_packed(qkv: torch.Tensor, B: int, S: int, H: int, KV: int, D: int,
         if qkv.dtype == torch.bfloat16 and flash_supported(D, S):
             return _FlashPacked.apply(qkv, B, S, H, KV, D, causal, int(window or 0), scale, out_pad, grad_pad, docs)
         if qkv.dtype == torch.bfloat16 and flash_usable(D, S, causal):
-            return _FlashPaddedTail.apply(qkv, B, S, H, KV, D, int(window or 0), scale, out_pad, grad_pad, docs)
+            return _FlashPaddedTail.apply(qkv, B, S, H, KV, D, int(window or 0), scale, out_pad, grad_pad, docs,
+                                          bool(causal))
         _warn_fallback(f"dtype={qkv.dtype}, head_dim={D}, seq_len={S}, causal={causal}")
     return _sdpa_packed(qkv, B, S, H, KV, D, causal, window, scale, docs)
 

@@ -19,9 +19,11 @@ class _TorchFlash:
     """The kernels' contract in torch (fp64 math)."""
 
     @staticmethod
-    def _mask(B, S, causal, window, doc_start, device):
+    def _mask(B, S, causal, window, doc_start, device, kv_valid=-1):
         i = torch.arange(S, device=device)
         allowed = torch.ones(S, S, dtype=torch.bool, device=device)
+        if 0 < kv_valid < S:  # keys past the valid length are masked for every query
+            allowed &= i[None, :] < kv_valid
         if causal:
             allowed &= i[None, :] <= i[:, None]
         if window:
@@ -32,34 +34,37 @@ class _TorchFlash:
             allowed = allowed & (i[None, None, None, :] >= ds[:, None, :, None])
         return allowed
 
-    def _fwd(self, q, k, v, B, S, H, KV, D, scale, causal, window, doc_start):
+    def _fwd(self, q, k, v, B, S, H, KV, D, scale, causal, window, doc_start, kv_valid=-1):
         qh = q.double().reshape(B, S, H, D).transpose(1, 2)
         kh = k.double().reshape(B, S, KV, D).transpose(1, 2).repeat_interleave(H // KV, 1)
         vh = v.double().reshape(B, S, KV, D).transpose(1, 2).repeat_interleave(H // KV, 1)
         s = (qh @ kh.transpose(-1, -2)) * scale
-        s = s.masked_fill(~self._mask(B, S, causal, window, doc_start, q.device), float("-inf"))
+        s = s.masked_fill(~self._mask(B, S, causal, window, doc_start, q.device, kv_valid), float("-inf"))
         lse = torch.logsumexp(s, -1)
         o = (s - lse[..., None]).exp() @ vh
         return o.transpose(1, 2).reshape(B * S, H * D), lse
 
-    def flash_fwd(self, q, k, v, B, S, H, KV, D, scale, causal, window, out_pad, doc_start):
-        o, lse = self._fwd(q, k, v, B, S, H, KV, D, scale, causal, window, doc_start)
+    def flash_fwd(self, q, k, v, B, S, H, KV, D, scale, causal, window, out_pad, doc_start, kv_valid=-1):
+        o, lse = self._fwd(q, k, v, B, S, H, KV, D, scale, causal, window, doc_start, kv_valid)
         buf = torch.empty(B * S, H * D + out_pad, dtype=q.dtype)[:, :H * D]
         buf.copy_(o)
         return buf, lse.float()
 
-    def flash_bwd(self, q, k, v, o, do, lse, dq, dk, dv, B, S, H, KV, D, scale, causal, window, doc_start, doc_end):
+    def flash_bwd(self, q, k, v, o, do, lse, dq, dk, dv, B, S, H, KV, D, scale, causal, window, doc_start, doc_end,
+                  kv_valid=-1):
         with torch.enable_grad():  # called from inside autograd's backward
             qq, kk, vv = (t.detach().double().requires_grad_(True) for t in (q, k, v))
-            out, _ = self._fwd(qq, kk, vv, B, S, H, KV, D, scale, causal, window, doc_start)
+            out, _ = self._fwd(qq, kk, vv, B, S, H, KV, D, scale, causal, window, doc_start, kv_valid)
             gq, gk, gv = torch.autograd.grad(out, (qq, kk, vv), do.double())
         dq.copy_(gq)
         dk.copy_(gk)
         dv.copy_(gv)
 
 
-@pytest.mark.parametrize("S,window,docs", [(300, 0, False), (1000, 0, False), (300, 64, False), (520, 0, True)])
-def test_padded_tail_matches_reference(monkeypatch, S, window, docs):
+@pytest.mark.parametrize("S,window,docs,causal", [(300, 0, False, True), (1000, 0, False, True), (300, 64, False, True),
+                                                  (520, 0, True, True), (300, 0, False, False),
+                                                  (1000, 0, False, False)])
+def test_padded_tail_matches_reference(monkeypatch, S, window, docs, causal):
     monkeypatch.setattr(A, "ext", lambda: _TorchFlash())
     B, H, KV, D = 2, 4, 2, 64
     torch.manual_seed(0)
@@ -73,10 +78,10 @@ def test_padded_tail_matches_reference(monkeypatch, S, window, docs):
     scale = 1 / math.sqrt(D)
     x1 = qkv.clone().requires_grad_(True)
     out_pad, grad_pad = 64, 32
-    o = A._FlashPaddedTail.apply(x1, B, S, H, KV, D, window, scale, out_pad, grad_pad, seg)
+    o = A._FlashPaddedTail.apply(x1, B, S, H, KV, D, window, scale, out_pad, grad_pad, seg, causal)
     assert o.shape == (B * S, H * D) and o.stride(0) == H * D + out_pad  # spare columns for the LoRA GEMM
     x2 = qkv.clone().requires_grad_(True)
-    ref = A.attention_reference(x2, B, S, H, KV, D, True, window, scale, seg)
+    ref = A.attention_reference(x2, B, S, H, KV, D, causal, window, scale, seg)
     assert torch.allclose(o, ref.double(), atol=2e-5, rtol=1e-4)  # the reference computes in fp32
     g = torch.randn_like(ref)
     o.backward(g.double())
@@ -87,7 +92,7 @@ def test_padded_tail_matches_reference(monkeypatch, S, window, docs):
 def test_flash_usable_policy():
     assert A.flash_supported(128, 4096) and not A.flash_supported(128, 4000)
     assert A.flash_usable(128, 4000, causal=True) and A.flash_usable(64, 77, causal=True)
-    assert not A.flash_usable(128, 4000, causal=False)  # non-causal pads would be attended
+    assert A.flash_usable(128, 4000, causal=False)  # non-causal: the kernels mask the pad keys (kv_valid)
     assert not A.flash_usable(96, 4096, causal=True)
 
 

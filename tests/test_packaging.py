@@ -102,7 +102,7 @@ def test_in_cluster_build_path(tmp_path):
     import yaml
 
     with open(os.path.join(ROOT, "deploy", "openshift", "buildconfigs.yaml")) as f:
-        items = yaml.safe_load(f)["items"]
+        items = [d for d in yaml.safe_load_all(f) if d]
     bcs = {i["metadata"]["name"]: i for i in items if i["kind"] == "BuildConfig"}
     assert set(bcs) == {"ftc-controlplane", "ftc-monitor", "ftc-worker-rocm"}
     for bc in bcs.values():
