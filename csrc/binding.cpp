@@ -44,6 +44,9 @@ int ftc_gemm_nt(const void* a, long long lda, const void* b, long long ldb, void
 int ftc_gemm_nt_pb_ok(const void* a, long long lda, const void* bp, const void* c, long long ldc, int M, int N, int K);
 int ftc_gemm_nt_pb(const void* a, long long lda, const void* bp, void* c, long long ldc, int c_fp32, int M, int N,
                    int K, float alpha, float beta, hipStream_t stream);
+int ftc_gemm_nt_rope(const void* a, long long lda, const void* b, long long ldb, void* c, long long ldc, int M, int N,
+                     int K, const float* cos_t, const float* sin_t, const int* positions, int seq_len, int rot_heads,
+                     hipStream_t stream);
 int ftc_copy2d_batched(const void* jobs, int njobs, long long max_elems, hipStream_t stream);
 int ftc_ce_fwd_bwd(void* logits, const long long* labels, float* loss, float* lse, long long rows, int V, long long ld,
                    float gscale, long long ignore_index, hipStream_t stream);
@@ -416,6 +419,29 @@ void gemm_nt_(at::Tensor& c, const at::Tensor& a, const at::Tensor& b, double al
         "gemm_nt_");
 }
 
+// qkv projection + RoPE epilogue (head_dim 128): c = rope(a b^T) on the first rot_heads heads
+void gemm_nt_rope_(at::Tensor& c, const at::Tensor& a, const at::Tensor& b, const at::Tensor& cos_t,
+                   const at::Tensor& sin_t, const c10::optional<at::Tensor>& positions, int64_t seq_len,
+                   int64_t rot_heads) {
+  TORCH_CHECK(c.scalar_type() == at::kBFloat16 && gemm_nt_ok(c, a, b), "gemm_nt_rope_: GEMM contract (bf16 c)");
+  need(cos_t, at::kFloat, "cos");
+  need(sin_t, at::kFloat, "sin");
+  TORCH_CHECK(cos_t.dim() == 2 && cos_t.size(1) == 64 && cos_t.is_contiguous() && sin_t.sizes() == cos_t.sizes() &&
+              sin_t.is_contiguous(), "gemm_nt_rope_: cos/sin [max_pos, 64] fp32 contiguous (head_dim 128)");
+  const int* pp = nullptr;
+  if (positions.has_value()) {
+    need(*positions, at::kInt, "positions");
+    TORCH_CHECK(positions->numel() == a.size(0) && positions->is_contiguous(), "gemm_nt_rope_: positions [M]");
+    pp = positions->data_ptr<int>();
+  } else {
+    TORCH_CHECK(seq_len > 0 && seq_len <= cos_t.size(0), "gemm_nt_rope_: seq_len within the table");
+  }
+  check(ftc_gemm_nt_rope(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
+                         (int)a.size(0), (int)b.size(0), (int)a.size(1), cos_t.data_ptr<float>(),
+                         sin_t.data_ptr<float>(), pp, (int)seq_len, (int)rot_heads, cur_stream()),
+        "gemm_nt_rope_");
+}
+
 // packed-B form: bp holds B [N, K] in MFMA fragment order ([N/32][K/32][2][64][8], ops/gemm.py pack_b_nt)
 bool gemm_nt_pb_ok(const at::Tensor& c, const at::Tensor& a, const at::Tensor& bp, int64_t N, int64_t K) {
   if (!a.is_cuda() || !bp.is_cuda() || !c.is_cuda() || a.dim() != 2 || c.dim() != 2) return false;
@@ -746,6 +772,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_tn_", &gemm_tn_);
   m.def("gemm_nt_ok", &gemm_nt_ok);
   m.def("gemm_nt_pb_ok", &gemm_nt_pb_ok);
+  m.def("gemm_nt_rope_", &gemm_nt_rope_, py::arg("c"), py::arg("a"), py::arg("b"), py::arg("cos"), py::arg("sin"),
+        py::arg("positions"), py::arg("seq_len"), py::arg("rot_heads"));
   m.def("gemm_nt_pb_", &gemm_nt_pb_, py::arg("c"), py::arg("a"), py::arg("bp"), py::arg("N"), py::arg("K"),
         py::arg("alpha") = 1.0, py::arg("beta") = 0.0);
   m.def("gemm_nt_", &gemm_nt_, py::arg("c"), py::arg("a"), py::arg("b"), py::arg("alpha") = 1.0, py::arg("beta") = 0.0);

@@ -52,6 +52,7 @@ constexpr int NSTAGE = 4;
 
 enum Epi : int {
   EPI_STORE = 0,  // C = alpha acc (+ beta C), bf16 or fp32
+  EPI_ROPE = 1,   // bf16 C = rope(alpha acc) on the q / k heads (the packed qkv projection), beta 0
 };
 
 struct NTArgs {
@@ -61,6 +62,13 @@ struct NTArgs {
   long long lda, ldb, ldc;
   int K, nm, nn, group_m;
   float alpha, beta;
+  // EPI_ROPE (head_dim 128): rotate the first rot_heads 128-column heads of every output row by
+  // (cos, sin)[pos] (fp32 [max_pos, 64], HF rotate_half pairs (i, i + 64)); pos = positions[row] or
+  // row % seq_len
+  const float* cos_t;
+  const float* sin_t;
+  const int* positions;
+  int seq_len, rot_heads;
 };
 
 FTC_DEV int swz(int row) { return (row >> 2) & 2; }
@@ -573,6 +581,72 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4_kernel(NTArgs p) {
   store_wave<F32C, 8, 8>(p, acc, m0 + wm * 128, n0 + wn * 128, lane);
 }
 
+// Epilogue of the head-aligned mapping: lane holds, for m tile mt, columns c0 + 8 kc + [0, 8) (pair 0:
+// acc[mt][0..1]) and c0 + 64 + 8 kc + [0, 8) (pair 1: acc[mt][2..3]), c0 = n0 + 128 (wn >> 1) + 32 (wn & 1).
+template <bool F32C, int EPI>
+FTC_DEV void store_v5(const NTArgs& p, const f32x4 (&acc)[8][4], long long m0, long long n0, int wm, int wn,
+                      int lane) {
+  const int li = lane & 15, kc = lane >> 4;
+  const long long mrow = m0 + wm * 128 + li;
+  const long long c0 = n0 + 128 * (wn >> 1) + 32 * (wn & 1);
+  const long long ncol = c0 + 8 * kc;
+  const bool accumulate = p.beta != 0.f;
+  bool rope = false;
+  if constexpr (EPI == EPI_ROPE) rope = (int)(c0 >> 7) < p.rot_heads;  // wave-uniform
+  const int ri = 32 * (wn & 1) + 8 * kc;  // rotation-pair index of this lane's first column (0..63)
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt) {
+    float v[2][8];
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[pr][j] = p.alpha * acc[mt][2 * pr][j];
+        v[pr][4 + j] = p.alpha * acc[mt][2 * pr + 1][j];
+      }
+    const long long row = mrow + 16 * mt;
+    if constexpr (EPI == EPI_ROPE) {
+      if (rope) {
+        const int pos = p.positions ? p.positions[row] : (int)(row % p.seq_len);
+        const float4* cp = reinterpret_cast<const float4*>(p.cos_t + (long long)pos * 64 + ri);
+        const float4* sp = reinterpret_cast<const float4*>(p.sin_t + (long long)pos * 64 + ri);
+        const float4 c0v = cp[0], c1v = cp[1], s0v = sp[0], s1v = sp[1];
+        const float cs[8] = {c0v.x, c0v.y, c0v.z, c0v.w, c1v.x, c1v.y, c1v.z, c1v.w};
+        const float sn[8] = {s0v.x, s0v.y, s0v.z, s0v.w, s1v.x, s1v.y, s1v.z, s1v.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x1 = v[0][j], x2 = v[1][j];
+          v[0][j] = x1 * cs[j] - x2 * sn[j];
+          v[1][j] = x2 * cs[j] + x1 * sn[j];
+        }
+      }
+    }
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const long long off = row * p.ldc + ncol + 64 * pr;
+      if constexpr (F32C) {
+        float4* cp = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.c) + off);
+        if (accumulate) {
+          const float4 o0 = cp[0], o1 = cp[1];
+          v[pr][0] += p.beta * o0.x; v[pr][1] += p.beta * o0.y; v[pr][2] += p.beta * o0.z; v[pr][3] += p.beta * o0.w;
+          v[pr][4] += p.beta * o1.x; v[pr][5] += p.beta * o1.y; v[pr][6] += p.beta * o1.z; v[pr][7] += p.beta * o1.w;
+        }
+        cp[0] = make_float4(v[pr][0], v[pr][1], v[pr][2], v[pr][3]);
+        cp[1] = make_float4(v[pr][4], v[pr][5], v[pr][6], v[pr][7]);
+      } else {
+        uint4* cp = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(p.c) + off);
+        if (accumulate) {
+          float o[8];
+          unpack8(*cp, o);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[pr][j] += p.beta * o[j];
+        }
+        *cp = pack8(v[pr]);
+      }
+    }
+  }
+}
+
 // ---- variant 5 (default): 64-deep super-stages, full 128-byte lines per DMA row --------------------------
 // rocprofv3 on variants 1-4 (profiles/r3/gemm_nt.md): the texture addresser was 95 % busy (hipBLASLt:
 // 60 %) -- with 32-deep tiles every DMA row is a 64-byte HALF line, so a 1 KiB piece touches 16 cache
@@ -588,7 +662,10 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4_kernel(NTArgs p) {
 //   even t: vmcnt(0) (super-stage t/2+1 landed) + lgkmcnt(0) + barrier.
 FTC_DEV int f5(int r) { return (r & 1) | (r & 2) | ((r >> 1) & 4); }
 
-template <bool F32C>
+// Column mapping: wave wn owns columns 128 (wn >> 1) + 32 (wn & 1) + [0, 32) and the same + 64 -- the two
+// halves of one 128-wide head that HF's rotate_half pairs up -- so a RoPE epilogue finds both elements
+// of every rotation pair in one lane, one register apart.
+template <bool F32C, int EPI = EPI_STORE>
 __global__ __launch_bounds__(512, 1) void gemm_nt_v5_kernel(NTArgs p) {
   constexpr int IMG2 = 256 * 64 * 2;  // one operand image of a super-stage: 32 KiB
   constexpr int SS = 2 * IMG2;        // super-stage: A | B
@@ -631,14 +708,14 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_v5_kernel(NTArgs p) {
   int a_off[2], b_off[2];
   {
     const int ra_ = wm * 128 + li;
-    const int rb_ = wn * 64 + 8 * (li >> 2) + (li & 3);
+    const int rb_ = 128 * (wn >> 1) + 32 * (wn & 1) + 8 * (li >> 2) + (li & 3);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       a_off[h] = ra_ * 128 + 16 * ((4 * h + kc) ^ f5(li));
       b_off[h] = IMG2 + rb_ * 128 + 16 * ((4 * h + kc) ^ f5(rb_));
     }
   }
-  auto bnt = [](int nt) { return (32 * (nt >> 1) + 4 * (nt & 1)) * 128; };
+  auto bnt = [](int nt) { return (64 * (nt >> 1) + 4 * (nt & 1)) * 128; };
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -689,7 +766,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_v5_kernel(NTArgs p) {
     iter(t + 1, std::true_type{}, yb, xb);
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no DMA may land in LDS after the workgroup ends
-  store_tile<F32C>(p, acc, m0, n0, wm, wn, lane);
+  store_v5<F32C, EPI>(p, acc, m0, n0, wm, wn, lane);
 }
 
 // ---- variant 0: ping-pong ---------------------------------------------------------------------------
@@ -876,5 +953,25 @@ extern "C" int ftc_gemm_nt_pb(const void* a, long long lda, const void* bp, void
     hipLaunchKernelGGL((gemm_nt_pb_kernel<false, 3>), dim3(grid), dim3(512), 0, stream, p);
   else
     hipLaunchKernelGGL((gemm_nt_pb_kernel<false>), dim3(grid), dim3(512), 0, stream, p);
+  return (int)hipGetLastError();
+}
+
+// qkv projection with RoPE fused into the epilogue: c[M, N] bf16 = rope(a b^T) on the first rot_heads
+// 128-wide heads (q then k), the rest (v) stored as is.  cos / sin: fp32 [max_pos, 64]; positions: int32
+// [M] or null (row % seq_len).
+extern "C" int ftc_gemm_nt_rope(const void* a, long long lda, const void* b, long long ldb, void* c, long long ldc,
+                                int M, int N, int K, const float* cos_t, const float* sin_t, const int* positions,
+                                int seq_len, int rot_heads, hipStream_t stream) {
+  if (!ftc_gemm_nt_ok(a, lda, b, ldb, c, ldc, 0, M, N, K)) return -1;
+  if (!cos_t || !sin_t || (reinterpret_cast<uintptr_t>(cos_t) | reinterpret_cast<uintptr_t>(sin_t)) & 15) return -1;
+  if (!positions && seq_len <= 0) return -1;
+  if (rot_heads < 0 || rot_heads * 128 > N) return -1;
+  static const int group_m = [] {
+    const char* e = getenv("FTC_GEMM_NT_GROUP");
+    return e ? atoi(e) : 4;
+  }();
+  NTArgs p{(const uint16_t*)a, (const uint16_t*)b, c, lda, ldb, ldc, K, M / BM, N / BN, group_m > 0 ? group_m : 4,
+           1.f, 0.f, cos_t, sin_t, positions, seq_len, rot_heads};
+  hipLaunchKernelGGL((gemm_nt_v5_kernel<false, EPI_ROPE>), dim3(p.nm * p.nn), dim3(512), 0, stream, p);
   return (int)hipGetLastError();
 }

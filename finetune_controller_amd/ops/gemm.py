@@ -54,3 +54,31 @@ def gemm_nt_packed(a: torch.Tensor, bp: torch.Tensor, N: int, out: torch.Tensor 
         ref += beta * out.float()
     out.copy_(ref)
     return out
+
+
+# ---- routing of the projection GEMMs: hand-written kernel vs hipBLASLt ---------------------------------
+# FTC_GEMM_NT: "0" -- hipBLASLt everywhere; "1" -- the gfx950 kernel wherever its contract holds;
+# "auto" (default) -- the kernel only for the (N, K) shapes listed in NT_WINS, i.e. where an interleaved
+# A/B on the MI355X measured it faster than hipBLASLt (tools/bench_gemm_nt.py, profiles/r3/gemm_nt.md).
+NT_WINS: set[tuple[int, int]] = set()
+
+
+def _nt_mode() -> str:
+    import os
+
+    return os.environ.get("FTC_GEMM_NT", "auto")
+
+
+def mm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor) -> bool:
+    """``out = a @ b^T`` (a [M, K], b [N, K] row views, K contiguous) on the hand-written kernel when the
+    routing policy picks it for this shape; False (nothing done) otherwise -- the caller then runs its
+    library GEMM."""
+    mode = _nt_mode()
+    if mode == "0" or not use_hip(a):
+        return False
+    if mode != "1" and (b.shape[0], b.shape[1]) not in NT_WINS:
+        return False
+    if not ext().gemm_nt_ok(out, a, b):
+        return False
+    ext().gemm_nt_(out, a, b, 1.0, 0.0)
+    return True

@@ -40,6 +40,7 @@ import weakref
 import torch
 
 from ._backend import ext, use_hip
+from .gemm import mm_nt
 
 _GRAD_READY_HOOK = None  # set by parallel.ddp to learn when a main_grad was written
 
@@ -540,7 +541,8 @@ class _LoRALinearFn(torch.autograd.Function):
             if not take_prefilled("fwd", x2, aug):
                 tail_product(x2, K, Rp, aug.big[N:, :K], aug.nct)
             xa = _tail(x2, K, aug.R)  # = s * x A^T
-            torch.mm(_wide(x2, K + Rp), aug.big[:N].t(), out=y)
+            if not mm_nt(_wide(x2, K + Rp), aug.big[:N], y):
+                torch.mm(_wide(x2, K + Rp), aug.big[:N].t(), out=y)
         else:
             if bias is None:
                 torch.mm(x2, W.t(), out=y)
@@ -588,7 +590,11 @@ class _LoRALinearFn(torch.autograd.Function):
                 tail_product(dy2, N, Rp, aug.bwd_tail_operand(A, B, s), aug.nct)
             dyb = _tail(dy2, N, aug.R)
             rhs = aug.bwd_operand() if _TN_BWD else aug.big[:, :aug.K]
-            dx = torch.mm(_wide(dy2, N + Rp), rhs).view(ctx.shp)
+            dx = torch.empty(dy2.shape[0], aug.K, dtype=dy2.dtype, device=dy2.device)
+            # rhs^T = bigT [K, N+Rp] row-major: the hand-written NT kernel's K-contiguous B operand
+            if not (_TN_BWD and mm_nt(_wide(dy2, N + Rp), rhs.t(), dx)):
+                torch.mm(_wide(dy2, N + Rp), rhs, out=dx)
+            dx = dx.view(ctx.shp)
         else:
             if A is not None and (need_x or need_a):
                 dyb = dy2 @ B  # [T, R]

@@ -66,16 +66,24 @@ def _a2a(send: torch.Tensor, group) -> torch.Tensor:
 
 
 def _tokens_to_heads(qkv: torch.Tensor, B: int, Sl: int, H: int, KV: int, D: int, sp: SeqGroup) -> torch.Tensor:
-    """[B*Sl, (H+2KV) D] (row view; extra columns ignored) -> [B*P*Sl, (H/P + 2 KV/P) D] contiguous."""
+    """[B*Sl, (H+2KV) D] (row view; extra columns ignored) -> [B*P*Sl, (H/P + 2 KV/P) D] contiguous.
+
+    The send buffer is filled by three strided copies straight from the projection output (one pass
+    over qkv, no concatenation temporary); with B == 1 the received [P(src), Sl, C, D] buffer already is
+    the token-major [P*Sl, C*D] row layout the flash kernels read, so it is returned without a copy."""
     P = sp.size
     Hp, KVp = H // P, KV // P
+    C = Hp + 2 * KVp
     x = qkv[:, :(H + 2 * KV) * D]
-    q = x[:, :H * D].reshape(B, Sl, P, Hp, D)
-    k = x[:, H * D:(H + KV) * D].reshape(B, Sl, P, KVp, D)
-    v = x[:, (H + KV) * D:].reshape(B, Sl, P, KVp, D)
-    send = torch.cat([q, k, v], dim=3).permute(2, 0, 1, 3, 4).contiguous()  # [P, B, Sl, C, D]
+    send = torch.empty(P, B, Sl, C, D, dtype=qkv.dtype, device=qkv.device)
+    sv = send.permute(1, 2, 0, 3, 4)  # [B, Sl, P, C, D] view of the send buffer
+    sv[:, :, :, :Hp].copy_(x[:, :H * D].reshape(B, Sl, P, Hp, D))
+    sv[:, :, :, Hp:Hp + KVp].copy_(x[:, H * D:(H + KV) * D].reshape(B, Sl, P, KVp, D))
+    sv[:, :, :, Hp + KVp:].copy_(x[:, (H + KV) * D:].reshape(B, Sl, P, KVp, D))
     recv = _a2a(send, sp.group)                                                 # [P(src), B, Sl, C, D]
-    return recv.permute(1, 0, 2, 3, 4).reshape(B * P * Sl, (Hp + 2 * KVp) * D)
+    if B == 1:
+        return recv.view(P * Sl, C * D)
+    return recv.permute(1, 0, 2, 3, 4).reshape(B * P * Sl, C * D)
 
 
 def _heads_to_tokens_qkv(g: torch.Tensor, B: int, Sl: int, H: int, KV: int, D: int, sp: SeqGroup) -> torch.Tensor:
@@ -95,7 +103,9 @@ def _heads_to_tokens_qkv(g: torch.Tensor, B: int, Sl: int, H: int, KV: int, D: i
 def _heads_to_tokens(a: torch.Tensor, B: int, Sl: int, nh: int, D: int, sp: SeqGroup) -> torch.Tensor:
     """Attention output [B*P*Sl, nh/P D] -> [B*Sl, nh D] (this rank's tokens, every head)."""
     P = sp.size
-    send = a.reshape(B, P, Sl, nh // P, D).permute(1, 0, 2, 3, 4).contiguous()
+    # B == 1: the output rows already are [P(dst tokens), Sl, ...] -- sent as they are
+    send = a.reshape(B, P, Sl, nh // P, D).permute(1, 0, 2, 3, 4)
+    send = send.contiguous() if B > 1 else send.reshape(P, 1, Sl, nh // P, D)
     recv = _a2a(send, sp.group)                                          # [P(src heads), B, Sl, nh/P, D]
     return recv.permute(1, 2, 0, 3, 4).reshape(B * Sl, nh * D)
 

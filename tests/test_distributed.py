@@ -288,9 +288,9 @@ def test_resume_rejects_foreign_parameter_set(tmp_path):
 
 
 # --------------------------------------------------------------------------- Ulysses sequence parallelism
-def _sp_worker(rank, world, port, tmp, q, method, window_model, doc_len):
+def _sp_worker(rank, world, port, tmp, q, method, window_model, doc_len, batch=2):
     _rank_env(rank, world, port, tmp)
-    tc = TrainConfig(model=window_model, method=method, batch_size=2, seq_len=64, synthetic=True, max_steps=1,
+    tc = TrainConfig(model=window_model, method=method, batch_size=batch, seq_len=64, synthetic=True, max_steps=1,
                      checkpoint_path=tmp, resume=False, device="cpu", dtype="fp32", lr=0.0, max_grad_norm=0.0,
                      save_model=False, sp=world, bucket_mb=0.05, synthetic_doc_len=doc_len, eval_batches=2)
     tr = Trainer(tc)
@@ -302,17 +302,19 @@ def _sp_worker(rank, world, port, tmp, q, method, window_model, doc_len):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("method,model,doc_len", [("full", "llama-tiny", 0), ("lora", "llama-tiny", 0),
-                                                  ("full", "mistral-tiny", 0), ("full", "llama-tiny", 40)])
-def test_sequence_parallel_matches_single_process(tmp_path, method, model, doc_len):
+@pytest.mark.parametrize("method,model,doc_len,batch", [("full", "llama-tiny", 0, 2), ("lora", "llama-tiny", 0, 2),
+                                                        ("full", "mistral-tiny", 0, 2), ("full", "llama-tiny", 40, 2),
+                                                        ("lora", "llama-tiny", 0, 1)])
+def test_sequence_parallel_matches_single_process(tmp_path, method, model, doc_len, batch):
     """Ulysses SP over 2 gloo ranks (each holds half of every sequence; attention all-to-alls heads <->
     tokens) against one process training the same full sequences: the mean of the ranks' losses and the
     all-reduced gradient equal the single-process loss / gradient (fp32, sliding window included), also
     when masked labels leave the two halves different valid-token counts (doc_len 40: the document
-    boundary's masked label falls in the second half only), and the held-out loss matches."""
+    boundary's masked label falls in the second half only), and the held-out loss matches.  batch 1
+    takes the all-to-all path without the token-major reorder copies."""
     world = 2
-    res = _run_ranks(_sp_worker, world, tmp_path, method, model, doc_len)
-    tc = TrainConfig(model=model, method=method, batch_size=2, seq_len=64, synthetic=True, max_steps=1,
+    res = _run_ranks(_sp_worker, world, tmp_path, method, model, doc_len, batch)
+    tc = TrainConfig(model=model, method=method, batch_size=batch, seq_len=64, synthetic=True, max_steps=1,
                      checkpoint_path=str(tmp_path), resume=False, device="cpu", dtype="fp32", lr=0.0,
                      max_grad_norm=0.0, save_model=False, synthetic_doc_len=doc_len, eval_batches=2)
     tr = Trainer(tc)

@@ -316,6 +316,28 @@ def test_gemm_nt_packed(C, cdtype, M, N, K, pad, beta):
     torch.testing.assert_close(c.float(), ref, atol=tol, rtol=1e-2 if cdtype == torch.bfloat16 else 1e-4)
 
 
+@pytest.mark.parametrize("with_pos", [False, True])
+def test_gemm_nt_rope_epilogue(C, with_pos):
+    """qkv projection with RoPE fused into the GEMM epilogue (head_dim 128, q and k heads rotated, v not)
+    vs the fp32 product rotated by the reference RoPE."""
+    from finetune_controller_amd.ops.rope import RotaryTable, _rope_ref
+
+    torch.manual_seed(5)
+    H, KV, D, S = 4, 2, 128, 256
+    M, K = 512, 320
+    N = (H + 2 * KV) * D
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    w = (torch.rand(N, K, device=DEV) * 2 - 1).to(torch.bfloat16)
+    tab = RotaryTable(D, 1024, 500000.0)
+    cos, sin = tab.get(DEV)
+    pos = (torch.arange(M, device=DEV, dtype=torch.int32) * 7 % 1000) if with_pos else None
+    c = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    C.gemm_nt_rope_(c, a, w, cos, sin, pos, S, H + KV)
+    ref = _rope_ref((a.float() @ w.float().t()), cos, sin, H + KV, D, S, pos, False)
+    tol = 2e-2 * (K ** 0.5) / 8
+    torch.testing.assert_close(c.float(), ref, atol=tol, rtol=1e-2)
+
+
 def test_gemm_nt_rejects(C):
     a = torch.zeros(256, 40, device=DEV, dtype=torch.bfloat16)  # K not a multiple of 32
     b = torch.zeros(256, 40, device=DEV, dtype=torch.bfloat16)
