@@ -120,7 +120,7 @@ class LlamaLayer(nn.Module):
                 out.append(AugProj(aw, pair))
         return tuple(out)
 
-    def proj(self, name: str, x: torch.Tensor) -> torch.Tensor:
+    def proj(self, name: str, x: torch.Tensor, rope: tuple | None = None) -> torch.Tensor:
         pair = self.lora[name] if name in self.lora else None
         qw = self.qweights.get(name)
         if qw is not None:
@@ -133,7 +133,7 @@ class LlamaLayer(nn.Module):
         if pair is None:
             return ops.lora_linear(x, W)
         return ops.lora_linear(x, W, pair.A, pair.B, pair.scale, blocks=pair.blocks, aug=self.aug.get(name),
-                               dropout=pair.dropout if self.training else 0.0)
+                               dropout=pair.dropout if self.training else 0.0, rope=rope)
 
     def forward(self, h, delta, rope: ops.RotaryTable, B: int, S: int, positions=None, docs=None, kv=None):
         cfg = self.cfg
@@ -141,8 +141,17 @@ class LlamaLayer(nn.Module):
         # grad_pad: delta came from the previous layer's down projection (same LoRA shape in every layer;
         # a pad that is too small just falls back to the two-GEMM backward)
         h, x = ops.add_rms_norm(h, delta, self.attn_norm, cfg.norm_eps, pad=p_qkv, grad_pad=p_down)
-        qkv = self.proj("qkv", x)
-        qkv = ops.apply_rope_packed(qkv, rope, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, S, positions)
+        # RoPE inside the qkv projection (fused into the GEMM epilogue where the hand-written kernel runs
+        # it) for the LoRA GPU path; elsewhere the separate in-place op
+        rargs = None
+        if ("qkv" in self.lora and "qkv" not in self.qweights and ops.use_hip(x) and x.dtype == torch.bfloat16
+                and cfg.head_dim == 128 and x.dim() == 2):
+            cos, sin = rope.get(x.device)
+            pos = positions.to(torch.int32).contiguous() if positions is not None else None
+            rargs = (cos, sin, pos, S, cfg.n_heads + cfg.n_kv_heads, cfg.head_dim)
+        qkv = self.proj("qkv", x, rope=rargs)
+        if rargs is None:
+            qkv = ops.apply_rope_packed(qkv, rope, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, S, positions)
         if kv is not None and kv[0].decoding:  # generation: one new token per sequence vs its cache
             cache, li = kv
             a = ops.decode_attention(qkv, cache.k[li], cache.v[li], cache.lens_next, cache.attend_len(),

@@ -82,3 +82,30 @@ def mm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor) -> bool:
         return False
     ext().gemm_nt_(out, a, b, 1.0, 0.0)
     return True
+
+
+def mm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """``a @ b`` for the projection GEMMs: when ``b`` is the transpose of a K-contiguous [N, K] matrix
+    (a weight ``W.t()`` or the TN copy's view) the routing policy may send it to the hand-written
+    kernel; otherwise / on fallback ``torch.mm`` (hipBLASLt)."""
+    if out is None:
+        out = torch.empty(a.shape[0], b.shape[1], dtype=a.dtype, device=a.device)
+    bt = b.t()
+    if bt.dim() == 2 and bt.stride(1) == 1 and mm_nt(a, bt, out):
+        return out
+    return torch.mm(a, b, out=out)
+
+
+def rope_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, rope: tuple) -> bool:
+    """``out = rope(a @ b^T)`` with the rotation in the hand-written kernel's epilogue (head_dim 128), when
+    the routing policy picks the kernel for this shape; False (nothing done) otherwise."""
+    cos, sin, pos, seq_len, n_rot, hd = rope
+    mode = _nt_mode()
+    if hd != 128 or mode == "0" or not use_hip(a) or out.dtype != torch.bfloat16:
+        return False
+    if mode != "1" and (b.shape[0], b.shape[1]) not in NT_WINS:
+        return False
+    if not ext().gemm_nt_ok(out, a, b) or cos.shape[-1] != 64:
+        return False
+    ext().gemm_nt_rope_(out, a, b, cos, sin, pos, seq_len, n_rot)
+    return True

@@ -40,7 +40,7 @@ import weakref
 import torch
 
 from ._backend import ext, use_hip
-from .gemm import mm_nt
+from .gemm import mm_nt, rope_nt
 
 _GRAD_READY_HOOK = None  # set by parallel.ddp to learn when a main_grad was written
 
@@ -516,7 +516,7 @@ def lora_weight_grads(direct, dy2, xa, xa_scaled, dyb, xin, s, blocks, need_a, n
 
 class _LoRALinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, W, bias, A, B, scale, blocks, aug, p_drop=0.0):
+    def forward(ctx, x, W, bias, A, B, scale, blocks, aug, p_drop=0.0, rope=None):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
         mask = None
@@ -526,6 +526,7 @@ class _LoRALinearFn(torch.autograd.Function):
             mask = torch.rand(x2.shape, device=x2.device, dtype=torch.float32) >= p_drop
             aug = None
         N, K = W.shape
+        rope_of = rope
         # allocate the output in its final shape: the returned tensor must not be a view (RoPE
         # rotates it in place downstream)
         out = torch.empty(*shp[:-1], N, dtype=x.dtype, device=x.device)
@@ -541,7 +542,9 @@ class _LoRALinearFn(torch.autograd.Function):
             if not take_prefilled("fwd", x2, aug):
                 tail_product(x2, K, Rp, aug.big[N:, :K], aug.nct)
             xa = _tail(x2, K, aug.R)  # = s * x A^T
-            if not mm_nt(_wide(x2, K + Rp), aug.big[:N], y):
+            if rope is not None and rope_nt(_wide(x2, K + Rp), aug.big[:N], y, rope):
+                rope = None  # RoPE applied in the GEMM epilogue (csrc/kernels/gemm_nt.hip EPI_ROPE)
+            elif not mm_nt(_wide(x2, K + Rp), aug.big[:N], y):
                 torch.mm(_wide(x2, K + Rp), aug.big[:N].t(), out=y)
         else:
             if bias is None:
@@ -563,6 +566,10 @@ class _LoRALinearFn(torch.autograd.Function):
         ctx.scale, ctx.blocks, ctx.shp, ctx.has_bias, ctx.aug = scale, blocks, shp, bias is not None, aug
         ctx.aug_fwd = use_aug  # saved xa is s * x A^T
         ctx.mask, ctx.p_drop = mask, p_drop
+        ctx.rope = rope_of  # the rotation the backward undoes on dy
+        if rope is not None:  # not fused into the GEMM: rotate the output in place (csrc/kernels/elementwise.hip)
+            cos, sin, pos, seq_len, n_rot, hd = rope
+            ext().rope_(y, cos, sin, pos, n_rot, hd, seq_len, False)
         # trainable A/B homed in a flat grad buffer (FlatAdamW sets .main_grad): their weight
         # gradients are accumulated in place by beta=1 GEMMs instead of returned (no temporaries, no
         # scale / accumulate kernels).  Block-masked packed pairs keep the returned-gradient path.
@@ -571,6 +578,12 @@ class _LoRALinearFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        if ctx.rope is not None:
+            # output was rope(x W^T ...): the gradient of the un-rotated product is the inverse rotation
+            cos, sin, pos, seq_len, n_rot, hd = ctx.rope
+            if dy.dim() != 2 or dy.stride(1) != 1 or dy.stride(0) % 8:
+                dy = dy.reshape(-1, dy.shape[-1]).contiguous()
+            ext().rope_(dy, cos, sin, pos, n_rot, hd, seq_len, True)
         x2, W, A, B, xa = ctx.saved_tensors
         if W is None:
             W = ctx.W
@@ -628,10 +641,14 @@ class _LoRALinearFn(torch.autograd.Function):
                 dyb = dy2 @ B
             xin = x2 if ctx.mask is None else x2 * ctx.mask / (1.0 - ctx.p_drop)
             dA, dB = lora_weight_grads(ctx.lora_params, dy2, xa, xa_scaled, dyb, xin, s, ctx.blocks, need_a, need_bb)
-        return dx, dW, db, dA, dB, None, None, None, None
+        return dx, dW, db, dA, dB, None, None, None, None, None
 
 
 def lora_linear(x: torch.Tensor, W: torch.Tensor, A: torch.Tensor | None = None, B: torch.Tensor | None = None,
                 scale: float = 1.0, bias: torch.Tensor | None = None, blocks=None,
-                aug: AugWeight | None = None, dropout: float = 0.0) -> torch.Tensor:
-    return _LoRALinearFn.apply(x, W, bias, A, B, scale, blocks, aug, float(dropout))
+                aug: AugWeight | None = None, dropout: float = 0.0, rope: tuple | None = None) -> torch.Tensor:
+    """``rope`` (GPU, bf16, 2-D x): ``(cos, sin, positions int32 | None, seq_len, n_rot_heads, head_dim)`` --
+    the output's first n_rot heads are rotated (RoPE, HF rotate_half) inside the op: in the GEMM epilogue
+    when the hand-written kernel runs the projection, else in place right after it; the backward undoes
+    the rotation on the incoming gradient."""
+    return _LoRALinearFn.apply(x, W, bias, A, B, scale, blocks, aug, float(dropout), rope)

@@ -29,6 +29,7 @@ import os
 import torch
 
 from ._backend import ext, use_hip
+from .gemm import mm as gemm_mm
 from .linear import _accum_xty, _grad_ready, _spare_cols, _tail, _wide, tail_product, tn_backward
 
 _OFF = os.environ.get("FTC_FUSED_MLP", "1") == "0"  # A/B switch: unfused composition
@@ -138,12 +139,12 @@ class _LoRAMLPFn(torch.autograd.Function):
         F, d = dn_p.K, dn_p.N
         # 1. gate|up projection, LoRA folded in through x's spare columns
         tail_product(x2, K, gu_p.Rp, gu_p.fwd_tail(), gu_p.nct)
-        gu = torch.mm(_wide(x2, K + gu_p.Rp), gu_p.fwd_weight().t())
+        gu = gemm_mm(_wide(x2, K + gu_p.Rp), gu_p.fwd_weight().t())
         # 2. SwiGLU + s h A_down^T into h's spare columns
         h = ext().swiglu_fwd_lora(gu, dn_p.Rp, dn_p.fwd_tail(), dn_p.nct)
         # 3. down projection
         y = torch.empty(*x.shape[:-1], d, dtype=x.dtype, device=x.device)
-        torch.mm(_wide(h, F + dn_p.Rp), dn_p.fwd_weight().t(), out=y.view(T, d))
+        gemm_mm(_wide(h, F + dn_p.Rp), dn_p.fwd_weight().t(), out=y.view(T, d))
         ctx.save_for_backward(x2, gu, h)
         ctx.params = (A_gu, B_gu, A_dn, B_dn)
         ctx.proj, ctx.shp = (gu_p, dn_p), x.shape
@@ -164,7 +165,7 @@ class _LoRAMLPFn(torch.autograd.Function):
         # 4. dy B_down into dy's spare columns, dh through the augmented (TN) operand
         tail_product(dy2, d, dn_p.Rp, dn_p.bwd_tail(), dn_p.nct)
         dyb_dn = _tail(dy2, d, dn_p.R)
-        dh = torch.mm(_wide(dy2, d + dn_p.Rp), dn_p.bwd_weight())
+        dh = gemm_mm(_wide(dy2, d + dn_p.Rp), dn_p.bwd_weight())
         # 5. dB_down += dy^T (s h A_down^T)
         _accum_xty(B_dn.main_grad, dy2, _tail(h, F, dn_p.R), 1.0)
         _grad_ready(B_dn)
@@ -176,7 +177,7 @@ class _LoRAMLPFn(torch.autograd.Function):
         # 7. dx and dA_gu += s x^T (dgu B_gu)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(_wide(dgu, N + gu_p.Rp), gu_p.bwd_weight()).view(ctx.shp)
+            dx = gemm_mm(_wide(dgu, N + gu_p.Rp), gu_p.bwd_weight()).view(ctx.shp)
         _accum_xty(A_gu.main_grad.t(), x2, _tail(dgu, N, gu_p.R), gu_p.s)
         _grad_ready(A_gu)
         return dx, None, None, None, None, None, None
