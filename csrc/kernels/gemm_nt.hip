@@ -665,7 +665,12 @@ FTC_DEV int f5(int r) { return (r & 1) | (r & 2) | ((r >> 1) & 4); }
 // Column mapping: wave wn owns columns 128 (wn >> 1) + 32 (wn & 1) + [0, 32) and the same + 64 -- the two
 // halves of one 128-wide head that HF's rotate_half pairs up -- so a RoPE epilogue finds both elements
 // of every rotation pair in one lane, one register apart.
-template <bool F32C, int EPI = EPI_STORE>
+// MODE (FTC_GEMM_NT_V5_MODE): bit 0 skips the DMA wait and bit 1 the loop's DMA (diagnostics: garbage
+// results); bit 2 issues an odd iteration's 8 DMA pieces up front instead of one per MFMA group (real);
+// bit 3 stages through registers instead of LDS-DMA (real): odd iteration t loads super-stage
+// (t+3)/2 into 8 x 16 B per lane, even iteration t+1 ds_writes them (the stage is dead by then) before
+// its barrier.
+template <bool F32C, int EPI = EPI_STORE, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void gemm_nt_v5_kernel(NTArgs p) {
   constexpr int IMG2 = 256 * 64 * 2;  // one operand image of a super-stage: 32 KiB
   constexpr int SS = 2 * IMG2;        // super-stage: A | B
@@ -724,6 +729,16 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_v5_kernel(NTArgs p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   bf16x8 fa[8], xb[4], yb[4];
+  constexpr bool RS = (MODE & 8) != 0;
+  u32x4 rs[RS ? 8 : 1];
+  auto rs_load = [&](int ss_src, int j) __attribute__((always_inline)) {
+    const int op = j >> 2, sub = j & 3;
+    return buf_load16(op ? rb : ra, vo[op][sub & 1], ss_src * 128 + sub * (op ? s8b : s8a));
+  };
+  auto rs_store = [&](int ss_dst, int j, const u32x4& v) __attribute__((always_inline)) {
+    const int op = j >> 2, sub = j & 3;
+    *reinterpret_cast<u32x4*>(ddst + (ss_dst & 1) * SS + op * IMG2 + sub * 1024 + lane * 16) = v;
+  };
 
   // ODD: compile-time parity of t (the loop is unrolled by 2)
   auto iter = [&](int t, auto odd_c, const bf16x8 (&cb)[4], bf16x8 (&nb_)[4]) __attribute__((always_inline)) {
@@ -732,29 +747,64 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_v5_kernel(NTArgs p) {
     const char* st = S + ((tn >> 1) & 1) * SS;
     const int h = ODD ? 0 : 1;  // tn & 1
     const int dsrc = min((t + 3) >> 1, ns - 1), ddst_ss = (t + 3) >> 1;
+    if constexpr (ODD && (MODE & 4) && !(MODE & 2)) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) piece(dsrc, ddst_ss, j);
+    }
 #pragma unroll
     for (int mt = 0; mt < 8; ++mt) {
+      if constexpr (MODE & 32) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cb[nt], fa[mt], acc[mt][nt], 0, 0, 0);
+      if constexpr (MODE & 32) __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);  // the MFMAs read fa[mt] before it is reloaded (same registers)
       fa[mt] = rd(st, a_off[h] + mt * 2048);
       if (mt < 4) nb_[mt] = rd(st, b_off[h] + bnt(mt));
-      if constexpr (ODD) piece(dsrc, ddst_ss, mt);
+      if constexpr (RS) {
+        if constexpr (ODD)
+          rs[mt] = rs_load(dsrc, mt);
+        else
+          rs_store((t + 2) >> 1, mt, rs[mt]);  // super-stage t/2+1 (past the end: a dead stage)
+      } else if constexpr (ODD && (MODE & 16)) {
+        // the two waves of a SIMD (wm 0 / 1) issue their pieces in different halves of the iteration, so
+        // one wave's DMA issue never coincides with its partner's
+        if ((mt >> 2) == wm) {
+          piece(dsrc, ddst_ss, 2 * (mt & 3));
+          piece(dsrc, ddst_ss, 2 * (mt & 3) + 1);
+        }
+      } else if constexpr (ODD && !(MODE & 6)) {
+        piece(dsrc, ddst_ss, mt);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (!ODD) {
-      __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) + lgkmcnt(0): super-stage t/2+1 landed, reads done
+      if constexpr (MODE & 1)
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only
+      else
+        __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) + lgkmcnt(0): super-stage t/2+1 landed, reads done
       barrier();
     }
   };
 
   // prologue: super-stages 0 and 1 in flight, wait for 0
+  if constexpr (RS) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) piece(0, 0, j);
+    for (int j = 0; j < 8; ++j) rs[j] = rs_load(0, j);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) piece(min(1, ns - 1), 1, j);
-  __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8)
+    for (int j = 0; j < 8; ++j) rs_store(0, j, rs[j]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) rs[j] = rs_load(min(1, ns - 1), j);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) rs_store(1, j, rs[j]);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) piece(0, 0, j);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) piece(min(1, ns - 1), 1, j);
+    __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8)
+  }
   barrier();
 #pragma unroll
   for (int mt = 0; mt < 8; ++mt) fa[mt] = rd(S, a_off[0] + mt * 2048);
@@ -767,6 +817,127 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_v5_kernel(NTArgs p) {
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no DMA may land in LDS after the workgroup ends
   store_v5<F32C, EPI>(p, acc, m0, n0, wm, wn, lane);
+}
+
+// ---- variant 6: one wave per SIMD, 128 x 128 per wave, 64-deep super-stages, register staging ---------
+// The 8-wave kernels pay ~17 % for moving operands into LDS even once the texture addresser is relieved
+// (variant 5 with the loop's DMA removed: 1.59-1.63 PF, above hipBLASLt).  Here 4 waves own 128 x 128 each
+// (256 accumulators in AGPRs): a fragment read feeds 8 MFMAs, per 64-deep super-stage a wave issues 16
+// global_load_dwordx4 (odd iteration) and 16 ds_write_b128 (even iteration) into the shadows of 128
+// MFMAs -- a register-staging load issues in a few cycles where an LDS-DMA piece would stall the lone
+// wave ~60-185 cycles.  Same 128-byte-row image and swizzle as variant 5.
+template <bool F32C>
+__global__ __launch_bounds__(256, 1) void gemm_nt_w4s_kernel(NTArgs p) {
+  constexpr int IMG2 = 256 * 64 * 2;
+  constexpr int SS = 2 * IMG2;
+  __shared__ __attribute__((aligned(16))) char S[2 * SS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  int mb, nb;
+  tile_of(p, mb, nb);
+  const long long m0 = (long long)mb * BM, n0 = (long long)nb * BN;
+  const int nk = p.K / BK;
+  const int ns = nk >> 1;
+
+  // staging: wave w fills rows [64 w, 64 w + 64) of both images: 8 pieces of 8 rows x 128 B per operand
+  int vo[2][2];
+  {
+    const int rr = lane >> 3, pc = lane & 7;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int lc = pc ^ f5(rr + 8 * q);
+      vo[0][q] = (int)(((64 * wave + rr) * p.lda + 8 * lc) * 2);
+      vo[1][q] = (int)(((64 * wave + rr) * p.ldb + 8 * lc) * 2);
+    }
+  }
+  const int s8a = (int)(8 * p.lda * 2), s8b = (int)(8 * p.ldb * 2);
+  const auto ra = make_rsrc(p.a + m0 * p.lda);
+  const auto rb = make_rsrc(p.b + n0 * p.ldb);
+  char* const wdst = S + 64 * wave * 128 + lane * 16;
+  // piece j (0..15): operand j >> 3, rows 64 w + 8 (j & 7)
+  auto ld = [&](int ss_src, int j) __attribute__((always_inline)) {
+    const int op = j >> 3, sub = j & 7;
+    return buf_load16(op ? rb : ra, vo[op][sub & 1], ss_src * 128 + sub * (op ? s8b : s8a));
+  };
+  auto st = [&](int ss_dst, int j, const u32x4& v) __attribute__((always_inline)) {
+    const int op = j >> 3, sub = j & 7;
+    *reinterpret_cast<u32x4*>(wdst + (ss_dst & 1) * SS + op * IMG2 + sub * 1024) = v;
+  };
+
+  const int li = lane & 15, kc = lane >> 4;
+  int a_off[2], b_off[2];
+  {
+    const int ra_ = wm * 128 + li;
+    // store_wave's mapping: tiles 2 p, 2 p + 1 give columns 128 wn + 32 p + 8 kc + [0, 8)
+    const int rb_ = 128 * wn + 8 * (li >> 2) + (li & 3);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      a_off[h] = ra_ * 128 + 16 * ((4 * h + kc) ^ f5(li));
+      b_off[h] = IMG2 + rb_ * 128 + 16 * ((4 * h + kc) ^ f5(rb_));
+    }
+  }
+  // B fragment nt (0..7): 32-column group g = nt >> 1 at offset 32 g, rows +4 (nt & 1)
+  auto bnt = [](int nt) { return (32 * (nt >> 1) + 4 * (nt & 1)) * 128; };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 fa[8], xb[8], yb[8];
+  u32x4 rs[16];
+
+  auto iter = [&](int t, auto odd_c, const bf16x8 (&cb)[8], bf16x8 (&nb_)[8]) __attribute__((always_inline)) {
+    constexpr bool ODD = decltype(odd_c)::value;
+    const int tn = t + 1;
+    const char* sr = S + ((tn >> 1) & 1) * SS;
+    const int h = ODD ? 0 : 1;
+    const int lsrc = min((t + 3) >> 1, ns - 1);
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cb[nt], fa[mt], acc[mt][nt], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      fa[mt] = rd(sr, a_off[h] + mt * 2048);
+      nb_[mt] = rd(sr, b_off[h] + bnt(mt));
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        if constexpr (ODD)
+          rs[2 * mt + k] = ld(lsrc, 2 * mt + k);
+        else
+          st((t + 2) >> 1, 2 * mt + k, rs[2 * mt + k]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (!ODD) {
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's writes of super-stage t/2+1 landed
+      barrier();
+    }
+  };
+
+#pragma unroll
+  for (int j = 0; j < 16; ++j) rs[j] = ld(0, j);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) st(0, j, rs[j]);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) rs[j] = ld(min(1, ns - 1), j);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) st(1, j, rs[j]);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  barrier();
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt) fa[mt] = rd(S, a_off[0] + mt * 2048);
+#pragma unroll
+  for (int nt = 0; nt < 8; ++nt) xb[nt] = rd(S, b_off[0] + bnt(nt));
+
+  for (int t = 0; t < nk; t += 2) {
+    iter(t, std::false_type{}, xb, yb);
+    iter(t + 1, std::true_type{}, yb, xb);
+  }
+  store_wave<F32C, 8, 8>(p, acc, m0 + wm * 128, n0 + wn * 128, lane);
 }
 
 // ---- variant 0: ping-pong ---------------------------------------------------------------------------
@@ -877,9 +1048,32 @@ extern "C" int ftc_gemm_nt(const void* a, long long lda, const void* b, long lon
     return e ? atoi(e) : 5;
   }();
   const int grid = p.nm * p.nn;
-  if (variant == 5) {
+  if (variant == 6) {
+    if (c_fp32)
+      hipLaunchKernelGGL((gemm_nt_w4s_kernel<true>), dim3(grid), dim3(256), 0, stream, p);
+    else
+      hipLaunchKernelGGL((gemm_nt_w4s_kernel<false>), dim3(grid), dim3(256), 0, stream, p);
+  } else if (variant == 5) {
+    static const int v5mode = [] {
+      const char* e = getenv("FTC_GEMM_NT_V5_MODE");
+      return e ? atoi(e) : 0;
+    }();
     if (c_fp32)
       hipLaunchKernelGGL((gemm_nt_v5_kernel<true>), dim3(grid), dim3(512), 0, stream, p);
+    else if (v5mode == 1)
+      hipLaunchKernelGGL((gemm_nt_v5_kernel<false, EPI_STORE, 1>), dim3(grid), dim3(512), 0, stream, p);
+    else if (v5mode == 2)
+      hipLaunchKernelGGL((gemm_nt_v5_kernel<false, EPI_STORE, 2>), dim3(grid), dim3(512), 0, stream, p);
+    else if (v5mode == 4)
+      hipLaunchKernelGGL((gemm_nt_v5_kernel<false, EPI_STORE, 4>), dim3(grid), dim3(512), 0, stream, p);
+    else if (v5mode == 8)
+      hipLaunchKernelGGL((gemm_nt_v5_kernel<false, EPI_STORE, 8>), dim3(grid), dim3(512), 0, stream, p);
+    else if (v5mode == 16)
+      hipLaunchKernelGGL((gemm_nt_v5_kernel<false, EPI_STORE, 16>), dim3(grid), dim3(512), 0, stream, p);
+    else if (v5mode == 32)
+      hipLaunchKernelGGL((gemm_nt_v5_kernel<false, EPI_STORE, 32>), dim3(grid), dim3(512), 0, stream, p);
+    else if (v5mode == 17)
+      hipLaunchKernelGGL((gemm_nt_v5_kernel<false, EPI_STORE, 17>), dim3(grid), dim3(512), 0, stream, p);
     else
       hipLaunchKernelGGL((gemm_nt_v5_kernel<false>), dim3(grid), dim3(512), 0, stream, p);
   } else if (variant == 4) {
