@@ -383,7 +383,8 @@ def test_sequence_parallel_rccl_matches_single_gpu(tmp_path, method):
 
 # --------------------------------------------------------------------------- DDP over RCCL on the GPU
 _DDP_GPU = dict(model="llama3-8b-1l", batch_size=2, seq_len=512, synthetic=True, max_steps=1, resume=False,
-                device="cuda", dtype="bf16", lr=0.0, max_grad_norm=0.0, save_model=False, grad_dtype="fp32")
+                device="cuda", dtype="bf16", lr=0.0, max_grad_norm=0.0, save_model=False, grad_dtype="fp32",
+                zero_stage=0)  # replicated all-reduce (full FT would default to ZeRO-1: test_zero1_rccl_* below)
 
 
 def _ddp_gpu_worker(rank, world, port, tmp, q, method, engine):
@@ -432,8 +433,8 @@ def test_ddp_rccl_matches_per_rank_sum(tmp_path, method, engine):
 def _zero_gpu_worker(rank, world, port, tmp, q, zero):
     os.environ["FTC_SHARE_GPU"] = "1"
     _rank_env(rank, world, port, tmp)
-    tr = Trainer(TrainConfig(method="full", checkpoint_path=tmp, zero_stage=zero,
-                             **{**_DDP_GPU, "lr": 1e-3, "max_grad_norm": 1.0}))
+    tr = Trainer(TrainConfig(method="full", checkpoint_path=tmp,
+                             **{**_DDP_GPU, "lr": 1e-3, "max_grad_norm": 1.0, "zero_stage": zero}))
     params = [p for p in tr.model.parameters() if p.requires_grad]
 
     def digest():
