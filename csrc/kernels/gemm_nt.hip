@@ -940,6 +940,141 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4s_kernel(NTArgs p) {
   store_wave<F32C, 8, 8>(p, acc, m0 + wm * 128, n0 + wn * 128, lane);
 }
 
+// ---- variant 7: one wave per SIMD with LDS-DMA, A/B-split release barriers -----------------------------
+// 4 waves own 128 x 128 each (256 AGPR accumulators, two full fragment sets X / Y of 8 A + 8 B), two
+// 64 KiB LDS buffers in variant 5's 128-byte-row image.  Iteration s computes super-stage s from buffer
+// s & 1 in two 32-deep halves and refills THAT buffer with super-stage s + 2 as soon as its regions are
+// released: half 0 reads Y.A, then (lgkmcnt + barrier: every wave is done with the A region) the 8 A
+// pieces of s + 2 go out between the MFMAs while Y.B is read; the barrier at the end of half 0 frees the
+// B region for its 8 pieces in half 1; a vmcnt + barrier in the middle of half 1 makes super-stage s + 1
+// (issued one iteration earlier) visible and the X fragments of s + 1 are read under the last 32 MFMAs.
+// Every DMA / LDS read sits between MFMAs of a dense 128-MFMA chain.  Three barriers per 64-deep step.
+template <bool F32C>
+__global__ __launch_bounds__(256, 1) void gemm_nt_w4d_kernel(NTArgs p) {
+  constexpr int IMG2 = 256 * 64 * 2;
+  constexpr int SS = 2 * IMG2;
+  __shared__ __attribute__((aligned(16))) char S[2 * SS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  int mb, nb;
+  tile_of(p, mb, nb);
+  const long long m0 = (long long)mb * BM, n0 = (long long)nb * BN;
+  const int ns = p.K / (2 * BK);
+
+  // DMA: wave w fills rows [64 w, 64 w + 64) of both images, piece j = rows 64 w + 8 j + (lane >> 3)
+  int vo[2][2];
+  {
+    const int rr = lane >> 3, pc = lane & 7;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int lc = pc ^ f5(rr + 8 * q);
+      vo[0][q] = (int)(((64 * wave + rr) * p.lda + 8 * lc) * 2);
+      vo[1][q] = (int)(((64 * wave + rr) * p.ldb + 8 * lc) * 2);
+    }
+  }
+  const int s8a = (int)(8 * p.lda * 2), s8b = (int)(8 * p.ldb * 2);
+  const auto ra = make_rsrc(p.a + m0 * p.lda);
+  const auto rb = make_rsrc(p.b + n0 * p.ldb);
+  char* const wbase = S + 64 * wave * 128;
+  auto dma = [&](int op, int ss, int j) __attribute__((always_inline)) {
+    lds_dma16(op ? rb : ra, wbase + (ss & 1) * SS + op * IMG2 + j * 1024, vo[op][j & 1],
+              ss * 128 + j * (op ? s8b : s8a));
+  };
+
+  const int li = lane & 15, kc = lane >> 4;
+  int a_off[2], b_off[2];
+  {
+    const int ra_ = wm * 128 + li;
+    const int rb_ = 128 * wn + 8 * (li >> 2) + (li & 3);  // store_wave's column mapping
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      a_off[h] = ra_ * 128 + 16 * ((4 * h + kc) ^ f5(li));
+      b_off[h] = IMG2 + rb_ * 128 + 16 * ((4 * h + kc) ^ f5(rb_));
+    }
+  }
+  auto bnt = [](int nt) { return (32 * (nt >> 1) + 4 * (nt & 1)) * 128; };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 xa[8], xb[8], ya[8], yb[8];
+
+  // one MFMA group (A fragment mt against the 8 B fragments) with up to 4 side operations after
+  // MFMAs 1, 3, 5, 7
+  auto group = [&](const bf16x8 (&fa)[8], const bf16x8 (&fb)[8], int mt, auto&& side) __attribute__((always_inline)) {
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) {
+      acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nt], fa[mt], acc[mt][nt], 0, 0, 0);
+      if (nt & 1) {
+        __builtin_amdgcn_sched_barrier(0);
+        side(nt >> 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+
+  // prologue: super-stages 0 and 1
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { dma(0, 0, j); dma(1, 0, j); }
+  if (ns > 1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { dma(0, 1, j); dma(1, 1, j); }
+    __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16) (bits 15:14 carry vmcnt[5:4])
+  } else {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  }
+  barrier();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    xa[i] = rd(S, a_off[0] + i * 2048);
+    xb[i] = rd(S, b_off[0] + bnt(i));
+  }
+
+  for (int s = 0; s < ns; ++s) {
+    const char* cur = S + (s & 1) * SS;
+    const char* nxt = S + ((s + 1) & 1) * SS;
+    const int sp = min(s + 2, ns - 1);  // past the end: reload the last super-stage into a dead region
+    // half 0 on X: read Y.A, release A, DMA A of s + 2 while reading Y.B, release B
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+      group(xa, xb, mt, [&](int k) __attribute__((always_inline)) {
+        if (k < 2) ya[2 * mt + k] = rd(cur, a_off[1] + (2 * mt + k) * 2048);
+      });
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    barrier();
+#pragma unroll
+    for (int mt = 4; mt < 8; ++mt)
+      group(xa, xb, mt, [&](int k) __attribute__((always_inline)) {
+        const int i = 2 * (mt - 4) + (k >> 1);
+        if (k & 1) yb[i] = rd(cur, b_off[1] + bnt(i));
+        else dma(0, sp, i);
+      });
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    barrier();
+    // half 1 on Y: DMA B of s + 2, wait for s + 1, read X of s + 1
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+      group(ya, yb, mt, [&](int k) __attribute__((always_inline)) {
+        if (!(k & 1)) dma(1, sp, 2 * mt + (k >> 1));
+      });
+    __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16): the 16 pieces of s + 1 landed
+    barrier();
+#pragma unroll
+    for (int mt = 4; mt < 8; ++mt)
+      group(ya, yb, mt, [&](int k) __attribute__((always_inline)) {
+        const int i = 2 * (mt - 4) + (k >> 1);
+        if (k & 1) xb[i] = rd(nxt, b_off[0] + bnt(i));
+        else xa[i] = rd(nxt, a_off[0] + i * 2048);
+      });
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // no LDS-DMA may outlive the workgroup
+  store_wave<F32C, 8, 8>(p, acc, m0 + wm * 128, n0 + wn * 128, lane);
+}
+
 // ---- variant 0: ping-pong ---------------------------------------------------------------------------
 // Each tile is two phases per wave (rows 0-63 / 64-127 of the wave's M range, 16 MFMAs each):
 //     [ds_read fragments for phase | 2 DMA pieces of tile t+2] barrier [16 MFMA] barrier
@@ -1048,7 +1183,12 @@ extern "C" int ftc_gemm_nt(const void* a, long long lda, const void* b, long lon
     return e ? atoi(e) : 5;
   }();
   const int grid = p.nm * p.nn;
-  if (variant == 6) {
+  if (variant == 7) {
+    if (c_fp32)
+      hipLaunchKernelGGL((gemm_nt_w4d_kernel<true>), dim3(grid), dim3(256), 0, stream, p);
+    else
+      hipLaunchKernelGGL((gemm_nt_w4d_kernel<false>), dim3(grid), dim3(256), 0, stream, p);
+  } else if (variant == 6) {
     if (c_fp32)
       hipLaunchKernelGGL((gemm_nt_w4s_kernel<true>), dim3(grid), dim3(256), 0, stream, p);
     else
