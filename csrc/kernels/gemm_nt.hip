@@ -949,7 +949,11 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4s_kernel(NTArgs p) {
 // B region for its 8 pieces in half 1; a vmcnt + barrier in the middle of half 1 makes super-stage s + 1
 // (issued one iteration earlier) visible and the X fragments of s + 1 are read under the last 32 MFMAs.
 // Every DMA / LDS read sits between MFMAs of a dense 128-MFMA chain.  Three barriers per 64-deep step.
-template <bool F32C>
+// MODE (FTC_GEMM_NT_V7_MODE, diagnostics): bit 0 sets M0 without saving it (the kernel's only M0 user;
+// audited in the ISA), bit 3 runs each MFMA group as one B fragment against the 8 A fragments; timing
+// only (results garbage): bit 1 drops the loop's DMA, bit 2 its barriers, bit 4 the DMA wait, bit 5
+// re-reads K-tile 0 in every DMA (L2-resident).
+template <bool F32C, int MODE = 0>
 __global__ __launch_bounds__(256, 1) void gemm_nt_w4d_kernel(NTArgs p) {
   constexpr int IMG2 = 256 * 64 * 2;
   constexpr int SS = 2 * IMG2;
@@ -978,8 +982,19 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4d_kernel(NTArgs p) {
   const auto rb = make_rsrc(p.b + n0 * p.ldb);
   char* const wbase = S + 64 * wave * 128;
   auto dma = [&](int op, int ss, int j) __attribute__((always_inline)) {
-    lds_dma16(op ? rb : ra, wbase + (ss & 1) * SS + op * IMG2 + j * 1024, vo[op][j & 1],
-              ss * 128 + j * (op ? s8b : s8a));
+    if constexpr (MODE & 2) return;
+    const void* dst = wbase + (ss & 1) * SS + op * IMG2 + j * 1024;
+    const int soff = ((MODE & 32) ? 0 : ss * 128) + j * (op ? s8b : s8a);
+    if constexpr (MODE & 1) {
+      const unsigned d = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)dst;
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
+                   :: "v"(vo[op][j & 1]), "s"(op ? rb : ra), "s"(d), "s"(soff) : "memory");
+    } else {
+      lds_dma16(op ? rb : ra, dst, vo[op][j & 1], soff);
+    }
+  };
+  auto sync = [&]() __attribute__((always_inline)) {
+    if constexpr (!(MODE & 4)) barrier();
   };
 
   const int li = lane & 15, kc = lane >> 4;
@@ -1005,13 +1020,15 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4d_kernel(NTArgs p) {
 
   // one MFMA group (A fragment mt against the 8 B fragments) with up to 4 side operations after
   // MFMAs 1, 3, 5, 7
-  auto group = [&](const bf16x8 (&fa)[8], const bf16x8 (&fb)[8], int mt, auto&& side) __attribute__((always_inline)) {
+  // (MODE bit 3: B fragment g against the 8 A fragments instead -- src0 of consecutive MFMAs constant)
+  auto group = [&](const bf16x8 (&fa)[8], const bf16x8 (&fb)[8], int g, auto&& side) __attribute__((always_inline)) {
 #pragma unroll
-    for (int nt = 0; nt < 8; ++nt) {
+    for (int q = 0; q < 8; ++q) {
+      const int mt = (MODE & 8) ? q : g, nt = (MODE & 8) ? g : q;
       acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nt], fa[mt], acc[mt][nt], 0, 0, 0);
-      if (nt & 1) {
+      if (q & 1) {
         __builtin_amdgcn_sched_barrier(0);
-        side(nt >> 1);
+        side(q >> 1);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -1038,38 +1055,55 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4d_kernel(NTArgs p) {
     const char* cur = S + (s & 1) * SS;
     const char* nxt = S + ((s + 1) & 1) * SS;
     const int sp = min(s + 2, ns - 1);  // past the end: reload the last super-stage into a dead region
-    // half 0 on X: read Y.A, release A, DMA A of s + 2 while reading Y.B, release B
+    // Every wait sits at least one MFMA group (8 MFMAs) after the last LDS read it covers, so the
+    // read latency hides under the matrix pipe instead of stalling the lone wave.
+    // half 0 on X: Y.A in groups 0-1, release A after group 2; A pieces of s + 2 and Y.B in groups 3-6;
+    // release B after group 7
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-      group(xa, xb, mt, [&](int k) __attribute__((always_inline)) {
-        if (k < 2) ya[2 * mt + k] = rd(cur, a_off[1] + (2 * mt + k) * 2048);
-      });
+    for (int mt = 0; mt < 2; ++mt)
+      group(xa, xb, mt, [&](int k) __attribute__((always_inline)) { ya[4 * mt + k] = rd(cur, a_off[1] + (4 * mt + k) * 2048); });
+    group(xa, xb, 2, [&](int) __attribute__((always_inline)) {});
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-    barrier();
+    sync();
 #pragma unroll
-    for (int mt = 4; mt < 8; ++mt)
+    for (int mt = 3; mt < 7; ++mt)
       group(xa, xb, mt, [&](int k) __attribute__((always_inline)) {
-        const int i = 2 * (mt - 4) + (k >> 1);
+        const int i = 2 * (mt - 3) + (k >> 1);
         if (k & 1) yb[i] = rd(cur, b_off[1] + bnt(i));
         else dma(0, sp, i);
       });
+    group(xa, xb, 7, [&](int) __attribute__((always_inline)) {});
     __builtin_amdgcn_s_waitcnt(0xC07F);
-    barrier();
-    // half 1 on Y: DMA B of s + 2, wait for s + 1, read X of s + 1
+    sync();
+    // half 1 on Y: B pieces of s + 2 in groups 0-3, wait for s + 1, X of s + 1 in groups 4-6 (B first:
+    // the next iteration's first group needs all of X.B but only X.A[0])
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
       group(ya, yb, mt, [&](int k) __attribute__((always_inline)) {
         if (!(k & 1)) dma(1, sp, 2 * mt + (k >> 1));
       });
-    __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16): the 16 pieces of s + 1 landed
-    barrier();
+    if constexpr (!(MODE & 16)) __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16): the 16 pieces of s + 1 landed
+    sync();
+    group(ya, yb, 4, [&](int k) __attribute__((always_inline)) {
+      if constexpr (MODE & 8) {
+        xa[2 * k] = rd(nxt, a_off[0] + 2 * k * 2048);
+        xa[2 * k + 1] = rd(nxt, a_off[0] + (2 * k + 1) * 2048);
+      } else {
+        xb[2 * k] = rd(nxt, b_off[0] + bnt(2 * k));
+        xb[2 * k + 1] = rd(nxt, b_off[0] + bnt(2 * k + 1));
+      }
+    });
+    group(ya, yb, 5, [&](int k) __attribute__((always_inline)) {
+      if constexpr (MODE & 8) {
+        xb[2 * k] = rd(nxt, b_off[0] + bnt(2 * k));
+        xb[2 * k + 1] = rd(nxt, b_off[0] + bnt(2 * k + 1));
+      } else {
+        xa[2 * k] = rd(nxt, a_off[0] + 2 * k * 2048);
+        xa[2 * k + 1] = rd(nxt, a_off[0] + (2 * k + 1) * 2048);
+      }
+    });
 #pragma unroll
-    for (int mt = 4; mt < 8; ++mt)
-      group(ya, yb, mt, [&](int k) __attribute__((always_inline)) {
-        const int i = 2 * (mt - 4) + (k >> 1);
-        if (k & 1) xb[i] = rd(nxt, b_off[0] + bnt(i));
-        else xa[i] = rd(nxt, a_off[0] + i * 2048);
-      });
+    for (int mt = 6; mt < 8; ++mt) group(ya, yb, mt, [&](int) __attribute__((always_inline)) {});
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // no LDS-DMA may outlive the workgroup
   store_wave<F32C, 8, 8>(p, acc, m0 + wm * 128, n0 + wn * 128, lane);
@@ -1184,8 +1218,28 @@ extern "C" int ftc_gemm_nt(const void* a, long long lda, const void* b, long lon
   }();
   const int grid = p.nm * p.nn;
   if (variant == 7) {
+    static const int v7mode = [] {
+      const char* e = getenv("FTC_GEMM_NT_V7_MODE");
+      return e ? atoi(e) : 0;
+    }();
     if (c_fp32)
       hipLaunchKernelGGL((gemm_nt_w4d_kernel<true>), dim3(grid), dim3(256), 0, stream, p);
+    else if (v7mode == 1)
+      hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 1>), dim3(grid), dim3(256), 0, stream, p);
+    else if (v7mode == 2)
+      hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 2>), dim3(grid), dim3(256), 0, stream, p);
+    else if (v7mode == 6)
+      hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 6>), dim3(grid), dim3(256), 0, stream, p);
+    else if (v7mode == 25)
+      hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 25>), dim3(grid), dim3(256), 0, stream, p);
+    else if (v7mode == 41)
+      hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 41>), dim3(grid), dim3(256), 0, stream, p);
+    else if (v7mode == 13)
+      hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 13>), dim3(grid), dim3(256), 0, stream, p);
+    else if (v7mode == 9)
+      hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 9>), dim3(grid), dim3(256), 0, stream, p);
+    else if (v7mode == 10)
+      hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 10>), dim3(grid), dim3(256), 0, stream, p);
     else
       hipLaunchKernelGGL((gemm_nt_w4d_kernel<false>), dim3(grid), dim3(256), 0, stream, p);
   } else if (variant == 6) {
