@@ -940,6 +940,56 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4s_kernel(NTArgs p) {
   store_wave<F32C, 8, 8>(p, acc, m0 + wm * 128, n0 + wn * 128, lane);
 }
 
+// Epilogue of the 128 x 128 wave tile (store_wave's mapping): lane holds, for m tile mt, columns
+// c0 + 32 pr + 8 kc + [0, 8) in acc[mt][2 pr .. 2 pr + 1], c0 = the wave's first column -- a whole
+// 128-wide head when c0 % 128 == 0, so RoPE's rotate_half partners (d, d + 64) are pairs pr / pr + 2 of
+// the same lane.
+template <bool F32C, int EPI>
+FTC_DEV void store_w128(const NTArgs& p, const f32x4 (&acc)[8][8], long long row0, long long c0, int lane) {
+  if constexpr (EPI == EPI_STORE) {
+    store_wave<F32C, 8, 8>(p, acc, row0, c0, lane);
+  } else {
+    static_assert(!F32C, "RoPE epilogue is bf16");
+    const int li = lane & 15, kc = lane >> 4;
+    const bool rope = (int)(c0 >> 7) < p.rot_heads;  // wave-uniform
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      const long long row = row0 + li + 16 * mt;
+      int pos = 0;
+      if (rope) pos = p.positions ? p.positions[row] : (int)(row % p.seq_len);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float v[2][8];
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[q][j] = p.alpha * acc[mt][2 * (h + 2 * q)][j];
+            v[q][4 + j] = p.alpha * acc[mt][2 * (h + 2 * q) + 1][j];
+          }
+        if (rope) {
+          const int ri = 32 * h + 8 * kc;
+          const float4* cp = reinterpret_cast<const float4*>(p.cos_t + (long long)pos * 64 + ri);
+          const float4* sp = reinterpret_cast<const float4*>(p.sin_t + (long long)pos * 64 + ri);
+          const float4 c0v = cp[0], c1v = cp[1], s0v = sp[0], s1v = sp[1];
+          const float cs[8] = {c0v.x, c0v.y, c0v.z, c0v.w, c1v.x, c1v.y, c1v.z, c1v.w};
+          const float sn[8] = {s0v.x, s0v.y, s0v.z, s0v.w, s1v.x, s1v.y, s1v.z, s1v.w};
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float x1 = v[0][j], x2 = v[1][j];
+            v[0][j] = x1 * cs[j] - x2 * sn[j];
+            v[1][j] = x2 * cs[j] + x1 * sn[j];
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(p.c) + row * p.ldc + c0 + 64 * q + 32 * h + 8 * kc) =
+              pack8(v[q]);
+      }
+    }
+  }
+}
+
 // ---- variant 7: one wave per SIMD with LDS-DMA, A/B-split release barriers -----------------------------
 // 4 waves own 128 x 128 each (256 AGPR accumulators, two full fragment sets X / Y of 8 A + 8 B), two
 // 64 KiB LDS buffers in variant 5's 128-byte-row image.  Iteration s computes super-stage s from buffer
@@ -953,7 +1003,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4s_kernel(NTArgs p) {
 // audited in the ISA), bit 3 runs each MFMA group as one B fragment against the 8 A fragments; timing
 // only (results garbage): bit 1 drops the loop's DMA, bit 2 its barriers, bit 4 the DMA wait, bit 5
 // re-reads K-tile 0 in every DMA (L2-resident).
-template <bool F32C, int MODE = 0>
+template <bool F32C, int MODE = 0, int EPI = EPI_STORE>
 __global__ __launch_bounds__(256, 1) void gemm_nt_w4d_kernel(NTArgs p) {
   constexpr int IMG2 = 256 * 64 * 2;
   constexpr int SS = 2 * IMG2;
@@ -996,6 +1046,26 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4d_kernel(NTArgs p) {
   auto sync = [&]() __attribute__((always_inline)) {
     if constexpr (!(MODE & 4)) barrier();
   };
+  // MODE bit 6, the lean loop DMA: the descriptor base walks K (once per operand and iteration), so
+  // the per-piece soffsets are loop-invariant SGPRs; each piece's statement sets M0 for the NEXT piece
+  // after its load, so MFMAs separate every M0 write from the DMA reading it (no s_nop, no save).
+  int so[2][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    so[0][j] = j * s8a;
+    so[1][j] = j * s8b;
+  }
+  auto dmal = [&](int op, __amdgpu_buffer_rsrc_t r, unsigned base, int j) __attribute__((always_inline)) {
+    if (j == 0)
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds\n\ts_mov_b32 m0, %4"
+                   :: "v"(vo[op][0]), "s"(r), "s"(base), "s"(so[op][0]), "s"(base + 1024u) : "memory");
+    else if (j < 7)
+      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds\n\ts_mov_b32 m0, %3"
+                   :: "v"(vo[op][j & 1]), "s"(r), "s"(so[op][j]), "s"(base + (unsigned)(j + 1) * 1024u) : "memory");
+    else
+      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" :: "v"(vo[op][1]), "s"(r), "s"(so[op][7]) : "memory");
+  };
+  const unsigned lds0 = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)wbase;
 
   const int li = lane & 15, kc = lane >> 4;
   int a_off[2], b_off[2];
@@ -1055,6 +1125,9 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4d_kernel(NTArgs p) {
     const char* cur = S + (s & 1) * SS;
     const char* nxt = S + ((s + 1) & 1) * SS;
     const int sp = min(s + 2, ns - 1);  // past the end: reload the last super-stage into a dead region
+    const auto ras = make_rsrc(p.a + m0 * p.lda + 64 * sp);
+    const auto rbs = make_rsrc(p.b + n0 * p.ldb + 64 * sp);
+    const unsigned dA = lds0 + (unsigned)((s & 1) * SS), dB = dA + IMG2;
     // Every wait sits at least one MFMA group (8 MFMAs) after the last LDS read it covers, so the
     // read latency hides under the matrix pipe instead of stalling the lone wave.
     // half 0 on X: Y.A in groups 0-1, release A after group 2; A pieces of s + 2 and Y.B in groups 3-6;
@@ -1070,6 +1143,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4d_kernel(NTArgs p) {
       group(xa, xb, mt, [&](int k) __attribute__((always_inline)) {
         const int i = 2 * (mt - 3) + (k >> 1);
         if (k & 1) yb[i] = rd(cur, b_off[1] + bnt(i));
+        else if constexpr (MODE & 64) dmal(0, ras, dA, i);
         else dma(0, sp, i);
       });
     group(xa, xb, 7, [&](int) __attribute__((always_inline)) {});
@@ -1080,7 +1154,10 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4d_kernel(NTArgs p) {
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
       group(ya, yb, mt, [&](int k) __attribute__((always_inline)) {
-        if (!(k & 1)) dma(1, sp, 2 * mt + (k >> 1));
+        if (!(k & 1)) {
+          if constexpr (MODE & 64) dmal(1, rbs, dB, 2 * mt + (k >> 1));
+          else dma(1, sp, 2 * mt + (k >> 1));
+        }
       });
     if constexpr (!(MODE & 16)) __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16): the 16 pieces of s + 1 landed
     sync();
@@ -1106,7 +1183,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4d_kernel(NTArgs p) {
     for (int mt = 6; mt < 8; ++mt) group(ya, yb, mt, [&](int) __attribute__((always_inline)) {});
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // no LDS-DMA may outlive the workgroup
-  store_wave<F32C, 8, 8>(p, acc, m0 + wm * 128, n0 + wn * 128, lane);
+  store_w128<F32C, EPI>(p, acc, m0 + wm * 128, n0 + wn * 128, lane);
 }
 
 // ---- variant 0: ping-pong ---------------------------------------------------------------------------
@@ -1230,6 +1307,10 @@ extern "C" int ftc_gemm_nt(const void* a, long long lda, const void* b, long lon
       hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 2>), dim3(grid), dim3(256), 0, stream, p);
     else if (v7mode == 6)
       hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 6>), dim3(grid), dim3(256), 0, stream, p);
+    else if (v7mode == 72)
+      hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 72>), dim3(grid), dim3(256), 0, stream, p);
+    else if (v7mode == 73)
+      hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 73>), dim3(grid), dim3(256), 0, stream, p);
     else if (v7mode == 25)
       hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 25>), dim3(grid), dim3(256), 0, stream, p);
     else if (v7mode == 41)
@@ -1360,6 +1441,13 @@ extern "C" int ftc_gemm_nt_rope(const void* a, long long lda, const void* b, lon
   }();
   NTArgs p{(const uint16_t*)a, (const uint16_t*)b, c, lda, ldb, ldc, K, M / BM, N / BN, group_m > 0 ? group_m : 4,
            1.f, 0.f, cos_t, sin_t, positions, seq_len, rot_heads};
-  hipLaunchKernelGGL((gemm_nt_v5_kernel<false, EPI_ROPE>), dim3(p.nm * p.nn), dim3(512), 0, stream, p);
+  static const int variant = [] {
+    const char* e = getenv("FTC_GEMM_NT_VARIANT");
+    return e ? atoi(e) : 5;
+  }();
+  if (variant == 7)
+    hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 72, EPI_ROPE>), dim3(p.nm * p.nn), dim3(256), 0, stream, p);
+  else
+    hipLaunchKernelGGL((gemm_nt_v5_kernel<false, EPI_ROPE>), dim3(p.nm * p.nn), dim3(512), 0, stream, p);
   return (int)hipGetLastError();
 }
