@@ -999,6 +999,17 @@ FTC_DEV void store_w128(const NTArgs& p, const f32x4 (&acc)[8][8], long long row
 // B region for its 8 pieces in half 1; a vmcnt + barrier in the middle of half 1 makes super-stage s + 1
 // (issued one iteration earlier) visible and the X fragments of s + 1 are read under the last 32 MFMAs.
 // Every DMA / LDS read sits between MFMAs of a dense 128-MFMA chain.  Three barriers per 64-deep step.
+// Spread schedule (variant 7, MODE bit 7): the 16 pieces of super-stage s + 2 sit after MFMAs
+// 41, 47, ..., 127 of the iteration's 128 (one per ~5.5 MFMAs instead of bursts of one per 4), piece i
+// after MFMA 41 + 2 floor(43 i / 15); the 10 issued before MFMA 96 are what the s + 1 wait skips.
+FTC_DEV constexpr int v7_piece(int idx) {
+  if (idx < 41 || !(idx & 1)) return -1;
+  const int d = (idx - 41) / 2;
+  for (int i = 0; i < 16; ++i)
+    if ((43 * i) / 15 == d) return i;
+  return -1;
+}
+
 // MODE (FTC_GEMM_NT_V7_MODE, diagnostics): bit 0 sets M0 without saving it (the kernel's only M0 user;
 // audited in the ISA), bit 3 runs each MFMA group as one B fragment against the 8 A fragments; timing
 // only (results garbage): bit 1 drops the loop's DMA, bit 2 its barriers, bit 4 the DMA wait, bit 5
@@ -1121,6 +1132,58 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4d_kernel(NTArgs p) {
     xb[i] = rd(S, b_off[0] + bnt(i));
   }
 
+  if constexpr (MODE & 128) {
+    for (int s = 0; s < ns; ++s) {
+      const char* cur = S + (s & 1) * SS;
+      const char* nxt = S + ((s + 1) & 1) * SS;
+      const int sp = min(s + 2, ns - 1);
+      const auto ras = make_rsrc(p.a + m0 * p.lda + 64 * sp);
+      const auto rbs = make_rsrc(p.b + n0 * p.ldb + 64 * sp);
+      const unsigned dA = lds0 + (unsigned)((s & 1) * SS), dB = dA + IMG2;
+      auto piece = [&](int pc) __attribute__((always_inline)) {
+        if (pc < 0) return;
+        if constexpr (MODE & 64) dmal(pc >> 3, (pc >> 3) ? rbs : ras, (pc >> 3) ? dB : dA, pc & 7);
+        else dma(pc >> 3, sp, pc & 7);
+      };
+      // half 0 on X: all of Y (A then B) in groups 0-3, release the buffer after group 4
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        group(xa, xb, g, [&](int k) __attribute__((always_inline)) {
+          if (g < 4) {
+            const int r = 4 * g + k;
+            if (r < 8) ya[r] = rd(cur, a_off[1] + r * 2048);
+            else yb[r - 8] = rd(cur, b_off[1] + bnt(r - 8));
+          }
+          piece(v7_piece(8 * g + 2 * k + 1));
+        });
+        if (g == 4) {
+          __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+          sync();
+        }
+      }
+      // half 1 on Y: wait for s + 1 after group 3, X of s + 1 in groups 4-5
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        group(ya, yb, g, [&](int k) __attribute__((always_inline)) {
+          if (g == 4 || g == 5) {
+            const bool a_first = (MODE & 8) != 0;
+            if ((g == 4) == a_first) {
+              xa[2 * k] = rd(nxt, a_off[0] + 2 * k * 2048);
+              xa[2 * k + 1] = rd(nxt, a_off[0] + (2 * k + 1) * 2048);
+            } else {
+              xb[2 * k] = rd(nxt, b_off[0] + bnt(2 * k));
+              xb[2 * k + 1] = rd(nxt, b_off[0] + bnt(2 * k + 1));
+            }
+          }
+          piece(v7_piece(64 + 8 * g + 2 * k + 1));
+        });
+        if (g == 3) {
+          if constexpr (!(MODE & 16)) __builtin_amdgcn_s_waitcnt(0x0F7A);  // vmcnt(10): s + 1 landed
+          sync();
+        }
+      }
+    }
+  } else {
   for (int s = 0; s < ns; ++s) {
     const char* cur = S + (s & 1) * SS;
     const char* nxt = S + ((s + 1) & 1) * SS;
@@ -1181,6 +1244,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4d_kernel(NTArgs p) {
     });
 #pragma unroll
     for (int mt = 6; mt < 8; ++mt) group(ya, yb, mt, [&](int) __attribute__((always_inline)) {});
+  }
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // no LDS-DMA may outlive the workgroup
   store_w128<F32C, EPI>(p, acc, m0 + wm * 128, n0 + wn * 128, lane);
@@ -1307,6 +1371,10 @@ extern "C" int ftc_gemm_nt(const void* a, long long lda, const void* b, long lon
       hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 2>), dim3(grid), dim3(256), 0, stream, p);
     else if (v7mode == 6)
       hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 6>), dim3(grid), dim3(256), 0, stream, p);
+    else if (v7mode == 200)
+      hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 200>), dim3(grid), dim3(256), 0, stream, p);
+    else if (v7mode == 137)
+      hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 137>), dim3(grid), dim3(256), 0, stream, p);
     else if (v7mode == 72)
       hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 72>), dim3(grid), dim3(256), 0, stream, p);
     else if (v7mode == 73)
