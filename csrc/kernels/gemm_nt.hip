@@ -69,6 +69,10 @@ struct NTArgs {
   const float* sin_t;
   const int* positions;
   int seq_len, rot_heads;
+  // variant 7: K-loop stagger -- workgroup b starts at super-stage ((b & stagger_mask) * stagger_step) % ns
+  // and wraps, so co-running tiles do not stream the same K columns (the same HBM channel offsets) in
+  // lockstep
+  int stagger_mask, stagger_step;
 };
 
 FTC_DEV int swz(int row) { return (row >> 2) & 2; }
@@ -1026,6 +1030,8 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4d_kernel(NTArgs p) {
   tile_of(p, mb, nb);
   const long long m0 = (long long)mb * BM, n0 = (long long)nb * BN;
   const int ns = p.K / (2 * BK);
+  const int st0 = ((int)(blockIdx.x & p.stagger_mask) * p.stagger_step) % ns;
+  auto phys = [&](int ss) { const int q = ss + st0; return q >= ns ? q - ns : q; };
 
   // DMA: wave w fills rows [64 w, 64 w + 64) of both images, piece j = rows 64 w + 8 j + (lane >> 3)
   int vo[2][2];
@@ -1045,7 +1051,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4d_kernel(NTArgs p) {
   auto dma = [&](int op, int ss, int j) __attribute__((always_inline)) {
     if constexpr (MODE & 2) return;
     const void* dst = wbase + (ss & 1) * SS + op * IMG2 + j * 1024;
-    const int soff = ((MODE & 32) ? 0 : ss * 128) + j * (op ? s8b : s8a);
+    const int soff = ((MODE & 32) ? 0 : phys(ss) * 128) + j * (op ? s8b : s8a);
     if constexpr (MODE & 1) {
       const unsigned d = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)dst;
       asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
@@ -1137,8 +1143,8 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4d_kernel(NTArgs p) {
       const char* cur = S + (s & 1) * SS;
       const char* nxt = S + ((s + 1) & 1) * SS;
       const int sp = min(s + 2, ns - 1);
-      const auto ras = make_rsrc(p.a + m0 * p.lda + 64 * sp);
-      const auto rbs = make_rsrc(p.b + n0 * p.ldb + 64 * sp);
+      const auto ras = make_rsrc(p.a + m0 * p.lda + 64 * phys(sp));
+      const auto rbs = make_rsrc(p.b + n0 * p.ldb + 64 * phys(sp));
       const unsigned dA = lds0 + (unsigned)((s & 1) * SS), dB = dA + IMG2;
       auto piece = [&](int pc) __attribute__((always_inline)) {
         if (pc < 0) return;
@@ -1188,8 +1194,8 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4d_kernel(NTArgs p) {
     const char* cur = S + (s & 1) * SS;
     const char* nxt = S + ((s + 1) & 1) * SS;
     const int sp = min(s + 2, ns - 1);  // past the end: reload the last super-stage into a dead region
-    const auto ras = make_rsrc(p.a + m0 * p.lda + 64 * sp);
-    const auto rbs = make_rsrc(p.b + n0 * p.ldb + 64 * sp);
+    const auto ras = make_rsrc(p.a + m0 * p.lda + 64 * phys(sp));
+    const auto rbs = make_rsrc(p.b + n0 * p.ldb + 64 * phys(sp));
     const unsigned dA = lds0 + (unsigned)((s & 1) * SS), dB = dA + IMG2;
     // Every wait sits at least one MFMA group (8 MFMAs) after the last LDS read it covers, so the
     // read latency hides under the matrix pipe instead of stalling the lone wave.
@@ -1358,6 +1364,18 @@ extern "C" int ftc_gemm_nt(const void* a, long long lda, const void* b, long lon
     return e ? atoi(e) : 5;
   }();
   const int grid = p.nm * p.nn;
+  {
+    static const int su = [] {
+      const char* e = getenv("FTC_GEMM_NT_STAGGER");
+      return e ? atoi(e) : 0;
+    }();
+    static const int sus = [] {
+      const char* e = getenv("FTC_GEMM_NT_STAGGER_STEP");
+      return e ? atoi(e) : 2;
+    }();
+    p.stagger_mask = su > 1 ? su - 1 : 0;
+    p.stagger_step = sus;
+  }
   if (variant == 7) {
     static const int v7mode = [] {
       const char* e = getenv("FTC_GEMM_NT_V7_MODE");

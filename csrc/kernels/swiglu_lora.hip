@@ -317,6 +317,8 @@ constexpr int kCB = 512;  // gate|up column pairs per workgroup (128 per wave)
 // byte offset of (row, col) in a wave tile [16][128] bf16 with the 16-byte chunk swizzle of tile_off
 FTC_DEV int tcol_off(int row, int col) { return row * 256 + ((((col >> 3) ^ (row & 15)) & 15) << 4) + (col & 7) * 2; }
 
+// PF = false: the previous schedule (loads at the top of each sub-tile, __syncthreads), FTC_WGRAD_PF=0 (A/B)
+template <bool PF>
 __global__ __launch_bounds__(256, 2) void swiglu_bwd_wgrad_kernel(WgArgs a) {
   __shared__ __attribute__((aligned(16))) char tiles[kWaves][3][16 * 256];  // dg, du, h
   __shared__ __attribute__((aligned(16))) char xat[kWaves][16 * 64];       // xa sub-tile [16][32]
@@ -349,23 +351,35 @@ __global__ __launch_bounds__(256, 2) void swiglu_bwd_wgrad_kernel(WgArgs a) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) acca[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  int sub = 0;
-  for (long long r0 = rbeg; r0 < rend; r0 += 16, ++sub) {
-    const long long nrows = rend - r0 < 16 ? rend - r0 : 16;
-    // this sub-tile's rows as buffer resources: rows past the block read as zero, stores are dropped
-    const __amdgpu_buffer_rsrc_t rg = make_rsrc_n(a.gu + r0 * 2LL * F, (unsigned)(nrows * 4LL * F));
-    const __amdgpu_buffer_rsrc_t rd = make_rsrc_n(a.da + r0 * a.da_rs, (unsigned)(nrows * a.da_rs * 2));
-    const __amdgpu_buffer_rsrc_t ro = make_rsrc_n(a.dgu + r0 * a.dgu_rs, (unsigned)(nrows * a.dgu_rs * 2));
-    const __amdgpu_buffer_rsrc_t rx = make_rsrc_n(a.xa + r0 * a.xa_rs, (unsigned)(nrows * a.xa_rs * 2));
-    const __amdgpu_buffer_rsrc_t ry = make_rsrc_n(a.dyb + r0 * a.dyb_rs, (unsigned)(nrows * a.dyb_rs * 2));
-    uint4 gv[4], uv[4], dv[4];
+  // The g / u loads (2/3 of the streamed bytes) are issued one sub-tile ahead: rows r0 + 16.. leave
+  // right after the element-wise pass of rows r0.. has consumed their registers, so they fly under this
+  // sub-tile's MFMAs and row-tail reduction (whose barrier waits on LDS only, never on these loads).
+  // da stays in-iteration: prefetching it too spills at two workgroups per CU.
+  uint4 gv[4], uv[4];
+  auto issue = [&](long long r) __attribute__((always_inline)) {
+    const long long nr = rend - r < 16 ? rend - r : 16;
+    // this sub-tile's rows as buffer resources: rows past the block read as zero
+    const __amdgpu_buffer_rsrc_t rg = make_rsrc_n(a.gu + r * 2LL * F, (unsigned)(nr * 4LL * F));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = 4 * i + rq;
       gv[i] = bload16(rg, (int)((row * 2LL * F + cw + 8 * cq) * 2), 0);
       uv[i] = bload16(rg, (int)((row * 2LL * F + F + cw + 8 * cq) * 2), 0);
-      dv[i] = bload16(rd, (int)((row * a.da_rs + cw + 8 * cq) * 2), 0);
     }
+  };
+  if (PF && rbeg < rend) issue(rbeg);
+  int sub = 0;
+  for (long long r0 = rbeg; r0 < rend; r0 += 16, ++sub) {
+    if (!PF) issue(r0);
+    const long long nrows = rend - r0 < 16 ? rend - r0 : 16;
+    // stores past the block's rows are dropped
+    const __amdgpu_buffer_rsrc_t ro = make_rsrc_n(a.dgu + r0 * a.dgu_rs, (unsigned)(nrows * a.dgu_rs * 2));
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc_n(a.xa + r0 * a.xa_rs, (unsigned)(nrows * a.xa_rs * 2));
+    const __amdgpu_buffer_rsrc_t ry = make_rsrc_n(a.dyb + r0 * a.dyb_rs, (unsigned)(nrows * a.dyb_rs * 2));
+    const __amdgpu_buffer_rsrc_t rd = make_rsrc_n(a.da + r0 * a.da_rs, (unsigned)(nrows * a.da_rs * 2));
+    uint4 dv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dv[i] = bload16(rd, (int)(((4 * i + rq) * a.da_rs + cw + 8 * cq) * 2), 0);
     // xa [16][32]: lane -> row lane >> 2, chunk lane & 3;  dyb [16][16]: lanes 0..31 -> row lane >> 1, chunk lane & 1
     const uint4 xv = bload16(rx, (int)(((lane >> 2) * a.xa_rs + 8 * (lane & 3)) * 2), 0);
     const uint4 yv = lane < 32 ? bload16(ry, (int)(((lane >> 1) * a.dyb_rs + 8 * (lane & 1)) * 2), 0)
@@ -396,6 +410,7 @@ __global__ __launch_bounds__(256, 2) void swiglu_bwd_wgrad_kernel(WgArgs a) {
       *reinterpret_cast<uint4*>(my + 16 * 256 + off) = uq;
       *reinterpret_cast<uint4*>(my + 2 * 16 * 256 + off) = hq;
     }
+    if (PF && r0 + 16 < rend) issue(r0 + 16);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private tiles complete
 
     // ---- row tail: [16 rows] x (gate tile 0, up tile 1)
@@ -426,7 +441,14 @@ __global__ __launch_bounds__(256, 2) void swiglu_bwd_wgrad_kernel(WgArgs a) {
       rbuf[((wave * 2 + 0) * 4 + i) * 64 + lane] = tg[i];
       rbuf[((wave * 2 + 1) * 4 + i) * 64 + lane] = tu[i];
     }
-    __syncthreads();
+    // LDS-only barrier: __syncthreads' release fence would also drain the prefetch loads (vmcnt(0))
+    if constexpr (PF) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      __syncthreads();
+    }
     for (int idx = tid; idx < 2 * 4 * 64; idx += 256) {  // (tile, i, lane) -> row 4 (ln >> 4) + i, col tile*16 + (ln & 15)
       const int t = idx >> 8, i = (idx >> 6) & 3, ln = idx & 63;
       float s = 0.f;
@@ -540,7 +562,14 @@ extern "C" int ftc_swiglu_bwd_wgrad(const void* da, long long da_rs, const void*
   WgArgs a{(const uint16_t*)gu, (const uint16_t*)da, da_rs, (uint16_t*)dgu, dgu_rs, (const uint16_t*)bt, ldb,
            (const uint16_t*)xa, xa_rs, (const uint16_t*)dyb, dyb_rs, ws, ws + (long long)ncb * T * 32,
            ws + (long long)ncb * T * 32 + (long long)nrb * 2 * F * 16, (int)T, F, RB, ncb};
-  hipLaunchKernelGGL(swiglu_bwd_wgrad_kernel, dim3(ncb * nrb), dim3(256), 0, stream, a);
+  static const bool pf = [] {
+    const char* e = getenv("FTC_WGRAD_PF");
+    return !(e && e[0] == '0');
+  }();
+  if (pf)
+    hipLaunchKernelGGL(swiglu_bwd_wgrad_kernel<true>, dim3(ncb * nrb), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL(swiglu_bwd_wgrad_kernel<false>, dim3(ncb * nrb), dim3(256), 0, stream, a);
   const long long nt = T * (Rp / 8);
   hipLaunchKernelGGL(wgrad_tail_reduce_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, a.p_tail,
                      ncb, (int)T, (uint16_t*)dgu, dgu_rs, 2 * F, Rp);
