@@ -70,7 +70,8 @@ int ftc_flash_bwd(const void* q, const void* k, const void* v, const void* o, co
                   long long q_row_stride, long long kv_row_stride, long long o_row_stride, long long do_row_stride,
                   long long dq_row_stride,
                   long long dkv_row_stride, float scale, int causal, int window, const int* doc_start,
-                  const int* doc_end, int kv_valid, hipStream_t stream);
+                  const int* doc_end, int kv_valid, const float* rope_cos, const float* rope_sin,
+                  const int* rope_pos, hipStream_t stream);
 int ftc_nf4_dequant(const uint8_t* packed, const uint8_t* absmax_q, const float* absmax_scale, float absmax_offset,
                     void* out, long long n, int block, int block2, hipStream_t stream);
 int ftc_nf4_quant(const void* w, uint8_t* packed, float* absmax, long long n, int block, hipStream_t stream);
@@ -569,8 +570,30 @@ void flash_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, co
                const at::Tensor& dout, const at::Tensor& lse, at::Tensor& dq, at::Tensor& dk, at::Tensor& dv,
                int64_t B, int64_t S, int64_t H, int64_t KV, int64_t D, double scale, bool causal, int64_t window,
                const c10::optional<at::Tensor>& doc_start, const c10::optional<at::Tensor>& doc_end,
-               int64_t kv_valid) {
+               int64_t kv_valid, const c10::optional<at::Tensor>& rope_cos,
+               const c10::optional<at::Tensor>& rope_sin, const c10::optional<at::Tensor>& rope_pos) {
   TORCH_CHECK(doc_start.has_value() == doc_end.has_value(), "flash_bwd: doc_start and doc_end go together");
+  TORCH_CHECK(rope_cos.has_value() == rope_sin.has_value() && (!rope_pos.has_value() || rope_cos.has_value()),
+              "flash_bwd: rope_cos / rope_sin go together");
+  const float* rc = nullptr;
+  const float* rsn = nullptr;
+  const int* rp = nullptr;
+  if (rope_cos.has_value()) {
+    for (auto* t : {&*rope_cos, &*rope_sin}) {
+      need(*t, at::kFloat, "rope cos/sin");
+      TORCH_CHECK(t->dim() == 2 && t->size(1) == 64 && t->is_contiguous(), "flash_bwd: rope tables [max_pos, 64]");
+    }
+    TORCH_CHECK(D == 128, "flash_bwd: the RoPE epilogue needs head_dim 128");
+    rc = rope_cos->data_ptr<float>();
+    rsn = rope_sin->data_ptr<float>();
+    if (rope_pos.has_value()) {
+      need(*rope_pos, at::kInt, "rope_pos");
+      TORCH_CHECK(rope_pos->numel() == B * S, "flash_bwd: rope_pos [B*S]");
+      rp = rope_pos->data_ptr<int>();
+    } else {
+      TORCH_CHECK(rope_cos->size(0) >= S, "flash_bwd: rope tables shorter than the sequence");
+    }
+  }
   for (auto* t : {&q, &k, &v, &o, &dout}) need(*t, at::kBFloat16, "flash_bwd input");
   need(lse, at::kFloat, "lse");
   TORCH_CHECK(D == 128 || D == 64, "flash_bwd: head_dim");
@@ -587,7 +610,7 @@ void flash_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, co
                       (int)D, q.stride(0), k.stride(0), o.stride(0), dout.stride(0), dq.stride(0), dk.stride(0),
                       (float)scale,
                       causal ? 1 : 0, (int)window, doc_ptr(doc_start, B * S, "doc_start"),
-                      doc_ptr(doc_end, B * S, "doc_end"), (int)kv_valid, cur_stream()),
+                      doc_ptr(doc_end, B * S, "doc_end"), (int)kv_valid, rc, rsn, rp, cur_stream()),
         "flash_bwd");
 }
 
@@ -788,7 +811,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("flash_bwd", &flash_bwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("dout"),
         py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("B"), py::arg("S"), py::arg("H"),
         py::arg("KV"), py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("window"),
-        py::arg("doc_start") = py::none(), py::arg("doc_end") = py::none(), py::arg("kv_valid") = -1);
+        py::arg("doc_start") = py::none(), py::arg("doc_end") = py::none(), py::arg("kv_valid") = -1,
+        py::arg("rope_cos") = py::none(), py::arg("rope_sin") = py::none(), py::arg("rope_pos") = py::none());
   m.def("decode_attention", &decode_attention);
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequantize", &nf4_dequantize);

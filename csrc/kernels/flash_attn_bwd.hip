@@ -135,7 +135,40 @@ struct BwdArgs {
   // the dQ pass masks them: dK / dV rows of those keys are discarded by the caller, and a masked key
   // never reaches a valid key's dK / dV.
   int kv_valid;
+  // RoPE folded into the epilogues (D = 128): q and k were rotated (HF rotate_half, fp32 cos / sin
+  // [max_pos, 64]) by their producer, so dQ and dK leave as the gradients of the UN-rotated q / k --
+  // the inverse rotation the producer's backward would otherwise run as a separate pass over dq / dk.
+  // pos = rpos[token] or (token % S); rcos == null: no rotation
+  const float* rcos;
+  const float* rsin;
+  const int* rpos;
 };
+
+// Inverse rotation of one row's gradient held as store_rows' accumulators: element i of tile dt is
+// d = 32 dt + 8 (i >> 2) + 4 hh + (i & 3), so d and d + 64 are tiles dt and dt + 2 of the same lane.
+// (y1, y2) = (u1 c - u2 s, u2 c + u1 s)  =>  (du1, du2) = (g1 c + g2 s, g2 c - g1 s)
+template <int DT>
+FTC_DEV void rope_inv_rows(f32x16* acc, const BwdArgs& a, long long token, int hh) {
+  static_assert(DT == 4, "RoPE epilogue: head_dim 128");
+  const int pos = a.rpos ? a.rpos[token] : (int)(token % a.S);
+  const float* cr = a.rcos + (long long)pos * 64 + 4 * hh;
+  const float* sr = a.rsin + (long long)pos * 64 + 4 * hh;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const float4 c = *reinterpret_cast<const float4*>(cr + 32 * dt + 8 * g4);
+      const float4 sn = *reinterpret_cast<const float4*>(sr + 32 * dt + 8 * g4);
+      const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = 4 * g4 + e;
+        const float g1 = acc[dt][i], g2 = acc[dt + 2][i];
+        acc[dt][i] = g1 * cc[e] + g2 * ss[e];
+        acc[dt + 2][i] = g2 * cc[e] - g1 * ss[e];
+      }
+    }
+}
 
 // ---------------------------------------------------------------- 1. delta
 template <int D>
@@ -666,6 +699,9 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
     uint16_t* dkp = a.dk + ((long long)b * S + key) * a.dkv_rs + (long long)kvh * D;
     uint16_t* dvp = a.dv + ((long long)b * S + key) * a.dkv_rs + (long long)kvh * D;
     const bool wide = (a.dkv_rs & 7) == 0;
+    if constexpr (D == 128) {
+      if (a.rcos) rope_inv_rows<DT>(dk[j], a, (long long)b * S + key, hh);
+    }
     store_rows<DT>(dkp, dk[j], a.scale, hh, wide);
     store_rows<DT>(dvp, dv[j], 1.0f, hh, wide);
   }
@@ -842,6 +878,9 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
     if (t + 1 < ntiles) tile(t + 1, Kt1, Vt1, Kt0, Vt0);
   }
   uint16_t* op = a.dq + ((long long)b * S + qrow) * a.dq_rs + (long long)hq * D;
+  if constexpr (D == 128) {
+    if (a.rcos) rope_inv_rows<DT>(dq, a, (long long)b * S + qrow, hh);
+  }
   store_rows<DT>(op, dq, a.scale, hh, (a.dq_rs & 7) == 0);
 }
 
@@ -916,15 +955,20 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
                              const float* lse, void* dq, void* dk, void* dv, void* workspace, int B, int S, int H,
                              int KV, int D, long long q_rs, long long kv_rs, long long o_rs, long long do_rs,
                              long long dq_rs, long long dkv_rs, float scale, int causal, int window,
-                             const int* doc_start, const int* doc_end, int kv_valid, hipStream_t stream) {
+                             const int* doc_start, const int* doc_end, int kv_valid, const float* rope_cos,
+                             const float* rope_sin, const int* rope_pos, hipStream_t stream) {
   if (S % 256 != 0 || H % KV != 0 || (D != 128 && D != 64)) return -1;
+  if (rope_cos && (D != 128 || !rope_sin || ((reinterpret_cast<uintptr_t>(rope_cos) |
+                                               reinterpret_cast<uintptr_t>(rope_sin)) & 15)))
+    return -1;
   if (kv_valid <= 0 || kv_valid > S) kv_valid = S;
   // the dK/dV kernel addresses one batch's Q / dO rows and the workspace with 32-bit buffer offsets
   const long long max_rs = q_rs > do_rs ? (q_rs > kv_rs ? q_rs : kv_rs) : (do_rs > kv_rs ? do_rs : kv_rs);
   if ((long long)S * max_rs * 2 >= (1LL << 31) || 2LL * B * H * S * 4 >= (1LL << 31)) return -1;
   BwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)o, (const uint16_t*)dout,
             lse, (float*)workspace, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, q_rs, kv_rs, o_rs, dq_rs, dkv_rs, do_rs,
-            B, S, H, KV, scale, scale * LOG2E, causal, window, 0, doc_start, doc_end, kv_valid};
+            B, S, H, KV, scale, scale * LOG2E, causal, window, 0, doc_start, doc_end, kv_valid,
+            rope_cos, rope_sin, rope_pos};
   static const int prio = [] {
     const char* e = getenv("FTC_FLASH_BWD_PRIO");
     return (e && e[0] == '1') ? 1 : 0;

@@ -148,7 +148,9 @@ class LlamaLayer(nn.Module):
                 and cfg.head_dim == 128 and x.dim() == 2):
             cos, sin = rope.get(x.device)
             pos = positions.to(torch.int32).contiguous() if positions is not None else None
-            rargs = (cos, sin, pos, S, cfg.n_heads + cfg.n_kv_heads, cfg.head_dim)
+            # full-sequence attention on this rank: the flash backward may take the inverse rotation
+            rgrad = ops.RopeGrad(cos, sin, pos) if (kv is None and getattr(self, "sp", None) is None) else None
+            rargs = (cos, sin, pos, S, cfg.n_heads + cfg.n_kv_heads, cfg.head_dim, rgrad)
         qkv = self.proj("qkv", x, rope=rargs)
         if rargs is None:
             qkv = ops.apply_rope_packed(qkv, rope, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, S, positions)
@@ -166,7 +168,8 @@ class LlamaLayer(nn.Module):
                 a = sp_attention(qkv, B, S, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, cfg.sliding_window, sp)
             else:
                 a = ops.attention_packed(qkv, B, S, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, True,
-                                         cfg.sliding_window, out_pad=p_o, grad_pad=p_qkv, docs=docs)
+                                         cfg.sliding_window, out_pad=p_o, grad_pad=p_qkv, docs=docs,
+                                         rope_grad=rargs[6] if rargs is not None else None)
         o = self.proj("o", a)
         h, x = ops.add_rms_norm(h, o, self.mlp_norm, cfg.norm_eps, pad=p_gu, grad_pad=p_o)
         mlp = self.mlp_projs(p_gu, p_down)

@@ -5,8 +5,8 @@ See ``_backend`` for the dispatch policy (HIP on GPU, loud failure if the extens
 """
 from ._backend import ext_available, kernel_mode, load_ext, use_hip  # noqa: F401
 from .activation import gelu_tanh, swiglu  # noqa: F401
-from .attention import (Segments, attention_packed, attention_reference, model_tile_len, pad_batch_to,  # noqa: F401
-                        segments_from_eos)
+from .attention import (RopeGrad, Segments, attention_packed, attention_reference, model_tile_len,  # noqa: F401
+                        pad_batch_to, segments_from_eos)
 from .decode import KVCache, decode_attention  # noqa: F401
 from .cross_entropy import cross_entropy_reference, fused_linear_cross_entropy  # noqa: F401
 from .linear import lora_linear  # noqa: F401

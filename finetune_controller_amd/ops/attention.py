@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import logging
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -157,9 +158,26 @@ def _sdpa_packed(qkv, B, S, H, KV, D, causal, window, scale, docs: Segments | No
     return o.transpose(1, 2).reshape(B * S, H * D)
 
 
+# kill switch of the RoPE-backward handoff (FTC_ROPE_BWD_FUSE=0: the producer runs the separate pass)
+ROPE_BWD_FUSE = os.environ.get("FTC_ROPE_BWD_FUSE", "1") != "0"
+
+
+class RopeGrad:
+    """Handoff between a producer that applied RoPE to the packed q / k heads (``ops.lora_linear(...,
+    rope=)``) and this attention: when the flash path runs it takes the rotation's backward into the dQ /
+    dK epilogues (``taken``; csrc/kernels/flash_attn_bwd.hip ``rope_inv_rows``) and the producer's
+    backward skips its separate inverse-rotation pass over dq / dk.  Positions: ``pos`` int32 [B*S] or
+    the row index within its sequence."""
+
+    __slots__ = ("cos", "sin", "pos", "taken")
+
+    def __init__(self, cos: torch.Tensor, sin: torch.Tensor, pos: torch.Tensor | None):
+        self.cos, self.sin, self.pos, self.taken = cos, sin, pos, False
+
+
 class _FlashPacked(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, B, S, H, KV, D, causal, window, scale, out_pad=0, grad_pad=0, docs=None):
+    def forward(ctx, qkv, B, S, H, KV, D, causal, window, scale, out_pad=0, grad_pad=0, docs=None, rope_grad=None):
         q, k, v = _split(qkv, B, S, H, KV, D)
         o, lse = ext().flash_fwd(q, k, v, B, S, H, KV, D, scale, causal, window, out_pad,
                                  docs.doc_start if docs is not None else None)
@@ -171,6 +189,11 @@ class _FlashPacked(torch.autograd.Function):
         ctx.cfg = (B, S, H, KV, D, causal, window, scale)
         ctx.grad_pad = grad_pad
         ctx.docs = docs
+        ctx.rope_grad = None
+        if rope_grad is not None and ROPE_BWD_FUSE and D == 128 and rope_grad.cos.shape[-1] == 64 and (
+                rope_grad.pos is not None or rope_grad.cos.shape[0] >= S):
+            rope_grad.taken = True
+            ctx.rope_grad = rope_grad
         return o
 
     @staticmethod
@@ -187,9 +210,12 @@ class _FlashPacked(torch.autograd.Function):
         dqkv = torch.empty(qkv.shape[0], Wd + ctx.grad_pad, dtype=qkv.dtype, device=qkv.device)[:, :Wd]
         dq, dk, dv = _split(dqkv, B, S, H, KV, D)
         docs = ctx.docs
+        rg = ctx.rope_grad
         ext().flash_bwd(q, k, v, o, do, lse, dq, dk, dv, B, S, H, KV, D, scale, causal, window,
-                        docs.doc_start if docs is not None else None, docs.doc_end if docs is not None else None)
-        return dqkv, None, None, None, None, None, None, None, None, None, None, None
+                        docs.doc_start if docs is not None else None, docs.doc_end if docs is not None else None,
+                        -1, rg.cos if rg is not None else None, rg.sin if rg is not None else None,
+                        rg.pos if rg is not None else None)
+        return dqkv, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 def _pad_segments(docs: Segments, B: int, S: int, Sp: int) -> Segments:
@@ -256,18 +282,20 @@ class _FlashPaddedTail(torch.autograd.Function):
 
 def attention_packed(qkv: torch.Tensor, B: int, S: int, H: int, KV: int, D: int, causal: bool = True,
                      window: int = 0, scale: float | None = None, out_pad: int = 0,
-                     grad_pad: int = 0, docs: Segments | None = None) -> torch.Tensor:
+                     grad_pad: int = 0, docs: Segments | None = None,
+                     rope_grad: RopeGrad | None = None) -> torch.Tensor:
     """Causal / sliding-window GQA attention on a packed ``[B*S, (H+2KV)*D]`` projection.
 
     ``out_pad`` / ``grad_pad``: the output / the gradient of ``qkv`` are column views of
     row-padded buffers (spare columns for the augmented LoRA GEMMs, ``ops.linear``).  ``docs``: packed
-    documents (causal only)."""
+    documents (causal only).  ``rope_grad``: see :class:`RopeGrad` (taken on the untiled flash path)."""
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if docs is not None and not causal:
         raise ValueError("document-masked attention is causal")
     if use_hip(qkv):
         if qkv.dtype == torch.bfloat16 and flash_supported(D, S):
-            return _FlashPacked.apply(qkv, B, S, H, KV, D, causal, int(window or 0), scale, out_pad, grad_pad, docs)
+            return _FlashPacked.apply(qkv, B, S, H, KV, D, causal, int(window or 0), scale, out_pad, grad_pad, docs,
+                                      rope_grad)
         if qkv.dtype == torch.bfloat16 and flash_usable(D, S, causal):
             return _FlashPaddedTail.apply(qkv, B, S, H, KV, D, int(window or 0), scale, out_pad, grad_pad, docs,
                                           bool(causal))

@@ -99,7 +99,7 @@ def mm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> tor
 def rope_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, rope: tuple) -> bool:
     """``out = rope(a @ b^T)`` with the rotation in the hand-written kernel's epilogue (head_dim 128), when
     the routing policy picks the kernel for this shape; False (nothing done) otherwise."""
-    cos, sin, pos, seq_len, n_rot, hd = rope
+    cos, sin, pos, seq_len, n_rot, hd = rope[:6]
     mode = _nt_mode()
     if hd != 128 or mode == "0" or not use_hip(a) or out.dtype != torch.bfloat16:
         return False

@@ -568,7 +568,7 @@ class _LoRALinearFn(torch.autograd.Function):
         ctx.mask, ctx.p_drop = mask, p_drop
         ctx.rope = rope_of  # the rotation the backward undoes on dy
         if rope is not None:  # not fused into the GEMM: rotate the output in place (csrc/kernels/elementwise.hip)
-            cos, sin, pos, seq_len, n_rot, hd = rope
+            cos, sin, pos, seq_len, n_rot, hd = rope[:6]
             ext().rope_(y, cos, sin, pos, n_rot, hd, seq_len, False)
         # trainable A/B homed in a flat grad buffer (FlatAdamW sets .main_grad): their weight
         # gradients are accumulated in place by beta=1 GEMMs instead of returned (no temporaries, no
@@ -578,9 +578,10 @@ class _LoRALinearFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        if ctx.rope is not None:
+        if ctx.rope is not None and not (len(ctx.rope) > 6 and ctx.rope[6].taken):
             # output was rope(x W^T ...): the gradient of the un-rotated product is the inverse rotation
-            cos, sin, pos, seq_len, n_rot, hd = ctx.rope
+            # (unless the consumer -- the flash backward -- already emitted it: ops.attention.RopeGrad)
+            cos, sin, pos, seq_len, n_rot, hd = ctx.rope[:6]
             if dy.dim() != 2 or dy.stride(1) != 1 or dy.stride(0) % 8:
                 dy = dy.reshape(-1, dy.shape[-1]).contiguous()
             ext().rope_(dy, cos, sin, pos, n_rot, hd, seq_len, True)
@@ -647,8 +648,9 @@ class _LoRALinearFn(torch.autograd.Function):
 def lora_linear(x: torch.Tensor, W: torch.Tensor, A: torch.Tensor | None = None, B: torch.Tensor | None = None,
                 scale: float = 1.0, bias: torch.Tensor | None = None, blocks=None,
                 aug: AugWeight | None = None, dropout: float = 0.0, rope: tuple | None = None) -> torch.Tensor:
-    """``rope`` (GPU, bf16, 2-D x): ``(cos, sin, positions int32 | None, seq_len, n_rot_heads, head_dim)`` --
-    the output's first n_rot heads are rotated (RoPE, HF rotate_half) inside the op: in the GEMM epilogue
-    when the hand-written kernel runs the projection, else in place right after it; the backward undoes
-    the rotation on the incoming gradient."""
+    """``rope`` (GPU, bf16, 2-D x): ``(cos, sin, positions int32 | None, seq_len, n_rot_heads, head_dim
+    [, RopeGrad])`` -- the output's first n_rot heads are rotated (RoPE, HF rotate_half) inside the op: in
+    the GEMM epilogue when the hand-written kernel runs the projection, else in place right after it; the
+    backward undoes the rotation on the incoming gradient, unless the optional ``ops.attention.RopeGrad``
+    handoff was taken by the consumer (the flash backward then emits dq / dk already un-rotated)."""
     return _LoRALinearFn.apply(x, W, bias, A, B, scale, blocks, aug, float(dropout), rope)

@@ -411,6 +411,92 @@ def test_flash_attention_fwd_bwd(C, B, S, H, KV, D, causal, window):
         assert err <= 2e-2 * mag + 2e-2, (lo, err, mag)
 
 
+@pytest.mark.parametrize("positions", [False, True])
+def test_flash_bwd_rope_epilogue(C, positions):
+    """flash_bwd with rope_cos / rope_sin: dq and dk leave inverse-rotated (the gradient w.r.t. the
+    un-rotated q / k, csrc/kernels/flash_attn_bwd.hip rope_inv_rows), dv untouched -- against the plain
+    kernel's dq / dk rotated back in fp32 torch (HF rotate_half, position = row in sequence or an
+    explicit int32 [B*S] table)."""
+    from finetune_controller_amd.ops.attention import _split
+
+    torch.manual_seed(0)
+    B, S, H, KV, D = 2, 512, 8, 2, 128
+    W = (H + 2 * KV) * D
+    qkv = bf(torch.randn(B * S, W, device=DEV))
+    scale = 1.0 / math.sqrt(D)
+    q, k, v = _split(qkv, B, S, H, KV, D)
+    o, lse = C.flash_fwd(q, k, v, B, S, H, KV, D, scale, True, 0, 0, None)
+    do = bf(torch.randn(B * S, H * D, device=DEV))
+    inv = 1.0 / (10000.0 ** (torch.arange(0, 64, device=DEV, dtype=torch.float32) / 64))
+    ang = torch.arange(4096, device=DEV, dtype=torch.float32)[:, None] * inv[None]
+    cos, sin = torch.cos(ang).contiguous(), torch.sin(ang).contiguous()
+    pos = (torch.randint(0, 4096, (B * S,), device=DEV, dtype=torch.int32) if positions else None)
+    outs = []
+    for rope in (False, True):
+        dqkv = torch.empty_like(qkv)
+        dq, dk, dv = _split(dqkv, B, S, H, KV, D)
+        C.flash_bwd(q, k, v, o, do, lse, dq, dk, dv, B, S, H, KV, D, scale, True, 0, None, None, -1,
+                    cos if rope else None, sin if rope else None, pos if rope else None)
+        outs.append(dqkv.float())
+    plain, fused = outs
+    p_ = pos.long() if positions else torch.arange(S, device=DEV).repeat(B)
+    c, sn = cos[p_], sin[p_]                                        # [B*S, 64]
+    ref = plain.clone()
+    for h in range(H + KV):                                         # q and k heads
+        g1, g2 = plain[:, h * D:h * D + 64], plain[:, h * D + 64:(h + 1) * D]
+        ref[:, h * D:h * D + 64] = g1 * c + g2 * sn
+        ref[:, h * D + 64:(h + 1) * D] = g2 * c - g1 * sn
+    err = (fused - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item(), err              # one bf16 rounding of a rotated value
+    torch.testing.assert_close(fused[:, (H + KV) * D:], plain[:, (H + KV) * D:], atol=0, rtol=0)  # dv
+
+
+def test_llama_rope_grad_handoff(C, monkeypatch):
+    """The LoRA qkv projection of the HIP path (head_dim 128) hands RoPE's backward to the flash
+    backward (ops.attention.RopeGrad): the handoff is taken, and every gradient of a step matches the
+    same step with the separate inverse-rotation pass (ROPE_BWD_FUSE off) to bf16 rounding."""
+    import finetune_controller_amd.ops.attention as att
+    from finetune_controller_amd.models import LoRAConfig, build_model
+    from finetune_controller_amd.models.config import ModelConfig
+
+    cfg = ModelConfig("llama", 512, 512, 2, 4, 2, 1024, 1024, 10000.0, name="llama-rope-test")  # head_dim 128
+    torch.manual_seed(0)
+    m = build_model(cfg, LoRAConfig(r=16, alpha=32), device=DEV, dtype=torch.bfloat16)
+    m.init_weights(seed=5)
+    m.freeze_base()
+    g = torch.Generator(device=DEV).manual_seed(1)
+    with torch.no_grad():
+        for layer in m.layers:
+            for p in layer.lora.values():
+                for _, _, B_s in p.segment_tensors():
+                    B_s.data.normal_(0, 0.05, generator=g)
+    ids = torch.randint(0, cfg.vocab_size, (2, 512), device=DEV)
+    labels = torch.roll(ids, -1, 1)
+    made = []
+    orig = att.RopeGrad.__init__
+
+    def spy(self, *a):
+        orig(self, *a)
+        made.append(self)
+
+    monkeypatch.setattr(att.RopeGrad, "__init__", spy)
+    monkeypatch.setenv("FTC_KERNELS", "hip")
+    grads = {}
+    for fuse in (True, False):
+        monkeypatch.setattr(att, "ROPE_BWD_FUSE", fuse)
+        made.clear()
+        for p in m.parameters():
+            p.grad = None
+        m(ids, labels).backward()
+        assert made and all(h.taken == fuse for h in made), [h.taken for h in made]
+        grads[fuse] = {n: p.grad.float().clone() for n, p in m.named_parameters() if p.grad is not None}
+    assert grads[True].keys() == grads[False].keys() and grads[True]
+    for n, ref in grads[False].items():
+        den = ref.norm().item()
+        err = (grads[True][n] - ref).norm().item() / max(den, 1e-30)
+        assert err < 2e-2, (n, err)
+
+
 @pytest.mark.parametrize("B,S,H,KV,D,window,docs", [
     (1, 1000, 8, 2, 128, 0, False),
     (1, 3000, 8, 2, 128, 0, False),
