@@ -143,17 +143,21 @@ class LlamaLayer(nn.Module):
         h, x = ops.add_rms_norm(h, delta, self.attn_norm, cfg.norm_eps, pad=p_qkv, grad_pad=p_down)
         # RoPE inside the qkv projection (fused into the GEMM epilogue where the hand-written kernel runs
         # it) for the LoRA GPU path; elsewhere the separate in-place op
-        rargs = None
-        if ("qkv" in self.lora and "qkv" not in self.qweights and ops.use_hip(x) and x.dtype == torch.bfloat16
-                and cfg.head_dim == 128 and x.dim() == 2):
+        rargs = rgrad = None
+        hip_bf16 = ops.use_hip(x) and x.dtype == torch.bfloat16 and cfg.head_dim == 128 and x.dim() == 2
+        if hip_bf16 and kv is None and getattr(self, "sp", None) is None:
+            # full-sequence attention on this rank: the flash backward may take RoPE's inverse rotation
             cos, sin = rope.get(x.device)
             pos = positions.to(torch.int32).contiguous() if positions is not None else None
-            # full-sequence attention on this rank: the flash backward may take the inverse rotation
-            rgrad = ops.RopeGrad(cos, sin, pos) if (kv is None and getattr(self, "sp", None) is None) else None
+            rgrad = ops.RopeGrad(cos, sin, pos)
+        if hip_bf16 and "qkv" in self.lora and "qkv" not in self.qweights:
+            cos, sin = rope.get(x.device)
+            pos = positions.to(torch.int32).contiguous() if positions is not None else None
             rargs = (cos, sin, pos, S, cfg.n_heads + cfg.n_kv_heads, cfg.head_dim, rgrad)
         qkv = self.proj("qkv", x, rope=rargs)
         if rargs is None:
-            qkv = ops.apply_rope_packed(qkv, rope, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, S, positions)
+            qkv = ops.apply_rope_packed(qkv, rope, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, S, positions,
+                                        handoff=rgrad)
         if kv is not None and kv[0].decoding:  # generation: one new token per sequence vs its cache
             cache, li = kv
             a = ops.decode_attention(qkv, cache.k[li], cache.v[li], cache.lens_next, cache.attend_len(),
@@ -169,7 +173,7 @@ class LlamaLayer(nn.Module):
             else:
                 a = ops.attention_packed(qkv, B, S, cfg.n_heads, cfg.n_kv_heads, cfg.head_dim, True,
                                          cfg.sliding_window, out_pad=p_o, grad_pad=p_qkv, docs=docs,
-                                         rope_grad=rargs[6] if rargs is not None else None)
+                                         rope_grad=rgrad)
         o = self.proj("o", a)
         h, x = ops.add_rms_norm(h, o, self.mlp_norm, cfg.norm_eps, pad=p_gu, grad_pad=p_o)
         mlp = self.mlp_projs(p_gu, p_down)

@@ -67,28 +67,33 @@ def _rope_ref(qkv: torch.Tensor, cos, sin, n_rot: int, D: int, seq_len: int, pos
 
 class _RopeHip(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, cos, sin, n_rot, D, seq_len, positions):
+    def forward(ctx, qkv, cos, sin, n_rot, D, seq_len, positions, handoff=None):
         ext().rope_(qkv, cos, sin, positions, n_rot, D, seq_len, False)
         ctx.mark_dirty(qkv)
         ctx.args = (cos, sin, n_rot, D, seq_len, positions)
+        ctx.handoff = handoff
         return qkv
 
     @staticmethod
     def backward(ctx, g):
+        if ctx.handoff is not None and ctx.handoff.taken:  # the flash backward emitted un-rotated dq / dk
+            return g, None, None, None, None, None, None, None
         cos, sin, n_rot, D, seq_len, positions = ctx.args
         if g.dim() != 2 or g.stride(1) != 1 or g.stride(0) % 8:
             g = g.contiguous()  # (a row-padded 2-D view is rotated in place, keeping its spare columns)
         ext().rope_(g, cos, sin, positions, n_rot, D, seq_len, True)
-        return g, None, None, None, None, None, None
+        return g, None, None, None, None, None, None, None
 
 
 def apply_rope_packed(qkv: torch.Tensor, table: RotaryTable, n_q: int, n_kv: int, head_dim: int, seq_len: int,
-                      positions: torch.Tensor | None = None) -> torch.Tensor:
-    """Rotate q and k heads of a packed ``[T, (H+2KV)*D]`` projection (in place on GPU)."""
+                      positions: torch.Tensor | None = None, handoff=None) -> torch.Tensor:
+    """Rotate q and k heads of a packed ``[T, (H+2KV)*D]`` projection (in place on GPU).  ``handoff``
+    (GPU path): an ``ops.attention.RopeGrad`` given to the consuming attention -- when the flash
+    backward takes it, this op's backward is the identity (dq / dk arrive un-rotated)."""
     cos, sin = table.get(qkv.device)
     n_rot = n_q + n_kv
     if use_hip(qkv) and qkv.dtype == torch.bfloat16:
         if positions is not None:
             positions = positions.to(torch.int32).contiguous()
-        return _RopeHip.apply(qkv, cos, sin, n_rot, head_dim, seq_len, positions)
+        return _RopeHip.apply(qkv, cos, sin, n_rot, head_dim, seq_len, positions, handoff)
     return _rope_ref(qkv, cos, sin, n_rot, head_dim, seq_len, positions, False)

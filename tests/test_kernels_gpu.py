@@ -451,25 +451,28 @@ def test_flash_bwd_rope_epilogue(C, positions):
     torch.testing.assert_close(fused[:, (H + KV) * D:], plain[:, (H + KV) * D:], atol=0, rtol=0)  # dv
 
 
-def test_llama_rope_grad_handoff(C, monkeypatch):
-    """The LoRA qkv projection of the HIP path (head_dim 128) hands RoPE's backward to the flash
-    backward (ops.attention.RopeGrad): the handoff is taken, and every gradient of a step matches the
-    same step with the separate inverse-rotation pass (ROPE_BWD_FUSE off) to bf16 rounding."""
+@pytest.mark.parametrize("method", ["lora", "full"])
+def test_llama_rope_grad_handoff(C, monkeypatch, method):
+    """RoPE's producer on the HIP path (head_dim 128: the LoRA qkv projection, or the standalone op of
+    full fine-tuning) hands its backward to the flash backward (ops.attention.RopeGrad): the handoff is
+    taken, and every gradient of a step matches the same step with the separate inverse-rotation pass
+    (ROPE_BWD_FUSE off) to bf16 rounding."""
     import finetune_controller_amd.ops.attention as att
     from finetune_controller_amd.models import LoRAConfig, build_model
     from finetune_controller_amd.models.config import ModelConfig
 
     cfg = ModelConfig("llama", 512, 512, 2, 4, 2, 1024, 1024, 10000.0, name="llama-rope-test")  # head_dim 128
     torch.manual_seed(0)
-    m = build_model(cfg, LoRAConfig(r=16, alpha=32), device=DEV, dtype=torch.bfloat16)
+    m = build_model(cfg, LoRAConfig(r=16, alpha=32) if method == "lora" else None, device=DEV, dtype=torch.bfloat16)
     m.init_weights(seed=5)
-    m.freeze_base()
-    g = torch.Generator(device=DEV).manual_seed(1)
-    with torch.no_grad():
-        for layer in m.layers:
-            for p in layer.lora.values():
-                for _, _, B_s in p.segment_tensors():
-                    B_s.data.normal_(0, 0.05, generator=g)
+    if method == "lora":
+        m.freeze_base()
+        g = torch.Generator(device=DEV).manual_seed(1)
+        with torch.no_grad():
+            for layer in m.layers:
+                for p in layer.lora.values():
+                    for _, _, B_s in p.segment_tensors():
+                        B_s.data.normal_(0, 0.05, generator=g)
     ids = torch.randint(0, cfg.vocab_size, (2, 512), device=DEV)
     labels = torch.roll(ids, -1, 1)
     made = []
