@@ -119,6 +119,11 @@ FTC_DEV bf16x8 tr_read(const char* img, int kb, int2 off) {
   return __builtin_bit_cast(bf16x8, va);
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+#ifndef BWD_PK_EXP  // dQ pass: packed-fp32 scale / shift ahead of the exponentials
+#define BWD_PK_EXP 1
+#endif
+
 struct BwdArgs {
   const uint16_t *q, *k, *v, *o, *dout;
   const float* lse;
@@ -836,10 +841,23 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
     __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    if constexpr (BWD_PK_EXP) {
+      // scale / shift as packed fp32 pairs (v_pk_fma_f32: 16 instead of 32), exponentials scalar
+      const f32x2 c2 = {a.c, a.c}, l2 = {-lse2, -lse2};
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+      for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) s[kt][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(a.c, s[kt][i], -lse2));
+        for (int i = 0; i < 16; i += 2) {
+          const f32x2 y = __builtin_elementwise_fma((f32x2){s[kt][i], s[kt][i + 1]}, c2, l2);
+          s[kt][i] = __builtin_amdgcn_exp2f(y[0]);
+          s[kt][i + 1] = __builtin_amdgcn_exp2f(y[1]);
+        }
+    } else {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[kt][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(a.c, s[kt][i], -lse2));
+    }
     const int qmin_w = q0 + wave * 32;
     const bool need_mask = (a.causal && kv0 + BK - 1 > qmin_w) || (a.window > 0 && qmin_w + 31 - kv0 >= a.window) ||
                            kv0 + BK > a.kv_valid ||
