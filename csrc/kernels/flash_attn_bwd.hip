@@ -120,8 +120,10 @@ FTC_DEV bf16x8 tr_read(const char* img, int kb, int2 off) {
 }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-#ifndef BWD_PK_EXP  // dQ pass: packed-fp32 scale / shift ahead of the exponentials
-#define BWD_PK_EXP 1
+// dQ pass: packed-fp32 scale / shift ahead of the exponentials -- off: the forward's packed form measured
+// slower (tools/pk_softmax_ab.sh, profiles/r3/pk_softmax/)
+#ifndef BWD_PK_EXP
+#define BWD_PK_EXP 0
 #endif
 
 struct BwdArgs {

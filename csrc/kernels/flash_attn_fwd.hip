@@ -50,8 +50,11 @@ constexpr int BK = 64;   // keys per tile
 #ifndef FWD_WIDE_STORE  // 16-byte O stores in the epilogue (tools/fwd_knobs_ab.sh)
 #define FWD_WIDE_STORE 1
 #endif
-#ifndef FWD_PK_SOFTMAX  // packed-fp32 scale / row-sum in the online softmax (phase B1)
-#define FWD_PK_SOFTMAX 1
+// packed-fp32 scale / row-sum in the online softmax (phase B1).  Measured slower (tools/pk_softmax_ab.sh,
+// profiles/r3/pk_softmax/: forward 0.605 / 0.615 vs 0.589 / 0.578 ms, headline 35,376 / 35,429 vs
+// 35,533 / 35,527 tok/s, one box) -> off
+#ifndef FWD_PK_SOFTMAX
+#define FWD_PK_SOFTMAX 0
 #endif
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr float LOG2E = 1.4426950408889634f;

@@ -3,6 +3,9 @@
 # and row sum as v_pk_fma_f32 / v_pk_add_f32; BWD_PK_EXP: the dQ pass's scale / shift).
 #   bash tools/pk_softmax_ab.sh build   (CPU, after the in-tree build): ab_nopk/ = a copy of the package
 #                                       whose _C.so has both flash files built with the knobs at 0
+# Result (profiles/r3/pk_softmax/, one box, knobs at 1 in the tree): forward 0.605 / 0.615 vs 0.589 /
+# 0.578 ms, headline 35,376 / 35,429 vs 35,533 / 35,527 tok/s -> the packed form is slower; both knobs
+# default to 0 (to rerun: build the tree with them at 1)
 #   bash tools/pk_softmax_ab.sh run     (GPU box): numerics of the variant, interleaved attention timings
 #                                       and headline steps of both trees
 set -o pipefail
