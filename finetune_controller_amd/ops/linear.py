@@ -578,7 +578,7 @@ class _LoRALinearFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        if ctx.rope is not None and not (len(ctx.rope) > 6 and ctx.rope[6].taken):
+        if ctx.rope is not None and not (len(ctx.rope) > 6 and ctx.rope[6] is not None and ctx.rope[6].taken):
             # output was rope(x W^T ...): the gradient of the un-rotated product is the inverse rotation
             # (unless the consumer -- the flash backward -- already emitted it: ops.attention.RopeGrad)
             cos, sin, pos, seq_len, n_rot, hd = ctx.rope[:6]
