@@ -1033,24 +1033,29 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4d_kernel(NTArgs p) {
   const int st0 = ((int)(blockIdx.x & p.stagger_mask) * p.stagger_step) % ns;
   auto phys = [&](int ss) { const int q = ss + st0; return q >= ns ? q - ns : q; };
 
-  // DMA: wave w fills rows [64 w, 64 w + 64) of both images, piece j = rows 64 w + 8 j + (lane >> 3)
+  // DMA: wave w fills rows [64 w, 64 w + 64) of both images, piece j = rows 64 w + 8 j + (lane >> 3);
+  // MODE bit 8 (interleaved): piece j of wave w = rows 32 j + 8 w + (lane >> 3), i.e. the 4 waves'
+  // j-th pieces cover 32 consecutive rows (the library's order)
+  constexpr bool IL = (MODE & 256) != 0;
+  constexpr int PSTRIDE = IL ? 4096 : 1024;  // LDS bytes between a wave's consecutive pieces
   int vo[2][2];
   {
     const int rr = lane >> 3, pc = lane & 7;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const int lc = pc ^ f5(rr + 8 * q);
-      vo[0][q] = (int)(((64 * wave + rr) * p.lda + 8 * lc) * 2);
-      vo[1][q] = (int)(((64 * wave + rr) * p.ldb + 8 * lc) * 2);
+      const int r0 = IL ? 8 * wave + rr : 64 * wave + rr;
+      const int lc = pc ^ f5(IL ? rr + 8 * (wave & 1) : rr + 8 * q);
+      vo[0][q] = (int)((r0 * p.lda + 8 * lc) * 2);
+      vo[1][q] = (int)((r0 * p.ldb + 8 * lc) * 2);
     }
   }
-  const int s8a = (int)(8 * p.lda * 2), s8b = (int)(8 * p.ldb * 2);
+  const int s8a = (int)((IL ? 32 : 8) * p.lda * 2), s8b = (int)((IL ? 32 : 8) * p.ldb * 2);
   const auto ra = make_rsrc(p.a + m0 * p.lda);
   const auto rb = make_rsrc(p.b + n0 * p.ldb);
-  char* const wbase = S + 64 * wave * 128;
+  char* const wbase = S + (IL ? 8 : 64) * wave * 128;
   auto dma = [&](int op, int ss, int j) __attribute__((always_inline)) {
     if constexpr (MODE & 2) return;
-    const void* dst = wbase + (ss & 1) * SS + op * IMG2 + j * 1024;
+    const void* dst = wbase + (ss & 1) * SS + op * IMG2 + j * PSTRIDE;
     const int soff = ((MODE & 32) ? 0 : phys(ss) * 128) + j * (op ? s8b : s8a);
     if constexpr (MODE & 1) {
       const unsigned d = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)dst;
@@ -1075,10 +1080,10 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4d_kernel(NTArgs p) {
   auto dmal = [&](int op, __amdgpu_buffer_rsrc_t r, unsigned base, int j) __attribute__((always_inline)) {
     if (j == 0)
       asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds\n\ts_mov_b32 m0, %4"
-                   :: "v"(vo[op][0]), "s"(r), "s"(base), "s"(so[op][0]), "s"(base + 1024u) : "memory");
+                   :: "v"(vo[op][0]), "s"(r), "s"(base), "s"(so[op][0]), "s"(base + (unsigned)PSTRIDE) : "memory");
     else if (j < 7)
       asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds\n\ts_mov_b32 m0, %3"
-                   :: "v"(vo[op][j & 1]), "s"(r), "s"(so[op][j]), "s"(base + (unsigned)(j + 1) * 1024u) : "memory");
+                   :: "v"(vo[op][j & 1]), "s"(r), "s"(so[op][j]), "s"(base + (unsigned)((j + 1) * PSTRIDE)) : "memory");
     else
       asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" :: "v"(vo[op][1]), "s"(r), "s"(so[op][7]) : "memory");
   };
@@ -1389,6 +1394,10 @@ extern "C" int ftc_gemm_nt(const void* a, long long lda, const void* b, long lon
       hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 2>), dim3(grid), dim3(256), 0, stream, p);
     else if (v7mode == 6)
       hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 6>), dim3(grid), dim3(256), 0, stream, p);
+    else if (v7mode == 456)
+      hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 456>), dim3(grid), dim3(256), 0, stream, p);
+    else if (v7mode == 329)
+      hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 329>), dim3(grid), dim3(256), 0, stream, p);
     else if (v7mode == 200)
       hipLaunchKernelGGL((gemm_nt_w4d_kernel<false, 200>), dim3(grid), dim3(256), 0, stream, p);
     else if (v7mode == 137)
