@@ -97,6 +97,19 @@ FTC_DEV void glds16(__amdgpu_buffer_rsrc_t r, const char* lds, int voff, int sof
       : "memory");
 }
 
+// The same piece without the leading s_nop 4 (its operands are SALU-computed long before: no
+// readfirstlane -> SGPR hazard to cover); used inside the K loop of the spread schedule.
+FTC_DEV void glds16_fast(__amdgpu_buffer_rsrc_t r, const char* lds, int voff, int soff) {
+  const unsigned dst = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)lds;
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(r), "s"(dst), "s"(soff)
+      : "memory");
+}
+
 // One K-step's DMA for this wave: PW = 32 / NW pieces of each matrix (32 KiB = 32 x 1 KiB per K-step);
 // piece c = PW wave + j covers half image c >> 4, rows 4 (c & 15) .. +4 (lane-linear).  With the
 // (r & 3) << 2 swizzle every lane's row phase is lane >> 4 whatever the piece, so one source offset
@@ -118,7 +131,14 @@ FTC_DEV void tn_dma(__amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int vo
 // NW = 4: 2 x 2 waves of 128 x 128, one wave per SIMD (512 registers; the 256 accumulator registers
 //         live in AGPRs): per MFMA a wave reads 1 fragment instead of 1.5, which takes the LDS array
 //         (tr reads + the DMA's writes) from ~90 % to ~60 % of the MFMA time per K-step.
-template <bool F32C, int NW>
+// SCHED = 1 (NW = 4, the default since round 3): the K-step's DMA is spread over its four 16-deep
+// phases.  Rows 16 q .. 16 q + 15 of an image feed only k-step q, so once every wave has read k-step q
+// (lgkmcnt(0) + a barrier at the start of phase q + 1) the pieces covering those rows may be refilled
+// with step kt + 2: 4 pieces at phase 1 (k-step 0's rows), 4 at phase 2, 8 at phase 3, each one
+// between MFMAs instead of a 16-piece burst behind the step's single barrier (whose issue cost -- M0
+// save / restore, s_nop -- left the matrix pipe idle); the next step's buffer is waited for with a
+// counted vmcnt (this step's pieces stay in flight) before the last phase reads its k-step 0.
+template <bool F32C, int NW, int SCHED = 0>
 __global__ __launch_bounds__(NW * 64, 1) void gemm_tn_kernel(GemmTNArgs p) {
   constexpr int WN = NW / 2;         // waves along N
   constexpr int WNC = BN / WN;       // columns per wave: 64 or 128
@@ -235,14 +255,110 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_tn_kernel(GemmTNArgs p) {
     if (kt + 1 < nk) read_k(nxt, 0, pa, pb);
     mfma_k(qa, qb);
   };
-  issue(0, S);
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  __builtin_amdgcn_s_barrier();
-  if (nk > 1) issue(1, S + STAGE);
-  read_k(S, 0, pa, pb);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int so = (kt & 1) * STAGE;
-    step(kt, S + so, S + (STAGE - so));
+  if constexpr (SCHED == 1) {
+    static_assert(NW == 4, "spread schedule: one wave per SIMD");
+    // refill mapping: the 8 pieces (4 rows each) of k-step q's 16 rows across both half images are
+    // split 2 per wave -- wave w takes half image w >> 1, rows 16 q + 8 (w & 1) + 4 e (e = 0, 1) -- so
+    // every wave issues the same pieces in the same phase (no wave-dependent branch around the
+    // accumulators).  The (r & 3) << 2 swizzle is q / e independent: one source offset per matrix.
+    int va2, vb2;
+    {
+      const int r = 8 * (wave & 1) + (lane >> 4);
+      const int col = (wave >> 1) * 128 + 8 * ((lane & 15) ^ swz(r));
+      va2 = (r * (int)p.lda + col) * 2;
+      vb2 = (r * (int)p.ldb + col) * 2;
+    }
+    const int dst2 = (wave >> 1) * IMG + 2 * (wave & 1) * 1024;
+    // piece (q, e) of step kt2 into `stage`
+    auto piece = [&](int kt2, char* stage, int q, int e) __attribute__((always_inline)) {
+      if (kt2 >= nk || (p.mode & 2)) return;
+      const int kk = (p.mode & 8) ? 0 : kt2;
+      const auto ra = make_rsrc(abase + (long long)kk * BK * p.lda);
+      const auto rb = make_rsrc(bbase + (long long)kk * BK * p.ldb);
+      const int off = (4 * q + e) * 1024;
+      glds16_fast(ra, stage + dst2 + off, va2, (16 * q + 4 * e) * (int)p.lda * 2);
+      glds16_fast(rb, stage + 2 * IMG + dst2 + off, vb2, (16 * q + 4 * e) * (int)p.ldb * 2);
+    };
+    // the 16 MFMAs of a phase (rows mt_lo .. mt_hi of the 4 x 4 tile grid) with piece pairs after
+    // MFMAs 3, 7, 11, 15 (slot k gets pieces[k] if k < npc)
+    auto mfma_pieces = [&](const bf16x8 (&fa)[4], const bf16x8 (&fb)[4], int mt_lo, int mt_hi, int kt2,
+                           char* stage, const int (&pq)[4], const int (&pe)[4], int npc) __attribute__((always_inline)) {
+#pragma unroll
+      for (int mt = mt_lo; mt < mt_hi; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
+          if (nt == 3 && (mt - mt_lo) < npc) {
+            __builtin_amdgcn_sched_barrier(0);
+            piece(kt2, stage, pq[mt - mt_lo], pe[mt - mt_lo]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    issue(0, S);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    if (nk > 1) issue(1, S + STAGE);
+    read_k(S, 0, pa, pb);
+    const int q0[4] = {0, 0, 0, 0}, e01[4] = {0, 1, 0, 0};
+    const int q1[4] = {1, 1, 0, 0};
+    const int q23[4] = {2, 2, 3, 3}, e23[4] = {0, 1, 0, 1};
+    for (int kt = 0; kt < nk; ++kt) {
+      const int so = (kt & 1) * STAGE;
+      char* cur = S + so;
+      const char* nxt = S + (STAGE - so);
+      // phase 0: k-step 0 (P), read k-step 1 -> Q
+      lgkm0();
+      read_k(cur, 1, qa, qb);
+      mfma_k(pa, pb);
+      // phase 1: every wave has read k-steps 0 and 1 -> refill k-step 0's rows with step kt + 2
+      lgkm0();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      read_k(cur, 2, pa, pb);
+      mfma_pieces(qa, qb, 0, 4, kt + 2, cur, q0, e01, 2);
+      // phase 2: k-step 2 read -> refill k-step 1's rows
+      lgkm0();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      read_k(cur, 3, qa, qb);
+      mfma_pieces(pa, pb, 0, 4, kt + 2, cur, q1, e01, 2);
+      // phase 3: k-step 3 read -> refill k-steps 2 and 3 over the first half of the MFMAs; then step
+      // kt + 1's buffer (16 pieces issued during step kt - 1) must have landed: only this step's 16
+      // may still fly
+      lgkm0();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_pieces(qa, qb, 0, 2, kt + 2, cur, q23, e23, 2);
+      {
+        // the other two piece pairs of k-steps 2 / 3 between MFMAs of rows 2 .. 3 would follow the
+        // wait below; issue them here, back to back with the last two of the first half
+        const int q23b[4] = {3, 3, 0, 0}, e23b[4] = {0, 1, 0, 0};
+        piece(kt + 2, cur, q23b[0], e23b[0]);
+        piece(kt + 2, cur, q23b[1], e23b[1]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (!(p.mode & 1)) {
+        if (kt + 2 < nk && !(p.mode & 2)) __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
+        else __builtin_amdgcn_s_waitcnt(0x0F70);                             // vmcnt(0)
+      }
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 1 < nk) read_k(nxt, 0, pa, pb);
+      mfma_pieces(qa, qb, 2, 4, kt + 2, cur, q23, e23, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // no DMA may land after the workgroup ends
+  } else {
+    issue(0, S);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    if (nk > 1) issue(1, S + STAGE);
+    read_k(S, 0, pa, pb);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int so = (kt & 1) * STAGE;
+      step(kt, S + so, S + (STAGE - so));
+    }
   }
 
   // ---- epilogue: lane holds C[m0 + wm 128 + mt 32 + 8 (r >> 2) + 4 hh + (r & 3)][n0 + wn WNC + nt 32 + lr];
@@ -318,10 +434,22 @@ extern "C" int ftc_gemm_tn(const void* a, long long lda, const void* b, long lon
     else
       hipLaunchKernelGGL((gemm_tn_kernel<false, 8>), dim3(grid), dim3(512), 0, stream, p);
   } else {
-    if (c_fp32)
-      hipLaunchKernelGGL((gemm_tn_kernel<true, 4>), dim3(grid), dim3(256), 0, stream, p);
-    else
-      hipLaunchKernelGGL((gemm_tn_kernel<false, 4>), dim3(grid), dim3(256), 0, stream, p);
+    // FTC_GEMM_TN_SCHED=0: the round-2 schedule (one 16-piece DMA burst behind one barrier per step)
+    static const int sched = [] {
+      const char* e = getenv("FTC_GEMM_TN_SCHED");
+      return (e && e[0] == '0') ? 0 : 1;
+    }();
+    if (sched == 1) {
+      if (c_fp32)
+        hipLaunchKernelGGL((gemm_tn_kernel<true, 4, 1>), dim3(grid), dim3(256), 0, stream, p);
+      else
+        hipLaunchKernelGGL((gemm_tn_kernel<false, 4, 1>), dim3(grid), dim3(256), 0, stream, p);
+    } else {
+      if (c_fp32)
+        hipLaunchKernelGGL((gemm_tn_kernel<true, 4>), dim3(grid), dim3(256), 0, stream, p);
+      else
+        hipLaunchKernelGGL((gemm_tn_kernel<false, 4>), dim3(grid), dim3(256), 0, stream, p);
+    }
   }
   return (int)hipGetLastError();
 }
