@@ -43,10 +43,16 @@ def flash_supported(D: int, S: int) -> bool:
 
 
 def flash_usable(D: int, S: int, causal: bool) -> bool:
-    """The flash path handles this shape: natively, or -- S not a multiple of the tile -- through tail
-    padding (``_FlashPaddedTail``: causal attention never sees the pads; non-causal attention masks
-    keys past S in the kernels, ``kv_valid``)."""
-    return FLASH_READY and D in (64, 128)
+    """The flash path handles this shape: natively, or through padding (``_FlashPaddedTail``): S not a
+    multiple of the tile gets tail rows (causal attention never sees the pads; non-causal attention
+    masks keys past S in the kernels, ``kv_valid``), a head_dim the kernels are not built for (80, 96,
+    112, ... any D <= 128) gets zero columns up to the next kernel head_dim."""
+    return FLASH_READY and 0 < D <= 128
+
+
+def kernel_head_dim(D: int) -> int:
+    """The kernels' head_dim a D <= 128 head runs at (zero-padded columns: exact, see _FlashPaddedTail)."""
+    return 64 if D <= 64 else 128
 
 
 def model_tile_len(S: int, D: int, hip: bool, dtype: torch.dtype, max_len: int) -> int:
@@ -59,7 +65,7 @@ def model_tile_len(S: int, D: int, hip: bool, dtype: torch.dtype, max_len: int) 
     (profiles/r2/prof_tail4000_attention_only.md), model-level padding costs the padded tokens'
     compute only.  Exact for causal models: pads sit at the END of each row, so no real position
     attends to them, and their labels are ignored."""
-    if not hip or dtype != torch.bfloat16 or D not in (64, 128) or S % FLASH_TILE == 0:
+    if not hip or dtype != torch.bfloat16 or not 0 < D <= 128 or S % FLASH_TILE == 0:
         return S
     Sp = -(-S // FLASH_TILE) * FLASH_TILE
     return Sp if Sp <= max_len else S
@@ -229,54 +235,86 @@ def _pad_segments(docs: Segments, B: int, S: int, Sp: int) -> Segments:
     return Segments(ds, de, pad(docs.positions, 0))
 
 
+def _pad_heads(t: torch.Tensor, B: int, S: int, Sp: int, nh: int, D: int, Dp: int) -> torch.Tensor:
+    """[B*S, nh*D] (any row stride) -> zero-padded [B*Sp, nh*Dp]: rows S..Sp and head columns D..Dp zero."""
+    out = t.new_zeros(B, Sp, nh, Dp)
+    out[:, :S, :, :D].copy_(t.reshape(B, S, nh, D) if t.is_contiguous() else t.unflatten(0, (B, S)).unflatten(2, (nh, D)))
+    return out.view(B * Sp, nh * Dp)
+
+
+def _unpad_heads(t: torch.Tensor, out: torch.Tensor, B: int, S: int, Sp: int, nh: int, D: int, Dp: int):
+    """Inverse of _pad_heads into the (column-view) ``out`` [B*S, nh*D]."""
+    out.unflatten(0, (B, S)).unflatten(2, (nh, D)).copy_(t.view(B, Sp, nh, Dp)[:, :S, :, :D])
+
+
 class _FlashPaddedTail(torch.autograd.Function):
-    """Flash attention for S not a multiple of the 256-row tile: each row is padded to
-    Sp = ceil(S/256)*256 with zero q/k/v rows at the END.  Exact: under the causal mask no real
-    query (position < S) sees a pad key (position >= S); without it the kernels mask every key >= S
-    (``kv_valid``: forward and dQ pass).  Pad queries' outputs are dropped and their output gradient
-    is zero, so they add nothing to dK/dV; the pads of a packed-document batch form a document of
-    their own.  Costs one copy of qkv / o / do / dqkv per call (about a tenth of the attention time at
-    S ~ 4k) instead of the 3x slower SDPA fallback."""
+    """Flash attention on a padded copy of the problem, for shapes the kernels do not take natively.
+
+    * S not a multiple of the 256-row tile: each row is padded to Sp = ceil(S/256)*256 with zero q/k/v
+      rows at the END.  Exact: under the causal mask no real query (position < S) sees a pad key
+      (position >= S); without it the kernels mask every key >= S (``kv_valid``: forward and dQ pass).
+      Pad queries' outputs are dropped and their output gradient is zero, so they add nothing to dK/dV;
+      the pads of a packed-document batch form a document of their own.
+    * head_dim D not in {64, 128} (D <= 128): every head is zero-padded to Dp = kernel_head_dim(D)
+      columns, with the softmax scale of the real D.  Exact: zero q/k columns add nothing to QK^T, zero
+      v columns give zero output columns (dropped), the zero output-gradient columns add nothing to dP
+      or delta, and the dq/dk/dv pad columns are dropped.
+    Costs one copy of qkv / o / do / dqkv per call (about a tenth of the attention time at S ~ 4k; the
+    head pad adds (Dp - D) / D of the attention FLOPs) instead of the 3x slower SDPA fallback."""
 
     @staticmethod
     def forward(ctx, qkv, B, S, H, KV, D, window, scale, out_pad=0, grad_pad=0, docs=None, causal=True):
         Sp = -(-S // FLASH_TILE) * FLASH_TILE
-        W = qkv.shape[1]
-        qkv_p = qkv.new_zeros(B, Sp, W)
-        qkv_p[:, :S].copy_(qkv.unflatten(0, (B, S)))
-        qkv_p = qkv_p.view(B * Sp, W)
-        docs_p = _pad_segments(docs, B, S, Sp) if docs is not None else None
-        q, k, v = _split(qkv_p, B, Sp, H, KV, D)
+        Dp = kernel_head_dim(D)
+        nh = H + 2 * KV
+        if Dp == D:
+            W = qkv.shape[1]
+            qkv_p = qkv.new_zeros(B, Sp, W)
+            qkv_p[:, :S].copy_(qkv.unflatten(0, (B, S)))
+            qkv_p = qkv_p.view(B * Sp, W)
+        else:
+            qkv_p = _pad_heads(qkv, B, S, Sp, nh, D, Dp)
+        docs_p = _pad_segments(docs, B, S, Sp) if docs is not None and Sp != S else docs
+        q, k, v = _split(qkv_p, B, Sp, H, KV, Dp)
         # causal: the pads are invisible to every real query as they are (and masking them would leave
         # late pad queries under a window with no key at all); non-causal: mask keys >= S in the kernels
-        kv_valid = -1 if causal else S
-        o_p, lse = ext().flash_fwd(q, k, v, B, Sp, H, KV, D, scale, causal, window, 0,
+        kv_valid = -1 if causal or Sp == S else S
+        o_p, lse = ext().flash_fwd(q, k, v, B, Sp, H, KV, Dp, scale, causal, window, 0,
                                    docs_p.doc_start if docs_p is not None else None, kv_valid)
         HD = H * D
         out = torch.empty(B * S, HD + out_pad, dtype=qkv.dtype, device=qkv.device)[:, :HD]
-        out.unflatten(0, (B, S)).copy_(o_p.view(B, Sp, HD)[:, :S])
+        if Dp == D:
+            out.unflatten(0, (B, S)).copy_(o_p.view(B, Sp, HD)[:, :S])
+        else:
+            _unpad_heads(o_p, out, B, S, Sp, H, D, Dp)
         ctx.save_for_backward(qkv_p, o_p, lse)
-        ctx.cfg = (B, S, Sp, H, KV, D, window, scale, grad_pad, causal)
+        ctx.cfg = (B, S, Sp, H, KV, D, Dp, window, scale, grad_pad, causal, qkv.shape[1])
         ctx.docs = docs_p
         return out
 
     @staticmethod
     def backward(ctx, do):
         qkv_p, o_p, lse = ctx.saved_tensors
-        B, S, Sp, H, KV, D, window, scale, grad_pad, causal = ctx.cfg
-        HD, W = H * D, qkv_p.shape[1]
-        do_p = do.new_zeros(B, Sp, HD)
-        do_p[:, :S].copy_(do.unflatten(0, (B, S)))
-        do_p = do_p.view(B * Sp, HD)
+        B, S, Sp, H, KV, D, Dp, window, scale, grad_pad, causal, W = ctx.cfg
+        HD = H * D
+        if Dp == D:
+            do_p = do.new_zeros(B, Sp, HD)
+            do_p[:, :S].copy_(do.unflatten(0, (B, S)))
+            do_p = do_p.view(B * Sp, HD)
+        else:
+            do_p = _pad_heads(do, B, S, Sp, H, D, Dp)
         dqkv_p = torch.empty_like(qkv_p)
-        q, k, v = _split(qkv_p, B, Sp, H, KV, D)
-        dq, dk, dv = _split(dqkv_p, B, Sp, H, KV, D)
+        q, k, v = _split(qkv_p, B, Sp, H, KV, Dp)
+        dq, dk, dv = _split(dqkv_p, B, Sp, H, KV, Dp)
         docs = ctx.docs
-        ext().flash_bwd(q, k, v, o_p, do_p, lse, dq, dk, dv, B, Sp, H, KV, D, scale, causal, window,
+        ext().flash_bwd(q, k, v, o_p, do_p, lse, dq, dk, dv, B, Sp, H, KV, Dp, scale, causal, window,
                         docs.doc_start if docs is not None else None, docs.doc_end if docs is not None else None,
-                        -1 if causal else S)
+                        -1 if causal or Sp == S else S)
         dqkv = torch.empty(B * S, W + grad_pad, dtype=qkv_p.dtype, device=qkv_p.device)[:, :W]
-        dqkv.unflatten(0, (B, S)).copy_(dqkv_p.view(B, Sp, W)[:, :S])
+        if Dp == D:
+            dqkv.unflatten(0, (B, S)).copy_(dqkv_p.view(B, Sp, W)[:, :S])
+        else:
+            _unpad_heads(dqkv_p, dqkv, B, S, Sp, H + 2 * KV, D, Dp)
         return dqkv, None, None, None, None, None, None, None, None, None, None, None
 
 

@@ -61,12 +61,23 @@ class _TorchFlash:
         dv.copy_(gv)
 
 
-@pytest.mark.parametrize("S,window,docs,causal", [(300, 0, False, True), (1000, 0, False, True), (300, 64, False, True),
-                                                  (520, 0, True, True), (300, 0, False, False),
-                                                  (1000, 0, False, False)])
-def test_padded_tail_matches_reference(monkeypatch, S, window, docs, causal):
-    monkeypatch.setattr(A, "ext", lambda: _TorchFlash())
-    B, H, KV, D = 2, 4, 2, 64
+@pytest.mark.parametrize("S,window,docs,causal,D", [(300, 0, False, True, 64), (1000, 0, False, True, 64),
+                                                    (300, 64, False, True, 64), (520, 0, True, True, 64),
+                                                    (300, 0, False, False, 64), (1000, 0, False, False, 64),
+                                                    (256, 0, False, True, 96), (300, 0, False, True, 80),
+                                                    (520, 0, True, True, 96), (300, 0, False, False, 112),
+                                                    (256, 40, False, True, 32)])
+def test_padded_tail_matches_reference(monkeypatch, S, window, docs, causal, D):
+    """Tail rows (S off the tile) and/or zero head columns (D not a kernel head_dim) are exact."""
+    seen = []
+
+    class _Rec(_TorchFlash):
+        def flash_fwd(self, q, k, v, B, S, H, KV, D, *a):
+            seen.append((S, D))
+            return super().flash_fwd(q, k, v, B, S, H, KV, D, *a)
+
+    monkeypatch.setattr(A, "ext", lambda: _Rec())
+    B, H, KV = 2, 4, 2
     torch.manual_seed(0)
     W = (H + 2 * KV) * D
     qkv = torch.randn(B * S, W, dtype=torch.float64)
@@ -87,13 +98,16 @@ def test_padded_tail_matches_reference(monkeypatch, S, window, docs, causal):
     o.backward(g.double())
     ref.backward(g)
     assert torch.allclose(x1.grad, x2.grad, atol=2e-4, rtol=1e-3)
+    assert seen == [(-(-S // 256) * 256, A.kernel_head_dim(D))]  # the kernels only ever see their own shapes
 
 
 def test_flash_usable_policy():
     assert A.flash_supported(128, 4096) and not A.flash_supported(128, 4000)
     assert A.flash_usable(128, 4000, causal=True) and A.flash_usable(64, 77, causal=True)
     assert A.flash_usable(128, 4000, causal=False)  # non-causal: the kernels mask the pad keys (kv_valid)
-    assert not A.flash_usable(96, 4096, causal=True)
+    assert A.flash_usable(96, 4096, causal=True) and A.flash_usable(80, 1000, causal=False)  # zero-padded heads
+    assert not A.flash_supported(96, 4096) and not A.flash_usable(256, 4096, causal=True)
+    assert A.kernel_head_dim(32) == 64 and A.kernel_head_dim(96) == 128
 
 
 @pytest.mark.parametrize("preset,S,docs", [("llama-tiny", 200, False), ("mistral-tiny", 300, False),

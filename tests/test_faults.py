@@ -95,7 +95,7 @@ def test_slow_final_save_does_not_trip_the_watchdog(tmp_path, monkeypatch):
     real = trmod.StepWatchdog
 
     def make(default_s, rank=0):
-        return real(0.2, rank, exit_fn=codes.append, poll_s=0.02, first_timeout_s=30.0)
+        return real(1.5, rank, exit_fn=codes.append, poll_s=0.05, first_timeout_s=30.0)
 
     monkeypatch.setattr(trmod.StepWatchdog, "from_env", staticmethod(make))
     tr = Trainer(TrainConfig(model="llama-tiny", method="lora", batch_size=1, seq_len=16, synthetic=True,
@@ -103,7 +103,7 @@ def test_slow_final_save_does_not_trip_the_watchdog(tmp_path, monkeypatch):
     orig = tr.save_artifacts
 
     def slow_save():
-        time.sleep(0.6)  # 3x the step timeout
+        time.sleep(4.5)  # 3x the step timeout (steps themselves stay well inside 1.5 s, even under xdist load)
         return orig()
 
     tr.save_artifacts = slow_save

@@ -543,6 +543,39 @@ def test_flash_tail_lengths(C, B, S, H, KV, D, window, docs, causal):
         assert err <= 2e-2 * mag + 2e-2, (lo, err, mag)
 
 
+@pytest.mark.parametrize("B,S,H,KV,D,window,causal", [
+    (2, 512, 8, 2, 96, 0, True),
+    (1, 700, 4, 4, 80, 0, True),
+    (1, 512, 6, 2, 112, 200, True),
+    (2, 300, 4, 2, 96, 0, False),
+    (1, 256, 4, 2, 32, 0, True),
+])
+def test_flash_head_dim_padded(C, B, S, H, KV, D, window, causal):
+    """head_dim outside the kernels' {64, 128} (80 / 96 / 112 / 32): attention_packed zero-pads every head
+    to the next kernel head_dim and runs the flash kernels (not SDPA), forward and backward equal to the
+    fp32 reference at the real D's softmax scale."""
+    from finetune_controller_amd.ops import attention as A
+
+    assert not A.flash_supported(D, S) and A.flash_usable(D, S, causal)
+    torch.manual_seed(0)
+    W = (H + 2 * KV) * D
+    qkv = bf(torch.randn(B * S, W + 64, device=DEV))[:, :W]  # a column view, as the qkv GEMM hands it
+    scale = 1.0 / math.sqrt(D)
+    ref_in = qkv.float().clone().requires_grad_(True)
+    ref = A.attention_reference(ref_in, B, S, H, KV, D, causal, window, scale)
+    x = qkv.detach().clone().requires_grad_(True)
+    out = A.attention_packed(x, B, S, H, KV, D, causal, window, out_pad=64, grad_pad=64)
+    assert out.grad_fn is not None and "PaddedTail" in type(out.grad_fn).__name__
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+    dout = bf(torch.randn(B * S, H * D, device=DEV))
+    ref.backward(dout.float())
+    out.backward(dout)
+    g, gr = x.grad.float(), ref_in.grad
+    for lo, hi in ((0, H * D), (H * D, (H + KV) * D), ((H + KV) * D, W)):
+        rel = ((g[:, lo:hi] - gr[:, lo:hi]).norm() / gr[:, lo:hi].norm()).item()
+        assert rel < 1.5e-2, (lo, rel)
+
+
 def test_flash_lse(C):
     torch.manual_seed(1)
     B, S, H, KV, D = 1, 256, 4, 2, 128

@@ -107,6 +107,21 @@ for s in "${STEPS[@]}"; do
       timeout -k 10 600 python bench.py --method full --steps 4 --warmup 2 --grad-accum 2 --grad-dtype bf16 \
         > gpurun_out/full_bf16.log 2>&1
       fatal $? full_bf16; grep '^{' gpurun_out/full_bf16.log | cut -c1-600 ;;
+    tn)  # TN weight-gradient GEMM: numerics on both schedules, then the per-shape table (ours vs hipBLASLt)
+      for s in 1 0; do
+        FTC_GEMM_TN_SCHED=$s timeout -k 10 300 python -m pytest tests/test_kernels_gpu.py -m gpu -x -q -k gemm_tn \
+          > gpurun_out/pytest_tn_sched$s.log 2>&1
+        fatal $? pytest_tn_sched$s; tail -1 gpurun_out/pytest_tn_sched$s.log
+      done
+      for s in 1 0 1 0; do
+        FTC_GEMM_TN_SCHED=$s timeout -k 10 300 python tools/bench_gemm_tn.py --cdtype bf16 > gpurun_out/bench_tn_sched$s.log 2>&1
+        fatal $? bench_tn_sched$s; grep '^{' gpurun_out/bench_tn_sched$s.log | cut -c1-200
+      done ;;
+    full_tn)  # full FT step: weight gradients on hipBLASLt over transposed copies (0) vs the TN kernel (1)
+      for t in 0 1 0 1; do
+        FTC_GEMM_TN=$t timeout -k 10 400 python bench.py --method full --steps 6 --warmup 2 > gpurun_out/full_tn$t.log 2>&1
+        fatal $? full_tn$t; grep '^{' gpurun_out/full_tn$t.log | cut -c80-150
+      done ;;
     gemms)
       timeout -k 10 300 python tools/bench_gemms.py > gpurun_out/bench_gemms.log 2>&1
       fatal $? gemms; tail -3 gpurun_out/bench_gemms.log ;;
