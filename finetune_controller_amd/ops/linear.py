@@ -157,6 +157,77 @@ def _grad_ready(p):
         _GRAD_READY_HOOK(p)
 
 
+# ---- weight gradients on a side stream (full fine-tuning).  dW += dy^T x is off the backward's critical
+# path (nothing downstream reads it until the optimizer), so it can run on its own HIP stream beside the
+# input-gradient GEMM, the attention / SwiGLU / norm backward kernels and the transposes: the two queues'
+# workgroups fill each other's tail waves (the qkv dW GEMM is 1.5 waves of 256x256 tiles on 256 CUs, the
+# down dW 3.5) and HBM-bound kernels run under matrix-bound ones.  Ordering, by construction:
+#   * the side stream waits for the main stream before each dW (dy and x are final);
+#   * the NEXT linear backward (and ``join_wgrad_stream``, called by the trainer after backward) makes
+#     the main stream wait for the previous dW: an input gradient that autograd later accumulates into
+#     in place (the residual stream's gradient is the down / o projections' dy) is not touched before
+#     the dW that reads it has finished -- every such accumulation happens after at least one more
+#     projection backward;
+#   * dy / x / the transposed x are record_stream'ed on the side stream (no early allocator reuse);
+#   * gradient buckets (parallel.ddp) are launched from the side stream after it has waited for main.
+# ``FTC_DW_STREAM=1`` (opt-in until measured; ``set_wgrad_stream``).
+_DW_STREAM = os.environ.get("FTC_DW_STREAM", "0") == "1"
+_DW_SIDE: dict = {}
+_DW_PENDING: list = []  # [event] of the last side-stream dW not yet waited for by the main stream
+
+
+def set_wgrad_stream(on: bool) -> None:
+    global _DW_STREAM
+    join_wgrad_stream()
+    _DW_STREAM = bool(on)
+
+
+def wgrad_stream_active() -> bool:
+    return _DW_STREAM
+
+
+def _wgrad_side(device) -> torch.cuda.Stream:
+    st = _DW_SIDE.get(device)
+    if st is None:
+        st = _DW_SIDE[device] = torch.cuda.Stream(device=device)
+    return st
+
+
+def join_wgrad_stream() -> None:
+    """Order the current stream after every weight gradient issued on the side stream so far."""
+    while _DW_PENDING:
+        torch.cuda.current_stream(_DW_PENDING[0][1]).wait_event(_DW_PENDING.pop()[0])
+
+
+def wgrad_launch_stream():
+    """The stream gradient collectives must be enqueued on (parallel.ddp): the side stream, after it has
+    waited for the main stream, while side-stream weight gradients are in flight; else None (current)."""
+    if not _DW_PENDING:
+        return None
+    dev = _DW_PENDING[0][1]
+    side = _wgrad_side(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    return side
+
+
+def _wgrad_on_side(mg: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, tn_dw: bool):
+    dev = dy2.device
+    main = torch.cuda.current_stream(dev)
+    side = _wgrad_side(dev)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        if tn_dw:
+            xt = transpose2d(x2)
+            accum_mm(mg, dy2.t(), xt.t())
+        else:
+            accum_mm(mg, dy2.t(), x2)
+        ev = torch.cuda.Event()
+        ev.record(side)
+    dy2.record_stream(side)
+    x2.record_stream(side)
+    _DW_PENDING[:] = [(ev, dev)]
+
+
 def _mask_blocks(dB: torch.Tensor, blocks):
     """Zero everything outside the diagonal blocks [(row0,row1,col0,col1), ...]."""
     if blocks is None:
@@ -578,6 +649,7 @@ class _LoRALinearFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        join_wgrad_stream()  # the previous projection's side-stream dW (see _wgrad_on_side)
         if ctx.rope is not None and not (len(ctx.rope) > 6 and ctx.rope[6] is not None and ctx.rope[6].taken):
             # output was rope(x W^T ...): the gradient of the un-rotated product is the inverse rotation
             # (unless the consumer -- the flash backward -- already emitted it: ops.attention.RopeGrad)
@@ -624,7 +696,10 @@ class _LoRALinearFn(torch.autograd.Function):
         if need_w:
             mg = getattr(W, "main_grad", None)
             if mg is not None:
-                if own_wgrad(mg, dy2, x2):
+                if (_DW_STREAM and use_hip(x2) and not own_wgrad(mg, dy2, x2)
+                        and not torch.cuda.is_current_stream_capturing()):
+                    _wgrad_on_side(mg, dy2, x2, _TN_DW)
+                elif own_wgrad(mg, dy2, x2):
                     ext().gemm_tn_(mg, dy2, x2, 1.0, 1.0)  # both operands as stored, no copies
                 elif _TN_DW and use_hip(x2):
                     # hipBLASLt runs dW += dy^T x 14-24 % faster with x handed over transposed (K-major

@@ -120,6 +120,13 @@ class GradBucketer:
         if self.launched[b]:
             return
         self.launched[b] = True
+        side = _linear.wgrad_launch_stream()
+        if side is not None:  # weight gradients are being written on the side stream: enqueue behind them
+            with torch.cuda.stream(side):
+                return self._launch_now(b)
+        return self._launch_now(b)
+
+    def _launch_now(self, b: int):
         s, e = self.buckets[b]
         view = self.opt.grad_flat[s:e]
         if self.sharded:

@@ -30,6 +30,7 @@ import torch
 from .. import ops
 from ..models import LoRAConfig, build_model, get_config
 from ..models import checkpoint as ckpt
+from ..ops.linear import join_wgrad_stream
 from ..parallel import dist as pdist
 from ..parallel.ddp import GradBucketer
 from ..utils.faults import FaultInjector, StepWatchdog
@@ -350,6 +351,7 @@ class Trainer:
             if ev:
                 ev[1].record()  # (last micro-batch's forward end)
             loss.backward()
+            join_wgrad_stream()  # side-stream weight gradients (ops.linear, FTC_DW_STREAM) are complete
             total = loss.detach() if total is None else total + loss.detach()
         if ev:
             ev[2].record()

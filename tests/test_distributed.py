@@ -390,6 +390,11 @@ _DDP_GPU = dict(model="llama3-8b-1l", batch_size=2, seq_len=512, synthetic=True,
 def _ddp_gpu_worker(rank, world, port, tmp, q, method, engine):
     os.environ["FTC_SHARE_GPU"] = "1"
     _rank_env(rank, world, port, tmp)
+    if engine.endswith("-side"):  # weight gradients on the side stream: buckets launched behind them
+        from finetune_controller_amd.ops import linear as L
+
+        L.set_wgrad_stream(True)
+        engine = engine[: -len("-side")]
     tr = Trainer(TrainConfig(method=method, checkpoint_path=tmp, comm_engine=engine,
                              bucket_mb=0.25 if method == "lora" else 64.0, **_DDP_GPU))
     tr.train_step(0.0)
@@ -400,7 +405,8 @@ def _ddp_gpu_worker(rank, world, port, tmp, q, method, engine):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("method,engine", [("lora", "torch"), ("lora", "native"), ("full", "torch")])
+@pytest.mark.parametrize("method,engine", [("lora", "torch"), ("lora", "native"), ("full", "torch"),
+                                           ("full", "torch-side")])
 def test_ddp_rccl_matches_per_rank_sum(tmp_path, method, engine):
     """DDP with 2 ranks over RCCL (sharing the card; torch.distributed or the native engine): the bucketed
     all-reduce -- launched from grad hooks mid-backward, including the grad-ready hook of weights whose

@@ -1359,6 +1359,36 @@ def test_full_ft_overlapped_update_matches_serial(C, monkeypatch, tmp_path):
     assert torch.count_nonzero(g1) == 0 and torch.count_nonzero(g0) > 0
 
 
+@pytest.mark.parametrize("grad_dtype", ["bf16", "fp32"])
+def test_full_ft_side_stream_wgrad_matches_serial(C, tmp_path, grad_dtype):
+    """Full fine-tuning with every projection's weight gradient on the side stream (ops.linear
+    _wgrad_on_side, FTC_DW_STREAM) vs on the main stream: identical losses and bitwise-identical
+    parameters, moments and gradients after three steps (same GEMMs, same operands; only the queue
+    differs)."""
+    from finetune_controller_amd.ops import linear as L
+    from finetune_controller_amd.train.trainer import TrainConfig, Trainer
+
+    res = {}
+    try:
+        for side in (True, False):
+            L.set_wgrad_stream(side)
+            tc = TrainConfig(model="llama-smoke", method="full", batch_size=2, seq_len=256, synthetic=True,
+                             max_steps=3, warmup_steps=0, schedule="constant", lr=1e-3, save_model=False,
+                             resume=False, device="cuda", grad_dtype=grad_dtype, grad_accum=2,
+                             checkpoint_path=str(tmp_path / str(side)))
+            tr = Trainer(tc)
+            losses = [tr.train_step(1e-3).float().item() for _ in range(3)]
+            assert not L._DW_PENDING  # joined by the trainer after every backward
+            torch.cuda.synchronize()
+            res[side] = (losses, tr.opt.param_flat.clone(), tr.opt.exp_avg_sq.clone(), tr.opt.grad_flat.clone())
+            tr.close()
+    finally:
+        L.set_wgrad_stream(False)
+    (l1, p1, v1, g1), (l0, p0, v0, g0) = res[True], res[False]
+    assert l1 == l0, (l1, l0)
+    assert torch.equal(g1, g0) and torch.equal(p1, p0) and torch.equal(v1, v0)
+
+
 @pytest.mark.parametrize("method", ["full", "lora"])
 def test_gpt2_steps_hip_match_torch_path(C, monkeypatch, method):
     """GPT-2 geometry (d 768, 12 heads of 64, odd vocab 50257, tied lm_head, LayerNorm/GELU, learned

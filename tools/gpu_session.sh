@@ -122,6 +122,15 @@ for s in "${STEPS[@]}"; do
         FTC_GEMM_TN=$t timeout -k 10 400 python bench.py --method full --steps 6 --warmup 2 > gpurun_out/full_tn$t.log 2>&1
         fatal $? full_tn$t; grep '^{' gpurun_out/full_tn$t.log | cut -c80-150
       done ;;
+    dw_side)  # full FT: weight gradients on a side stream (FTC_DW_STREAM=1) -- numerics, then interleaved A/B
+      timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_distributed.py -m gpu -x -v \
+        --timeout 200 --timeout-method thread -k "side_stream or rccl_matches_per_rank or overlapped" \
+        > gpurun_out/pytest_dw_side.log 2>&1
+      fatal $? pytest_dw_side; tail -3 gpurun_out/pytest_dw_side.log
+      for t in 1 0 1 0; do
+        FTC_DW_STREAM=$t timeout -k 10 400 python bench.py --method full --steps 6 --warmup 2 > gpurun_out/full_dw$t.log 2>&1
+        fatal $? full_dw$t; grep '^{' gpurun_out/full_dw$t.log | cut -c80-150
+      done ;;
     gemms)
       timeout -k 10 300 python tools/bench_gemms.py > gpurun_out/bench_gemms.log 2>&1
       fatal $? gemms; tail -3 gpurun_out/bench_gemms.log ;;
