@@ -75,6 +75,10 @@ int ftc_flash_bwd(const void* q, const void* k, const void* v, const void* o, co
 int ftc_nf4_dequant(const uint8_t* packed, const uint8_t* absmax_q, const float* absmax_scale, float absmax_offset,
                     void* out, long long n, int block, int block2, hipStream_t stream);
 int ftc_nf4_quant(const void* w, uint8_t* packed, float* absmax, long long n, int block, hipStream_t stream);
+int ftc_nf4_dequant_aug(const uint8_t* packed, const uint8_t* absmax_q, const float* absmax_scale, float absmax_offset,
+                        void* out, int rows, int cols, long long ldo, int block, int block2, int transpose, const void* B,
+                        long long ldb, void* out_b, long long ldob, const void* A, long long lda, void* out_a,
+                        long long ldoa, float s, int R, hipStream_t stream);
 int ftc_nf4_dequant_into(const uint8_t* packed, const uint8_t* absmax_q, const float* absmax_scale,
                          float absmax_offset, void* out, int rows, int cols, long long ldo, int block, int block2,
                          int transpose, hipStream_t stream);
@@ -694,6 +698,51 @@ void nf4_dequantize_into(const at::Tensor& packed, const at::Tensor& absmax_q, c
         "nf4_dequant_into");
 }
 
+// nf4_dequantize_into plus the rank-r operand parts in the same launch (csrc/kernels/nf4.hip AugTail):
+// out_b = B ([N, R] views), out_a = s * A ([R, K] views; transposed: out_a is a [K, R] view = (s A)^T).
+void nf4_dequantize_aug(const at::Tensor& packed, const at::Tensor& absmax_q, const at::Tensor& absmax_scale,
+                        double absmax_offset, at::Tensor& out, int64_t rows, int64_t cols, int64_t block,
+                        int64_t block2, bool transpose, const c10::optional<at::Tensor>& B,
+                        const c10::optional<at::Tensor>& out_b, const c10::optional<at::Tensor>& A,
+                        const c10::optional<at::Tensor>& out_a, double s) {
+  need(packed, at::kByte, "packed");
+  need(absmax_q, at::kByte, "absmax_q");
+  need(absmax_scale, at::kFloat, "absmax_scale");
+  need(out, at::kBFloat16, "out");
+  TORCH_CHECK(packed.numel() * 2 == rows * cols && absmax_q.numel() * block == rows * cols, "nf4_dequantize_aug: sizes");
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.stride(0) % 8 == 0, "nf4_dequantize_aug: out row view");
+  TORCH_CHECK(transpose ? (out.size(0) == cols && out.size(1) >= rows) : (out.size(0) == rows && out.size(1) >= cols),
+              "nf4_dequantize_aug: out shape");
+  TORCH_CHECK(B.has_value() == out_b.has_value() && A.has_value() == out_a.has_value(), "nf4_dequantize_aug: pairs");
+  int R = 0;
+  auto row_view = [](const at::Tensor& t, const char* name) {
+    need(t, at::kBFloat16, name);
+    TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1, "nf4_dequantize_aug: ", name, " must be a row view");
+  };
+  if (B) {
+    row_view(*B, "B");
+    row_view(*out_b, "out_b");
+    R = (int)B->size(1);
+    TORCH_CHECK(B->size(0) == rows && out_b->size(0) == rows && out_b->size(1) == R, "nf4_dequantize_aug: B shapes");
+  }
+  if (A) {
+    row_view(*A, "A");
+    row_view(*out_a, "out_a");
+    TORCH_CHECK(!B || A->size(0) == R, "nf4_dequantize_aug: rank of A and B");
+    R = (int)A->size(0);
+    TORCH_CHECK(A->size(1) == cols, "nf4_dequantize_aug: A shape");
+    TORCH_CHECK(transpose ? (out_a->size(0) == cols && out_a->size(1) == R) : (out_a->size(0) == R && out_a->size(1) == cols),
+                "nf4_dequantize_aug: out_a shape");
+  }
+  check(ftc_nf4_dequant_aug(packed.data_ptr<uint8_t>(), absmax_q.data_ptr<uint8_t>(), absmax_scale.data_ptr<float>(),
+                            (float)absmax_offset, out.data_ptr(), (int)rows, (int)cols, out.stride(0), (int)block,
+                            (int)block2, transpose ? 1 : 0, B ? B->data_ptr() : nullptr, B ? B->stride(0) : 0,
+                            out_b ? out_b->data_ptr() : nullptr, out_b ? out_b->stride(0) : 0,
+                            A ? A->data_ptr() : nullptr, A ? A->stride(0) : 0, out_a ? out_a->data_ptr() : nullptr,
+                            out_a ? out_a->stride(0) : 0, (float)s, R, cur_stream()),
+        "nf4_dequant_aug");
+}
+
 // y[M,N] = x[M,K] @ dequant(W)[N,K]^T  with the NF4 decode fused into the MFMA operand load
 at::Tensor nf4_linear(const at::Tensor& x, const at::Tensor& packed, const at::Tensor& absmax_q,
                       const at::Tensor& absmax_scale, double absmax_offset, int64_t N, int64_t block, int64_t block2) {
@@ -824,4 +873,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("ocol") = std::vector<int64_t>{});
   m.def("nf4_gemm_ready", [] { return true; });
   m.def("nf4_dequantize_into", &nf4_dequantize_into);
+  m.def("nf4_dequantize_aug", &nf4_dequantize_aug, py::arg("packed"), py::arg("absmax_q"), py::arg("absmax_scale"),
+        py::arg("absmax_offset"), py::arg("out"), py::arg("rows"), py::arg("cols"), py::arg("block"), py::arg("block2"),
+        py::arg("transpose"), py::arg("B") = py::none(), py::arg("out_b") = py::none(), py::arg("A") = py::none(),
+        py::arg("out_a") = py::none(), py::arg("s") = 1.0);
 }

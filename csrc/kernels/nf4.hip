@@ -47,6 +47,47 @@ FTC_DEV int nf4_encode(float x) {
   return best;
 }
 
+// The rank-r parts of the augmented QLoRA operands (ops/nf4.py _QScratch), written by extra workgroups
+// of the same dequant launch instead of 2-3 small copy / scale kernels per projection call:
+//   out_b[n * ldob + r] = B[n * ldb + r]                     (n < N, r < R; B copy)
+//   out_a[r * ldoa + k] = bf16(s * A[r * lda + k])           (forward: rows N.. of [W ; s A])
+//   out_a[k * ldoa + r] = bf16(s * A[r * lda + k])           (a_t: the transposed backward operand)
+// Same rounding as torch.mul on bf16 (fp32 product, round to nearest even).
+struct AugTail {
+  const uint16_t* B;
+  long long ldb;
+  uint16_t* out_b;
+  long long ldob;
+  const uint16_t* A;
+  long long lda;
+  uint16_t* out_a;
+  long long ldoa;
+  float s;
+  int N, R, K, a_t;
+};
+
+FTC_DEV void aug_tail_fill(const AugTail& t, long long i0, long long stride) {
+  const long long nb = t.B ? (long long)t.N * t.R : 0;
+  const long long na = t.A ? (long long)t.R * t.K : 0;
+  for (long long i = i0; i < nb + na; i += stride) {
+    if (i < nb) {
+      const long long n = i / t.R;
+      const int r = (int)(i - n * t.R);
+      t.out_b[n * t.ldob + r] = t.B[n * t.ldb + r];
+    } else {
+      const long long j = i - nb;
+      const int r = (int)(j / t.K), k = (int)(j - (long long)r * t.K);
+      const uint16_t v = f2bf(t.s * bf2f(t.A[(long long)r * t.lda + k]));
+      if (t.a_t)
+        t.out_a[(long long)k * t.ldoa + r] = v;
+      else
+        t.out_a[(long long)r * t.ldoa + k] = v;
+    }
+  }
+}
+
+constexpr int kTailBlocks = 64;  // extra workgroups of a dequant launch that carry an AugTail
+
 // one wave per block of 64 elements: lane j handles element j
 __global__ __launch_bounds__(256) void nf4_quant_kernel(const uint16_t* __restrict__ w, uint8_t* __restrict__ packed,
                                                         float* __restrict__ absmax, long long nblocks, int block) {
@@ -101,12 +142,18 @@ __global__ __launch_bounds__(256) void nf4_dequant_rows_kernel(const uint8_t* __
                                                                const uint8_t* __restrict__ aq,
                                                                const float* __restrict__ s2, float off,
                                                                uint16_t* __restrict__ out, long long n, int cols,
-                                                               long long ldo, int block, int block2) {
+                                                               long long ldo, int block, int block2, int main_blocks,
+                                                               AugTail tail) {
+  if ((int)blockIdx.x >= main_blocks) {  // block-uniform: the rank-r operand parts
+    aug_tail_fill(tail, (long long)(blockIdx.x - main_blocks) * 256 + threadIdx.x,
+                  (long long)(gridDim.x - main_blocks) * 256);
+    return;
+  }
   __shared__ float lut[16];
   nf4_lut_load(lut);
   const long long n16 = n >> 4;
   const int c16 = cols >> 4;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long long)gridDim.x * 256) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long long)main_blocks * 256) {
     const uint2 p = reinterpret_cast<const uint2*>(packed)[i];
     const long long e0 = i << 4;
     const long long bi = e0 / block;
@@ -136,7 +183,11 @@ __global__ __launch_bounds__(256) void nf4_dequant_t_kernel(const uint8_t* __res
                                                             const uint8_t* __restrict__ aq,
                                                             const float* __restrict__ s2, float off,
                                                             uint16_t* __restrict__ outT, int N, int K, long long ldo,
-                                                            int block2) {
+                                                            int block2, AugTail tail) {
+  if ((int)blockIdx.y == K / 64) {  // the extra row of workgroups: the rank-r operand parts
+    aug_tail_fill(tail, (long long)blockIdx.x * 256 + threadIdx.x, (long long)gridDim.x * 256);
+    return;
+  }
   __shared__ uint16_t tile[64][64 + 2];
   __shared__ float lut[16];
   nf4_lut_load(lut);
@@ -171,19 +222,41 @@ __global__ __launch_bounds__(256) void nf4_dequant_t_kernel(const uint8_t* __res
   }
 }
 
+extern "C" int ftc_nf4_dequant_aug(const uint8_t* packed, const uint8_t* absmax_q, const float* absmax_scale,
+                                   float absmax_offset, void* out, int rows, int cols, long long ldo, int block,
+                                   int block2, int transpose, const void* B, long long ldb, void* out_b,
+                                   long long ldob, const void* A, long long lda, void* out_a, long long ldoa, float s,
+                                   int R, hipStream_t stream);
+
 extern "C" int ftc_nf4_dequant_into(const uint8_t* packed, const uint8_t* absmax_q, const float* absmax_scale,
                                     float absmax_offset, void* out, int rows, int cols, long long ldo, int block,
                                     int block2, int transpose, hipStream_t stream) {
+  return ftc_nf4_dequant_aug(packed, absmax_q, absmax_scale, absmax_offset, out, rows, cols, ldo, block, block2,
+                             transpose, nullptr, 0, nullptr, 0, nullptr, 0, nullptr, 0, 0.f, 0, stream);
+}
+
+// As ftc_nf4_dequant_into, plus the AugTail writes (B -> out_b, s A -> out_a, transposed when a_t) in the
+// same launch; B / A may be null (that part is skipped).  R = rank rows of A / columns of B.
+extern "C" int ftc_nf4_dequant_aug(const uint8_t* packed, const uint8_t* absmax_q, const float* absmax_scale,
+                                   float absmax_offset, void* out, int rows, int cols, long long ldo, int block,
+                                   int block2, int transpose, const void* B, long long ldb, void* out_b,
+                                   long long ldob, const void* A, long long lda, void* out_a, long long ldoa, float s,
+                                   int R, hipStream_t stream) {
   if (cols % 64 != 0 || block != 64 || ldo % 8 != 0) return -1;
+  AugTail t{(const uint16_t*)B, ldb, (uint16_t*)out_b, ldob, (const uint16_t*)A, lda, (uint16_t*)out_a, ldoa, s,
+            rows, R, cols, transpose};
+  const bool has_tail = R > 0 && (B || A);
+  if (!has_tail) t.B = t.A = nullptr;
   if (transpose) {
     if (rows % 64 != 0) return -1;
-    hipLaunchKernelGGL(nf4_dequant_t_kernel, dim3(rows / 64, cols / 64), dim3(256), 0, stream, packed, absmax_q,
-                       absmax_scale, absmax_offset, (uint16_t*)out, rows, cols, ldo, block2);
+    hipLaunchKernelGGL(nf4_dequant_t_kernel, dim3(rows / 64, cols / 64 + (has_tail ? 1 : 0)), dim3(256), 0, stream,
+                       packed, absmax_q, absmax_scale, absmax_offset, (uint16_t*)out, rows, cols, ldo, block2, t);
   } else {
     const long long n = (long long)rows * cols;
     const int grid = ftc::stream_grid(n / 16, 256);
-    hipLaunchKernelGGL(nf4_dequant_rows_kernel, dim3(grid), dim3(256), 0, stream, packed, absmax_q, absmax_scale,
-                       absmax_offset, (uint16_t*)out, n, cols, ldo, block, block2);
+    hipLaunchKernelGGL(nf4_dequant_rows_kernel, dim3(grid + (has_tail ? kTailBlocks : 0)), dim3(256), 0, stream,
+                       packed, absmax_q, absmax_scale, absmax_offset, (uint16_t*)out, n, cols, ldo, block, block2, grid,
+                       t);
   }
   return (int)hipGetLastError();
 }

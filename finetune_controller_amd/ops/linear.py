@@ -168,9 +168,15 @@ def _grad_ready(p):
 #     in place (the residual stream's gradient is the down / o projections' dy) is not touched before
 #     the dW that reads it has finished -- every such accumulation happens after at least one more
 #     projection backward;
-#   * dy / x / the transposed x are record_stream'ed on the side stream (no early allocator reuse);
+#   * dy and x stay referenced until that join (no early allocator reuse, no record_stream: a
+#     record_stream'ed block is withheld from the main stream's pool until an event query says the side
+#     stream is done, which at full-FT memory pressure (218 GB of 288) ended in cache flushes and re-
+#     allocations -- 3x slower steps); the transposed x lives in one persistent side-stream buffer;
 #   * gradient buckets (parallel.ddp) are launched from the side stream after it has waited for main.
-# ``FTC_DW_STREAM=1`` (opt-in until measured; ``set_wgrad_stream``).
+# ``FTC_DW_STREAM=1`` / ``set_wgrad_stream``: opt-in.  Measured on Llama-3-8B full FT (profiles/r3/dw_side/,
+# interleaved on one box): 700.0 / 700.4 ms vs 696.8 / 697.0 ms serial -- the concurrent kernels stretch
+# (transposes 61 -> 141 us, residual adds 12 -> 1250 us while a GEMM holds the CUs) and the matrix-bound
+# GEMMs, already clock-limited by power, gain nothing from the filled tail waves.
 _DW_STREAM = os.environ.get("FTC_DW_STREAM", "0") == "1"
 _DW_SIDE: dict = {}
 _DW_PENDING: list = []  # [event] of the last side-stream dW not yet waited for by the main stream
@@ -194,9 +200,12 @@ def _wgrad_side(device) -> torch.cuda.Stream:
 
 
 def join_wgrad_stream() -> None:
-    """Order the current stream after every weight gradient issued on the side stream so far."""
-    while _DW_PENDING:
-        torch.cuda.current_stream(_DW_PENDING[0][1]).wait_event(_DW_PENDING.pop()[0])
+    """Order the current stream after every weight gradient issued on the side stream so far (and drop
+    the operand references held for it)."""
+    if _DW_PENDING:
+        ev, dev = _DW_PENDING[0][:2]
+        torch.cuda.current_stream(dev).wait_event(ev)
+        _DW_PENDING.clear()
 
 
 def wgrad_launch_stream():
@@ -210,22 +219,31 @@ def wgrad_launch_stream():
     return side
 
 
+_DW_XT: dict = {}  # device -> flat bf16 buffer for the transposed activation (side stream only)
+
+
 def _wgrad_on_side(mg: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, tn_dw: bool):
     dev = dy2.device
+    join_wgrad_stream()  # (already joined by the caller's backward; keeps one dW in flight at most)
     main = torch.cuda.current_stream(dev)
     side = _wgrad_side(dev)
+    xt = None
+    if tn_dw:
+        n = x2.shape[0] * x2.shape[1]
+        buf = _DW_XT.get(dev)
+        if buf is None or buf.numel() < n or buf.dtype != x2.dtype:
+            buf = _DW_XT[dev] = torch.empty(n, dtype=x2.dtype, device=dev)
+        xt = buf[:n].view(x2.shape[1], x2.shape[0])
     side.wait_stream(main)
     with torch.cuda.stream(side):
-        if tn_dw:
-            xt = transpose2d(x2)
+        if xt is not None:
+            transpose2d(x2, xt)
             accum_mm(mg, dy2.t(), xt.t())
         else:
             accum_mm(mg, dy2.t(), x2)
         ev = torch.cuda.Event()
         ev.record(side)
-    dy2.record_stream(side)
-    x2.record_stream(side)
-    _DW_PENDING[:] = [(ev, dev)]
+    _DW_PENDING[:] = [(ev, dev, dy2, x2)]
 
 
 def _mask_blocks(dB: torch.Tensor, blocks):

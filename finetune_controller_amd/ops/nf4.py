@@ -19,6 +19,8 @@ The backward needs ``W`` again for ``dx = dy W`` and re-decodes it (nothing weig
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ._backend import ext, use_hip
@@ -132,6 +134,27 @@ def _dequant_into(qw: NF4Weight, out: torch.Tensor, transpose: bool):
                               qw.shape[1], qw.block, qw.block2, transpose)
 
 
+# 0: the separate copy / scale kernels.  Mistral-7B QLoRA, interleaved on one box (profiles/r3/qlora_aug/):
+# 439.88 / 439.70 ms fused vs 439.85 / 439.67 separate -- neutral (the 5 us copies it removes were hidden
+# between launches); kept for the 4 fewer launches per projection call (hipGraph capture size)
+_NF4_AUG = os.environ.get("FTC_NF4_AUG", "1") != "0"
+
+
+def _dequant_aug(qw: NF4Weight, out: torch.Tensor, transpose: bool, B, out_b, A, out_a, s: float):
+    """``out`` = W (or W^T), ``out_b`` = B, ``out_a`` = s A (or (s A)^T) -- one kernel launch."""
+    if not _NF4_AUG:
+        _dequant_into(qw, out, transpose)
+        if B is not None:
+            out_b.copy_(B)
+        if transpose:
+            out_a.copy_((A * s).t())
+        else:
+            torch.mul(A, s, out=out_a)
+        return
+    ext().nf4_dequantize_aug(qw.packed, qw.absmax_q, qw.absmax_scale, qw.absmax_offset, out, qw.shape[0], qw.shape[1],
+                             qw.block, qw.block2, transpose, B, out_b, A, out_a, float(s))
+
+
 class _QLoRALinearFn(torch.autograd.Function):
     """y = x dequant(W)^T + s (x A^T) B^T with W in NF4.  On the GPU (LoRA present, padded producer
     buffers) the same augmented GEMMs as ops.linear run: the weight is dequantised straight into the
@@ -150,9 +173,8 @@ class _QLoRALinearFn(torch.autograd.Function):
         if use_aug:
             R = A.shape[0]
             sc = _QScratch.get(N, K, Rp, x2.device)
-            _dequant_into(qw, sc.fwd[:N, :K], False)
-            sc.fwd[:N, K:K + R].copy_(B)
-            torch.mul(A, scale, out=sc.fwd[N:N + R, :K])
+            # W, B and s A into [[W | B 0], [s A ; 0 | 0]] in one launch (csrc/kernels/nf4.hip AugTail)
+            _dequant_aug(qw, sc.fwd[:N, :K], False, B, sc.fwd[:N, K:K + R], A, sc.fwd[N:N + R, :K], scale)
             # the producer kernel (fused SwiGLU) may already have formed s x A^T in the spare columns
             if tails is None or not take_prefilled("fwd", x2, tails):
                 _mm_into(x2, sc.fwd[N:, :K].t(), _tail(x2, K, Rp))
@@ -183,12 +205,13 @@ class _QLoRALinearFn(torch.autograd.Function):
             if hip and A is not None and Rp > 0 and _spare_cols(dy2, N, Rp):
                 R = A.shape[0]
                 sc = _QScratch.get(N, K, Rp, dy2.device)
-                if ctx.tails is None or not take_prefilled("bwd", dy2, ctx.tails):
-                    sc.Bp[:, :R].copy_(B)
+                prefilled = ctx.tails is not None and take_prefilled("bwd", dy2, ctx.tails)
+                # W^T, (s A)^T and (unless the producer formed dy B already) B for the tail product, one launch
+                _dequant_aug(qw, sc.bwdT[:, :N], True, None if prefilled else B, None if prefilled else sc.Bp[:, :R],
+                             A, sc.bwdT[:, N:N + R], s)
+                if not prefilled:
                     _mm_into(dy2, sc.Bp, _tail(dy2, N, Rp))
                 dyb = _tail(dy2, N, R)
-                _dequant_into(qw, sc.bwdT[:, :N], True)
-                sc.bwdT[:, N:N + R].copy_((A * s).t())
                 dx = torch.mm(_wide(dy2, N + Rp), sc.bwdT.t())
             elif hip:
                 sc = _QScratch.get(N, K, 64, dy2.device)

@@ -761,6 +761,39 @@ def test_nf4_dequantize_into_rows_and_transposed(C):
     assert torch.equal(bufT[:, :N], ref.t()) and (bufT[:, N:] == 7.0).all()
 
 
+@pytest.mark.parametrize("with_b", [True, False])
+def test_nf4_dequantize_aug_fills_rank_parts(C, with_b):
+    """One launch writes W (or W^T) plus the rank-r operand parts the QLoRA augmented GEMMs need: B into
+    its columns and s*A into its rows (transposed: (s A)^T into columns) -- bitwise what the separate
+    copy / torch.mul kernels wrote, and nothing outside the views."""
+    from finetune_controller_amd.ops import nf4
+
+    torch.manual_seed(4)
+    N, K, R, Rp, s = 192, 320, 48, 64, 2.0
+    qw = nf4.NF4Weight.quantize(bf(torch.randn(N, K, device=DEV) * 0.05))
+    ref = qw.dequantize()
+    A, B = bf(torch.randn(R, K, device=DEV)), bf(torch.randn(N, R, device=DEV))
+    fwd = torch.full((N + Rp, K + Rp), 7.0, device=DEV, dtype=torch.bfloat16)
+    C.nf4_dequantize_aug(qw.packed, qw.absmax_q, qw.absmax_scale, qw.absmax_offset, fwd[:N, :K], N, K, 64, qw.block2,
+                         False, B if with_b else None, fwd[:N, K:K + R] if with_b else None, A, fwd[N:N + R, :K], s)
+    want = torch.full_like(fwd, 7.0)
+    want[:N, :K] = ref
+    if with_b:
+        want[:N, K:K + R] = B
+    want[N:N + R, :K] = A * s
+    assert torch.equal(fwd, want)
+    bwdT = torch.full((K, N + Rp), 7.0, device=DEV, dtype=torch.bfloat16)
+    Bp = torch.full((N, Rp), 7.0, device=DEV, dtype=torch.bfloat16)
+    C.nf4_dequantize_aug(qw.packed, qw.absmax_q, qw.absmax_scale, qw.absmax_offset, bwdT[:, :N], N, K, 64, qw.block2,
+                         True, B if with_b else None, Bp[:, :R] if with_b else None, A, bwdT[:, N:N + R], s)
+    wantT = torch.full_like(bwdT, 7.0)
+    wantT[:, :N] = ref.t()
+    wantT[:, N:N + R] = (A * s).t()
+    assert torch.equal(bwdT, wantT)
+    assert torch.equal(Bp[:, :R], B) if with_b else bool((Bp == 7.0).all())
+    assert (Bp[:, R:] == 7.0).all()
+
+
 def test_qlora_step_hip_matches_torch_path(C, monkeypatch):
     """Mistral-style trunk (sliding window) in QLoRA: NF4 base dequantised into the augmented operands
     (forward) and their transposed form (backward) vs the stock-PyTorch path on the same NF4 weights."""

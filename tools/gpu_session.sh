@@ -127,9 +127,21 @@ for s in "${STEPS[@]}"; do
         --timeout 200 --timeout-method thread -k "side_stream or rccl_matches_per_rank or overlapped" \
         > gpurun_out/pytest_dw_side.log 2>&1
       fatal $? pytest_dw_side; tail -3 gpurun_out/pytest_dw_side.log
-      for t in 1 0 1 0; do
-        FTC_DW_STREAM=$t timeout -k 10 400 python bench.py --method full --steps 6 --warmup 2 > gpurun_out/full_dw$t.log 2>&1
+      for t in 1a 0a 1b 0b; do
+        FTC_DW_STREAM=${t:0:1} timeout -k 10 400 python bench.py --method full --steps 6 --warmup 2 > gpurun_out/full_dw$t.log 2>&1
         fatal $? full_dw$t; grep '^{' gpurun_out/full_dw$t.log | cut -c80-150
+      done ;;
+    prof_full_dw)  # kernel table of the side-stream full-FT step
+      FTC_DW_STREAM=1 bash tools/prof_bench.sh full_dw --method full --steps 3 --warmup 2
+      fatal $? prof_full_dw ;;
+    qlora_aug)  # QLoRA: W / B / s A in one dequant launch (FTC_NF4_AUG=1) vs separate kernels -- numerics, A/B
+      timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -v --timeout 200 --timeout-method thread \
+        -k "nf4 or qlora" > gpurun_out/pytest_qlora_aug.log 2>&1
+      fatal $? pytest_qlora_aug; tail -3 gpurun_out/pytest_qlora_aug.log
+      for t in 1a 0a 1b 0b; do
+        FTC_NF4_AUG=${t:0:1} timeout -k 10 400 python bench.py --model mistral-7b --method qlora --steps 8 --warmup 3 \
+          > gpurun_out/qlora_aug$t.log 2>&1
+        fatal $? qlora_aug$t; grep '^{' gpurun_out/qlora_aug$t.log | cut -c80-150
       done ;;
     gemms)
       timeout -k 10 300 python tools/bench_gemms.py > gpurun_out/bench_gemms.log 2>&1
