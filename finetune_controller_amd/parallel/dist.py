@@ -83,12 +83,23 @@ def init_distributed(device_type: str = "auto", timeout_s: int = 1800) -> DistIn
             # one GPU per rank: a weak-scaling number from ranks sharing a card would be mislabelled
             import socket
 
-            props = torch.cuda.get_device_properties(device)
-            me = (socket.gethostname(), str(getattr(props, "uuid", "") or f"index{device.index}"), rank)
+            me = (socket.gethostname(), device_key(device), rank)
             allr: list = [None] * world
             dist.all_gather_object(allr, me)
             check_distinct_devices(allr)
     return DistInfo(rank, world, local, backend, device)
+
+
+def device_key(device: torch.device) -> str:
+    """A host-unique id of the physical GPU: its PCI domain:bus:device when the runtime reports one (never
+    shared by two cards, whatever HIP_VISIBLE_DEVICES each rank got), plus the UUID -- a UUID alone is not
+    trusted to differ between cards (some virtualised / containerised setups report one value for all)."""
+    props = torch.cuda.get_device_properties(device)
+    pci = [getattr(props, k, None) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id")]
+    uuid = str(getattr(props, "uuid", "") or "")
+    if all(v is not None for v in pci):
+        return "pci:%x:%x:%x/%s" % (pci[0], pci[1], pci[2], uuid)
+    return uuid or f"index{device.index}"
 
 
 def check_local_rank(local: int, count: int) -> None:

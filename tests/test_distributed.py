@@ -15,6 +15,7 @@ import torch
 import torch.multiprocessing as mp
 
 from finetune_controller_amd.models import checkpoint as ckpt
+from finetune_controller_amd.parallel import dist as pdist
 from finetune_controller_amd.train.data import SyntheticTokens
 from finetune_controller_amd.train.trainer import TrainConfig, Trainer
 
@@ -107,6 +108,27 @@ def test_bench_eight_ranks_on_cpu(tmp_path):
     assert out["n_gpus"] == 8 and out["world_size_pg"] == 8
     assert out["config"]["parallelism"] == "dp8" and out["config"]["global_batch"] == 8
     assert out["config"]["zero_stage"] == 0  # LoRA: plain bucketed all-reduce
+
+
+def test_device_key_prefers_pci_location(monkeypatch):
+    """Two cards that report one UUID (seen in some containerised setups) still get distinct keys from
+    their PCI location; without PCI fields the UUID, then the index, is used."""
+    from types import SimpleNamespace
+
+    props = {0: SimpleNamespace(uuid="same", pci_domain_id=0, pci_bus_id=0x11, pci_device_id=0),
+             1: SimpleNamespace(uuid="same", pci_domain_id=0, pci_bus_id=0x21, pci_device_id=0),
+             2: SimpleNamespace(uuid="u2"), 3: SimpleNamespace(uuid="")}
+    monkeypatch.setattr(torch.cuda, "get_device_properties", lambda d: props[d.index])
+    keys = [pdist.device_key(torch.device("cuda", i)) for i in range(4)]
+    assert keys[0] != keys[1] and keys[0].startswith("pci:0:11:0/")
+    assert keys[2] == "u2" and keys[3] == "index3"
+
+
+@pytest.mark.gpu
+def test_device_key_on_the_gpu():
+    key = pdist.device_key(torch.device("cuda", 0))
+    print("device key:", key)
+    assert key.startswith("pci:"), key  # this image's torch reports the PCI location
 
 
 def test_distinct_device_binding_checks():
