@@ -143,6 +143,13 @@ for s in "${STEPS[@]}"; do
           > gpurun_out/qlora_aug$t.log 2>&1
         fatal $? qlora_aug$t; grep '^{' gpurun_out/qlora_aug$t.log | cut -c80-150
       done ;;
+    hbm)  # per-kernel HBM read / write / TB/s of the 1-layer LoRA step, calibrated on a 1 GiB elementwise kernel
+      PMC_PASSES="FETCH_SIZE GRBM_GUI_ACTIVE;WRITE_SIZE GRBM_GUI_ACTIVE" timeout -k 10 600 bash tools/pmc_run.sh hbm \
+        -- python3 tools/hbm_probe.py > gpurun_out/hbm_run.log 2>&1
+      fatal $? hbm
+      python3 tools/pmc_md.py gpurun_out/pmc_hbm/p1 gpurun_out/pmc_hbm/p2 --hbm AUnaryFunctor \
+        --title "HBM per kernel: 1-layer Llama-3-8B LoRA step" > gpurun_out/hbm_step.md 2>&1
+      fatal $? hbm_md; head -30 gpurun_out/hbm_step.md ;;
     gemms)
       timeout -k 10 300 python tools/bench_gemms.py > gpurun_out/bench_gemms.log 2>&1
       fatal $? gemms; tail -3 gpurun_out/bench_gemms.log ;;

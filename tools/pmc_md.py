@@ -103,6 +103,9 @@ def main():
     ap.add_argument("--match", default=None, help="only kernels whose name contains this")
     ap.add_argument("--title", default="rocprofv3 PMC summary")
     ap.add_argument("--raw", action="store_true", help="every counter's mean per dispatch (custom passes)")
+    ap.add_argument("--hbm", default=None, metavar="CALIB_MATCH",
+                    help="per-kernel HBM read / write GB and TB/s from FETCH_SIZE + WRITE_SIZE, scaled by the "
+                         "kernel whose name contains CALIB_MATCH (1 GiB read + 1 GiB written per dispatch)")
     a = ap.parse_args()
     labels = json.load(open(a.labels)) if a.labels else None
     merged = {}
@@ -114,6 +117,8 @@ def main():
                 m["c"].setdefault(k, x / max(v["n"], 1))
     flops = {s["label"]: s for s in labels["shapes"]} if labels else {}
     print(f"# {a.title}\n")
+    if a.hbm:
+        return hbm_table(merged, a.hbm)
     if a.raw:  # per kernel: us, clock, then every counter as a mean per dispatch (cycles counters also / wave cycles)
         names = sorted({k for m in merged.values() for k in m["c"]})
         print("| kernel | disp | us | clock GHz | " + " | ".join(names) + " |")
@@ -152,6 +157,30 @@ def main():
             return "" if v is None else f"{v:.{p}f}"
         print(f"| `{key}` | {m['n']} | {us:.1f} | {f(clk, 2)} | {f(busy)} | {f(share)} | {f(tf, 0)} | {f(wia)} | "
               f"{f(wa)} | {f(lds)} | {f(hbm, 2)} |")
+
+
+def hbm_table(merged, calib_match):
+    """Achieved HBM bandwidth per kernel: counts scaled so the calibration kernel reads and writes 1 GiB."""
+    cal = [m for k, m in merged.items() if calib_match in k]
+    if not cal or "FETCH_SIZE" not in cal[0]["c"] or "WRITE_SIZE" not in cal[0]["c"]:
+        raise SystemExit(f"no calibration kernel matching {calib_match!r} with FETCH_SIZE and WRITE_SIZE")
+    gib = float(1 << 30)
+    rs, ws = gib / cal[0]["c"]["FETCH_SIZE"], gib / cal[0]["c"]["WRITE_SIZE"]
+    cus = cal[0]["ns"] / max(cal[0]["n"], 1) / 1e3
+    print(f"calibration `{calib_match}`: {cus:.1f} us per 1 GiB read + 1 GiB written = "
+          f"{2 * gib / (cus * 1e-6) / 1e12:.2f} TB/s; bytes per FETCH_SIZE count {rs:.1f}, per WRITE_SIZE count "
+          f"{ws:.1f}\n")
+    print("| kernel | disp | us | read GB | write GB | TB/s |\n|---|---|---|---|---|---|")
+    rows = []
+    for key, m in merged.items():
+        c = m["c"]
+        if "FETCH_SIZE" not in c or "WRITE_SIZE" not in c or calib_match in key:
+            continue
+        us = m["ns"] / max(m["n"], 1) / 1e3
+        rd, wr = c["FETCH_SIZE"] * rs / 1e9, c["WRITE_SIZE"] * ws / 1e9
+        rows.append((us * m["n"], key, m["n"], us, rd, wr, (rd + wr) / (us * 1e-6) / 1e3 if us else 0.0))
+    for _, key, n, us, rd, wr, tbs in sorted(rows, reverse=True):
+        print(f"| `{key}` | {n} | {us:.1f} | {rd:.3f} | {wr:.3f} | {tbs:.2f} |")
 
 
 if __name__ == "__main__":
