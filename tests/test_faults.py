@@ -61,7 +61,7 @@ def test_step_watchdog_exits_124_with_stacks(capfd):
         codes.append(code)
         fired.set()
 
-    wd = StepWatchdog(0.3, rank=3, exit_fn=exit_fn, poll_s=0.02)
+    wd = StepWatchdog(1.0, rank=3, exit_fn=exit_fn, poll_s=0.02)
     for i in range(10):  # beating keeps it quiet
         time.sleep(0.05)
         wd.beat(f"step {i}")
@@ -77,11 +77,11 @@ def test_step_watchdog_exits_124_with_stacks(capfd):
 
 def test_step_watchdog_first_step_grace():
     codes = []
-    wd = StepWatchdog(0.1, exit_fn=codes.append, poll_s=0.02, first_timeout_s=0.6)
+    wd = StepWatchdog(0.1, exit_fn=codes.append, poll_s=0.02, first_timeout_s=3.0)
     time.sleep(0.3)  # a slow first step (warm-up): past timeout_s, inside the first-step limit
     assert codes == []
     wd.beat("step 1")
-    time.sleep(0.4)  # from now on the plain limit applies
+    time.sleep(0.6)  # from now on the plain limit applies
     wd.close()
     assert codes and codes[0] == WATCHDOG_EXIT
 
