@@ -173,11 +173,11 @@ def _grad_ready(p):
 #     stream is done, which at full-FT memory pressure (218 GB of 288) ended in cache flushes and re-
 #     allocations -- 3x slower steps); the transposed x lives in one persistent side-stream buffer;
 #   * gradient buckets (parallel.ddp) are launched from the side stream after it has waited for main.
-# ``FTC_DW_STREAM=1`` / ``set_wgrad_stream``: opt-in.  Measured on Llama-3-8B full FT (profiles/r3/dw_side/,
-# interleaved on one box): 700.0 / 700.4 ms vs 696.8 / 697.0 ms serial -- the concurrent kernels stretch
-# (transposes 61 -> 141 us, residual adds 12 -> 1250 us while a GEMM holds the CUs) and the matrix-bound
-# GEMMs, already clock-limited by power, gain nothing from the filled tail waves.
-_DW_STREAM = os.environ.get("FTC_DW_STREAM", "0") == "1"
+# ``FTC_DW_STREAM`` (default on; ``0`` = every dW on the main stream) / ``set_wgrad_stream``.  Measured on
+# Llama-3-8B full FT, interleaved on one box (profiles/r3/dw_side/): with the dW issued BEFORE the input-
+# gradient GEMM (the two run concurrently) 702.1 / 700.8 ms vs 705.2 / 705.9 ms serial (+0.5 %); issued
+# after it (so only the following kernels overlap) it had measured 700.0 / 700.4 vs 696.8 / 697.0 (-0.5 %).
+_DW_STREAM = os.environ.get("FTC_DW_STREAM", "1") != "0"
 _DW_SIDE: dict = {}
 _DW_PENDING: list = []  # [event] of the last side-stream dW not yet waited for by the main stream
 
@@ -686,6 +686,13 @@ class _LoRALinearFn(torch.autograd.Function):
         dx = dW = db = dA = dB = None
         dyb = None
         xa_scaled = ctx.aug_fwd
+        side_dw = False
+        if need_w and _DW_STREAM and use_hip(x2) and not torch.cuda.is_current_stream_capturing():
+            mg = getattr(W, "main_grad", None)
+            if mg is not None and not own_wgrad(mg, dy2, x2):
+                # issued before the input-gradient GEMM so that the two run concurrently
+                _wgrad_on_side(mg, dy2, x2, _TN_DW)
+                side_dw = True
         if (need_x and aug is not None and A is not None and aug.owns(W) and _spare_cols(dy2, N, aug.Rp)):
             # dx = [dy | dy B | 0] . [W ; s A ; 0]: dy B lands in the spare columns of the producer's buffer
             Rp = aug.Rp
@@ -714,9 +721,8 @@ class _LoRALinearFn(torch.autograd.Function):
         if need_w:
             mg = getattr(W, "main_grad", None)
             if mg is not None:
-                if (_DW_STREAM and use_hip(x2) and not own_wgrad(mg, dy2, x2)
-                        and not torch.cuda.is_current_stream_capturing()):
-                    _wgrad_on_side(mg, dy2, x2, _TN_DW)
+                if side_dw:
+                    pass  # issued above, on the side stream
                 elif own_wgrad(mg, dy2, x2):
                     ext().gemm_tn_(mg, dy2, x2, 1.0, 1.0)  # both operands as stored, no copies
                 elif _TN_DW and use_hip(x2):

@@ -412,11 +412,12 @@ _DDP_GPU = dict(model="llama3-8b-1l", batch_size=2, seq_len=512, synthetic=True,
 def _ddp_gpu_worker(rank, world, port, tmp, q, method, engine):
     os.environ["FTC_SHARE_GPU"] = "1"
     _rank_env(rank, world, port, tmp)
-    if engine.endswith("-side"):  # weight gradients on the side stream: buckets launched behind them
-        from finetune_controller_amd.ops import linear as L
+    from finetune_controller_amd.ops import linear as L
 
-        L.set_wgrad_stream(True)
-        engine = engine[: -len("-side")]
+    # "-side": weight gradients on the side stream (the default), buckets launched behind them; plain
+    # engine names pin the main-stream path
+    L.set_wgrad_stream(engine.endswith("-side"))
+    engine = engine.removesuffix("-side")
     tr = Trainer(TrainConfig(method=method, checkpoint_path=tmp, comm_engine=engine,
                              bucket_mb=0.25 if method == "lora" else 64.0, **_DDP_GPU))
     tr.train_step(0.0)

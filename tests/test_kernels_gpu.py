@@ -1402,6 +1402,7 @@ def test_full_ft_side_stream_wgrad_matches_serial(C, tmp_path, grad_dtype):
     from finetune_controller_amd.train.trainer import TrainConfig, Trainer
 
     res = {}
+    prior = L.wgrad_stream_active()
     try:
         for side in (True, False):
             L.set_wgrad_stream(side)
@@ -1416,7 +1417,7 @@ def test_full_ft_side_stream_wgrad_matches_serial(C, tmp_path, grad_dtype):
             res[side] = (losses, tr.opt.param_flat.clone(), tr.opt.exp_avg_sq.clone(), tr.opt.grad_flat.clone())
             tr.close()
     finally:
-        L.set_wgrad_stream(False)
+        L.set_wgrad_stream(prior)
     (l1, p1, v1, g1), (l0, p0, v0, g0) = res[True], res[False]
     assert l1 == l0, (l1, l0)
     assert torch.equal(g1, g0) and torch.equal(p1, p0) and torch.equal(v1, v0)
