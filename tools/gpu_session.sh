@@ -150,6 +150,14 @@ for s in "${STEPS[@]}"; do
       python3 tools/pmc_md.py gpurun_out/pmc_hbm/p1 gpurun_out/pmc_hbm/p2 --hbm AUnaryFunctor \
         --title "HBM per kernel: 1-layer Llama-3-8B LoRA step" > gpurun_out/hbm_step.md 2>&1
       fatal $? hbm_md; head -30 gpurun_out/hbm_step.md ;;
+    lora_wg)  # LoRA: adapter weight gradients on the side stream (FTC_LORA_WG_STREAM=1) -- numerics, headline A/B
+      timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -v --timeout 200 --timeout-method thread \
+        -k "side_stream" > gpurun_out/pytest_lora_wg.log 2>&1
+      fatal $? pytest_lora_wg; tail -3 gpurun_out/pytest_lora_wg.log
+      for t in 1a 0a 1b 0b; do
+        FTC_LORA_WG_STREAM=${t:0:1} timeout -k 10 400 python bench.py --steps 10 --warmup 3 > gpurun_out/lora_wg$t.log 2>&1
+        fatal $? lora_wg$t; grep '^{' gpurun_out/lora_wg$t.log | cut -c80-150
+      done ;;
     gemms)
       timeout -k 10 300 python tools/bench_gemms.py > gpurun_out/bench_gemms.log 2>&1
       fatal $? gemms; tail -3 gpurun_out/bench_gemms.log ;;
