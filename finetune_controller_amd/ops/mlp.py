@@ -29,6 +29,7 @@ import os
 import torch
 
 from ._backend import ext, use_hip
+from . import linear as _L
 from .gemm import mm as gemm_mm
 from .linear import _accum_xty, _grad_ready, _spare_cols, _tail, _wide, tail_product, tn_backward
 
@@ -152,6 +153,7 @@ class _LoRAMLPFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        _L.join_wgrad_stream()  # the previous projection's side-stream weight gradients (ops.linear)
         x2, gu, h = ctx.saved_tensors
         A_gu, B_gu, A_dn, B_dn = ctx.params
         gu_p, dn_p = ctx.proj
@@ -162,24 +164,41 @@ class _LoRAMLPFn(torch.autograd.Function):
             buf = torch.empty(dy2.shape[0], d + dn_p.Rp, dtype=dy2.dtype, device=dy2.device)
             buf[:, :d].copy_(dy2)
             dy2 = buf[:, :d]
+        side = _L._LORA_WG_STREAM and dy2.is_cuda and not torch.cuda.is_current_stream_capturing()
         # 4. dy B_down into dy's spare columns, dh through the augmented (TN) operand
         tail_product(dy2, d, dn_p.Rp, dn_p.bwd_tail(), dn_p.nct)
         dyb_dn = _tail(dy2, d, dn_p.R)
+        # 5. dB_down += dy^T (s h A_down^T) -- on the side stream under the dh GEMM (ops.linear _on_side)
+        hta = _tail(h, F, dn_p.R)
+
+        def db_down():
+            _accum_xty(B_dn.main_grad, dy2, hta, 1.0)
+            _grad_ready(B_dn)
+
+        if side:
+            _L._on_side(dy2.device, db_down, dy2, hta)
         dh = gemm_mm(_wide(dy2, d + dn_p.Rp), dn_p.bwd_weight())
-        # 5. dB_down += dy^T (s h A_down^T)
-        _accum_xty(B_dn.main_grad, dy2, _tail(h, F, dn_p.R), 1.0)
-        _grad_ready(B_dn)
+        if not side:
+            db_down()
         # 6. SwiGLU backward + dgu B_gu + dB_gu + dA_down
         dgu = ext().swiglu_bwd_wgrad(dh, gu, gu_p.Rp, gu_p.bwd_tail(), _tail(x2, K, 32), dyb_dn, B_gu.main_grad,
                                      A_dn.main_grad, 1.0, dn_p.s)
         _grad_ready(B_gu)
         _grad_ready(A_dn)
-        # 7. dx and dA_gu += s x^T (dgu B_gu)
+        # 7. dx and dA_gu += s x^T (dgu B_gu) (the latter on the side stream under the dx GEMM)
+        dgt = _tail(dgu, N, gu_p.R)
+
+        def da_gu():
+            _accum_xty(A_gu.main_grad.t(), x2, dgt, gu_p.s)
+            _grad_ready(A_gu)
+
+        if side:
+            _L._on_side(dgu.device, da_gu, x2, dgt, dgu)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = gemm_mm(_wide(dgu, N + gu_p.Rp), gu_p.bwd_weight()).view(ctx.shp)
-        _accum_xty(A_gu.main_grad.t(), x2, _tail(dgu, N, gu_p.R), gu_p.s)
-        _grad_ready(A_gu)
+        if not side:
+            da_gu()
         return dx, None, None, None, None, None, None
 
 
