@@ -248,7 +248,9 @@ def _wgrad_on_side(mg: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, tn_dw:
 
 # LoRA adapter weight gradients (dA, dB into their flat-buffer main_grad) on the same side stream, issued
 # between the rank-r tail product and the input-gradient GEMM so they run under it; same ordering rules
-# as the full-FT dW above.  ``FTC_LORA_WG_STREAM=1`` (opt-in until measured on the headline step).
+# as the full-FT dW above.  ``FTC_LORA_WG_STREAM=1``: opt-in -- measured on the headline step (interleaved, one
+# box, profiles/r3/lora_wg/): 35,213 / 35,138 vs 35,562 / 35,473 tok/s serial (-1.0 %): the 30 us rank-r
+# kernels stretch the big GEMMs they share the CUs with more than their own time.
 _LORA_WG_STREAM = os.environ.get("FTC_LORA_WG_STREAM", "0") == "1"
 
 
