@@ -158,6 +158,11 @@ for s in "${STEPS[@]}"; do
         FTC_LORA_WG_STREAM=${t:0:1} timeout -k 10 400 python bench.py --steps 10 --warmup 3 > gpurun_out/lora_wg$t.log 2>&1
         fatal $? lora_wg$t; grep '^{' gpurun_out/lora_wg$t.log | cut -c80-150
       done ;;
+    wgrad_wgs)  # swiglu_bwd_wgrad workgroup-count sweep (FTC_WGRAD_WGS: token-row blocks x column blocks)
+      for w in 512 256 768 1024 1536 2048 512; do
+        FTC_WGRAD_WGS=$w timeout -k 10 200 python tools/bench_swiglu_tail.py > gpurun_out/wgrad_wgs$w.log 2>&1
+        fatal $? wgrad_wgs$w; echo "WGS=$w $(grep -E 'bwd_fused_wgrad|bwd_swiglu_only' gpurun_out/wgrad_wgs$w.log | tr '\n' ' ')"
+      done ;;
     gemms)
       timeout -k 10 300 python tools/bench_gemms.py > gpurun_out/bench_gemms.log 2>&1
       fatal $? gemms; tail -3 gpurun_out/bench_gemms.log ;;
