@@ -222,7 +222,7 @@ def wgrad_launch_stream():
 _DW_XT: dict = {}  # device -> flat bf16 buffer for the transposed activation (side stream only)
 
 
-def _wgrad_on_side(mg: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, tn_dw: bool):
+def _wgrad_on_side(mg: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, tn_dw: bool, beta: float = 1.0):
     dev = dy2.device
     join_wgrad_stream()  # (already joined by the caller's backward; keeps one dW in flight at most)
     main = torch.cuda.current_stream(dev)
@@ -238,9 +238,9 @@ def _wgrad_on_side(mg: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, tn_dw:
     with torch.cuda.stream(side):
         if xt is not None:
             transpose2d(x2, xt)
-            accum_mm(mg, dy2.t(), xt.t())
+            accum_mm(mg, dy2.t(), xt.t(), beta=beta)
         else:
-            accum_mm(mg, dy2.t(), x2)
+            accum_mm(mg, dy2.t(), x2, beta=beta)
         ev = torch.cuda.Event()
         ev.record(side)
     _DW_PENDING[:] = [(ev, dev, dy2, x2)]
@@ -392,15 +392,70 @@ def transposed_weight(W: torch.Tensor) -> torch.Tensor | None:
     return (param_t if W.requires_grad else frozen_t).get(W)
 
 
-def accum_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, alpha: float = 1.0) -> torch.Tensor:
-    """``out += alpha * a @ b``.  ``out`` may be wider than the operands (fp32 gradient buffer with
-    bf16 activations): on the GPU one GEMM with bf16 A/B and an fp32 C/D (beta = 1, in place), so
-    the accumulation never rounds to bf16."""
+def accum_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, alpha: float = 1.0,
+             beta: float = 1.0) -> torch.Tensor:
+    """``out = beta * out + alpha * a @ b`` (beta 0: ``out``'s old values are ignored, NaNs included).
+    ``out`` may be wider than the operands (fp32 gradient buffer with bf16 activations): on the GPU one
+    GEMM with bf16 A/B and an fp32 C/D (in place), so the accumulation never rounds to bf16."""
     if out.dtype == a.dtype:
-        return out.addmm_(a, b, alpha=alpha)
+        return out.addmm_(a, b, beta=beta, alpha=alpha)
     if a.is_cuda:
-        return torch.addmm(out, a, b, alpha=alpha, out_dtype=out.dtype, out=out)
-    return out.addmm_(a.to(out.dtype), b.to(out.dtype), alpha=alpha)
+        return torch.addmm(out, a, b, beta=beta, alpha=alpha, out_dtype=out.dtype, out=out)
+    return out.addmm_(a.to(out.dtype), b.to(out.dtype), beta=beta, alpha=alpha)
+
+
+# ---- first-write weight gradients (full fine-tuning).  Zeroing the 16 GB gradient buffer of Llama-3-8B
+# costs 2.8 ms per step; the projection weights (7 of its 8 B parameters) are each written by exactly one
+# beta = 1 GEMM per micro-batch, so the optimizer skips their slices (FlatAdamW.zero_grad) and marks them
+# "fresh": their first GEMM of the step runs with beta = 0 instead.  A weight joins the set only after a
+# step in which it was zeroed and written by that GEMM; one that a step leaves fresh (never written) is
+# zeroed by ``flush_fresh`` before the gradients are used.  ``FTC_GRAD_FIRST_WRITE=1`` (opt-in).
+_FIRST_WRITE = os.environ.get("FTC_GRAD_FIRST_WRITE", "0") == "1"
+# id(param) -> (weakref(param), its main_grad view): weights only a projection GEMM writes.  Entries are
+# identity-checked (a dead parameter's id can be reused by a new tensor of another trainer)
+_GRAD_OWNED: dict = {}
+_GRAD_FRESH: set = set()  # ids whose main_grad still holds last step's values
+
+
+def set_first_write(on: bool) -> None:
+    global _FIRST_WRITE
+    _FIRST_WRITE = bool(on)
+    _GRAD_OWNED.clear()
+    _GRAD_FRESH.clear()
+
+
+def is_grad_owned(p) -> bool:
+    e = _GRAD_OWNED.get(id(p)) if _FIRST_WRITE else None
+    return e is not None and e[0]() is p
+
+
+def mark_fresh(ids) -> None:
+    _GRAD_FRESH.update(ids)
+
+
+def take_fresh(p, mg: torch.Tensor) -> float:
+    """beta for the projection GEMM that writes ``p``'s gradient now: 0 on its first write of the step
+    when the optimizer skipped zeroing it, else 1 (and ``p`` is registered for the next step)."""
+    if not _FIRST_WRITE or (mg.is_cuda and torch.cuda.is_current_stream_capturing()):
+        return 1.0
+    pid = id(p)
+    e = _GRAD_OWNED.get(pid)
+    if e is None or e[0]() is not p:  # first sight of this parameter: its gradient was zeroed this step
+        _GRAD_OWNED[pid] = (weakref.ref(p), mg)
+        _GRAD_FRESH.discard(pid)
+        return 1.0
+    if pid in _GRAD_FRESH:
+        _GRAD_FRESH.discard(pid)
+        return 0.0
+    return 1.0
+
+
+def flush_fresh() -> None:
+    """Zero the gradient of every skipped weight that this step did not write (call before reading them)."""
+    while _GRAD_FRESH:
+        e = _GRAD_OWNED.get(_GRAD_FRESH.pop())
+        if e is not None and e[0]() is not None:
+            e[1].zero_()
 
 
 def _mm_into(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor):
@@ -719,7 +774,7 @@ class _LoRALinearFn(torch.autograd.Function):
             mg = getattr(W, "main_grad", None)
             if mg is not None and not own_wgrad(mg, dy2, x2):
                 # issued before the input-gradient GEMM so that the two run concurrently
-                _wgrad_on_side(mg, dy2, x2, _TN_DW)
+                _wgrad_on_side(mg, dy2, x2, _TN_DW, take_fresh(W, mg))
                 side_dw = True
         if (need_x and aug is not None and A is not None and aug.owns(W) and _spare_cols(dy2, N, aug.Rp)):
             # dx = [dy | dy B | 0] . [W ; s A ; 0]: dy B lands in the spare columns of the producer's buffer
@@ -759,13 +814,13 @@ class _LoRALinearFn(torch.autograd.Function):
                 if side_dw:
                     pass  # issued above, on the side stream
                 elif own_wgrad(mg, dy2, x2):
-                    ext().gemm_tn_(mg, dy2, x2, 1.0, 1.0)  # both operands as stored, no copies
+                    ext().gemm_tn_(mg, dy2, x2, 1.0, take_fresh(W, mg))  # both operands as stored, no copies
                 elif _TN_DW and use_hip(x2):
                     # hipBLASLt runs dW += dy^T x 14-24 % faster with x handed over transposed (K-major
                     # reduction operand, tools/bench_dw_gemm.py); the transpose streams at HBM rate
-                    accum_mm(mg, dy2.t(), transpose2d(x2).t())
+                    accum_mm(mg, dy2.t(), transpose2d(x2).t(), beta=take_fresh(W, mg))
                 else:
-                    accum_mm(mg, dy2.t(), x2)
+                    accum_mm(mg, dy2.t(), x2, beta=take_fresh(W, mg))
                 _grad_ready(W)
             else:
                 dW = dy2.t() @ x2

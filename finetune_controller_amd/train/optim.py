@@ -34,6 +34,7 @@ import math
 import torch
 
 from ..ops._backend import ext, use_hip
+from ..ops import linear as _linear
 from ..ops.linear import bump_param_generation
 
 ALIGN = 64  # elements: keeps every view 128-byte aligned for 16-byte vector access
@@ -180,7 +181,31 @@ class FlatAdamW:
 
     def zero_grad(self):
         if self._events is None:
-            self.grad_flat.zero_()
+            mine = [i for i, p in enumerate(self.params) if _linear.is_grad_owned(p)] if _linear._FIRST_WRITE else []
+            if mine and not (self.grad_flat.is_cuda and torch.cuda.is_current_stream_capturing()):
+                # projection weights: their first GEMM of the step overwrites (ops.linear take_fresh)
+                key = tuple(mine)
+                if getattr(self, "_zero_key", None) != key:
+                    skip = set(mine)
+                    runs, lo, hi = [], None, None
+                    for i, (o, n) in enumerate(self.offsets):
+                        end = self.offsets[i + 1][0] if i + 1 < len(self.offsets) else self.numel
+                        if i in skip:
+                            continue
+                        if lo is not None and o == hi:
+                            hi = end
+                        else:
+                            if lo is not None:
+                                runs.append((lo, hi))
+                            lo, hi = o, end
+                    if lo is not None:
+                        runs.append((lo, hi))
+                    self._zero_key, self._zero_runs = key, runs
+                for lo, hi in self._zero_runs:
+                    self.grad_flat[lo:hi].zero_()
+                _linear.mark_fresh(id(self.params[i]) for i in mine)
+            else:
+                self.grad_flat.zero_()
         if self._fold_hooks:
             for p in self.params:
                 p.grad = None

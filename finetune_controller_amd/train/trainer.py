@@ -30,7 +30,7 @@ import torch
 from .. import ops
 from ..models import LoRAConfig, build_model, get_config
 from ..models import checkpoint as ckpt
-from ..ops.linear import join_wgrad_stream
+from ..ops.linear import flush_fresh, join_wgrad_stream
 from ..parallel import dist as pdist
 from ..parallel.ddp import GradBucketer
 from ..utils.faults import FaultInjector, StepWatchdog
@@ -353,6 +353,7 @@ class Trainer:
             loss.backward()
             join_wgrad_stream()  # side-stream weight gradients (ops.linear, FTC_DW_STREAM) are complete
             total = loss.detach() if total is None else total + loss.detach()
+        flush_fresh()  # skipped-zeroing weights this step never wrote (ops.linear first-write gradients)
         if ev:
             ev[2].record()
         probe = tc.comm_probe and self.device.type == "cuda" and self.ddp.enabled

@@ -1423,6 +1423,39 @@ def test_full_ft_side_stream_wgrad_matches_serial(C, tmp_path, grad_dtype):
     assert torch.equal(g1, g0) and torch.equal(p1, p0) and torch.equal(v1, v0)
 
 
+@pytest.mark.parametrize("grad_dtype", ["bf16", "fp32"])
+def test_full_ft_first_write_grads_match_zeroed(C, tmp_path, grad_dtype):
+    """Full fine-tuning with the projection weights' gradient slices left unzeroed and written by a beta = 0
+    first GEMM (ops.linear FTC_GRAD_FIRST_WRITE) vs the zeroed buffer: same losses, gradients and
+    parameters over three steps of grad accumulation 2 (the library may pick another GEMM solution for
+    beta = 0: equal up to its rounding)."""
+    from finetune_controller_amd.ops import linear as L
+    from finetune_controller_amd.train.trainer import TrainConfig, Trainer
+
+    res = {}
+    prior = L._FIRST_WRITE
+    try:
+        for fw in (True, False):
+            L.set_first_write(fw)
+            tc = TrainConfig(model="llama-smoke", method="full", batch_size=2, seq_len=256, synthetic=True,
+                             max_steps=3, warmup_steps=0, schedule="constant", lr=1e-3, save_model=False,
+                             resume=False, device="cuda", grad_dtype=grad_dtype, grad_accum=2,
+                             checkpoint_path=str(tmp_path / str(fw)))
+            tr = Trainer(tc)
+            losses = [tr.train_step(1e-3).float().item() for _ in range(3)]
+            torch.cuda.synchronize()
+            res[fw] = (losses, tr.opt.param_flat.float().clone(), tr.opt.grad_flat.float().clone(),
+                       sum(1 for p in tr.opt.params if L.is_grad_owned(p)))
+            tr.close()
+    finally:
+        L.set_first_write(prior)
+    (l1, p1, g1, owned), (l0, p0, g0, _) = res[True], res[False]
+    assert owned > 0  # the projection weights were taken off the zeroing pass
+    assert max(abs(a - b) / abs(b) for a, b in zip(l1, l0)) < 1e-3, (l1, l0)
+    assert ((g1 - g0).norm() / g0.norm()).item() < 1e-2
+    assert ((p1 - p0).norm() / p0.norm()).item() < 1e-4
+
+
 def test_lora_side_stream_wgrad_matches_serial(C, tmp_path):
     """LoRA adapter weight gradients of the attention projections on the side stream (ops.linear
     FTC_LORA_WG_STREAM) vs on the main stream: bitwise-identical losses, adapter gradients and

@@ -163,6 +163,15 @@ for s in "${STEPS[@]}"; do
         FTC_WGRAD_WGS=$w timeout -k 10 200 python tools/bench_swiglu_tail.py > gpurun_out/wgrad_wgs$w.log 2>&1
         fatal $? wgrad_wgs$w; echo "WGS=$w $(grep -E 'bwd_fused_wgrad|bwd_swiglu_only' gpurun_out/wgrad_wgs$w.log | tr '\n' ' ')"
       done ;;
+    first_write)  # full FT: projection-weight gradients written by a beta = 0 first GEMM instead of zeroed -- A/B
+      timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -v --timeout 200 --timeout-method thread \
+        -k "first_write or side_stream" > gpurun_out/pytest_first_write.log 2>&1
+      fatal $? pytest_first_write; tail -3 gpurun_out/pytest_first_write.log
+      for t in 1a 0a 1b 0b; do
+        FTC_GRAD_FIRST_WRITE=${t:0:1} timeout -k 10 400 python bench.py --method full --steps 6 --warmup 2 \
+          > gpurun_out/first_write$t.log 2>&1
+        fatal $? first_write$t; grep '^{' gpurun_out/first_write$t.log | cut -c80-150
+      done ;;
     gemms)
       timeout -k 10 300 python tools/bench_gemms.py > gpurun_out/bench_gemms.log 2>&1
       fatal $? gemms; tail -3 gpurun_out/bench_gemms.log ;;
