@@ -409,8 +409,10 @@ def accum_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, alpha: float =
 # beta = 1 GEMM per micro-batch, so the optimizer skips their slices (FlatAdamW.zero_grad) and marks them
 # "fresh": their first GEMM of the step runs with beta = 0 instead.  A weight joins the set only after a
 # step in which it was zeroed and written by that GEMM; one that a step leaves fresh (never written) is
-# zeroed by ``flush_fresh`` before the gradients are used.  ``FTC_GRAD_FIRST_WRITE=1`` (opt-in).
-_FIRST_WRITE = os.environ.get("FTC_GRAD_FIRST_WRITE", "0") == "1"
+# zeroed by ``flush_fresh`` before the gradients are used.  Default on (``FTC_GRAD_FIRST_WRITE=0``: zero
+# the whole buffer): Llama-3-8B full FT, interleaved on one box (profiles/r3/first_write/), 690.1 / 692.0 ms
+# vs 693.7 / 694.4 ms/step (+0.4 %).
+_FIRST_WRITE = os.environ.get("FTC_GRAD_FIRST_WRITE", "1") != "0"
 # id(param) -> (weakref(param), its main_grad view): weights only a projection GEMM writes.  Entries are
 # identity-checked (a dead parameter's id can be reused by a new tensor of another trainer)
 _GRAD_OWNED: dict = {}
