@@ -172,6 +172,12 @@ for s in "${STEPS[@]}"; do
           > gpurun_out/first_write$t.log 2>&1
         fatal $? first_write$t; grep '^{' gpurun_out/first_write$t.log | cut -c80-150
       done ;;
+    defaults_ab)  # headline LoRA step: this round's new defaults on vs off (side-stream dW, first-write gradients)
+      for t in 1a 0a 1b 0b; do
+        if [ "${t:0:1}" = 1 ]; then E="FTC_DW_STREAM=1 FTC_GRAD_FIRST_WRITE=1"; else E="FTC_DW_STREAM=0 FTC_GRAD_FIRST_WRITE=0"; fi
+        env $E timeout -k 10 400 python bench.py --steps 10 --warmup 3 > gpurun_out/defaults$t.log 2>&1
+        fatal $? defaults$t; grep '^{' gpurun_out/defaults$t.log | cut -c80-150
+      done ;;
     gemms)
       timeout -k 10 300 python tools/bench_gemms.py > gpurun_out/bench_gemms.log 2>&1
       fatal $? gemms; tail -3 gpurun_out/bench_gemms.log ;;
