@@ -200,9 +200,8 @@ class FlatAdamW:
                             lo, hi = o, end
                     if lo is not None:
                         runs.append((lo, hi))
-                    self._zero_key, self._zero_runs = key, runs
-                for lo, hi in self._zero_runs:
-                    self.grad_flat[lo:hi].zero_()
+                    self._zero_key, self._zero_runs = key, [self.grad_flat[lo:hi] for lo, hi in runs]
+                torch._foreach_zero_(self._zero_runs)  # one multi-tensor launch for the ~2 runs per layer
                 _linear.mark_fresh(id(self.params[i]) for i in mine)
             else:
                 self.grad_flat.zero_()
