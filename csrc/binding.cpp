@@ -41,9 +41,7 @@ int ftc_gemm_nt_ok(const void* a, long long lda, const void* b, long long ldb, c
                    int M, int N, int K);
 int ftc_gemm_nt(const void* a, long long lda, const void* b, long long ldb, void* c, long long ldc, int c_fp32, int M,
                 int N, int K, float alpha, float beta, hipStream_t stream);
-int ftc_gemm_nt_pb_ok(const void* a, long long lda, const void* bp, const void* c, long long ldc, int M, int N, int K);
-int ftc_gemm_nt_pb(const void* a, long long lda, const void* bp, void* c, long long ldc, int c_fp32, int M, int N,
-                   int K, float alpha, float beta, hipStream_t stream);
+void ftc_gemm_nt_config(int grid_cap, int group, int xcc, int nt_store);
 int ftc_gemm_nt_rope(const void* a, long long lda, const void* b, long long ldb, void* c, long long ldc, int M, int N,
                      int K, const float* cos_t, const float* sin_t, const int* positions, int seq_len, int rot_heads,
                      hipStream_t stream);
@@ -447,27 +445,10 @@ void gemm_nt_rope_(at::Tensor& c, const at::Tensor& a, const at::Tensor& b, cons
         "gemm_nt_rope_");
 }
 
-// packed-B form: bp holds B [N, K] in MFMA fragment order ([N/32][K/32][2][64][8], ops/gemm.py pack_b_nt)
-bool gemm_nt_pb_ok(const at::Tensor& c, const at::Tensor& a, const at::Tensor& bp, int64_t N, int64_t K) {
-  if (!a.is_cuda() || !bp.is_cuda() || !c.is_cuda() || a.dim() != 2 || c.dim() != 2) return false;
-  if (a.device() != bp.device() || a.device() != c.device()) return false;
-  if (a.scalar_type() != at::kBFloat16 || bp.scalar_type() != at::kBFloat16) return false;
-  if (c.scalar_type() != at::kBFloat16 && c.scalar_type() != at::kFloat) return false;
-  if (a.stride(1) != 1 || c.stride(1) != 1 || !bp.is_contiguous() || bp.numel() != N * K) return false;
-  if (a.size(1) != K || c.size(0) != a.size(0) || c.size(1) != N) return false;
-  if (a.size(0) > INT32_MAX || N > INT32_MAX || K > INT32_MAX) return false;
-  return ftc_gemm_nt_pb_ok(a.data_ptr(), a.stride(0), bp.data_ptr(), c.data_ptr(), c.stride(0), (int)a.size(0), (int)N,
-                           (int)K) != 0;
-}
-
-void gemm_nt_pb_(at::Tensor& c, const at::Tensor& a, const at::Tensor& bp, int64_t N, int64_t K, double alpha,
-                 double beta) {
-  TORCH_CHECK(gemm_nt_pb_ok(c, a, bp, N, K), "gemm_nt_pb_: shapes / layouts outside the kernel contract (M, N % 256, "
-              "K % 64, a [M, K] bf16 row view, bp packed [N * K] bf16, c [M, N] bf16/fp32, 16-byte aligned)");
-  check(ftc_gemm_nt_pb(a.data_ptr(), a.stride(0), bp.data_ptr(), c.data_ptr(), c.stride(0),
-                       c.scalar_type() == at::kFloat, (int)a.size(0), (int)N, (int)K, (float)alpha, (float)beta,
-                       cur_stream()),
-        "gemm_nt_pb_");
+// launch configuration of the projection GEMM (persistent grid cap, tile order, store policy); the
+// defaults are the measured best (profiles/r4/gemm_nt.md) -- tools/bench_gemm_nt.py sweeps it
+void gemm_nt_config(int64_t grid_cap, int64_t group, int64_t xcc, int64_t nt_store) {
+  ftc_gemm_nt_config((int)grid_cap, (int)group, (int)xcc, nt_store ? 1 : 0);
 }
 
 // ---------------- cross entropy (in place on logits) ----------------
@@ -843,11 +824,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_tn_ok", &gemm_tn_ok);
   m.def("gemm_tn_", &gemm_tn_);
   m.def("gemm_nt_ok", &gemm_nt_ok);
-  m.def("gemm_nt_pb_ok", &gemm_nt_pb_ok);
   m.def("gemm_nt_rope_", &gemm_nt_rope_, py::arg("c"), py::arg("a"), py::arg("b"), py::arg("cos"), py::arg("sin"),
         py::arg("positions"), py::arg("seq_len"), py::arg("rot_heads"));
-  m.def("gemm_nt_pb_", &gemm_nt_pb_, py::arg("c"), py::arg("a"), py::arg("bp"), py::arg("N"), py::arg("K"),
-        py::arg("alpha") = 1.0, py::arg("beta") = 0.0);
+  m.def("gemm_nt_config", &gemm_nt_config, py::arg("grid_cap"), py::arg("group"), py::arg("xcc"), py::arg("nt_store"));
   m.def("gemm_nt_", &gemm_nt_, py::arg("c"), py::arg("a"), py::arg("b"), py::arg("alpha") = 1.0, py::arg("beta") = 0.0);
   m.def("ce_fwd_bwd_", &ce_fwd_bwd_);
   m.def("adamw_", &adamw_, py::arg("param"), py::arg("master"), py::arg("m"), py::arg("v"), py::arg("grad"),

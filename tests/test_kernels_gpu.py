@@ -288,32 +288,49 @@ def test_gemm_nt(C, cdtype, M, N, K, pad, beta):
     torch.testing.assert_close(c.float(), ref, atol=tol, rtol=1e-2 if cdtype == torch.bfloat16 else 1e-4)
 
 
-@pytest.mark.parametrize("cdtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("M,N,K,pad,beta", [(256, 256, 64, 0, 0.0), (512, 768, 4160, 64, 0.0), (768, 512, 128, 8, 1.0),
-                                            (256, 1024, 1088, 0, -0.5)])
-def test_gemm_nt_packed(C, cdtype, M, N, K, pad, beta):
-    """Packed-B projection GEMM (B in MFMA fragment order, ops/gemm.py) vs an exact integer product and
-    an fp32 reference."""
-    from finetune_controller_amd.ops.gemm import pack_b_nt
+@pytest.fixture
+def nt_config(C):
+    """Restores the projection GEMM's default launch configuration after a test that changes it."""
+    yield C
+    C.gemm_nt_config(0, -8, 32, 0)
 
-    torch.manual_seed(4)
-    abuf = torch.randint(-3, 4, (M, K + pad), device=DEV).to(torch.bfloat16)
-    a = abuf[:, :K]
-    b = (torch.arange(N * K, device=DEV).reshape(N, K) % 7 - 3).to(torch.bfloat16)
-    bp = pack_b_nt(b)
-    c = torch.zeros(M, N, device=DEV, dtype=cdtype)
-    assert C.gemm_nt_pb_ok(c, a, bp, N, K)
-    C.gemm_nt_pb_(c, a, bp, N, K, 1.0, 0.0)
-    assert torch.equal(c, (a.double() @ b.double().t()).to(cdtype))
-    abuf = (torch.rand(M, K + pad, device=DEV) * 2 - 1).to(torch.bfloat16)
-    a = abuf[:, :K]
-    b = (torch.rand(N, K, device=DEV) * 2 - 1).to(torch.bfloat16)
-    bp = pack_b_nt(b)
-    c = torch.randn(M, N, device=DEV).to(cdtype)
-    ref = beta * c.float() + 0.5 * (a.float() @ b.float().t())
-    C.gemm_nt_pb_(c, a, bp, N, K, 0.5, beta)
-    tol = 2e-2 * (K ** 0.5) / 8 if cdtype == torch.bfloat16 else 1e-3 * (K ** 0.5) / 8
-    torch.testing.assert_close(c.float(), ref, atol=tol, rtol=1e-2 if cdtype == torch.bfloat16 else 1e-4)
+
+@pytest.mark.parametrize("cfg", [(1, 1, 1, 0), (3, 4, 1, 0), (8, -2, 1, 1), (16, 2, 2, 0), (5, -16, 1, 0)])
+@pytest.mark.parametrize("M,N,K", [(1024, 768, 64), (768, 1280, 128), (512, 1024, 448)])
+def test_gemm_nt_persistent(nt_config, cfg, M, N, K):
+    """The persistent grid walks several tiles per workgroup (grid capped below the tile count) with the
+    super-stage stream running across tile boundaries -- including K = 64 (one stage per tile: the next
+    tile's first stage is prefetched while the current one is still being read) -- under every tile
+    order / store policy: exact integer products, every tile checked."""
+    C = nt_config
+    C.gemm_nt_config(cfg[0], cfg[1], cfg[2], cfg[3])
+    torch.manual_seed(11)
+    a = torch.randint(-3, 4, (M, K), device=DEV).to(torch.bfloat16)
+    b = (torch.arange(N * K, device=DEV).reshape(N, K) % 5 - 2).to(torch.bfloat16)
+    c = torch.full((M, N), 7.0, device=DEV, dtype=torch.bfloat16)
+    C.gemm_nt_(c, a, b, 1.0, 0.0)
+    assert torch.equal(c, (a.double() @ b.double().t()).to(torch.bfloat16))
+    cf = torch.zeros(M, N, device=DEV, dtype=torch.float32)
+    C.gemm_nt_(cf, a, b, 1.0, 0.0)
+    assert torch.equal(cf, (a.double() @ b.double().t()).float())
+
+
+@pytest.mark.parametrize("name,K,N", [("qkv_fwd", 4096 + 64, 6144), ("down_dx", 4096 + 64, 14336)])
+def test_gemm_nt_production_shape(C, name, K, N):
+    """The headline step's shapes (T = 4 x 4096 tokens, LoRA-augmented K): bit-identical to torch.mm
+    (hipBLASLt accumulates the same 16x16x32 MFMA chain in K order) and close to an fp32 reference on a
+    row sample spread over every M tile."""
+    torch.manual_seed(12)
+    M = 16384
+    a = torch.empty(M, K, device=DEV, dtype=torch.bfloat16).uniform_(-1, 1)
+    b = torch.empty(N, K, device=DEV, dtype=torch.bfloat16).uniform_(-1, 1)
+    c = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    C.gemm_nt_(c, a, b, 1.0, 0.0)
+    lib = torch.mm(a, b.t())
+    rows = torch.arange(0, M, 97, device=DEV)
+    ref = a[rows].float() @ b.float().t()
+    torch.testing.assert_close(c[rows].float(), ref, atol=3e-2 * (K ** 0.5) / 8, rtol=1e-2)
+    assert torch.equal(c, lib), f"{name}: {(c.float() - lib.float()).abs().max().item()} max |ours - torch.mm|"
 
 
 @pytest.mark.parametrize("with_pos", [False, True])
