@@ -250,6 +250,7 @@ def main(argv=None) -> int:
     pdist.barrier(info)
     sync()
     tr.comm_exposed_ms()  # drop the warm-up steps' probes (events only: nothing synchronises in the loop)
+    tr.param_sync_exposed_ms()
     if cuda:
         _mark("push")  # roctx range "ftc_timed" (rocprofv3 --marker-trace; tools/kstats_md.py filters on it)
     t0 = time.perf_counter()
@@ -267,6 +268,9 @@ def main(argv=None) -> int:
     # gradient-reduction time backward did not hide, measured by device events inside the timed steps
     exposed = tr.comm_exposed_ms()
     exposed = pdist.all_reduce_max(exposed, info) if exposed is not None else None
+    # ZeRO-1: the parameter all-gather time the update / next forward did not hide
+    psync = tr.param_sync_exposed_ms()
+    psync = pdist.all_reduce_max(psync, info) if psync is not None else None
     loss = float(last.float().item()) if last is not None else float("nan")
 
     n = info.world_size
@@ -359,6 +363,8 @@ def main(argv=None) -> int:
             **({"allreduce_bucket": comm} if comm else {}),
             "comm": {
                 "comm_exposed_ms": None if exposed is None else round(exposed, 3),
+                "param_sync_exposed_ms": None if psync is None else round(psync, 3),
+                "zero_gather_overlap": bool(tr.zero_stage and getattr(tr.opt, "_stage_buckets", None) is not None),
                 "wire_GB_per_step": round(tr.ddp.wire_bytes_per_step() / 1e9, 4),
                 "n_buckets": tr.ddp.n_collectives(),
                 "bucket_mb": a.bucket_mb,

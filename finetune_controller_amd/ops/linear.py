@@ -413,8 +413,9 @@ def accum_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, alpha: float =
 # the whole buffer): Llama-3-8B full FT, interleaved on one box (profiles/r3/first_write/), 690.1 / 692.0 ms
 # vs 693.7 / 694.4 ms/step (+0.4 %).
 _FIRST_WRITE = os.environ.get("FTC_GRAD_FIRST_WRITE", "1") != "0"
-# id(param) -> (weakref(param), its main_grad view): weights only a projection GEMM writes.  Entries are
-# identity-checked (a dead parameter's id can be reused by a new tensor of another trainer)
+# id(param) -> weakref(param): weights only a projection GEMM writes.  Entries are identity-checked (a dead
+# parameter's id can be reused by a new tensor of another trainer) and hold no reference to the gradient
+# buffer (a main_grad view would keep a whole flat fp32 buffer alive after its optimizer is gone)
 _GRAD_OWNED: dict = {}
 _GRAD_FRESH: set = set()  # ids whose main_grad still holds last step's values
 
@@ -426,9 +427,16 @@ def set_first_write(on: bool) -> None:
     _GRAD_FRESH.clear()
 
 
+def reset_grad_owned() -> None:
+    """Forget every registered weight (a new optimizer re-homes the gradients: each weight is zeroed and
+    written once more before it may skip zeroing again)."""
+    _GRAD_OWNED.clear()
+    _GRAD_FRESH.clear()
+
+
 def is_grad_owned(p) -> bool:
     e = _GRAD_OWNED.get(id(p)) if _FIRST_WRITE else None
-    return e is not None and e[0]() is p
+    return e is not None and e() is p
 
 
 def mark_fresh(ids) -> None:
@@ -442,8 +450,8 @@ def take_fresh(p, mg: torch.Tensor) -> float:
         return 1.0
     pid = id(p)
     e = _GRAD_OWNED.get(pid)
-    if e is None or e[0]() is not p:  # first sight of this parameter: its gradient was zeroed this step
-        _GRAD_OWNED[pid] = (weakref.ref(p), mg)
+    if e is None or e() is not p:  # first sight of this parameter: its gradient was zeroed this step
+        _GRAD_OWNED[pid] = weakref.ref(p)
         _GRAD_FRESH.discard(pid)
         return 1.0
     if pid in _GRAD_FRESH:
@@ -453,11 +461,23 @@ def take_fresh(p, mg: torch.Tensor) -> float:
 
 
 def flush_fresh() -> None:
-    """Zero the gradient of every skipped weight that this step did not write (call before reading them)."""
+    """Zero the gradient of every skipped weight that this step did not write (call before reading them:
+    the optimizers and the gradient bucketer do, see ``gradients_final``)."""
     while _GRAD_FRESH:
         e = _GRAD_OWNED.get(_GRAD_FRESH.pop())
-        if e is not None and e[0]() is not None:
-            e[1].zero_()
+        p = e() if e is not None else None
+        mg = getattr(p, "main_grad", None) if p is not None else None
+        if mg is not None:
+            mg.zero_()
+
+
+def gradients_final() -> None:
+    """Make the gradient buffer safe to read on the current stream: join the side-stream weight
+    gradients and zero the skipped weights this step never wrote.  Cheap no-ops when nothing is pending;
+    called at the top of every optimizer step / gradient-norm / bucket-finish, so a plain
+    ``zero_grad(); loss.backward(); step()`` loop is correct without trainer help."""
+    join_wgrad_stream()
+    flush_fresh()
 
 
 def _mm_into(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor):

@@ -142,6 +142,7 @@ class GradBucketer:
 
     def finish(self):
         """Launch anything not yet launched (unused params, deferred tied weights) and wait."""
+        _linear.gradients_final()  # a bucket still unlaunched may hold a skipped weight this step never wrote
         if not self.enabled:
             if self.sharded:  # world 1: the owned slice is the whole bucket
                 for b, (s, e) in enumerate(self.buckets):

@@ -60,6 +60,7 @@ class FlatAdamW:
             raise ValueError(f"FlatAdamW: trainable params must share one dtype, got {dtypes}")
         self.dtype = plist[0].dtype
         self.device = plist[0].device
+        _linear.reset_grad_owned()  # the gradients are re-homed below: nothing may skip zeroing yet
         self.params = list(reversed(plist))
         self.offsets: list[tuple[int, int]] = []
         # bucket plan (ZeRO-1 sharding): contiguous [start, end) ranges closed once they reach
@@ -241,6 +242,7 @@ class FlatAdamW:
 
     @torch.no_grad()
     def step(self, lr: float | None = None):
+        _linear.gradients_final()  # side-stream dW joined, never-written skipped weights zeroed
         lr = self.lr if lr is None else lr
         self.step_count += 1
         bump_param_generation()  # the update below rewrites param_flat in place
@@ -337,6 +339,81 @@ class ShardedFlatAdamW(FlatAdamW):
     def __init__(self, params, world: int, rank: int, group=None, bucket_elems: int = 16 << 20, **kw):
         self.world, self.rank, self.group = world, rank, group
         super().__init__(params, bucket_elems=bucket_elems, pad_multiple=world, **kw)
+        # parameter all-gather: one async collective per bucket, issued right after that bucket's AdamW in
+        # the order the next forward reads the buckets; without gates (enable_gather_overlap) step() waits
+        # for all of them itself
+        self._pending: dict = {}  # bucket -> all-gather work not waited for yet
+        self._stage_buckets: list[list[int]] | None = None
+        self._gather_order = list(range(len(self.buckets)))[::-1]  # the layout is reversed: last bucket first
+        self.probe = False  # device events around every gather wait (param_sync_exposed_ms)
+        self._sync_ev: list[tuple] = []
+        self._sync_steps = 0
+
+    def enable_gather_overlap(self, stages: list[list[torch.Tensor]]) -> bool:
+        """Let the next forward start while later buckets' parameters are still being all-gathered: the
+        model calls ``wait_stage(i)`` before it reads stage i's parameters (``stages``: the trainable
+        parameters grouped in forward order, as ``FlatAdamW.enable_overlap``), which waits only for the
+        buckets that hold them.  The buckets are updated and gathered in the order of the stage that first
+        needs them.  Returns False (nothing changed) when some bucket belongs to no stage."""
+        where = {id(p): (o, _align(n)) for p, (o, n) in zip(self.params, self.offsets)}
+        sb, order = [], []
+        for group in stages:
+            bs = sorted({b for o, n in (where[id(p)] for p in group if id(p) in where)
+                         for b, (s, e) in enumerate(self.buckets) if o < e and o + n > s})
+            sb.append(bs)
+            order += [b for b in bs if b not in order]
+        if sorted(order) != list(range(len(self.buckets))):
+            return False
+        self._stage_buckets, self._gather_order = sb, order
+        return True
+
+    def _wait(self, w):
+        if self.probe and self.device.type == "cuda":
+            e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            e[0].record()
+            w.wait()  # the current stream waits for the gather (device-side for RCCL)
+            e[1].record()
+            self._sync_ev.append(e)
+        else:
+            w.wait()
+
+    def wait_stage(self, i: int):
+        """The current stream waits for the parameter all-gathers of stage i's buckets."""
+        if not self._pending or self._stage_buckets is None or i >= len(self._stage_buckets):
+            return
+        for b in self._stage_buckets[i]:
+            w = self._pending.pop(b, None)
+            if w is not None:
+                self._wait(w)
+
+    def join(self):
+        """Every pending parameter all-gather is ordered before the current stream's next work (call before
+        reading parameters outside the gated forward: checkpoints, exports, evaluation without gates)."""
+        for b in list(self._pending):
+            self._wait(self._pending.pop(b))
+
+    def param_sync_exposed_ms(self, reset: bool = True) -> float | None:
+        """Mean device time per optimizer step that streams spent waiting for the ZeRO-1 parameter
+        all-gather (the part neither the rest of the update nor the next forward hid); None without
+        probes.  Synchronises the device."""
+        if not self.probe or not self._sync_steps:
+            return None
+        torch.cuda.synchronize(self.device)
+        v = sum(a.elapsed_time(b) for a, b in self._sync_ev) / self._sync_steps
+        if reset:
+            self._sync_ev, self._sync_steps = [], 0
+        return v
+
+    def _launch_gather(self, b: int):
+        import torch.distributed as dist
+
+        s, e = self.buckets[b]
+        lo, hi = self.shard_ranges[b]
+        src = self.param_flat[lo:hi]
+        # RCCL gathers in place (input == output + rank * count); gloo gets a private copy
+        gloo = dist.get_backend(self.group) == "gloo"
+        self._pending[b] = dist.all_gather_into_tensor(self.param_flat[s:e], src.clone() if gloo else src,
+                                                       group=self.group, async_op=True)
 
     def _init_state(self):
         world, rank = self.world, self.rank
@@ -359,6 +436,7 @@ class ShardedFlatAdamW(FlatAdamW):
 
     @torch.no_grad()
     def sync_master(self):
+        self.join()
         for b, (lo, hi) in enumerate(self.shard_ranges):
             self.shard_view(b, self.master).copy_(self.param_flat[lo:hi])
 
@@ -367,24 +445,12 @@ class ShardedFlatAdamW(FlatAdamW):
         o = self.shard_offsets[b]
         return t[o:o + hi - lo]
 
-    def _all_gather_params(self):
-        import torch.distributed as dist
-
-        gloo = dist.get_backend(self.group) == "gloo"
-        works = []
-        for b, (s, e) in enumerate(self.buckets):
-            lo, hi = self.shard_ranges[b]
-            src = self.param_flat[lo:hi]
-            # RCCL gathers in place (input == output + rank * count); gloo gets a private copy
-            works.append(dist.all_gather_into_tensor(self.param_flat[s:e], src.clone() if gloo else src,
-                                                     group=self.group, async_op=True))
-        for w in works:
-            w.wait()
-
     @torch.no_grad()
     def step(self, lr: float | None = None):
         import torch.distributed as dist
 
+        _linear.gradients_final()
+        self.join()  # a bucket the last forward never gated on (the param_flat slices are rewritten below)
         lr = self.lr if lr is None else lr
         self.step_count += 1
         bump_param_generation()
@@ -399,7 +465,7 @@ class ShardedFlatAdamW(FlatAdamW):
                 coef = torch.where(norm > self.max_grad_norm, self.max_grad_norm / (norm + 1e-6), coef)
             gscale = coef * self.grad_scale
             self.last_grad_norm = stats[0:1]
-            for b in range(len(self.buckets)):
+            for b in self._gather_order:  # each bucket's gather goes out right after its update
                 lo, hi = self.shard_ranges[b]
                 param = self.param_flat[lo:hi] if self.dtype == torch.bfloat16 else None
                 ext().adamw_(param, self.shard_view(b, self.master), self.shard_view(b, self.exp_avg),
@@ -407,6 +473,7 @@ class ShardedFlatAdamW(FlatAdamW):
                              self.wd, self.step_count, gscale)
                 if param is None:
                     self.param_flat[lo:hi].copy_(self.shard_view(b, self.master))
+                self._launch_gather(b)
         else:
             gf = g.float() * self.grad_scale
             sq = (gf * gf).sum().reshape(1)
@@ -420,10 +487,13 @@ class ShardedFlatAdamW(FlatAdamW):
             self.exp_avg_sq.mul_(b2).addcmul_(gf, gf, value=1 - b2)
             self.master.mul_(1 - lr * self.wd)
             self.master.addcdiv_(self.exp_avg / bc1, (self.exp_avg_sq / bc2).sqrt_().add_(self.eps), value=-lr)
-            for b in range(len(self.buckets)):
+            for b in self._gather_order:
                 lo, hi = self.shard_ranges[b]
                 self.param_flat[lo:hi].copy_(self.shard_view(b, self.master))
-        self._all_gather_params()
+                self._launch_gather(b)
+        self._sync_steps += 1
+        if self._stage_buckets is None:  # no gated forward follows: the update ends with the parameters
+            self.join()
 
     def grad_norm(self) -> float:
         if self.last_grad_norm is None:
@@ -441,13 +511,24 @@ class ShardedFlatAdamW(FlatAdamW):
             out[s:e].copy_(full.cpu())
         return out
 
+    def export_params(self) -> torch.Tensor:
+        self.join()
+        return super().export_params()
+
+    @torch.no_grad()
+    def import_params(self, compact: torch.Tensor):
+        self.join()
+        super().import_params(compact)
+
     def state_dict(self) -> dict:
+        self.join()
         return {"format": "compact", "layout": self.layout(),
                 **{k: self.compact(self._gather_full(getattr(self, k))) for k in ("master", "exp_avg", "exp_avg_sq")},
                 "step": self.step_count, "lr": self.lr}
 
     @torch.no_grad()
     def load_state_dict(self, sd: dict):
+        self.join()
         self._check_layout(sd)
         for name in ("master", "exp_avg", "exp_avg_sq"):
             full = self.expand_(sd[name], torch.zeros(self.numel, dtype=torch.float32))

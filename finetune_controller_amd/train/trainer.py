@@ -200,6 +200,17 @@ class Trainer:
         import os
 
         tc = self.tc
+        if isinstance(self.opt, ShardedFlatAdamW):
+            # ZeRO-1: each bucket's parameter all-gather goes out right after its AdamW and the next
+            # forward waits per layer for the buckets it reads (ShardedFlatAdamW.enable_gather_overlap);
+            # FTC_ZERO_GATHER_OVERLAP=0 waits for every gather inside step()
+            self.opt.probe = bool(tc.comm_probe and self.device.type == "cuda")
+            if (os.environ.get("FTC_ZERO_GATHER_OVERLAP", "1") != "0" and not tc.graph
+                    and hasattr(self.model, "param_stages") and self.opt.enable_gather_overlap(self.model.param_stages())):
+                self.model.param_gate = self.opt.wait_stage
+                log.info("ZeRO-1 parameter all-gather overlapped with the next forward (%d buckets)",
+                         len(self.opt.buckets))
+            return
         if (os.environ.get("FTC_OPT_OVERLAP", "0") != "1" or tc.method != "full" or type(self.opt) is not FlatAdamW
                 or tc.graph or tc.timers or self.device.type != "cuda" or not hasattr(self.model, "param_stages")):
             return
@@ -428,6 +439,12 @@ class Trainer:
             self._comm_ev = []
         return v
 
+    def param_sync_exposed_ms(self, reset: bool = True) -> float | None:
+        """ZeRO-1: mean device time per step the streams waited for the parameter all-gather (None
+        otherwise / without probes; ShardedFlatAdamW.param_sync_exposed_ms).  Synchronises the device."""
+        f = getattr(self.opt, "param_sync_exposed_ms", None)
+        return f(reset) if f is not None else None
+
     def _phase_ms(self) -> dict:
         """Mean fwd/bwd/comm/optim milliseconds of the steps since the last call (after a sync)."""
         if not self._timing:
@@ -531,11 +548,15 @@ class Trainer:
                 watchdog.beat(f"checkpoint at step {self.step}")
         metrics.close()
         # training is over: the final save (a full-FT model or merged adapter can take minutes on rank 0)
-        # and the barrier non-main ranks wait in must not trip the step watchdog
-        watchdog.close()
+        # and the barrier non-main ranks wait in get a phase limit of their own (FTC_SAVE_TIMEOUT_S,
+        # default max(10 x the step limit, 1800 s)) -- long enough for the save, still an exit when a peer
+        # hangs or dies there
+        save_s = float(os.environ.get("FTC_SAVE_TIMEOUT_S", 0) or max(10 * watchdog.timeout_s, 1800.0))
+        watchdog.phase("final save + barrier", save_s)
         if tc.save_model:
             self.save_artifacts()
         pdist.barrier(self.info)
+        watchdog.close()
         return last
 
     def _resume_state(self) -> dict | None:
@@ -603,5 +624,7 @@ class Trainer:
         wd = getattr(self, "watchdog", None)
         if wd is not None:
             wd.close()
+        if getattr(self, "opt", None) is not None:
+            self._join_update()  # no collective may outlive the process group
         self.ddp.close()
         pdist.destroy(self.info)

@@ -105,6 +105,7 @@ class StepWatchdog:
         # the first beat the limit is max(3 x timeout, 300 s) unless given
         self.first_timeout_s = float(first_timeout_s) if first_timeout_s is not None else max(3 * self.timeout_s, 300.0)
         self._beats = 0
+        self._phase_s = None  # one-off limit of the current phase (set by phase(), cleared by beat())
         self.rank = rank
         self._exit = exit_fn or os._exit
         self._last = time.monotonic()
@@ -122,8 +123,16 @@ class StepWatchdog:
 
     def beat(self, what: str = ""):
         self._beats += 1
+        self._phase_s = None
         self._last = time.monotonic()
         self._what = what or self._what
+
+    def phase(self, what: str, timeout_s: float):
+        """Start a phase with its own limit (the final save, the closing barrier): a rank whose peer died
+        there still exits instead of hanging in a collective until the process-group timeout."""
+        self._last = time.monotonic()
+        self._what = what
+        self._phase_s = float(timeout_s)
 
     def close(self):
         self._stop.set()
@@ -133,7 +142,8 @@ class StepWatchdog:
     def _run(self):
         while not self._stop.wait(self._poll):
             idle = time.monotonic() - self._last
-            if idle > (self.timeout_s if self._beats else self.first_timeout_s):
+            limit = self._phase_s if self._phase_s is not None else (self.timeout_s if self._beats else self.first_timeout_s)
+            if idle > limit:
                 print(f"[watchdog] rank {self.rank}: no progress for {idle:.0f} s (last: {self._what}); "
                       f"dumping stacks and exiting {WATCHDOG_EXIT}", file=sys.stderr, flush=True)
                 try:

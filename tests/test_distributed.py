@@ -110,6 +110,57 @@ def test_bench_eight_ranks_on_cpu(tmp_path):
     assert out["config"]["zero_stage"] == 0  # LoRA: plain bucketed all-reduce
 
 
+@pytest.mark.slow
+def test_bench_eight_ranks_full_ft_zero1_on_cpu(tmp_path):
+    """The 8-rank command for full fine-tuning: ZeRO-1 by default, with the parameter all-gather overlapped
+    with the next forward and its exposed time reported beside the gradient reduction's (device events:
+    None on CPU, a number on the GPU)."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "FTC_INIT_METHOD"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "2", "--warmup", "1",
+                        "--device", "cpu", "--model", "llama-tiny", "--method", "full", "--batch-size", "1",
+                        "--seq-len", "16", "--launcher-timeout", "400"],
+                       capture_output=True, text=True, timeout=480, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][-1])
+    assert out["n_gpus"] == 8 and out["config"]["zero_stage"] == 1
+    assert out["config"]["parallelism"] == "dp8-zero1"
+    assert "param_sync_exposed_ms" in out["comm"] and out["comm"]["param_sync_exposed_ms"] is None
+    assert out["comm"]["zero_gather_overlap"] is True
+
+
+def _zero_overlap_worker(rank, world, port, tmp, q, overlap):
+    os.environ["FTC_ZERO_GATHER_OVERLAP"] = "1" if overlap else "0"
+    _rank_env(rank, world, port, tmp)
+    tc = TrainConfig(model="llama-tiny", method="full", batch_size=2, seq_len=16, synthetic=True, max_steps=3,
+                     checkpoint_path=tmp, resume=False, device="cpu", dtype="bf16", lr=1e-2, bucket_mb=0.05,
+                     max_grad_norm=1.0, save_model=False, zero_stage=1, weight_decay=0.1)
+    tr = Trainer(tc)
+    gated = tr.model.param_gate is not None
+    losses = [float(tr.train_step(1e-2)) for _ in range(3)]
+    pending = len(tr.opt._pending)  # the last step's gathers, waited for by the next forward / join
+    q.put((rank, {"losses": losses, "params": tr.opt.export_params().float().clone(), "gated": gated,
+                  "buckets": len(tr.opt.buckets), "pending": pending}))
+    tr.close()
+    _hold(tmp, port)
+
+
+@pytest.mark.slow
+def test_zero1_overlapped_gather_matches_synchronous(tmp_path):
+    """ZeRO-1 with each bucket's parameter all-gather issued after its own update and the next forward
+    gated per layer (ShardedFlatAdamW.enable_gather_overlap) trains exactly like the synchronous gather:
+    equal losses and parameters after three steps on 2 gloo ranks with several buckets."""
+    ov = _run_ranks(_zero_overlap_worker, 2, tmp_path, True)
+    sy = _run_ranks(_zero_overlap_worker, 2, tmp_path, False)
+    assert ov[0]["gated"] and not sy[0]["gated"]
+    assert ov[0]["buckets"] > 2 and ov[0]["pending"] > 0 and sy[0]["pending"] == 0
+    for r in (0, 1):
+        assert ov[r]["losses"] == sy[r]["losses"]
+        torch.testing.assert_close(ov[r]["params"], sy[r]["params"], atol=0, rtol=0)
+    torch.testing.assert_close(ov[0]["params"], ov[1]["params"], atol=0, rtol=0)
+
+
 def test_device_key_prefers_pci_location(monkeypatch):
     """Two cards that report one UUID (seen in some containerised setups) still get distinct keys from
     their PCI location; without PCI fields the UUID, then the index, is used."""
@@ -471,6 +522,7 @@ def _zero_gpu_worker(rank, world, port, tmp, q, zero):
 
     before = digest()
     tr.train_step(1e-3)
+    tr._join_update()  # the overlapped parameter all-gather (waited for by the next forward otherwise)
     torch.cuda.synchronize()
     q.put((rank, {"before": before, "after": digest()}))
     tr.close()

@@ -86,9 +86,24 @@ def test_step_watchdog_first_step_grace():
     assert codes and codes[0] == WATCHDOG_EXIT
 
 
+def test_step_watchdog_phase_limit():
+    """A phase (the final save + closing barrier) gets its own limit: longer than a step's, still an exit
+    when the phase never ends (a peer died in the barrier)."""
+    codes = []
+    wd = StepWatchdog(0.1, exit_fn=codes.append, poll_s=0.02, first_timeout_s=3.0)
+    wd.beat("step 1")
+    wd.phase("final save", 0.8)
+    time.sleep(0.4)  # past the step limit, inside the phase limit
+    assert codes == []
+    time.sleep(0.8)
+    wd.close()
+    assert codes and codes[0] == WATCHDOG_EXIT
+
+
 def test_slow_final_save_does_not_trip_the_watchdog(tmp_path, monkeypatch):
     """The watchdog covers steps, evaluations and checkpoints; the final artifact save (minutes for a
-    full-FT model on rank 0, with the other ranks waiting in the barrier) runs after it is closed."""
+    full-FT model on rank 0, with the other ranks waiting in the barrier) runs under the save phase's
+    longer limit."""
     from finetune_controller_amd.train import trainer as trmod
 
     codes = []
@@ -218,3 +233,36 @@ def test_lost_peer_job_restarts_and_completes(tmp_path):
         assert [t for j, t in ctx.kube.history if j == jid].count("Restarting") >= 2  # both pods
         m = c.get(f"/api/v1/jobs/{jid}/metrics").json()["metrics"]
         assert max(int(row["step"]) for row in m) == 6
+
+
+def test_first_write_registry_flushes_unwritten_weight():
+    """ops.linear first-write gradients: a registered projection weight that a step leaves unwritten is
+    zeroed by flush_fresh through its CURRENT main_grad (the registry holds only a weak reference), a
+    dead parameter is skipped, and a new optimizer resets the registry."""
+    from finetune_controller_amd.ops import linear as L
+
+    prior = L._FIRST_WRITE
+    try:
+        L.set_first_write(True)
+        p = torch.nn.Parameter(torch.zeros(4, 4))
+        p.main_grad = torch.zeros(4, 4)
+        assert L.take_fresh(p, p.main_grad) == 1.0  # first sight: registered, zeroed this step
+        assert L.is_grad_owned(p)
+        L.mark_fresh([id(p)])  # the optimizer skipped zeroing it
+        p.main_grad = torch.full((4, 4), 3.0)  # a re-homed buffer: the flush must use the current one
+        L.gradients_final()  # nothing wrote it this step
+        assert torch.count_nonzero(p.main_grad) == 0
+        L.mark_fresh([id(p)])
+        assert L.take_fresh(p, p.main_grad) == 0.0  # written by a beta = 0 GEMM: no flush needed
+        q = torch.nn.Parameter(torch.zeros(2))
+        q.main_grad = torch.zeros(2)
+        L.take_fresh(q, q.main_grad)
+        L.mark_fresh([id(q)])
+        del q
+        L.flush_fresh()  # dead parameter: skipped
+        from finetune_controller_amd.train.optim import FlatAdamW
+
+        FlatAdamW([torch.nn.Parameter(torch.zeros(8))])
+        assert not L.is_grad_owned(p)
+    finally:
+        L.set_first_write(prior)

@@ -1461,15 +1461,20 @@ def test_full_ft_first_write_grads_match_zeroed(C, tmp_path, grad_dtype):
             tr = Trainer(tc)
             losses = [tr.train_step(1e-3).float().item() for _ in range(3)]
             torch.cuda.synchronize()
+            L.gradients_final()  # what any reader of the buffer does first (the optimizer step already did)
             res[fw] = (losses, tr.opt.param_flat.float().clone(), tr.opt.grad_flat.float().clone(),
-                       sum(1 for p in tr.opt.params if L.is_grad_owned(p)))
+                       sum(1 for p in tr.opt.params if L.is_grad_owned(p)), list(tr.opt.offsets))
             tr.close()
     finally:
         L.set_first_write(prior)
-    (l1, p1, g1, owned), (l0, p0, g0, _) = res[True], res[False]
+    (l1, p1, g1, owned, offs), (l0, p0, g0, _, _) = res[True], res[False]
     assert owned > 0  # the projection weights were taken off the zeroing pass
     assert max(abs(a - b) / abs(b) for a, b in zip(l1, l0)) < 1e-3, (l1, l0)
-    assert ((g1 - g0).norm() / g0.norm()).item() < 1e-2
+    # per parameter slice: a stale or unzeroed slice of one weight cannot hide in a whole-buffer norm
+    tol = 1e-4 if grad_dtype == "fp32" else 2e-2
+    for o, n in offs:
+        a, b = g1[o:o + n], g0[o:o + n]
+        assert ((a - b).norm() / b.norm().clamp_min(1e-30)).item() < tol, (o, n)
     assert ((p1 - p0).norm() / p0.norm()).item() < 1e-4
 
 
