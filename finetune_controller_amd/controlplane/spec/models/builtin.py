@@ -101,7 +101,9 @@ class MNIST_MI355X(MNIST):
 class LMTrainingArguments(TrainingArguments):
     """Flags of ``finetune_controller_amd.train.cli`` exposed to the UI form."""
 
-    batch_size: int = Field(default=4, ge=1, description="Micro-batch (sequences) per GPU")
+    batch_size: int | Literal["auto"] = Field(
+        default=4, description="Micro-batch (sequences) per GPU, or auto: the largest that fits 90 % of the GPU's "
+                               "HBM (utils/memplan.py), capped at 16k tokens")
     seq_len: int = Field(default=4096, ge=16, description="Tokens per sequence")
     grad_accum: int = Field(default=1, ge=1, description="Gradient accumulation steps")
     epochs: int = Field(default=1, ge=1, description="Passes over the dataset")
@@ -114,7 +116,9 @@ class LMTrainingArguments(TrainingArguments):
     seed: int = Field(default=1, description="Random seed")
     log_interval: int = Field(default=10, ge=1, description="Steps between metrics.csv rows / Epoch log lines")
     save_every: int = Field(default=0, ge=0, description="Resume checkpoint every N steps (0 = only at the end)")
-    checkpoint_layers: bool = Field(default=False, description="Activation checkpointing per decoder layer")
+    checkpoint_layers: bool | Literal["auto"] = Field(
+        default=False, description="Activation checkpointing per decoder layer (auto: only when the micro-batch "
+                                   "does not fit without it)")
     zero_stage: int = Field(default=-1, ge=-1, le=1,
                             description="1: ZeRO-1 -- AdamW state sharded over the data-parallel ranks; "
                                         "-1 (auto): ZeRO-1 for full fine-tuning on > 1 GPU")
@@ -156,9 +160,29 @@ class _WorkerSpec(BaseFineTuneModel):
         description="Optional: tokens (.bin uint16/uint32, .npy) or text (.jsonl with 'text', .txt, .csv). "
                     "Without a dataset the worker trains on synthetic tokens.", dataset_required=False)
 
+    accelerator_memory_gb: float = Field(default=288.0, gt=0,
+                                         description="HBM per GPU the auto batch planner sizes for (MI355X: 288 GB)")
+
     # subclass knobs (class-level, not form fields)
     model_preset: ClassVar[str] = "llama3-8b"
     method: ClassVar[str] = "lora"
+
+    def memory_plan(self):
+        """``utils.memplan.plan`` for this spec's model / method / world; None for a CPU job."""
+        from finetune_controller_amd.models.config import get_config
+        from finetune_controller_amd.utils import memplan
+
+        t = self.training_arguments
+        n = max(0, int(self.accelerator_count or 0)) * max(1, int(self.cluster_nodes or 1))
+        if n == 0:
+            return None
+        ck = t.checkpoint_layers
+        return memplan.plan(memplan.Dims.of(get_config(self.model_preset)), self.method, t.seq_len,
+                            self.accelerator_memory_gb,
+                            batch_size=0 if t.batch_size == "auto" else int(t.batch_size),
+                            checkpoint_layers=None if ck == "auto" else bool(ck), world=n,
+                            zero_stage=t.zero_stage, grad_dtype=t.grad_dtype, grad_accum=t.grad_accum,
+                            lora_r=getattr(t, "lora_r", 16), sp=t.sp)
 
     def _launcher(self) -> str:
         n = max(1, int(self.accelerator_count))
@@ -171,8 +195,13 @@ class _WorkerSpec(BaseFineTuneModel):
 
     def run_cmd(self) -> list[str]:
         t = self.training_arguments
+        vals = t.model_dump()
+        if vals.get("batch_size") == "auto" or vals.get("checkpoint_layers") == "auto":
+            p = self.memory_plan()  # the pod command carries the chosen numbers (the worker re-checks them)
+            if p is not None:
+                vals["batch_size"], vals["checkpoint_layers"] = p.batch_size, p.checkpoint_layers
         args = [f"--model={self.model_preset}", f"--method={self.method}"]
-        for k, v in t.model_dump().items():
+        for k, v in vals.items():
             if isinstance(v, bool):
                 if v:
                     args.append(f"--{k.replace('_', '-')}")

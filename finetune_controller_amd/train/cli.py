@@ -25,7 +25,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--lora-dropout", type=float, default=0.0)
     ap.add_argument("--use-rslora", action="store_true", help="LoRA scale alpha / sqrt(r)")
     ap.add_argument("--lora-targets", default="q_proj,k_proj,v_proj,o_proj,gate_proj,up_proj,down_proj")
-    ap.add_argument("--batch-size", type=int, default=4)
+    ap.add_argument("--batch-size", type=_int_or_auto, default=4,
+                    help="micro-batch per GPU, or auto: the largest that fits 90 %% of the device (utils/memplan.py)")
     ap.add_argument("--seq-len", type=int, default=4096)
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--epochs", type=int, default=1)
@@ -38,7 +39,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--log-interval", type=int, default=10)
     ap.add_argument("--save-every", type=int, default=0)
-    ap.add_argument("--checkpoint-layers", action="store_true")
+    ap.add_argument("--checkpoint-layers", nargs="?", const="1", default="0", choices=["0", "1", "auto"],
+                    help="activation checkpointing per decoder layer (auto: only when the micro-batch needs it)")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--comm-engine", default="torch", choices=["torch", "native"])
     ap.add_argument("--sp", type=int, default=1,
@@ -73,6 +75,16 @@ def build_parser() -> argparse.ArgumentParser:
     return ap
 
 
+def _int_or_auto(v: str) -> int:
+    """argparse type: a positive int, or "auto" -> 0 (the trainer plans it)."""
+    if v == "auto":
+        return 0
+    n = int(v)
+    if n < 1:
+        raise argparse.ArgumentTypeError("batch size must be >= 1 or auto")
+    return n
+
+
 def config_from_args(a) -> TrainConfig:
     return TrainConfig(model=a.model, method=a.method, lora_r=a.lora_r, lora_alpha=a.lora_alpha,
                        lora_dropout=a.lora_dropout, use_rslora=a.use_rslora,
@@ -83,7 +95,8 @@ def config_from_args(a) -> TrainConfig:
                        dataset_path=a.dataset_path, checkpoint_path=a.checkpoint_path, log_interval=a.log_interval,
                        save_every=a.save_every, resume=not a.no_resume, synthetic=a.synthetic, bucket_mb=a.bucket_mb,
                        comm_engine=a.comm_engine, zero_stage=a.zero_stage, grad_dtype=a.grad_dtype, sp=a.sp,
-                       checkpoint_layers=a.checkpoint_layers, init_from=a.init_from,
+                       checkpoint_layers="auto" if a.checkpoint_layers == "auto" else a.checkpoint_layers == "1",
+                       init_from=a.init_from,
                        dtype=a.dtype, device=a.device, timers=a.timers, profile_steps=a.profile_steps,
                        eval_every=a.eval_every, eval_batches=a.eval_batches, eval_holdout=a.eval_holdout,
                        pack_documents=a.pack_documents, eos_id=a.eos_id,

@@ -51,7 +51,7 @@ class TrainConfig:
     use_rslora: bool = False  # LoRA scale alpha / sqrt(r) instead of alpha / r
     lora_targets: list[str] = field(default_factory=lambda: ["q_proj", "k_proj", "v_proj", "o_proj", "gate_proj",
                                                               "up_proj", "down_proj"])
-    batch_size: int = 4  # micro-batch per GPU
+    batch_size: int = 4  # micro-batch per GPU (0: auto -- the HBM planner, utils/memplan.py)
     seq_len: int = 4096
     grad_accum: int = 1
     epochs: int = 1
@@ -80,7 +80,7 @@ class TrainConfig:
     # gradient buffer / reduction dtype: fp32 | bf16 | auto (fp32 for full fine-tuning with gradient
     # accumulation or data parallelism -- summing 4+ bf16 micro-batch / rank gradients loses mantissa)
     grad_dtype: str = "auto"
-    checkpoint_layers: bool = False
+    checkpoint_layers: bool | str = False  # "auto": only when the planned micro-batch needs it
     init_from: str = ""
     dtype: str = "auto"  # auto: bf16 on GPU, fp32 on CPU
     device: str = "auto"
@@ -133,6 +133,7 @@ class Trainer:
         if tc.seq_len > self.cfg.max_seq_len:
             self.cfg.max_seq_len = tc.seq_len
         self.lora = tc.lora_config()
+        self.mem_plan = self._plan_memory()
         self.model = build_model(self.cfg, self.lora, device=self.device, dtype=self.dtype,
                                  checkpoint_layers=tc.checkpoint_layers)
         self.model.ce_chunk_rows = tc.ce_chunk_rows
@@ -218,6 +219,31 @@ class Trainer:
             opt = self.opt
             self.model.param_gate = opt.wait_stage
             log.info("optimizer update overlapped with the next forward (%d stages)", len(opt._stages))
+
+    def _plan_memory(self):
+        """``batch_size`` 0 / ``checkpoint_layers`` "auto": pick them from the model shape and this device's
+        memory (utils.memplan; CPU runs plan against the host's free memory).  Fills in tc."""
+        tc = self.tc
+        if tc.batch_size > 0 and tc.checkpoint_layers != "auto":
+            return None
+        from ..utils import memplan
+
+        if self.device.type == "cuda":
+            dev_gb = torch.cuda.get_device_properties(self.device).total_memory / 1e9
+        else:
+            import psutil
+
+            dev_gb = psutil.virtual_memory().available / 1e9
+        p = memplan.plan(memplan.Dims.of(self.cfg), tc.method, tc.seq_len, dev_gb,
+                         batch_size=tc.batch_size, checkpoint_layers=None if tc.checkpoint_layers == "auto"
+                         else bool(tc.checkpoint_layers), world=self.info.world_size, zero_stage=tc.zero_stage,
+                         grad_dtype=tc.grad_dtype, grad_accum=tc.grad_accum, lora_r=tc.lora_r, sp=tc.sp,
+                         ce_chunk_rows=tc.ce_chunk_rows)
+        tc.batch_size, tc.checkpoint_layers = p.batch_size, p.checkpoint_layers
+        if self.info.is_main:
+            log.info("memory plan: micro-batch %d x %d, checkpointing %s, %.1f of %.1f GB budget (%s)", p.batch_size,
+                     tc.seq_len, "on" if p.checkpoint_layers else "off", p.peak_gb, p.budget_gb, p.parts_gb)
+        return p
 
     def _grad_dtype(self) -> torch.dtype:
         tc = self.tc
