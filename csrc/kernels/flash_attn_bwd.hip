@@ -135,9 +135,8 @@ struct BwdArgs {
   int B, S, H, KV;
   float scale, c;  // c = scale * log2(e)
   int causal, window;
-  int prio_young;
   const int* doc_start;  // [B*S] packed-sequence document bounds (null: one document per sequence):
-  const int* doc_end;    //   key k visible to query q iff doc_start[q] <= k, i.e. q < doc_end[k]  // dK/dV, 8 waves: s_setprio 1 for the second-dispatched half (guide T5 static form)
+  const int* doc_end;    //   key k visible to query q iff doc_start[q] <= k, i.e. q < doc_end[k]
   // keys >= kv_valid are masked for every query (right-padded tail of non-causal attention).  Only
   // the dQ pass masks them: dK / dV rows of those keys are discarded by the caller, and a masked key
   // never reaches a valid key's dK / dV.
@@ -266,13 +265,10 @@ FTC_DEV void dkdv_dma(__amdgpu_buffer_rsrc_t qr, __amdgpu_buffer_rsrc_t dr, __am
 // SIMD").  Slice j is read by half 1 one barrier interval later, so the Q/dO ring has 4 slots.
 // QR = 32-row query blocks per slice: QR = 2 (D = 64) doubles the MFMA work between two barriers,
 // which at D = 64 is otherwise half of D = 128's (the per-slice barrier / DMA cost stays the same).
-// PP2 (with PP, DIST = 3): half 1 runs B1(j - 1) B2(j - 1) A(j) instead of B2(j - 1) A(j) B1(j), carrying
-// the raw S / dP' accumulators of slice j - 1 across the barrier (not the packed P / dS): both halves
-// then end each interval on MFMAs and each half's softmax VALU issues beside the other half's MFMAs
-// (tools/stamp_dkdv.hip: with PP alone half 1's B1 ran alone at the end of every interval).  Measured:
-// bwd 2.03 vs 1.96 ms, 36.1k vs 36.5k tok/s (profiles/r2/stamp_dkdv.md) -- the MFMA phases wait on the
-// 8 waves' LDS reads, not on the partner's VALU; opt-in (FTC_FLASH_DKDV_PP2=1).
-template <int D, int HW, bool PP = false, int DIST = 2, int QR = 1, bool PP2 = false>
+// (Measured and removed, git history / profiles/r2/stamp_dkdv.md: a B1 B2 A order for half 1 carrying the
+// raw S / dP' across the barrier -- bwd 2.03 vs 1.96 ms: the MFMA phases wait on the 8 waves' LDS reads,
+// not on the partner's VALU.)
+template <int D, int HW, bool PP = false, int DIST = 2, int QR = 1>
 __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
   static_assert(DIST == 2 || (PP && DIST == 3), "DMA distance 3 needs the ping-pong 5-slot ring");
   static_assert(QR == 1 || QR == 2, "one or two 32-row query blocks per slice");
@@ -398,9 +394,6 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
   constexpr int LGKM_ZERO = 0xC07F;                                             // lgkmcnt(0)
 
   const int total = G * nqt;
-  // two waves per SIMD: the younger half loses VALU arbitration on every segment; one static
-  // priority raise (no per-segment flips) hands it the older half's timing (guide T5, static form)
-  if (WAVES == 8 && a.prio_young && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
   // K staging and the V fragments are ordinary loads: retire them before the first DMA so no
   // compiler-inserted wait inside the loop has to count them
   __builtin_amdgcn_s_waitcnt(VM_ZERO);
@@ -602,32 +595,6 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
           if (it + 2 < total) body(it + 2, slot2, slot0);
           if (it + 3 < total) body(it + 3, slot3, slot1);
           if (it + 4 < total) body(it + 4, slot4, slot2);
-        }
-      } else if constexpr (PP2) {
-        auto body = [&](const int it, const char* Qs, const char* Qprev, char* dma_slot) __attribute__((always_inline)) {
-          SEG_START();
-          sync_slice(it, dma_slot);
-          SEG_END(0);
-          if (it > 0) {
-            phaseB1(it - 1);
-            SEG_END(2);
-            phaseB2(Qprev);
-            SEG_END(3);
-          }
-          phaseA(Qs);
-          SEG_END(1);
-        };
-        for (int it = 0; it < total; it += 5) {
-          body(it, slot0, slot4, slot3);
-          if (it + 1 < total) body(it + 1, slot1, slot0, slot4);
-          if (it + 2 < total) body(it + 2, slot2, slot1, slot0);
-          if (it + 3 < total) body(it + 3, slot3, slot2, slot1);
-          if (it + 4 < total) body(it + 4, slot4, slot3, slot2);
-        }
-        if (total > 0) {
-          const int r = (total - 1) % 5;
-          phaseB1(total - 1);
-          phaseB2(r == 0 ? slot0 : r == 1 ? slot1 : r == 2 ? slot2 : r == 3 ? slot3 : slot4);
         }
       } else {
         auto body = [&](const int it, const char* Qs, const char* Qprev, char* dma_slot) __attribute__((always_inline)) {
@@ -914,17 +881,8 @@ void launch_dkdv(const BwdArgs& a, int grid, int waves, bool pp, bool dist3, hip
     const char* e = getenv("FTC_FLASH_DKDV_QR");
     return !(e && e[0] == '1');
   }();
-  // FTC_FLASH_DKDV_PP2=1: half 1 in B1 B2 A order (see bwd_dkdv_kernel)
-  static const bool pp2 = [] {
-    const char* e = getenv("FTC_FLASH_DKDV_PP2");
-    return e && e[0] == '1';
-  }();
-  if (D == 64 && qr2 && waves == 8 && pp && dist3 && pp2)
-    hipLaunchKernelGGL((bwd_dkdv_kernel<64, 1, true, 3, 2, true>), dim3(grid), dim3(512), 0, stream, a);
-  else if (D == 64 && qr2 && waves == 8 && pp && dist3)
+  if (D == 64 && qr2 && waves == 8 && pp && dist3)
     hipLaunchKernelGGL((bwd_dkdv_kernel<64, 1, true, 3, 2>), dim3(grid), dim3(512), 0, stream, a);
-  else if (waves == 8 && pp && dist3 && pp2)
-    hipLaunchKernelGGL((bwd_dkdv_kernel<D, 1, true, 3, 1, true>), dim3(grid), dim3(512), 0, stream, a);
   else if (waves == 8 && pp && dist3)
     hipLaunchKernelGGL((bwd_dkdv_kernel<D, 1, true, 3>), dim3(grid), dim3(512), 0, stream, a);
   else if (waves == 8 && pp)
@@ -943,34 +901,8 @@ extern "C" int ftc_flash_bwd_workspace(int B, int S, int H, int D, long long* by
   return 0;
 }
 
-// Second stream of the calling process's current device for the dQ kernel (FTC_FLASH_BWD_CONCURRENT=1):
-// dK/dV and dQ only share read-only inputs and the delta workspace, so dQ could fill the CUs that
-// dK/dV's causal tail leaves idle.  Measured at the Llama-3-8B layer shape: 2.017 vs 2.016 ms for the
-// backward and 35.3k vs 35.4k tok/s end to end (profiles/r2/s8_*conc*.log) -- dK/dV holds every CU's
-// registers until its last workgroups retire, so the dQ workgroups find no room earlier; off by default.  Fork / join by events keeps the pair one unit on the caller's
-// stream (and capturable in a hipGraph).  One process drives one GPU here; a per-device table
-// still keeps a multi-device caller correct.
-namespace {
-struct SideStream {
-  hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
-SideStream& side_stream() {
-  static SideStream per_dev[64];
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  SideStream& ss = per_dev[dev & 63];
-  if (ss.s == nullptr) {
-    int lo = 0, hi = 0;
-    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-    (void)hipStreamCreateWithPriority(&ss.s, hipStreamNonBlocking, lo);
-    (void)hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming);
-    (void)hipEventCreateWithFlags(&ss.join, hipEventDisableTiming);
-  }
-  return ss;
-}
-}  // namespace
-
+// (Removed: dQ on a second stream beside dK/dV, FTC_FLASH_BWD_CONCURRENT -- 2.017 vs 2.016 ms,
+// profiles/r2/s8_*conc*.log: dK/dV holds every CU's registers until its last workgroups retire.)
 extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
                              const float* lse, void* dq, void* dk, void* dv, void* workspace, int B, int S, int H,
                              int KV, int D, long long q_rs, long long kv_rs, long long o_rs, long long do_rs,
@@ -987,13 +919,8 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
   if ((long long)S * max_rs * 2 >= (1LL << 31) || 2LL * B * H * S * 4 >= (1LL << 31)) return -1;
   BwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)o, (const uint16_t*)dout,
             lse, (float*)workspace, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, q_rs, kv_rs, o_rs, dq_rs, dkv_rs, do_rs,
-            B, S, H, KV, scale, scale * LOG2E, causal, window, 0, doc_start, doc_end, kv_valid,
+            B, S, H, KV, scale, scale * LOG2E, causal, window, doc_start, doc_end, kv_valid,
             rope_cos, rope_sin, rope_pos};
-  static const int prio = [] {
-    const char* e = getenv("FTC_FLASH_BWD_PRIO");
-    return (e && e[0] == '1') ? 1 : 0;
-  }();
-  a.prio_young = prio;
   const int grid_d = ftc::stream_grid((long long)B * S, 4);
   const int g_kv = B * KV * (S / 256);
   const int g_q = B * H * (S / 128);
@@ -1021,21 +948,11 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
     const char* e = getenv("FTC_FLASH_DKDV_DIST");
     return !(e && e[0] == '2');
   }();
-  static const bool concurrent = [] {
-    const char* e = getenv("FTC_FLASH_BWD_CONCURRENT");
-    return e && e[0] == '1';
-  }();
   hipStream_t qs = stream;
-  SideStream* ss = nullptr;
   if (D == 128) {
     hipLaunchKernelGGL(bwd_delta_kernel<128>, dim3(grid_d), dim3(256), 0, stream, a);
   } else {
     hipLaunchKernelGGL(bwd_delta_kernel<64>, dim3(grid_d), dim3(256), 0, stream, a);
-  }
-  if (concurrent) {  // dK/dV first on the caller's stream, dQ on the side stream after the delta pass
-    ss = &side_stream();
-    qs = ss->s;
-    if (hipEventRecord(ss->fork, stream) != hipSuccess || hipStreamWaitEvent(qs, ss->fork, 0) != hipSuccess) return -2;
   }
   if (D == 128) {
     launch_dkdv<128>(a, g_kv, dkdv_waves, pp, dist3, stream);
@@ -1047,9 +964,6 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
   } else {
     launch_dkdv<64>(a, g_kv, dkdv_waves, pp, dist3, stream);
     hipLaunchKernelGGL((bwd_dq_kernel<64, 2>), dim3(g_q), dim3(256), 0, qs, a);
-  }
-  if (ss) {
-    if (hipEventRecord(ss->join, qs) != hipSuccess || hipStreamWaitEvent(stream, ss->join, 0) != hipSuccess) return -2;
   }
   return (int)hipGetLastError();
 }

@@ -33,8 +33,11 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-// query rows per workgroup = 32 x waves (WAVES = 4: 256 threads, two workgroups per CU; WAVES = 8: 512
-// threads, one workgroup per CU sharing every K/V tile between twice the query rows)
+// query rows per workgroup = 32 x 4 waves (256 threads, two workgroups per CU).  Measured and removed
+// (git history, profiles/r1_attn_fwd_pp.log, profiles/r2/s9_attn_pipe*.log): 8 waves per workgroup
+// (0.617 vs 0.604 ms), an 8-wave ping-pong phase order (0.64 ms) and an in-wave software pipeline across
+// tiles (0.626 ms at 2 waves/SIMD, 0.85 at 1) at the Llama-3-8B layer shape.
+constexpr int WAVES = 4;
 constexpr int BK = 64;   // keys per tile
 // build-time A/B knobs (tools/fwd_knobs_ab.sh): K-fragment reads issued ahead of the S MFMA chain, and a
 // raised wave priority over the S MFMA phase
@@ -72,16 +75,11 @@ FTC_DEV bf16x8 as_bf8(const uint4& v) { return __builtin_bit_cast(bf16x8, v); }
 
 // max over lanes l and l ^ 32: v_permlane32_swap (gfx950 VALU, one instruction) instead of
 // ds_bpermute -- the row max sits on the softmax's dependency chain every tile, and the LDS permute's
-// round trip was part of it.  PL = false: the ds_bpermute form (FTC_FLASH_FWD_XHALF=0, A/B).
-template <bool PL>
+// round trip was part of it.
 FTC_DEV float xhalf_max(float v) {
-  if constexpr (PL) {
-    const auto pr = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    const float a = __uint_as_float(pr[0]), b = __uint_as_float(pr[1]);
-    return a > b ? a : b;  // lane l holds {v_l, v_(l^32)} in some order
-  } else {
-    return fmaxf(v, __shfl_xor(v, 32, 64));
-  }
+  const auto pr = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  const float a = __uint_as_float(pr[0]), b = __uint_as_float(pr[1]);
+  return a > b ? a : b;  // lane l holds {v_l, v_(l^32)} in some order
 }
 
 FTC_DEV bf16x8 pack_p(const f32x16& p, int base) {
@@ -148,14 +146,7 @@ FTC_DEV void fwd_dma(__amdgpu_buffer_rsrc_t kr, __amdgpu_buffer_rsrc_t vr, const
   }
 }
 
-// PP (WAVES = 8 only): ping-pong phase order for the two waves sharing a SIMD (w, w + 4): half 0 runs
-// A(t) B1(t) B2(t) and half 1 runs B2(t-1) A(t) B1(t) between the same barriers (A = S MFMAs, B1 =
-// mask / online softmax / pack VALU, B2 = PV MFMAs), so one wave's softmax issues under the other's
-// MFMAs.  Half 1 reads V of tile t-1 one interval late: V has a 4-slot ring (K keeps 2).  Measured
-// at the Llama-3-8B layer shape: 0.64 ms vs 0.617 (8 waves) and 0.604 (4 waves, the default) -- unlike
-// the dK/dV kernel, the forward's softmax already overlaps across the two co-resident 4-wave
-// workgroups, so PP stays opt-in (FTC_FLASH_FWD_WAVES=8 FTC_FLASH_FWD_PP=1; profiles/r1_attn_fwd_pp.log).
-template <int D, int WAVES, bool PP = false, bool PL = true>
+template <int D>
 __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArgs a) {
   constexpr int BQ = 32 * WAVES;
   constexpr int NCH = D / 8;           // 16-byte chunks per row
@@ -171,8 +162,6 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
   __shared__ __attribute__((aligned(16))) char V0[TILE_BYTES];
   __shared__ __attribute__((aligned(16))) char K1[TILE_BYTES];
   __shared__ __attribute__((aligned(16))) char V1[TILE_BYTES];
-  __shared__ __attribute__((aligned(16))) char V2[PP ? TILE_BYTES : 16];
-  __shared__ __attribute__((aligned(16))) char V3[PP ? TILE_BYTES : 16];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform -> scalar branches
@@ -264,8 +253,8 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
   }
 
   f32x16 s[2];   // S^T of the current tile, then its P (registers between the phases)
-  bf16x8 pf[4];  // packed P^T operand of the PV MFMAs (carried across a barrier by PP's half 1)
-  // wait for tile t, barrier, then DMA tile t+1 into the slots that held tile t-1 (PP: V of t-3)
+  bf16x8 pf[4];  // packed P^T operand of the PV MFMAs
+  // wait for tile t, barrier, then DMA tile t+1 into the slots that held tile t-1
   auto sync_tile = [&](const int t, char* Kn, char* Vn) __attribute__((always_inline)) {
     __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's pieces of tile t landed (vmcnt(0))
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
@@ -324,7 +313,7 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[kt][i]);  // (a depth-5 fmaxf tree measured 3-4 % slower)
-    mt = xhalf_max<PL>(mt) * c;  // c > 0: max commutes with the scale
+    mt = xhalf_max(mt) * c;  // c > 0: max commutes with the scale
     // deferred rescale (guide T13): the running reference m moves -- and O, l are rescaled -- only
     // when some row's max grew by more than 2^8; otherwise P <= 256 (exact in bf16's exponent range,
     // fp32 accumulation) and the 64 multiplies of O are skipped.  Wave-uniform branch.
@@ -392,55 +381,19 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
       }
     }
   };
-  if constexpr (!PP) {
-    // tile t reads (Kc, Vc); tile t+1 is DMA'd into (Kn, Vn), which held tile t-1 -- free once every
-    // wave passed this tile's barrier
-    auto tile = [&](const int t, const char* Kc, const char* Vc, char* Kn, char* Vn) __attribute__((always_inline)) {
-      sync_tile(t, Kn, Vn);
-      if constexpr (FWD_PRIO) __builtin_amdgcn_s_setprio(1);  // S MFMA phase ahead of the partner wave's VALU
-      phaseA(Kc);
-      if constexpr (FWD_PRIO) __builtin_amdgcn_s_setprio(0);
-      phaseB1(t);
-      phaseB2(Vc);
-    };
-    for (int t = 0; t < ntiles; t += 2) {
-      tile(t, K0, V0, K1, V1);
-      if (t + 1 < ntiles) tile(t + 1, K1, V1, K0, V0);
-    }
-  } else {
-    // K ring of 2 (K of tile t-1 is free after its interval), V ring of 4 (half 1 reads V of t-1 in
-    // interval t); separate straight-line loops per half, equal barrier counts
-    if (wave < 4) {
-      auto tile = [&](const int t, const char* Kc, const char* Vc, char* Kn, char* Vn) __attribute__((always_inline)) {
-        sync_tile(t, Kn, Vn);
-        phaseA(Kc);
-        phaseB1(t);
-        phaseB2(Vc);
-      };
-      for (int t = 0; t < ntiles; t += 4) {
-        tile(t, K0, V0, K1, V1);
-        if (t + 1 < ntiles) tile(t + 1, K1, V1, K0, V2);
-        if (t + 2 < ntiles) tile(t + 2, K0, V2, K1, V3);
-        if (t + 3 < ntiles) tile(t + 3, K1, V3, K0, V0);
-      }
-    } else {
-      auto tile = [&](const int t, const char* Kc, const char* Vprev, char* Kn, char* Vn) __attribute__((always_inline)) {
-        sync_tile(t, Kn, Vn);
-        if (t > 0) phaseB2(Vprev);
-        phaseA(Kc);
-        phaseB1(t);
-      };
-      for (int t = 0; t < ntiles; t += 4) {
-        tile(t, K0, V3, K1, V1);
-        if (t + 1 < ntiles) tile(t + 1, K1, V0, K0, V2);
-        if (t + 2 < ntiles) tile(t + 2, K0, V1, K1, V3);
-        if (t + 3 < ntiles) tile(t + 3, K1, V2, K0, V0);
-      }
-      if (ntiles > 0) {
-        const int last = ntiles - 1;
-        phaseB2((last & 3) == 0 ? V0 : (last & 3) == 1 ? V1 : (last & 3) == 2 ? V2 : V3);
-      }
-    }
+  // tile t reads (Kc, Vc); tile t+1 is DMA'd into (Kn, Vn), which held tile t-1 -- free once every
+  // wave passed this tile's barrier
+  auto tile = [&](const int t, const char* Kc, const char* Vc, char* Kn, char* Vn) __attribute__((always_inline)) {
+    sync_tile(t, Kn, Vn);
+    if constexpr (FWD_PRIO) __builtin_amdgcn_s_setprio(1);  // S MFMA phase ahead of the partner wave's VALU
+    phaseA(Kc);
+    if constexpr (FWD_PRIO) __builtin_amdgcn_s_setprio(0);
+    phaseB1(t);
+    phaseB2(Vc);
+  };
+  for (int t = 0; t < ntiles; t += 2) {
+    tile(t, K0, V0, K1, V1);
+    if (t + 1 < ntiles) tile(t + 1, K1, V1, K0, V0);
   }
 
   // ---- epilogue: normalise, store O (bf16) and LSE (natural log)
@@ -491,265 +444,6 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
   }
 }
 
-// PIPE (FTC_FLASH_FWD_PIPE=1; 4 waves, D = 64 / 128): software pipeline across tiles inside ONE wave
-// (guide T15) -- the S MFMAs of tile t+1 are issued in the same basic block as the exponentials /
-// row sums / packing of tile t, so the matrix pipe and the VALU of one wave overlap instead of
-// alternating A -> B1 -> B2.  Two named S buffers (no runtime-indexed register arrays); the mask,
-// row max and rescale decision of tile t (branches) stay before the merged block; PV of tile t after
-// it.  K of tile t+1 and V of tile t are live together: K keeps a 2-slot ring, V a 3-slot ring
-// (80 KiB per workgroup, two workgroups per CU = the whole 160 KiB LDS).  One barrier per tile.
-// Measured at the Llama-3-8B layer shape (profiles/r2/s9_attn_pipe*.log, interleaved runs in one
-// call): 0.626-0.628 ms at 2 waves/SIMD (two S buffers push the D=128 build to 256 VGPRs + 56 B of
-// spills) and 0.85 ms at 1 wave/SIMD, against 0.594-0.601 ms for the default kernel -- two
-// co-resident workgroups already overlap one wave's softmax with the other's MFMAs, so the in-wave
-// pipeline only adds register pressure here.  Kept as an opt-in variant (numerics covered by the
-// same GPU tests: profiles/r2/s9_pytest_pipe*.log).
-#ifndef PIPE_VALU_PER_MFMA
-#define PIPE_VALU_PER_MFMA 6
-#endif
-// OCC = waves per SIMD: 2 (two workgroups per CU, 256 registers: a few spill at D=128) or 1 (one
-// workgroup per CU, 512 registers: the in-wave pipeline is the only overlap)
-template <int D, int OCC>
-__global__ __launch_bounds__(256, OCC) void flash_fwd_pipe_kernel(FwdArgs a) {
-  constexpr int WAVES = 4;
-  constexpr int BQ = 32 * WAVES;
-  constexpr int NCH = D / 8;
-  constexpr int DSTEPS = D / 16;
-  constexpr int DT = D / 32;
-  constexpr int TILE_BYTES = BK * D * 2;
-  constexpr int NGT = TILE_BYTES / 1024 / WAVES;
-  constexpr int RPG = 1024 / (D * 2);
-  static_assert(NGT >= 1, "tile too small for the wave count");
-  __shared__ __attribute__((aligned(16))) char K0[TILE_BYTES];
-  __shared__ __attribute__((aligned(16))) char K1[TILE_BYTES];
-  __shared__ __attribute__((aligned(16))) char V0[TILE_BYTES];
-  __shared__ __attribute__((aligned(16))) char V1[TILE_BYTES];
-  __shared__ __attribute__((aligned(16))) char V2[TILE_BYTES];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int hh = lane >> 5, lr = lane & 31;
-  int qb, b, hq, kvh;
-  decode_block(a, qb, b, hq, kvh);
-  const int S = a.S;
-  const int q0 = qb * BQ;
-  const int qrow = q0 + wave * 32 + lr;
-  const bool qvalid = qrow < S;
-
-  bf16x8 qf[DSTEPS];
-  {
-    const uint16_t* qp = a.q + ((long long)b * S + (qvalid ? qrow : 0)) * a.q_rs + (long long)hq * D + 8 * hh;
-#pragma unroll
-    for (int st = 0; st < DSTEPS; ++st) {
-      uint4 v = qvalid ? *reinterpret_cast<const uint4*>(qp + 16 * st) : make_uint4(0, 0, 0, 0);
-      qf[st] = as_bf8(v);
-    }
-  }
-  const int q_last = min(S, q0 + BQ) - 1;
-  int kv_end = min(a.causal ? q_last + 1 : S, a.kv_valid);
-  int kv_begin = 0;
-  if (a.window > 0) {
-    kv_begin = max(0, q0 - a.window + 1);
-    kv_begin = (kv_begin / BK) * BK;
-  }
-  int dlo = -0x3fffffff, wdmax = -0x3fffffff;
-  if (a.doc_start) {
-    const int* ds = a.doc_start + (long long)b * S;
-    dlo = ds[qvalid ? qrow : S - 1];
-    wdmax = ds[min(S - 1, q0 + wave * 32 + 31)];
-    kv_begin = max(kv_begin, (ds[q0] / BK) * BK);
-  }
-  const int ntiles = (kv_end - kv_begin + BK - 1) / BK;
-
-  const uint16_t* kbase = a.k + (long long)b * S * a.kv_rs + (long long)kvh * D;
-  const uint16_t* vbase = a.v + (long long)b * S * a.kv_rs + (long long)kvh * D;
-  const auto krs = make_rsrc(kbase), vrs = make_rsrc(vbase);
-  int voff[NGT];
-#pragma unroll
-  for (int i = 0; i < NGT; ++i) {
-    const int row = (wave * NGT + i) * RPG + lane / NCH, pc = lane % NCH;
-    voff[i] = (row * (int)a.kv_rs + ((pc ^ swz(row)) & (NCH - 1)) * 8) * 2;
-  }
-
-  f32x16 o[DT];
-#pragma unroll
-  for (int t = 0; t < DT; ++t)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) o[t][i] = 0.f;
-  float m = -INFINITY, l = 0.f;
-  const float c = a.scale_log2;
-  const int gi = lane >> 4, li = lane & 15;
-  const int trq = li >> 2, trp = li & 3;
-
-  auto kslot = [&](const int t) -> char* { return (t & 1) ? K1 : K0; };
-  auto vslot = [&](const int t) -> char* {
-    const int r = t % 3;
-    return r == 0 ? V0 : (r == 1 ? V1 : V2);
-  };
-  auto dma = [&](const int t) __attribute__((always_inline)) {
-    fwd_dma<D, NGT, RPG>(krs, vrs, voff, (kv_begin + t * BK) * (int)a.kv_rs * 2, kslot(t), vslot(t), wave);
-  };
-  // S^T = K Q^T of one tile into sd (two 32-key blocks); K reads issued ahead of each MFMA chain
-  auto phaseA = [&](const char* Kc, f32x16* sd) __attribute__((always_inline)) {
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      const int r = kt * 32 + lr;
-      uint4 kf[DSTEPS];
-#pragma unroll
-      for (int st = 0; st < DSTEPS; ++st) kf[st] = *reinterpret_cast<const uint4*>(Kc + lds_off<D>(r, 2 * st + hh));
-      f32x16 acc;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-#pragma unroll
-      for (int st = 0; st < DSTEPS; ++st) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(kf[st]), qf[st], acc, 0, 0, 0);
-      sd[kt] = acc;
-    }
-  };
-  // mask + row max + (deferred) rescale decision of tile t: the branchy part, before the merged block
-  auto phaseB1a = [&](const int t, f32x16* sc) __attribute__((always_inline)) -> float {
-    const int kv0 = kv_begin + t * BK;
-    const int qmin_w = q0 + wave * 32;
-    const bool need_mask = (a.causal && kv0 + BK - 1 > qmin_w) || (a.window > 0 && qmin_w + 31 - kv0 >= a.window) ||
-                           kv0 + BK > a.kv_valid ||
-                           kv0 < wdmax;
-    if (need_mask) {
-      const int base = kv0 + 4 * hh;
-      const int hi = min(a.causal ? qrow : 0x3fffffff, a.kv_valid - 1) - base;
-      const int lo = max(a.window > 0 ? qrow - a.window + 1 : -0x3fffffff, dlo) - base;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int off = kt * 32 + (i & 3) + 8 * (i >> 2);
-          sc[kt][i] = (off >= lo && off <= hi) ? sc[kt][i] : -INFINITY;
-        }
-    }
-    float mt = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sc[kt][i]);
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * c;
-    if (__builtin_amdgcn_ballot_w64(mt > m + 8.0f) != 0) {
-      const float mn = fmaxf(m, mt);
-      const float alpha = __builtin_amdgcn_exp2f(m - ((mn == -INFINITY) ? 0.f : mn));
-      m = mn;
-      l *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
-    }
-    return (m == -INFINITY) ? 0.f : m;
-  };
-  // exponentials, row sum and bf16 packing of tile t (straight-line VALU)
-  bf16x8 pf[4];
-  auto phaseB1b = [&](f32x16* sc, const float mref) __attribute__((always_inline)) {
-    float rs = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[kt][i], c, -mref));
-        sc[kt][i] = p;
-        rs += p;
-      }
-    l += rs;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) pf[ks] = pack_p(sc[ks >> 1], 8 * (ks & 1));
-  };
-  auto phaseB2 = [&](const char* Vc) __attribute__((always_inline)) {
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      const int col = dt * 32 + 16 * (gi & 1) + 4 * trp;
-      const int chunk = col >> 3, half8 = (col & 7) ? 8 : 0;
-      s16x4 vt[8];
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const int r1 = 16 * ks + 4 * hh + trq;
-        vt[2 * ks] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vc + lds_off<D>(r1, chunk) + half8));
-        vt[2 * ks + 1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vc + lds_off<D>(r1 + 8, chunk) + half8));
-      }
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const s16x4 v1 = vt[2 * ks], v2 = vt[2 * ks + 1];
-        s16x8 va = {v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
-        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, va), pf[ks], o[dt], 0, 0, 0);
-      }
-    }
-  };
-  // one pipelined tile with a successor: [barrier, DMA t+2] -> B1a(t) -> {A(t+1) || B1b(t)} -> B2(t).
-  // No branch after B1a: the merged block stays one scheduling region (a branch around it lets the
-  // compiler hoist B1b's exponentials above it, which undoes the overlap).
-  auto step = [&](const int t, f32x16* cur, f32x16* nxt) __attribute__((always_inline)) {
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's DMA pieces of tile t+1 landed (vmcnt(0))
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-    __builtin_amdgcn_s_barrier();        // ... everyone's; A(t) and B2(t-1) done by every wave
-    if (t + 2 < ntiles) dma(t + 2);      // K slot of t, V slot of t-1: both free now
-    const float mref = phaseB1a(t, cur);
-    phaseA(kslot(t + 1), nxt);
-    phaseB1b(cur, mref);
-    // interleave: block 0's K reads, then per S MFMA a slice of tile t's exp / sum / pack VALU
-    // (mask 0x402 = VALU | TRANS), block 1's K reads after the first MFMAs
-    __builtin_amdgcn_sched_group_barrier(0x100, DSTEPS, 0);
-#pragma unroll
-    for (int i = 0; i < 2 * DSTEPS; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x402, PIPE_VALU_PER_MFMA, 0);
-      if (i == DSTEPS - 2) __builtin_amdgcn_sched_group_barrier(0x100, DSTEPS, 0);
-    }
-    phaseB2(vslot(t));
-  };
-  // the last tile: already landed (waited for by the previous step), no successor
-  auto last = [&](const int t, f32x16* cur) __attribute__((always_inline)) {
-    const float mref = phaseB1a(t, cur);
-    phaseB1b(cur, mref);
-    phaseB2(vslot(t));
-  };
-
-  f32x16 sA[2], sB[2];
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // Q fragments retired before any DMA
-  if (ntiles > 0) {
-    dma(0);
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
-    if (ntiles > 1) dma(1);
-    phaseA(K0, sA);
-    int t = 0;
-    for (; t + 2 < ntiles; t += 2) {
-      step(t, sA, sB);
-      step(t + 1, sB, sA);
-    }
-    if (t + 1 < ntiles) {
-      step(t, sA, sB);
-      last(t + 1, sB);
-    } else {
-      last(t, sA);
-    }
-  }
-
-  const float ltot = l + __shfl_xor(l, 32, 64);
-  const float inv = ltot > 0.f ? 1.0f / ltot : 0.f;
-  if (qvalid) {
-    uint16_t* op = a.o + ((long long)b * S + qrow) * a.o_rs + (long long)hq * D;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = dt * 32 + 8 * g4 + 4 * hh;
-        uint2 w;
-        w.x = pack_bf2(o[dt][4 * g4 + 0] * inv, o[dt][4 * g4 + 1] * inv);
-        w.y = pack_bf2(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
-        *reinterpret_cast<uint2*>(op + d) = w;
-      }
-    if (hh == 0) {
-      const float lse2 = (m == -INFINITY) ? -INFINITY : m + __log2f(ltot);
-      a.lse[((long long)b * a.H + hq) * S + qrow] = lse2 * LN2;
-    }
-  }
-}
-
 }  // namespace
 
 extern "C" int ftc_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H,
@@ -757,54 +451,13 @@ extern "C" int ftc_flash_fwd(const void* q, const void* k, const void* v, void* 
                              int window, const int* doc_start, int kv_valid, hipStream_t stream) {
   if (S % BK != 0 || H % KV != 0 || (D != 128 && D != 64)) return -1;
   if (kv_valid <= 0 || kv_valid > S) kv_valid = S;
-  static const int waves = [] {
-    const char* e = getenv("FTC_FLASH_FWD_WAVES");
-    return (e && e[0] == '8') ? 8 : 4;
-  }();
-  const int BQ = 32 * waves;
+  constexpr int BQ = 32 * 4;
   FwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, q_rs, kv_rs, o_rs,
             B, S, H, KV, (S + BQ - 1) / BQ, scale * LOG2E, causal, window, doc_start, kv_valid};
   const int nblocks = a.nqb * B * H;
-  const size_t lds = 0;  // static: K/V double buffers
-  static const bool pp = [] {
-    const char* e = getenv("FTC_FLASH_FWD_PP");
-    return e && e[0] == '1';
-  }();
-  // FTC_FLASH_FWD_PIPE=1: in-wave software pipeline at 2 waves/SIMD; =2: the same at 1 wave/SIMD
-  static const int pipe = [] {
-    const char* e = getenv("FTC_FLASH_FWD_PIPE");
-    return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
-  }();
-  // FTC_FLASH_FWD_XHALF=0: the row max's lane l <-> l ^ 32 exchange by ds_bpermute instead of
-  // v_permlane32_swap (A/B of xhalf_max)
-  static const bool xhalf_pl = [] {
-    const char* e = getenv("FTC_FLASH_FWD_XHALF");
-    return !(e && e[0] == '0');
-  }();
-  if (pipe && waves == 4) {
-    if (D == 128 && pipe == 1)
-      hipLaunchKernelGGL((flash_fwd_pipe_kernel<128, 2>), dim3(nblocks), dim3(256), lds, stream, a);
-    else if (D == 128)
-      hipLaunchKernelGGL((flash_fwd_pipe_kernel<128, 1>), dim3(nblocks), dim3(256), lds, stream, a);
-    else if (pipe == 1)
-      hipLaunchKernelGGL((flash_fwd_pipe_kernel<64, 2>), dim3(nblocks), dim3(256), lds, stream, a);
-    else
-      hipLaunchKernelGGL((flash_fwd_pipe_kernel<64, 1>), dim3(nblocks), dim3(256), lds, stream, a);
-  } else if (waves == 8 && pp && D == 128) {
-    hipLaunchKernelGGL((flash_fwd_kernel<128, 8, true>), dim3(nblocks), dim3(512), lds, stream, a);
-  } else if (waves == 8) {
-    if (D == 128)
-      hipLaunchKernelGGL((flash_fwd_kernel<128, 8>), dim3(nblocks), dim3(512), lds, stream, a);
-    else
-      hipLaunchKernelGGL((flash_fwd_kernel<64, 8>), dim3(nblocks), dim3(512), lds, stream, a);
-  } else {
-    if (D == 128)
-      if (xhalf_pl)
-        hipLaunchKernelGGL((flash_fwd_kernel<128, 4>), dim3(nblocks), dim3(256), lds, stream, a);
-      else
-        hipLaunchKernelGGL((flash_fwd_kernel<128, 4, false, false>), dim3(nblocks), dim3(256), lds, stream, a);
-    else
-      hipLaunchKernelGGL((flash_fwd_kernel<64, 4>), dim3(nblocks), dim3(256), lds, stream, a);
-  }
+  if (D == 128)
+    hipLaunchKernelGGL((flash_fwd_kernel<128>), dim3(nblocks), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL((flash_fwd_kernel<64>), dim3(nblocks), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }

@@ -109,6 +109,24 @@ FTC_DEV void barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// Diagnostic build only (tools/gemm_lab/build_stamp.sh defines FTC_GEMM_STAMP; the extension build never
+// does): per-wave cycle sums of the K loop's wait segments for the first 8 workgroups (guide "In-kernel
+// stamps": s_memtime + lgkmcnt(0), placed only where no LDS read is outstanding or right before the
+// lgkmcnt wait that follows anyway -- shares, not exact lengths).
+#ifdef FTC_GEMM_STAMP
+__device__ unsigned long long g_gemm_stamps[8][4][8];  // [block][wave][lgkm1, bar1, lgkm2, bar2, vm, bar3, loop, iters]
+FTC_DEV unsigned long long stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define FTC_GS(...) __VA_ARGS__
+#else
+#define FTC_GS(...)
+#endif
+
 template <bool NTS, typename T>
 FTC_DEV void st(T* p, const T& v) {
   if constexpr (NTS) __builtin_nontemporal_store(v, p);
@@ -319,6 +337,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(NTArgs p) {
     }
   };
   auto nop = [](int) __attribute__((always_inline)) {};
+  FTC_GS(unsigned long long gs[8] = {}; unsigned long long t_a, t_b;)
 
   // one super-stage.  first: the tile's first stage (zero accumulators); after_epi: an epilogue's
   // stores were issued between the DMA of stage g+1 and this iteration's pieces, so the wait for stage
@@ -337,8 +356,11 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(NTArgs p) {
         ya[4 * gi + k] = rd(cur, a_off[1] + (4 * gi + k) * 2048);
       });
     group(xa, xb, 2, first, nop);
+    FTC_GS(t_a = stamp();)
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    FTC_GS(t_b = stamp(); gs[0] += t_b - t_a;)
     barrier();
+    FTC_GS(t_a = stamp(); gs[1] += t_a - t_b;)
 #pragma unroll
     for (int gi = 3; gi < 7; ++gi)
       group(xa, xb, gi, first, [&](int k) __attribute__((always_inline)) {
@@ -347,8 +369,11 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(NTArgs p) {
         else dma(0, ras, dA, i);
       });
     group(xa, xb, 7, first, nop);
+    FTC_GS(t_a = stamp();)
     __builtin_amdgcn_s_waitcnt(0xC07F);
+    FTC_GS(t_b = stamp(); gs[2] += t_b - t_a;)
     barrier();
+    FTC_GS(t_a = stamp(); gs[3] += t_a - t_b;)
     // half 1 on Y: B pieces in groups 0-3, wait for stage g+1, X of g+1 in groups 4-5 (A first: the
     // next iteration's first group needs all of X.A but only X.B[0])
 #pragma unroll
@@ -356,13 +381,16 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(NTArgs p) {
       group(ya, yb, gi, std::false_type{}, [&](int k) __attribute__((always_inline)) {
         if (!(k & 1)) dma(1, rbs, dB, 2 * gi + (k >> 1));
       });
+    FTC_GS(t_a = stamp();)
     if (after_epi) {
       constexpr int n = 16 + kEpiStores<F32C> > 63 ? 63 : 16 + kEpiStores<F32C>;
       __builtin_amdgcn_s_waitcnt(0x0F70 | (n & 15) | ((n >> 4) << 14));
     } else {
       __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16): the 16 pieces of g+1 landed
     }
+    FTC_GS(t_b = stamp(); gs[4] += t_b - t_a;)
     barrier();
+    FTC_GS(t_a = stamp(); gs[5] += t_a - t_b; gs[7] += 1;)
     group(ya, yb, 4, std::false_type{}, [&](int k) __attribute__((always_inline)) {
       xa[2 * k] = rd(nxt, a_off[0] + 2 * k * 2048);
       xa[2 * k + 1] = rd(nxt, a_off[0] + (2 * k + 1) * 2048);
@@ -398,6 +426,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(NTArgs p) {
     xb[i] = rd(S, b_off[0] + bnt(i));
   }
 
+  FTC_GS(const unsigned long long t_loop = stamp();)
   int g = 0;
   for (int ti = 0; ti < my; ++ti) {
     iteration(g++, std::true_type{}, ti > 0);
@@ -407,6 +436,11 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(NTArgs p) {
     store_w128<F32C, EPI, NTS, BETA>(p, acc, (long long)mb * BM + wm * 128, (long long)nb * BN + wn * 128);
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no LDS-DMA may outlive the workgroup
+#ifdef FTC_GEMM_STAMP
+  gs[6] = stamp() - t_loop;
+  if (blockIdx.x < 8 && lane == 0)
+    for (int i = 0; i < 8; ++i) g_gemm_stamps[blockIdx.x][wave][i] = gs[i];
+#endif
 }
 
 // ---- launch configuration ----------------------------------------------------------------------------
@@ -465,6 +499,12 @@ int launch(NTArgs& p, hipStream_t stream) {
 extern "C" void ftc_gemm_nt_config(int grid_cap, int group, int xcc, int nt_store) {
   config() = Config{grid_cap, group, xcc, nt_store};
 }
+
+#ifdef FTC_GEMM_STAMP
+extern "C" int ftc_gemm_nt_stamps(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_stamps), sizeof(g_gemm_stamps));
+}
+#endif
 
 // C[M, N] (ldc) = alpha A B^T + beta C; A [M, K] (lda), B [N, K] (ldb) bf16 row-major, K contiguous.
 // Returns 0 when the shape / alignment is outside the kernel's contract.

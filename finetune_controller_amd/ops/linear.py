@@ -246,32 +246,9 @@ def _wgrad_on_side(mg: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, tn_dw:
     _DW_PENDING[:] = [(ev, dev, dy2, x2)]
 
 
-# LoRA adapter weight gradients (dA, dB into their flat-buffer main_grad) on the same side stream, issued
-# between the rank-r tail product and the input-gradient GEMM so they run under it; same ordering rules
-# as the full-FT dW above.  ``FTC_LORA_WG_STREAM=1``: opt-in -- measured on the headline step (interleaved, one
-# box, profiles/r3/lora_wg/): 35,213 / 35,138 vs 35,562 / 35,473 tok/s serial (-1.0 %): the 30 us rank-r
-# kernels stretch the big GEMMs they share the CUs with more than their own time.
-_LORA_WG_STREAM = os.environ.get("FTC_LORA_WG_STREAM", "0") == "1"
-
-
-def set_lora_wgrad_stream(on: bool) -> None:
-    global _LORA_WG_STREAM
-    join_wgrad_stream()
-    _LORA_WG_STREAM = bool(on)
-
-
-def _on_side(dev, fn, *keep):
-    """Run ``fn()`` on the side stream after everything the main stream has enqueued so far; ``keep``
-    (the operands) stays referenced until the main stream joins (``join_wgrad_stream``)."""
-    main = torch.cuda.current_stream(dev)
-    side = _wgrad_side(dev)
-    side.wait_stream(main)
-    with torch.cuda.stream(side):
-        fn()
-        ev = torch.cuda.Event()
-        ev.record(side)
-    held = _DW_PENDING[0][2:] if _DW_PENDING else ()
-    _DW_PENDING[:] = [(ev, dev) + tuple(held) + keep]
+# (Removed: LoRA adapter weight gradients on the side stream under the input-gradient GEMM --
+# 35,213 / 35,138 vs 35,562 / 35,473 tok/s serial, profiles/r3/lora_wg/: the 30 us rank-r kernels stretch
+# the big GEMMs they share the CUs with more than their own time.)
 
 
 def _mask_blocks(dB: torch.Tensor, blocks):
@@ -805,13 +782,6 @@ class _LoRALinearFn(torch.autograd.Function):
             if not take_prefilled("bwd", dy2, aug):
                 tail_product(dy2, N, Rp, aug.bwd_tail_operand(A, B, s), aug.nct)
             dyb = _tail(dy2, N, aug.R)
-            if (_LORA_WG_STREAM and use_hip(dy2) and ctx.lora_params is not None and ctx.mask is None
-                    and (need_a or need_bb) and not torch.cuda.is_current_stream_capturing()):
-                # adapter weight gradients under the input-gradient GEMM (direct main_grad: nothing returned)
-                lp, xa_, blk = ctx.lora_params, xa, ctx.blocks
-                _on_side(dy2.device, lambda: lora_weight_grads(lp, dy2, xa_, xa_scaled, dyb, x2, s, blk, need_a,
-                                                               need_bb), dy2, x2, xa_, dyb)
-                need_a = need_bb = False  # done
             rhs = aug.bwd_operand() if _TN_BWD else aug.big[:, :aug.K]
             dx = torch.empty(dy2.shape[0], aug.K, dtype=dy2.dtype, device=dy2.device)
             # rhs^T = bigT [K, N+Rp] row-major: the hand-written NT kernel's K-contiguous B operand

@@ -164,41 +164,26 @@ class _LoRAMLPFn(torch.autograd.Function):
             buf = torch.empty(dy2.shape[0], d + dn_p.Rp, dtype=dy2.dtype, device=dy2.device)
             buf[:, :d].copy_(dy2)
             dy2 = buf[:, :d]
-        side = _L._LORA_WG_STREAM and dy2.is_cuda and not torch.cuda.is_current_stream_capturing()
         # 4. dy B_down into dy's spare columns, dh through the augmented (TN) operand
         tail_product(dy2, d, dn_p.Rp, dn_p.bwd_tail(), dn_p.nct)
         dyb_dn = _tail(dy2, d, dn_p.R)
-        # 5. dB_down += dy^T (s h A_down^T) -- on the side stream under the dh GEMM (ops.linear _on_side)
+        # 5. dB_down += dy^T (s h A_down^T)
         hta = _tail(h, F, dn_p.R)
-
-        def db_down():
-            _accum_xty(B_dn.main_grad, dy2, hta, 1.0)
-            _grad_ready(B_dn)
-
-        if side:
-            _L._on_side(dy2.device, db_down, dy2, hta)
         dh = gemm_mm(_wide(dy2, d + dn_p.Rp), dn_p.bwd_weight())
-        if not side:
-            db_down()
+        _accum_xty(B_dn.main_grad, dy2, hta, 1.0)
+        _grad_ready(B_dn)
         # 6. SwiGLU backward + dgu B_gu + dB_gu + dA_down
         dgu = ext().swiglu_bwd_wgrad(dh, gu, gu_p.Rp, gu_p.bwd_tail(), _tail(x2, K, 32), dyb_dn, B_gu.main_grad,
                                      A_dn.main_grad, 1.0, dn_p.s)
         _grad_ready(B_gu)
         _grad_ready(A_dn)
-        # 7. dx and dA_gu += s x^T (dgu B_gu) (the latter on the side stream under the dx GEMM)
+        # 7. dx and dA_gu += s x^T (dgu B_gu)
         dgt = _tail(dgu, N, gu_p.R)
-
-        def da_gu():
-            _accum_xty(A_gu.main_grad.t(), x2, dgt, gu_p.s)
-            _grad_ready(A_gu)
-
-        if side:
-            _L._on_side(dgu.device, da_gu, x2, dgt, dgu)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = gemm_mm(_wide(dgu, N + gu_p.Rp), gu_p.bwd_weight()).view(ctx.shp)
-        if not side:
-            da_gu()
+        _accum_xty(A_gu.main_grad.t(), x2, dgt, gu_p.s)
+        _grad_ready(A_gu)
         return dx, None, None, None, None, None, None
 
 

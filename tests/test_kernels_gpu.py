@@ -1478,34 +1478,6 @@ def test_full_ft_first_write_grads_match_zeroed(C, tmp_path, grad_dtype):
     assert ((p1 - p0).norm() / p0.norm()).item() < 1e-4
 
 
-def test_lora_side_stream_wgrad_matches_serial(C, tmp_path):
-    """LoRA adapter weight gradients of the attention projections on the side stream (ops.linear
-    FTC_LORA_WG_STREAM) vs on the main stream: bitwise-identical losses, adapter gradients and
-    parameters after three steps."""
-    from finetune_controller_amd.ops import linear as L
-    from finetune_controller_amd.train.trainer import TrainConfig, Trainer
-
-    res = {}
-    prior = L._LORA_WG_STREAM
-    try:
-        for side in (True, False):
-            L.set_lora_wgrad_stream(side)
-            tc = TrainConfig(model="llama-smoke", method="lora", batch_size=2, seq_len=256, synthetic=True,
-                             max_steps=3, warmup_steps=0, schedule="constant", lr=1e-3, save_model=False,
-                             resume=False, device="cuda", checkpoint_path=str(tmp_path / str(side)))
-            tr = Trainer(tc)
-            losses = [tr.train_step(1e-3).float().item() for _ in range(3)]
-            assert not L._DW_PENDING
-            torch.cuda.synchronize()
-            res[side] = (losses, tr.opt.param_flat.clone(), tr.opt.grad_flat.clone())
-            tr.close()
-    finally:
-        L.set_lora_wgrad_stream(prior)
-    (l1, p1, g1), (l0, p0, g0) = res[True], res[False]
-    assert l1 == l0, (l1, l0)
-    assert torch.count_nonzero(g0) > 0 and torch.equal(g1, g0) and torch.equal(p1, p0)
-
-
 @pytest.mark.parametrize("method", ["full", "lora"])
 def test_gpt2_steps_hip_match_torch_path(C, monkeypatch, method):
     """GPT-2 geometry (d 768, 12 heads of 64, odd vocab 50257, tied lm_head, LayerNorm/GELU, learned
