@@ -75,7 +75,7 @@ struct GemmTNArgs {
   long long lda, ldb, ldc;
   int K, nm, nn;
   float alpha, beta;
-  int mode;  // diagnostics (FTC_GEMM_TN_MODE, tools/bench_gemm_tn.py only): 1 no DMA wait, 2 no DMA,
+  int mode;  // diagnostics (FTC_GEMM_TN_MODE in an FTC_EXPERIMENTS build only; 0 in the extension): 1 no DMA wait, 2 no DMA,
              // 8 every DMA re-reads K-step 0 (L2-resident operands)
   int group_m;  // M-blocks per tile group (XCD-local operand reuse)
 };
@@ -412,10 +412,14 @@ extern "C" int ftc_gemm_tn_ok(const void* a, long long lda, const void* b, long 
 extern "C" int ftc_gemm_tn(const void* a, long long lda, const void* b, long long ldb, void* c, long long ldc,
                            int c_fp32, int M, int N, int K, float alpha, float beta, hipStream_t stream) {
   if (!ftc_gemm_tn_ok(a, lda, b, ldb, c, ldc, M, N, K)) return -1;
+#ifdef FTC_EXPERIMENTS  // timing-only modes with wrong results: tools builds only, never the extension
   static const int mode = [] {
     const char* e = getenv("FTC_GEMM_TN_MODE");
     return e ? atoi(e) : 0;
   }();
+#else
+  constexpr int mode = 0;
+#endif
   static const int group_m = [] {
     const char* e = getenv("FTC_GEMM_TN_GROUP");
     return e ? atoi(e) : 4;
