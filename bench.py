@@ -305,6 +305,15 @@ def main(argv=None) -> int:
             rccl = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
         except Exception:
             rccl = None
+    # peer access from this rank's GPU (xGMI P2P: RCCL's direct transport on an 8-GPU node; a rehearsal
+    # on one shared card reports none) -- makes the first multi-GPU record self-describing
+    p2p = None
+    if cuda and n > 1:
+        try:
+            me = dev.index if dev.index is not None else torch.cuda.current_device()
+            p2p = sum(1 for j in range(torch.cuda.device_count()) if j != me and torch.cuda.can_device_access_peer(me, j))
+        except Exception:
+            p2p = None
 
     if a.profile_steps:
         from torch.profiler import ProfilerActivity, profile
@@ -359,6 +368,7 @@ def main(argv=None) -> int:
             "world_size_pg": pg_world,
             "dist_backend": info.backend,
             "rccl_version": rccl,
+            "p2p_peers": p2p,
             "rank_ms_per_step": {"max": round(ms, 2), "min": round(fastest / a.steps * 1000, 2)},
             **({"allreduce_bucket": comm} if comm else {}),
             "comm": {
