@@ -395,6 +395,15 @@ def test_lora_merge(C):
     torch.testing.assert_close(W.float(), ref, atol=3e-2, rtol=1e-2)
 
 
+@pytest.fixture(params=[1, 2], ids=["qb1", "qb2"])
+def fwd_qb(C, request):
+    """Both flash-forward variants: 32 query rows per wave (two workgroups per CU) and two 32-row blocks
+    per wave (one workgroup per CU, csrc/kernels/flash_attn_fwd.hip QB2)."""
+    C.flash_fwd_config(request.param)
+    yield request.param
+    C.flash_fwd_config(1)
+
+
 @pytest.mark.parametrize("B,S,H,KV,D,causal,window", [
     (2, 256, 8, 2, 128, True, 0),
     (1, 768, 4, 4, 128, False, 0),
@@ -405,7 +414,7 @@ def test_lora_merge(C):
     (1, 512, 8, 2, 64, False, 0),
     (1, 768, 8, 4, 64, True, 320),
 ])
-def test_flash_attention_fwd_bwd(C, B, S, H, KV, D, causal, window):
+def test_flash_attention_fwd_bwd(C, fwd_qb, B, S, H, KV, D, causal, window):
     from finetune_controller_amd.ops.attention import _FlashPacked, attention_reference
 
     torch.manual_seed(0)
@@ -526,7 +535,7 @@ def test_llama_rope_grad_handoff(C, monkeypatch, method):
     (2, 700, 4, 2, 128, 0, True),
 ])
 @pytest.mark.parametrize("causal", [True, False])
-def test_flash_tail_lengths(C, B, S, H, KV, D, window, docs, causal):
+def test_flash_tail_lengths(C, fwd_qb, B, S, H, KV, D, window, docs, causal):
     """S not a multiple of the 256-row tile: attention_packed takes the tail-padded flash path (not
     SDPA) and matches the fp32 reference, forward and backward -- causal (pads never visible) and
     non-causal (pad keys masked in the kernels through kv_valid)."""
@@ -567,7 +576,7 @@ def test_flash_tail_lengths(C, B, S, H, KV, D, window, docs, causal):
     (2, 300, 4, 2, 96, 0, False),
     (1, 256, 4, 2, 32, 0, True),
 ])
-def test_flash_head_dim_padded(C, B, S, H, KV, D, window, causal):
+def test_flash_head_dim_padded(C, fwd_qb, B, S, H, KV, D, window, causal):
     """head_dim outside the kernels' {64, 128} (80 / 96 / 112 / 32): attention_packed zero-pads every head
     to the next kernel head_dim and runs the flash kernels (not SDPA), forward and backward equal to the
     fp32 reference at the real D's softmax scale."""
@@ -593,7 +602,7 @@ def test_flash_head_dim_padded(C, B, S, H, KV, D, window, causal):
         assert rel < 1.5e-2, (lo, rel)
 
 
-def test_flash_lse(C):
+def test_flash_lse(C, fwd_qb):
     torch.manual_seed(1)
     B, S, H, KV, D = 1, 256, 4, 2, 128
     qkv = bf(torch.randn(B * S, (H + 2 * KV) * D, device=DEV))
@@ -1118,7 +1127,7 @@ def _doc_ids(B, S, lens_per_row, eos=2):
 
 
 @pytest.mark.parametrize("D,H,KV,window", [(128, 8, 2, 0), (64, 8, 2, 0), (128, 4, 4, 200), (64, 4, 2, 0)])
-def test_flash_attention_packed_documents(C, D, H, KV, window):
+def test_flash_attention_packed_documents(C, fwd_qb, D, H, KV, window):
     """Document-masked flash attention (doc_start / doc_end bounds, tile skipping, boundary masks)
     against the fp32 reference: documents shorter than a tile, spanning several 256-key blocks, and a
     row that is one document."""
