@@ -46,6 +46,8 @@ int ftc_gemm_nt_rope(const void* a, long long lda, const void* b, long long ldb,
                      int K, const float* cos_t, const float* sin_t, const int* positions, int seq_len, int rot_heads,
                      hipStream_t stream);
 int ftc_copy2d_batched(const void* jobs, int njobs, long long max_elems, hipStream_t stream);
+int ftc_splitk_sum(const float* parts, int nsplit, long long pstride, void* c, int c_fp32, long long rows, int cols,
+                   long long ldc, float beta, hipStream_t stream);
 int ftc_ce_fwd_bwd(void* logits, const long long* labels, float* loss, float* lse, long long rows, int V, long long ld,
                    float gscale, long long ignore_index, hipStream_t stream);
 int ftc_adamw(void* param_bf16, float* master, float* m, float* v, const void* grad, int grad_is_fp32, long long n,
@@ -398,6 +400,19 @@ void gemm_tn_(at::Tensor& c, const at::Tensor& a, const at::Tensor& b, double al
                     c.scalar_type() == at::kFloat, (int)a.size(1), (int)b.size(1), (int)a.size(0), (float)alpha,
                     (float)beta, cur_stream()),
         "gemm_tn_");
+}
+
+// ---------------- split-K partials: c = beta c + sum_s parts[s] ----------------
+// parts [S, M, N] fp32 contiguous; c [M, N] bf16 or fp32 row view (unit column stride)
+void splitk_sum_(at::Tensor& c, const at::Tensor& parts, double beta) {
+  TORCH_CHECK(parts.is_cuda() && c.is_cuda() && parts.dim() == 3 && c.dim() == 2 && parts.is_contiguous() &&
+                  parts.scalar_type() == at::kFloat && c.stride(1) == 1 && parts.size(1) == c.size(0) &&
+                  parts.size(2) == c.size(1) && (c.scalar_type() == at::kBFloat16 || c.scalar_type() == at::kFloat),
+              "splitk_sum_: parts [S, M, N] fp32 contiguous, c [M, N] bf16/fp32 row view");
+  check(ftc_splitk_sum(parts.data_ptr<float>(), (int)parts.size(0), parts.size(1) * parts.size(2), c.data_ptr(),
+                       c.scalar_type() == at::kFloat, c.size(0), (int)c.size(1), c.stride(0), (float)beta,
+                       cur_stream()),
+        "splitk_sum_");
 }
 
 // ---------------- projection GEMM: c = alpha a b^T + beta c ----------------
@@ -824,6 +839,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("transpose2d", &transpose2d, py::arg("x"), py::arg("out") = py::none());
   m.def("gemm_tn_ok", &gemm_tn_ok);
   m.def("gemm_tn_", &gemm_tn_);
+  m.def("splitk_sum_", &splitk_sum_);
   m.def("gemm_nt_ok", &gemm_nt_ok);
   m.def("gemm_nt_rope_", &gemm_nt_rope_, py::arg("c"), py::arg("a"), py::arg("b"), py::arg("cos"), py::arg("sin"),
         py::arg("positions"), py::arg("seq_len"), py::arg("rot_heads"));

@@ -159,3 +159,66 @@ extern "C" int ftc_copy2d_batched(const void* jobs, int njobs, long long max_ele
   hipLaunchKernelGGL(copy2d_batched_kernel, dim3(gx, njobs), dim3(256), 0, stream, (const Copy2DJob*)jobs);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------- split-K partial sum
+// C[r, c] = beta C + sum_s P[s][r, c]: the fp32 partials of a weight-gradient GEMM split along the token
+// dimension (ops/linear.py `_dw_split`) folded into the (bf16 or fp32) gradient in one pass -- 8 columns
+// per work item, 16-byte (bf16 C) / 2 x 16-byte (fp32 C) accesses, the partials read once.
+template <bool F32C>
+__global__ __launch_bounds__(256) void splitk_sum_kernel(const float* __restrict__ parts, int nsplit,
+                                                         long long pstride, void* __restrict__ c, long long rows,
+                                                         int cols, long long ldc, float beta) {
+  const int cv = cols >> 3;
+  const long long total = rows * cv;
+  for (long long it = (long long)blockIdx.x * 256 + threadIdx.x; it < total; it += (long long)gridDim.x * 256) {
+    const long long row = it / cv;
+    const int col = (int)(it - row * cv) * 8;
+    float acc[8];
+    {
+      const float4* p = reinterpret_cast<const float4*>(parts + row * cols + col);
+      const float4 a0 = p[0], a1 = p[1];
+      acc[0] = a0.x; acc[1] = a0.y; acc[2] = a0.z; acc[3] = a0.w;
+      acc[4] = a1.x; acc[5] = a1.y; acc[6] = a1.z; acc[7] = a1.w;
+    }
+    for (int s = 1; s < nsplit; ++s) {
+      const float4* p = reinterpret_cast<const float4*>(parts + s * pstride + row * cols + col);
+      const float4 a0 = p[0], a1 = p[1];
+      acc[0] += a0.x; acc[1] += a0.y; acc[2] += a0.z; acc[3] += a0.w;
+      acc[4] += a1.x; acc[5] += a1.y; acc[6] += a1.z; acc[7] += a1.w;
+    }
+    if constexpr (F32C) {
+      float4* q = reinterpret_cast<float4*>(reinterpret_cast<float*>(c) + row * ldc + col);
+      if (beta != 0.f) {
+        const float4 o0 = q[0], o1 = q[1];
+        acc[0] += beta * o0.x; acc[1] += beta * o0.y; acc[2] += beta * o0.z; acc[3] += beta * o0.w;
+        acc[4] += beta * o1.x; acc[5] += beta * o1.y; acc[6] += beta * o1.z; acc[7] += beta * o1.w;
+      }
+      q[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      q[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    } else {
+      uint4* q = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(c) + row * ldc + col);
+      if (beta != 0.f) {
+        float o[8];
+        unpack8(*q, o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += beta * o[j];
+      }
+      *q = pack8(acc);
+    }
+  }
+}
+
+extern "C" int ftc_splitk_sum(const float* parts, int nsplit, long long pstride, void* c, int c_fp32, long long rows,
+                              int cols, long long ldc, float beta, hipStream_t stream) {
+  if (nsplit < 1 || cols % 8 != 0 || ldc % 8 != 0 || (reinterpret_cast<uintptr_t>(parts) & 15) ||
+      (reinterpret_cast<uintptr_t>(c) & 15) || pstride % 8 != 0)
+    return -1;
+  const int grid = ftc::stream_grid(rows * (cols / 8), 256);
+  if (c_fp32)
+    hipLaunchKernelGGL(splitk_sum_kernel<true>, dim3(grid), dim3(256), 0, stream, parts, nsplit, pstride, c, rows, cols,
+                       ldc, beta);
+  else
+    hipLaunchKernelGGL(splitk_sum_kernel<false>, dim3(grid), dim3(256), 0, stream, parts, nsplit, pstride, c, rows,
+                       cols, ldc, beta);
+  return (int)hipGetLastError();
+}

@@ -453,7 +453,8 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
 //     A0 (S of block 0)  |  m0  |  A1 (S of block 1) x P0 (exp / row sum / pack of block 0)
 //                        |  m1  |  PV0 x P1  |  PV1
 // where m = mask + row max + deferred rescale (branches: between the interleaved regions) and "x" = one
-// basic block whose MFMAs and VALU the compiler interleaves (sched_group_barrier pattern).  K / V tiles
+// two-element exp chunk after every MFMA, placed by sched_barrier fences (a sched_group_barrier pattern
+// left the compiler clustering all 32 exponentials ahead of the MFMAs); the V^T reads are A0's fillers.  K / V tiles
 // arrive by LDS-DMA two tiles ahead into a 3-slot ring (counted vmcnt, one barrier per tile); a wave
 // past its last visible tile (causal diagonal) keeps joining the DMA / barrier only.
 template <int D>
@@ -541,8 +542,17 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_qb2_kernel(FwdArgs a) {
   const float c = a.scale_log2;
 
   __builtin_amdgcn_s_waitcnt(0x0F70);  // Q fragments (plain loads) retired before any DMA: vmcnt(0)
+  // the DMA as inline asm (common.h lds_dma16): the compiler's own waits would otherwise treat every
+  // later LDS read as possibly aliasing the in-flight tile and drain it (vmcnt) ahead of the V^T reads;
+  // the counted waits below are the only ones the pipeline needs
   auto dma = [&](int t, char* Kd, char* Vd) __attribute__((always_inline)) {
-    fwd_dma<D, NGT, RPG>(krs, vrs, voff, (kv_begin + t * BK) * (int)a.kv_rs * 2, Kd, Vd, wave);
+    const int toff = (kv_begin + t * BK) * (int)a.kv_rs * 2;
+#pragma unroll
+    for (int i = 0; i < NGT; ++i) {
+      const int r0 = (wave * NGT + i) * RPG;
+      lds_dma16(krs, Kd + r0 * D * 2, voff[i], toff);
+      lds_dma16(vrs, Vd + r0 * D * 2, voff[i], toff);
+    }
   };
   // prologue: tiles 0 and 1 in flight (a missing tile is replaced by a repeat of tile 0 into its slot,
   // so every wave always has the same number of DMA instructions outstanding)
@@ -567,14 +577,6 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_qb2_kernel(FwdArgs a) {
   uint4 kf[2][DSTEPS];
   s16x4 vt[DT][8];
 
-  auto mma_s = [&](int j, int kt) __attribute__((always_inline)) {
-    f32x16 acc;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-#pragma unroll
-    for (int st = 0; st < DSTEPS; ++st) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(kf[kt][st]), qf[j][st], acc, 0, 0, 0);
-    s[j][kt] = acc;
-  };
   // mask + row max + deferred rescale of block j (branches; before its interleaved exp region)
   auto rowmax = [&](int j, int t) __attribute__((always_inline)) -> float {
     const int kv0 = kv_begin + t * BK;
@@ -611,66 +613,112 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_qb2_kernel(FwdArgs a) {
     }
     return (m[j] == -INFINITY) ? 0.f : m[j];
   };
-  auto expsum = [&](int j, float mref) __attribute__((always_inline)) {
-    float rs = 0.f;
+  // exponentials / row sum / bf16 packing of block j in 16 chunks of two elements (element e = 16 kt + i of
+  // s[j]); chunk idx packs P fragment ks once its 8 elements are done
+  float rs[QB] = {0.f, 0.f};
+  auto exp_chunk = [&](int j, int idx, float mref) __attribute__((always_inline)) {
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][kt][i], c, -mref));
-        s[j][kt][i] = p;
-        rs += p;
-      }
-    l[j] += rs;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) pf[j][ks] = pack_p(s[j][ks >> 1], 8 * (ks & 1));
-  };
-  auto mma_pv = [&](int j) __attribute__((always_inline)) {
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const s16x4 v1 = vt[dt][2 * ks], v2 = vt[dt][2 * ks + 1];
-        s16x8 va = {v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
-        o[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, va), pf[j][ks], o[j][dt], 0, 0, 0);
-      }
-  };
-  // interleave of an MFMA chain of n with the VALU work placed in the same basic block
-  auto interleave = [](auto n_mfma) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < decltype(n_mfma)::value; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
-      __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);  // up to six VALU
+    for (int e = 2 * idx; e < 2 * idx + 2; ++e) {
+      const int kt = e >> 4, i = e & 15;
+      const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][kt][i], c, -mref));
+      s[j][kt][i] = pv;
+      rs[j] += pv;
+      asm volatile("" ::"v"(pv));  // pin: pure arithmetic would otherwise sink past the fences (IR level)
     }
+    if ((idx & 3) == 3) pf[j][idx >> 2] = pack_p(s[j][idx >> 3], 8 * ((idx >> 2) & 1));
+  };
+  auto fence = []() __attribute__((always_inline)) { __builtin_amdgcn_sched_barrier(0); };
+  auto mfma_s = [&](int j, int kt, int st, f32x16& acc) __attribute__((always_inline)) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(kf[kt][st]), qf[j][st], acc, 0, 0, 0);
+  };
+  auto mfma_pv = [&](int j, int dt, int ks) __attribute__((always_inline)) {
+    const s16x4 v1 = vt[dt][2 * ks], v2 = vt[dt][2 * ks + 1];
+    s16x8 va = {v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
+    o[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, va), pf[j][ks], o[j][dt], 0, 0, 0);
+  };
+  auto read_vt = [&](const char* Vc, int r) __attribute__((always_inline)) {  // transposed V read r of 8 * DT
+    const int dt = r >> 3, q = r & 7, ks = q >> 1;
+    vt[dt][q] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vc + vto[dt][q & 1] + ks * 16 * D * 2));
   };
 
+  // one tile, hand-interleaved (sched_barrier fences fix the order the compiler would otherwise cluster):
+  //   A0: S of block 0; K fragments of 32-key half 1 read under half 0's MFMAs, V^T d-tile 0 under half 1's
+  //   mask / max / rescale of block 0
+  //   A1: S of block 1, one exp chunk of block 0 after every MFMA
+  //   mask / max / rescale of block 1
+  //   PV0: O0 += V^T P0, per d tile dt: an exp chunk of block 1 and the V^T reads of d tile dt + 1
+  //   PV1: O1 += V^T P1 (every V^T fragment already in registers)
   auto compute = [&](const int t, const char* Kc, const char* Vc) __attribute__((always_inline)) {
+    auto read_k = [&](int kt, int st) __attribute__((always_inline)) {
+      kf[kt][st] = *reinterpret_cast<const uint4*>(Kc + lds_off<D>(kt * 32 + lr, 2 * st + hh));
+    };
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+    for (int st = 0; st < DSTEPS; ++st) read_k(0, st);
+    constexpr int RV = 8 / DSTEPS;  // V^T reads per A0 half-1 MFMA (d tile 0: 8 reads)
 #pragma unroll
-      for (int st = 0; st < DSTEPS; ++st) kf[kt][st] = *reinterpret_cast<const uint4*>(Kc + lds_off<D>(kt * 32 + lr, 2 * st + hh));
-    mma_s(0, 0);
-    mma_s(0, 1);
+    for (int kt = 0; kt < 2; ++kt) {
+      f32x16 acc;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+      for (int st = 0; st < DSTEPS; ++st) {
+        mfma_s(0, kt, st, acc);
+        fence();
+        if (kt == 0) {
+          read_k(1, st);
+        } else {
+#pragma unroll
+          for (int r = st * RV; r < (st + 1) * RV; ++r) read_vt(Vc, r);
+        }
+        fence();
+      }
+      s[0][kt] = acc;
+    }
     const float mref0 = rowmax(0, t);
-    // A1 x P0
-    mma_s(1, 0);
-    mma_s(1, 1);
-    expsum(0, mref0);
-    interleave(std::integral_constant<int, 2 * DSTEPS>{});
-    // V^T fragments for both blocks' PV
+    rs[0] = 0.f;
+    fence();
+    constexpr int NS = 2 * DSTEPS;  // S MFMAs per block
+    constexpr int CH = 16 / NS;     // exp chunks per S MFMA (D = 128: 1; D = 64: 2)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      f32x16 acc;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+      for (int st = 0; st < DSTEPS; ++st) {
+        mfma_s(1, kt, st, acc);
+        fence();
+#pragma unroll
+        for (int c2 = 0; c2 < CH; ++c2) exp_chunk(0, (kt * DSTEPS + st) * CH + c2, mref0);
+        fence();
+      }
+      s[1][kt] = acc;
+    }
+    l[0] += rs[0];
+    const float mref1 = rowmax(1, t);
+    rs[1] = 0.f;
+    fence();
+    constexpr int NP = 4 * DT;   // PV MFMAs per block
+    constexpr int CP = 16 / NP;  // exp chunks per PV MFMA (D = 128: 1; D = 64: 2)
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        vt[dt][2 * ks] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vc + vto[dt][0] + ks * 16 * D * 2));
-        vt[dt][2 * ks + 1] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vc + vto[dt][1] + ks * 16 * D * 2));
+        mfma_pv(0, dt, ks);
+        fence();
+#pragma unroll
+        for (int c2 = 0; c2 < CP; ++c2) exp_chunk(1, (dt * 4 + ks) * CP + c2, mref1);
+        if (dt + 1 < DT) {
+          read_vt(Vc, 8 * (dt + 1) + 2 * ks);
+          read_vt(Vc, 8 * (dt + 1) + 2 * ks + 1);
+        }
+        fence();
       }
-    const float mref1 = rowmax(1, t);
-    // PV0 x P1
-    mma_pv(0);
-    expsum(1, mref1);
-    interleave(std::integral_constant<int, 4 * DT>{});
-    mma_pv(1);
+    l[1] += rs[1];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) mfma_pv(1, dt, ks);
   };
   // tile t: wait for it (tile t+1 may still fly: vmcnt(PER_TILE)), barrier, DMA tile t+2 into the slot
   // tile t-1 used; compute when this wave sees tile t

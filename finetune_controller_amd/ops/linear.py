@@ -238,9 +238,9 @@ def _wgrad_on_side(mg: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, tn_dw:
     with torch.cuda.stream(side):
         if xt is not None:
             transpose2d(x2, xt)
-            accum_mm(mg, dy2.t(), xt.t(), beta=beta)
+            wgrad_mm(mg, dy2.t(), xt.t(), beta=beta)
         else:
-            accum_mm(mg, dy2.t(), x2, beta=beta)
+            wgrad_mm(mg, dy2.t(), x2, beta=beta)
         ev = torch.cuda.Event()
         ev.record(side)
     _DW_PENDING[:] = [(ev, dev, dy2, x2)]
@@ -379,6 +379,55 @@ def accum_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, alpha: float =
     if a.is_cuda:
         return torch.addmm(out, a, b, beta=beta, alpha=alpha, out_dtype=out.dtype, out=out)
     return out.addmm_(a.to(out.dtype), b.to(out.dtype), beta=beta, alpha=alpha)
+
+
+# ---- split-K weight gradients (full fine-tuning).  The weight-gradient GEMMs reduce over all T tokens
+# of the micro-batch; two of the Llama-3-8B shapes leave the last wave of 256 x 256 tiles half empty on
+# 256 CUs (qkv: 384 tiles = 1.5 waves, down: 896 = 3.5).  Split along the tokens into S slices so that
+# S x tiles is a whole number of waves: ONE batched hipBLASLt GEMM writes the S fp32 partials, one HIP
+# pass (csrc/kernels/elementwise.hip splitk_sum_kernel) folds them into the gradient (beta C + sum).
+# FTC_DW_SPLIT: "0" off, "auto" (wave-quantised shapes only), or a fixed S.
+_DW_SPLIT = os.environ.get("FTC_DW_SPLIT", "0")
+_DW_PARTS: dict = {}  # (device, stream) -> flat fp32 scratch for the partials
+_WAVE = 256  # workgroups per wave: one 256 x 256 tile per CU
+
+
+def dw_splits(M: int, N: int, K: int, mode: str | None = None) -> int:
+    """Token slices for the weight gradient of an [M, N] weight reduced over K tokens (1 = no split)."""
+    mode = _DW_SPLIT if mode is None else mode
+    if mode == "0":
+        return 1
+    if mode != "auto":
+        s = int(mode)
+        return s if s > 1 and K % (64 * s) == 0 else 1
+    tiles = -(-M // 256) * -(-N // 256)
+    if tiles % _WAVE == 0 or tiles > 8 * _WAVE:
+        return 1
+    for s in (2, 4):
+        if (tiles * s) % _WAVE == 0 and K % (64 * s) == 0:
+            return s
+    return 1
+
+
+def wgrad_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, beta: float = 1.0) -> torch.Tensor:
+    """``out = beta * out + a @ b`` for a weight gradient (``a`` = dy^T [M, T], ``b`` = x [T, N], any
+    strides): split along T when ``dw_splits`` says so, else ``accum_mm``."""
+    M, K = a.shape
+    N = b.shape[1]
+    s = dw_splits(M, N, K) if (use_hip(a) and out.stride(1) == 1) else 1
+    if s == 1:
+        return accum_mm(out, a, b, beta=beta)
+    k = K // s
+    A = a.as_strided((s, M, k), (k * a.stride(1), a.stride(0), a.stride(1)))
+    B = b.as_strided((s, k, N), (k * b.stride(0), b.stride(0), b.stride(1)))
+    key = (a.device, torch.cuda.current_stream(a.device).cuda_stream)
+    buf = _DW_PARTS.get(key)
+    if buf is None or buf.numel() < s * M * N:
+        buf = _DW_PARTS[key] = torch.empty(s * M * N, dtype=torch.float32, device=a.device)
+    parts = buf[:s * M * N].view(s, M, N)
+    torch.bmm(A, B, out_dtype=torch.float32, out=parts)
+    ext().splitk_sum_(out, parts, float(beta))
+    return out
 
 
 # ---- first-write weight gradients (full fine-tuning).  Zeroing the 16 GB gradient buffer of Llama-3-8B
@@ -810,9 +859,9 @@ class _LoRALinearFn(torch.autograd.Function):
                 elif _TN_DW and use_hip(x2):
                     # hipBLASLt runs dW += dy^T x 14-24 % faster with x handed over transposed (K-major
                     # reduction operand, tools/bench_dw_gemm.py); the transpose streams at HBM rate
-                    accum_mm(mg, dy2.t(), transpose2d(x2).t(), beta=take_fresh(W, mg))
+                    wgrad_mm(mg, dy2.t(), transpose2d(x2).t(), beta=take_fresh(W, mg))
                 else:
-                    accum_mm(mg, dy2.t(), x2, beta=take_fresh(W, mg))
+                    wgrad_mm(mg, dy2.t(), x2, beta=take_fresh(W, mg))
                 _grad_ready(W)
             else:
                 dW = dy2.t() @ x2

@@ -263,6 +263,34 @@ def test_gemm_tn_rejects(C):
 
 
 @pytest.mark.parametrize("cdtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("splits", ["2", "4", "auto"])
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_wgrad_split(C, cdtype, splits, beta):
+    """Split-K weight gradient (ops.linear.wgrad_mm: batched GEMM into fp32 partials + splitk_sum_) on the
+    operands of the production paths (dy^T as a transposed view, x transposed or as stored) vs fp32.
+    768 x 512 = 6 tiles: "auto" splits it 2 ways only at _WAVE = 4 (patched), as qkv dW is at 256."""
+    from finetune_controller_amd.ops import linear as L
+    torch.manual_seed(5)
+    T, M, N = 1024, 768, 512
+    dy = (torch.rand(T, M, device=DEV) * 2 - 1).to(torch.bfloat16)
+    x = (torch.rand(T, N, device=DEV) * 2 - 1).to(torch.bfloat16)
+    old = L._WAVE
+    L._WAVE = 4
+    try:
+        assert L.dw_splits(M, N, T, splits) == (2 if splits == "auto" else int(splits))
+        for b in (x, L.transpose2d(x).t()):
+            c = torch.randn(M, N, device=DEV).to(cdtype)
+            ref = beta * c.float() + dy.float().t() @ x.float()
+            L._DW_SPLIT = splits
+            L.wgrad_mm(c, dy.t(), b, beta)
+            tol = 2e-2 * (T ** 0.5) / 8 if cdtype == torch.bfloat16 else 1e-3 * (T ** 0.5) / 8
+            torch.testing.assert_close(c.float(), ref, atol=tol, rtol=1e-2 if cdtype == torch.bfloat16 else 1e-4)
+    finally:
+        L._WAVE = old
+        L._DW_SPLIT = "0"
+
+
+@pytest.mark.parametrize("cdtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("M,N,K,pad,beta", [(256, 256, 64, 0, 0.0), (512, 768, 4160, 64, 0.0), (768, 512, 128, 8, 1.0),
                                             (256, 1024, 1088, 0, -0.5), (512, 256, 192, 0, 0.0)])
 def test_gemm_nt(C, cdtype, M, N, K, pad, beta):
