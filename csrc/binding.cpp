@@ -41,11 +41,13 @@ int ftc_gemm_nt_ok(const void* a, long long lda, const void* b, long long ldb, c
                    int M, int N, int K);
 int ftc_gemm_nt(const void* a, long long lda, const void* b, long long ldb, void* c, long long ldc, int c_fp32, int M,
                 int N, int K, float alpha, float beta, hipStream_t stream);
-void ftc_gemm_nt_config(int grid_cap, int group, int xcc, int nt_store);
+void ftc_gemm_nt_config(int grid_cap, int group, int xcc, int nt_store, int load_policy);
 int ftc_gemm_nt_rope(const void* a, long long lda, const void* b, long long ldb, void* c, long long ldc, int M, int N,
                      int K, const float* cos_t, const float* sin_t, const int* positions, int seq_len, int rot_heads,
                      hipStream_t stream);
 int ftc_copy2d_batched(const void* jobs, int njobs, long long max_elems, hipStream_t stream);
+int ftc_gemm_tn_split(const void* a, long long lda, const void* b, long long ldb, float* parts, int M, int N, int K,
+                      int splits, hipStream_t stream);
 int ftc_splitk_sum(const float* parts, int nsplit, long long pstride, void* c, int c_fp32, long long rows, int cols,
                    long long ldc, float beta, hipStream_t stream);
 int ftc_ce_fwd_bwd(void* logits, const long long* labels, float* loss, float* lse, long long rows, int V, long long ld,
@@ -402,6 +404,18 @@ void gemm_tn_(at::Tensor& c, const at::Tensor& a, const at::Tensor& b, double al
         "gemm_tn_");
 }
 
+// parts [S, M, N] fp32 contiguous = the S token slices of a^T b (a [K, M], b [K, N] bf16 row views)
+void gemm_tn_split_(at::Tensor& parts, const at::Tensor& a, const at::Tensor& b) {
+  TORCH_CHECK(parts.is_cuda() && parts.dim() == 3 && parts.is_contiguous() && parts.scalar_type() == at::kFloat &&
+                  a.dim() == 2 && b.dim() == 2 && parts.size(1) == a.size(1) && parts.size(2) == b.size(1) &&
+                  a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && a.stride(1) == 1 &&
+                  b.stride(1) == 1 && a.size(0) == b.size(0),
+              "gemm_tn_split_: parts [S, M, N] fp32, a [K, M], b [K, N] bf16 row views");
+  check(ftc_gemm_tn_split(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), parts.data_ptr<float>(),
+                          (int)a.size(1), (int)b.size(1), (int)a.size(0), (int)parts.size(0), cur_stream()),
+        "gemm_tn_split_ (shape outside the kernel contract: M, N % 256, K % (64 S))");
+}
+
 // ---------------- split-K partials: c = beta c + sum_s parts[s] ----------------
 // parts [S, M, N] fp32 contiguous; c [M, N] bf16 or fp32 row view (unit column stride)
 void splitk_sum_(at::Tensor& c, const at::Tensor& parts, double beta) {
@@ -463,8 +477,9 @@ void gemm_nt_rope_(at::Tensor& c, const at::Tensor& a, const at::Tensor& b, cons
 
 // launch configuration of the projection GEMM (persistent grid cap, tile order, store policy); the
 // defaults are the measured best (profiles/r4/gemm_nt.md) -- tools/bench_gemm_nt.py sweeps it
-void gemm_nt_config(int64_t grid_cap, int64_t group, int64_t xcc, int64_t nt_store) {
-  ftc_gemm_nt_config((int)grid_cap, (int)group, (int)xcc, nt_store ? 1 : 0);
+void gemm_nt_config(int64_t grid_cap, int64_t group, int64_t xcc, int64_t nt_store, int64_t load_policy) {
+  TORCH_CHECK(load_policy >= 0 && load_policy <= 4, "gemm_nt_config: load_policy 0..4");
+  ftc_gemm_nt_config((int)grid_cap, (int)group, (int)xcc, nt_store ? 1 : 0, (int)load_policy);
 }
 
 // ---------------- cross entropy (in place on logits) ----------------
@@ -840,11 +855,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_tn_ok", &gemm_tn_ok);
   m.def("gemm_tn_", &gemm_tn_);
   m.def("splitk_sum_", &splitk_sum_);
+  m.def("gemm_tn_split_", &gemm_tn_split_);
   m.def("gemm_nt_ok", &gemm_nt_ok);
   m.def("gemm_nt_rope_", &gemm_nt_rope_, py::arg("c"), py::arg("a"), py::arg("b"), py::arg("cos"), py::arg("sin"),
         py::arg("positions"), py::arg("seq_len"), py::arg("rot_heads"));
   m.def("flash_fwd_config", [](int64_t qb) { ftc_flash_fwd_config((int)qb); }, py::arg("qb"));
-  m.def("gemm_nt_config", &gemm_nt_config, py::arg("grid_cap"), py::arg("group"), py::arg("xcc"), py::arg("nt_store"));
+  m.def("gemm_nt_config", &gemm_nt_config, py::arg("grid_cap"), py::arg("group"), py::arg("xcc"), py::arg("nt_store"),
+        py::arg("load_policy") = 0);
   m.def("gemm_nt_", &gemm_nt_, py::arg("c"), py::arg("a"), py::arg("b"), py::arg("alpha") = 1.0, py::arg("beta") = 0.0);
   m.def("ce_fwd_bwd_", &ce_fwd_bwd_);
   m.def("adamw_", &adamw_, py::arg("param"), py::arg("master"), py::arg("m"), py::arg("v"), py::arg("grad"),

@@ -229,7 +229,7 @@ FTC_DEV void store_w128(const NTArgs& p, const f32x4 (&acc)[8][8], long long row
 template <bool F32C>
 constexpr int kEpiStores = F32C ? 64 : 32;
 
-template <bool F32C, int EPI, bool NTS, bool BETA>
+template <bool F32C, int EPI, bool NTS, bool BETA, int LP = 0>
 __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(NTArgs p) {
   __shared__ __attribute__((aligned(16))) char S[2 * SS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -263,21 +263,38 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(NTArgs p) {
   }
   char* const wbase = S + 64 * wave * 128;
   const unsigned lds0 = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)wbase;
-  // One piece; each statement sets M0 for the NEXT piece after its load, so MFMAs separate every M0
-  // write from the DMA reading it.  M0 has no other user in this kernel (checked on the ISA by
-  // tests/test_build.py::test_gemm_nt_m0_single_user).
-  auto dma = [&](int op, __amdgpu_buffer_rsrc_t r, unsigned base, int j) __attribute__((always_inline)) {
-    if (j == 0)
-      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds\n\ts_mov_b32 m0, %4"
-                   :: "v"(vo[op][0]), "s"(r), "s"(base), "s"(so[op][0]), "s"(base + (unsigned)PSTRIDE) : "memory");
-    else if (j < 7)
-      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds\n\ts_mov_b32 m0, %3"
-                   :: "v"(vo[op][j & 1]), "s"(r), "s"(so[op][j]), "s"(base + (unsigned)((j + 1) * PSTRIDE)) : "memory");
-    else
-      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" :: "v"(vo[op][1]), "s"(r), "s"(so[op][7]) : "memory");
+  // One piece.  M0 (the LDS destination) walks with the pieces: every piece's statement advances it by
+  // one piece after its load (s_add, like the library's loop), the last piece of a chain loads M0 with
+  // the first destination of the NEXT chain (A -> B of the same stage, B -> A of the next stage), so the
+  // loop never writes M0 right before a DMA (MFMAs separate them: the SALU-write -> LDS-DMA hazard) and
+  // needs one SALU per piece.  NOP: a wait state before the load (back-to-back pieces, prologue only).
+  // M0 has no other user in this kernel (tests/test_build.py checks the ISA).
+  // LP: the pieces' cache policy (0 default, 1 sc0, 2 sc1, 3 sc0 sc1, 4 nt; Config::load_policy)
+#define FTC_NT_PIECE(POL)                                                                          \
+  if (j < 7)                                                                                       \
+    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen " POL "lds\n\ts_add_u32 m0, m0, 0x400"    \
+                 ::"v"(vo[op][j & 1]), "s"(r), "s"(so[op][j]) : "memory");                       \
+  else                                                                                             \
+    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen " POL "lds\n\ts_mov_b32 m0, %3"            \
+                 ::"v"(vo[op][1]), "s"(r), "s"(so[op][7]), "s"(next) : "memory");
+  auto dma = [&](int op, __amdgpu_buffer_rsrc_t r, int j, unsigned next, bool nop) __attribute__((always_inline)) {
+    if (nop) asm volatile("s_nop 0" ::: "memory");
+    if constexpr (LP == 1) {
+      FTC_NT_PIECE("sc0 ")
+    } else if constexpr (LP == 2) {
+      FTC_NT_PIECE("sc1 ")
+    } else if constexpr (LP == 3) {
+      FTC_NT_PIECE("sc0 sc1 ")
+    } else if constexpr (LP == 4) {
+      FTC_NT_PIECE("nt ")
+    } else {
+      FTC_NT_PIECE("")
+    }
   };
+#undef FTC_NT_PIECE
+  static_assert(PSTRIDE == 0x400, "the M0 walk adds one 1 KiB piece");
 
-  // prefetch cursor: global stage pg = (tile pi, stage ps); operand bases of tile pi
+  // prefetch cursor: global stage pg = (tile pi, stage ps); pa / pb = the operands at stage ps of tile pi
   int pg = 0, pi = 0, ps = 0;
   const uint16_t* pa;
   const uint16_t* pb;
@@ -298,6 +315,9 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(NTArgs p) {
         ps = 0;
         ++pi;
         tile_bases(pi, pa, pb);
+      } else {
+        pa += BKS;
+        pb += BKS;
       }
     }
   };
@@ -345,9 +365,10 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(NTArgs p) {
   auto iteration = [&](int g, auto first, bool after_epi) __attribute__((always_inline)) {
     const char* cur = S + (g & 1) * SS;
     const char* nxt = S + ((g + 1) & 1) * SS;
-    const auto ras = make_rsrc(pa + BKS * ps);
-    const auto rbs = make_rsrc(pb + BKS * ps);
-    const unsigned dA = lds0 + (unsigned)((g & 1) * SS), dB = dA + IMG;
+    const auto ras = make_rsrc(pa);
+    const auto rbs = make_rsrc(pb);
+    const unsigned dB = lds0 + (unsigned)((g & 1) * SS) + IMG;      // M0 after the A chain
+    const unsigned dA_next = lds0 + (unsigned)(((g + 1) & 1) * SS);  // M0 after the B chain
     // half 0 on X: Y.A in groups 0-1, release A after group 2; A pieces and Y.B in groups 3-6;
     // release B after group 7.  Every wait sits at least one group after the reads it covers.
 #pragma unroll
@@ -366,7 +387,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(NTArgs p) {
       group(xa, xb, gi, first, [&](int k) __attribute__((always_inline)) {
         const int i = 2 * (gi - 3) + (k >> 1);
         if (k & 1) yb[i] = rd(cur, b_off[1] + bnt(i));
-        else dma(0, ras, dA, i);
+        else dma(0, ras, i, dB, false);
       });
     group(xa, xb, 7, first, nop);
     FTC_GS(t_a = stamp();)
@@ -379,7 +400,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(NTArgs p) {
 #pragma unroll
     for (int gi = 0; gi < 4; ++gi)
       group(ya, yb, gi, std::false_type{}, [&](int k) __attribute__((always_inline)) {
-        if (!(k & 1)) dma(1, rbs, dB, 2 * gi + (k >> 1));
+        if (!(k & 1)) dma(1, rbs, 2 * gi + (k >> 1), dA_next, false);
       });
     FTC_GS(t_a = stamp();)
     if (after_epi) {
@@ -404,18 +425,19 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(NTArgs p) {
     advance();
   };
 
-  // prologue: global stages 0 and 1
+  // prologue: global stages 0 and 1 (back-to-back pieces: a wait state before each load)
   {
     const unsigned d0 = lds0, d1 = lds0 + (unsigned)SS;
+    asm volatile("s_mov_b32 m0, %0" :: "s"(d0) : "memory");
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dma(0, make_rsrc(pa + BKS * ps), d0, j);
+    for (int j = 0; j < 8; ++j) dma(0, make_rsrc(pa), j, d0 + IMG, true);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dma(1, make_rsrc(pb + BKS * ps), d0 + IMG, j);
+    for (int j = 0; j < 8; ++j) dma(1, make_rsrc(pb), j, d1, true);
     advance();
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dma(0, make_rsrc(pa + BKS * ps), d1, j);
+    for (int j = 0; j < 8; ++j) dma(0, make_rsrc(pa), j, d1 + IMG, true);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dma(1, make_rsrc(pb + BKS * ps), d1 + IMG, j);
+    for (int j = 0; j < 8; ++j) dma(1, make_rsrc(pb), j, d0, true);  // M0 = iteration 0's A chain (buffer 0)
     advance();
     __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16): stage 0 landed
   }
@@ -448,13 +470,15 @@ struct Config {
   int grid_cap;  // persistent grid: min(tiles, grid_cap) workgroups (0: number of CUs)
   int group;     // tile order, see NTArgs
   int xcc;
-  int nt_store;  // non-temporal C stores
+  int nt_store;     // non-temporal C stores
+  int load_policy;  // cache policy of the operand DMA: 0 default, 1 sc0, 2 sc1, 3 sc0 sc1, 4 nt
 };
 
 Config& config() {
   static Config c = [] {
-    Config d{0, -8, 32, 0};
-    if (const char* e = getenv("FTC_GEMM_NT_ORDER")) sscanf(e, "%d,%d,%d,%d", &d.grid_cap, &d.group, &d.xcc, &d.nt_store);
+    Config d{0, -8, 32, 0, 0};
+    if (const char* e = getenv("FTC_GEMM_NT_ORDER"))
+      sscanf(e, "%d,%d,%d,%d,%d", &d.grid_cap, &d.group, &d.xcc, &d.nt_store, &d.load_policy);
     return d;
   }();
   return c;
@@ -487,6 +511,14 @@ int launch(NTArgs& p, hipStream_t stream) {
     hipLaunchKernelGGL((gemm_nt_kernel<F32C, EPI, false, EPI == EPI_STORE>), dim3(grid), dim3(256), 0, stream, p);
   else if (c.nt_store)
     hipLaunchKernelGGL((gemm_nt_kernel<F32C, EPI, true, false>), dim3(grid), dim3(256), 0, stream, p);
+  else if (c.load_policy == 1)
+    hipLaunchKernelGGL((gemm_nt_kernel<F32C, EPI, false, false, 1>), dim3(grid), dim3(256), 0, stream, p);
+  else if (c.load_policy == 2)
+    hipLaunchKernelGGL((gemm_nt_kernel<F32C, EPI, false, false, 2>), dim3(grid), dim3(256), 0, stream, p);
+  else if (c.load_policy == 3)
+    hipLaunchKernelGGL((gemm_nt_kernel<F32C, EPI, false, false, 3>), dim3(grid), dim3(256), 0, stream, p);
+  else if (c.load_policy == 4)
+    hipLaunchKernelGGL((gemm_nt_kernel<F32C, EPI, false, false, 4>), dim3(grid), dim3(256), 0, stream, p);
   else
     hipLaunchKernelGGL((gemm_nt_kernel<F32C, EPI, false, false>), dim3(grid), dim3(256), 0, stream, p);
   return (int)hipGetLastError();
@@ -495,9 +527,9 @@ int launch(NTArgs& p, hipStream_t stream) {
 }  // namespace
 
 // Launch configuration of every later call (tools/bench_gemm_nt.py sweeps it in one process):
-// grid_cap (0 = CU count), group (> 0 M-fast, < 0 N-fast), xcc, nt_store.
-extern "C" void ftc_gemm_nt_config(int grid_cap, int group, int xcc, int nt_store) {
-  config() = Config{grid_cap, group, xcc, nt_store};
+// grid_cap (0 = CU count), group (> 0 M-fast, < 0 N-fast), xcc, nt_store, load_policy.
+extern "C" void ftc_gemm_nt_config(int grid_cap, int group, int xcc, int nt_store, int load_policy) {
+  config() = Config{grid_cap, group, xcc, nt_store, load_policy};
 }
 
 #ifdef FTC_GEMM_STAMP

@@ -78,6 +78,7 @@ struct GemmTNArgs {
   int mode;  // diagnostics (FTC_GEMM_TN_MODE in an FTC_EXPERIMENTS build only; 0 in the extension): 1 no DMA wait, 2 no DMA,
              // 8 every DMA re-reads K-step 0 (L2-resident operands)
   int group_m;  // M-blocks per tile group (XCD-local operand reuse)
+  long long cstride;  // split-K: elements between the splits' C (fp32 partial) matrices; K = one split's rows
 };
 
 // One LDS-DMA instruction (buffer_load_dwordx4 ... lds) as inline asm: hipcc then keeps it out of its
@@ -155,8 +156,11 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_tn_kernel(GemmTNArgs p) {
 
   // ---- block -> tile
   int mb, nb;
+  // split-K (grid = splits x tiles, split-major): split `ks` reduces rows [ks K, ks K + K) of A and B
+  // into its own C matrix (fp32 partials, summed by splitk_sum_kernel)
+  const int ks = blockIdx.x / (p.nm * p.nn);
   {
-    const int nblk = p.nm * p.nn, bid = blockIdx.x;
+    const int nblk = p.nm * p.nn, bid = blockIdx.x - ks * nblk;
     const int xcd = bid & 7, q = nblk >> 3, rr = nblk & 7;
     const int t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
     const int gm = p.group_m;
@@ -179,8 +183,8 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_tn_kernel(GemmTNArgs p) {
     vob = (r * (int)p.ldb + col) * 2;
   }
   const int sa4 = 4 * (int)p.lda * 2, sb4 = 4 * (int)p.ldb * 2;
-  const uint16_t* abase = p.a + m0;
-  const uint16_t* bbase = p.b + n0;
+  const uint16_t* abase = p.a + m0 + (long long)ks * p.K * p.lda;
+  const uint16_t* bbase = p.b + n0 + (long long)ks * p.K * p.ldb;
   auto issue = [&](int kt, char* stage) {
     if (p.mode & 8) kt = 0;
     const auto ra = make_rsrc(abase + (long long)kt * BK * p.lda);
@@ -365,7 +369,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_tn_kernel(GemmTNArgs p) {
   // per accumulator tile, the 16 old C values are loaded together (one latency, not 16) -- beta is
   // tested once, outside the loops (a per-element branch around a load serialises the round trips)
   using CT = typename std::conditional<F32C, float, uint16_t>::type;
-  CT* cbase = reinterpret_cast<CT*>(p.c) + (m0 + wm * 128 + 4 * hh) * p.ldc + n0 + wn * WNC + lr;
+  CT* cbase = reinterpret_cast<CT*>(p.c) + ks * p.cstride + (m0 + wm * 128 + 4 * hh) * p.ldc + n0 + wn * WNC + lr;
   const bool accumulate = p.beta != 0.f;
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
@@ -425,7 +429,7 @@ extern "C" int ftc_gemm_tn(const void* a, long long lda, const void* b, long lon
     return e ? atoi(e) : 4;
   }();
   GemmTNArgs p{(const uint16_t*)a, (const uint16_t*)b, c, lda, ldb, ldc, K, M / BM, N / BN, alpha, beta, mode,
-               group_m > 0 ? group_m : 4};
+               group_m > 0 ? group_m : 4, 0};
   const int grid = p.nm * p.nn;
   // FTC_GEMM_TN_WAVES=8: the two-waves-per-SIMD variant (A/B only)
   static const int waves = [] {
@@ -455,5 +459,24 @@ extern "C" int ftc_gemm_tn(const void* a, long long lda, const void* b, long lon
         hipLaunchKernelGGL((gemm_tn_kernel<false, 4>), dim3(grid), dim3(256), 0, stream, p);
     }
   }
+  return (int)hipGetLastError();
+}
+
+// Split-K weight gradient: parts[s] (fp32 [M, N], contiguous) = A[s K' : (s + 1) K']^T B[s K' : (s + 1) K']
+// for s < splits, K' = K / splits -- one launch of splits x tiles workgroups (whole waves where the tile
+// grid alone is not: qkv dW 384 -> 768, down dW 896 -> 1792); the caller folds the partials into the
+// gradient with splitk_sum.
+extern "C" int ftc_gemm_tn_split(const void* a, long long lda, const void* b, long long ldb, float* parts, int M, int N,
+                                 int K, int splits, hipStream_t stream) {
+  if (splits < 1 || K % splits || !ftc_gemm_tn_ok(a, lda, b, ldb, parts, N, M, N, K / splits)) return -1;
+  static const int group_m = [] {
+    const char* e = getenv("FTC_GEMM_TN_GROUP");
+    return e ? atoi(e) : 4;
+  }();
+  GemmTNArgs p{(const uint16_t*)a, (const uint16_t*)b, parts, lda, ldb, N, K / splits, M / BM, N / BN, 1.0f, 0.0f, 0,
+               group_m > 0 ? group_m : 4, (long long)M * N};
+  const long long grid = (long long)p.nm * p.nn * splits;
+  if (grid > 0x7fffffffLL) return -1;
+  hipLaunchKernelGGL((gemm_tn_kernel<true, 4, 1>), dim3((unsigned)grid), dim3(256), 0, stream, p);
   return (int)hipGetLastError();
 }

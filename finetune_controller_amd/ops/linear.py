@@ -420,12 +420,30 @@ def wgrad_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, beta: float = 
     k = K // s
     A = a.as_strided((s, M, k), (k * a.stride(1), a.stride(0), a.stride(1)))
     B = b.as_strided((s, k, N), (k * b.stride(0), b.stride(0), b.stride(1)))
-    key = (a.device, torch.cuda.current_stream(a.device).cuda_stream)
+    parts = _dw_parts(a.device, s, M, N)
+    torch.bmm(A, B, out_dtype=torch.float32, out=parts)
+    ext().splitk_sum_(out, parts, float(beta))
+    return out
+
+
+def _dw_parts(device, s: int, M: int, N: int) -> torch.Tensor:
+    key = (device, torch.cuda.current_stream(device).cuda_stream)
     buf = _DW_PARTS.get(key)
     if buf is None or buf.numel() < s * M * N:
-        buf = _DW_PARTS[key] = torch.empty(s * M * N, dtype=torch.float32, device=a.device)
-    parts = buf[:s * M * N].view(s, M, N)
-    torch.bmm(A, B, out_dtype=torch.float32, out=parts)
+        buf = _DW_PARTS[key] = torch.empty(s * M * N, dtype=torch.float32, device=device)
+    return buf[:s * M * N].view(s, M, N)
+
+
+def wgrad_tn(out: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, beta: float = 1.0) -> torch.Tensor:
+    """``out = beta * out + dy2^T x2`` on the hand-written TN kernel (operands as stored), split along
+    the tokens like ``wgrad_mm`` when ``dw_splits`` says so (``gemm_tn_split_`` + ``splitk_sum_``)."""
+    M, N, K = dy2.shape[1], x2.shape[1], dy2.shape[0]
+    s = dw_splits(M, N, K)
+    if s == 1:
+        ext().gemm_tn_(out, dy2, x2, 1.0, float(beta))
+        return out
+    parts = _dw_parts(dy2.device, s, M, N)
+    ext().gemm_tn_split_(parts, dy2, x2)
     ext().splitk_sum_(out, parts, float(beta))
     return out
 
@@ -855,7 +873,7 @@ class _LoRALinearFn(torch.autograd.Function):
                 if side_dw:
                     pass  # issued above, on the side stream
                 elif own_wgrad(mg, dy2, x2):
-                    ext().gemm_tn_(mg, dy2, x2, 1.0, take_fresh(W, mg))  # both operands as stored, no copies
+                    wgrad_tn(mg, dy2, x2, take_fresh(W, mg))  # both operands as stored, no copies
                 elif _TN_DW and use_hip(x2):
                     # hipBLASLt runs dW += dy^T x 14-24 % faster with x handed over transposed (K-major
                     # reduction operand, tools/bench_dw_gemm.py); the transpose streams at HBM rate

@@ -278,12 +278,15 @@ def test_wgrad_split(C, cdtype, splits, beta):
     L._WAVE = 4
     try:
         assert L.dw_splits(M, N, T, splits) == (2 if splits == "auto" else int(splits))
-        for b in (x, L.transpose2d(x).t()):
+        L._DW_SPLIT = splits
+        tol = 2e-2 * (T ** 0.5) / 8 if cdtype == torch.bfloat16 else 1e-3 * (T ** 0.5) / 8
+        for b in (x, L.transpose2d(x).t(), None):
             c = torch.randn(M, N, device=DEV).to(cdtype)
             ref = beta * c.float() + dy.float().t() @ x.float()
-            L._DW_SPLIT = splits
-            L.wgrad_mm(c, dy.t(), b, beta)
-            tol = 2e-2 * (T ** 0.5) / 8 if cdtype == torch.bfloat16 else 1e-3 * (T ** 0.5) / 8
+            if b is None:  # the hand-written TN kernel's split mode (operands as stored)
+                L.wgrad_tn(c, dy, x, beta)
+            else:
+                L.wgrad_mm(c, dy.t(), b, beta)
             torch.testing.assert_close(c.float(), ref, atol=tol, rtol=1e-2 if cdtype == torch.bfloat16 else 1e-4)
     finally:
         L._WAVE = old
@@ -323,15 +326,16 @@ def nt_config(C):
     C.gemm_nt_config(0, -8, 32, 0)
 
 
-@pytest.mark.parametrize("cfg", [(1, 1, 1, 0), (3, 4, 1, 0), (8, -2, 1, 1), (16, 2, 2, 0), (5, -16, 1, 0)])
+@pytest.mark.parametrize("cfg", [(1, 1, 1, 0), (3, 4, 1, 0), (8, -2, 1, 1), (16, 2, 2, 0), (5, -16, 1, 0),
+                                 (4, -8, 1, 0, 1), (4, -8, 1, 0, 2), (4, -8, 1, 0, 3), (4, -8, 1, 0, 4)])
 @pytest.mark.parametrize("M,N,K", [(1024, 768, 64), (768, 1280, 128), (512, 1024, 448)])
 def test_gemm_nt_persistent(nt_config, cfg, M, N, K):
     """The persistent grid walks several tiles per workgroup (grid capped below the tile count) with the
     super-stage stream running across tile boundaries -- including K = 64 (one stage per tile: the next
     tile's first stage is prefetched while the current one is still being read) -- under every tile
-    order / store policy: exact integer products, every tile checked."""
+    order / store policy / operand-DMA cache policy: exact integer products, every tile checked."""
     C = nt_config
-    C.gemm_nt_config(cfg[0], cfg[1], cfg[2], cfg[3])
+    C.gemm_nt_config(*cfg)
     torch.manual_seed(11)
     a = torch.randint(-3, 4, (M, K), device=DEV).to(torch.bfloat16)
     b = (torch.arange(N * K, device=DEV).reshape(N, K) % 5 - 2).to(torch.bfloat16)

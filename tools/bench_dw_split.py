@@ -90,7 +90,17 @@ def main():
                 ext().splitk_sum_(c, p, 0.0)
             return run
 
-        arms = {"base": base, "split2_hip": split_hip(2), "wgrad_mm": lambda: L.wgrad_mm(c, dy.t(), L.transpose2d(x, xt).t(), 0.0), "split2": split(2), "split4": split(4), "split2_bf16": split(2, False),
+        def tn(s):  # the hand-written TN kernel (operands as stored, no transposed copy), split s ways
+            def run():
+                if s == 1:
+                    ext().gemm_tn_(c, dy, x, 1.0, 0.0)
+                else:
+                    p = parts[s]
+                    ext().gemm_tn_split_(p, dy, x)
+                    ext().splitk_sum_(c, p, 0.0)
+            return run
+
+        arms = {"base": base, "tn1": tn(1), "tn2": tn(2), "tn4": tn(4), "split2_hip": split_hip(2), "wgrad_mm": lambda: L.wgrad_mm(c, dy.t(), L.transpose2d(x, xt).t(), 0.0), "split2": split(2), "split4": split(4), "split2_bf16": split(2, False),
                 "split2_tt": split_tt(2)}
         errs = {}
         for k, fn in arms.items():

@@ -6,9 +6,10 @@ augmented LoRA forms of ops/linear.py (k = K + 64 forward, the transposed frozen
     python tools/bench_gemm_nt.py [--iters 20] [--rounds 5] [--shapes qkv_fwd,o_fwd] \
         [--configs "0,8,32,0;0,16,2,1"]
 
-Each config is ``grid_cap,group,xcc,nt_store`` (ext().gemm_nt_config: grid_cap 0 = one persistent
+Each config is ``grid_cap,group,xcc,nt_store[,load_policy]`` (ext().gemm_nt_config: grid_cap 0 = one persistent
 workgroup per CU, a large cap = one workgroup per tile; group > 0 M-fast / < 0 N-fast tile groups; xcc
-logical ids per XCD slot; nt_store non-temporal C stores).  Every config and the library are timed in
+logical ids per XCD slot; nt_store non-temporal C stores; load_policy the operand DMA's cache bits:
+0 default, 1 sc0, 2 sc1, 3 sc0 sc1, 4 nt).  Every config and the library are timed in
 INTERLEAVED rounds on the same uniform random [-1, 1) operands (zeros read fast: DVFS), so box-to-box
 clock differences cancel; one JSON line per (shape, config) with the median / min ms, TF/s on the
 median, the speed-up over the library and the max |ours - lib| / max |lib| of one product."""
@@ -63,7 +64,7 @@ def main():
         torch.mm(x, w.t(), out=y0)
         errs = []
         for cfg in cfgs:
-            C.gemm_nt_config(cfg[0], cfg[1], cfg[2], cfg[3])
+            C.gemm_nt_config(*cfg)
             y1.zero_()
             C.gemm_nt_(y1, x, w)
             torch.cuda.synchronize()
@@ -72,7 +73,7 @@ def main():
         lib = []
         for _ in range(a.rounds):
             for i, cfg in enumerate(cfgs):
-                C.gemm_nt_config(cfg[0], cfg[1], cfg[2], cfg[3])
+                C.gemm_nt_config(*cfg)
                 ours[i].append(timeit(lambda: C.gemm_nt_(y1, x, w), a.iters))
             lib.append(timeit(lambda: torch.mm(x, w.t(), out=y0), a.iters))
         fl = 2.0 * a.T * n * k

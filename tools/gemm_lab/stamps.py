@@ -36,7 +36,7 @@ def main():
     lib.ftc_gemm_nt.argtypes = [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p,
                                 ctypes.c_longlong, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                 ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
-    lib.ftc_gemm_nt_config.argtypes = [ctypes.c_int] * 4
+    lib.ftc_gemm_nt_config.argtypes = [ctypes.c_int] * 5
     lib.ftc_gemm_nt_stamps.argtypes = [ctypes.c_void_p]
     torch.manual_seed(0)
     for name in a.shapes.split(","):
@@ -46,7 +46,7 @@ def main():
         y = torch.empty(T, n, device="cuda", dtype=torch.bfloat16)
         ref = torch.mm(x, w.t())
         for cfg in a.configs.split(";"):
-            lib.ftc_gemm_nt_config(*[int(v) for v in cfg.split(",")])
+            lib.ftc_gemm_nt_config(*([int(v) for v in cfg.split(",")] + [0, 0])[:5])
             st = torch.cuda.current_stream().cuda_stream
 
             def run():
