@@ -681,6 +681,321 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
   }
 }
 
+// ---- IL (round 4): 4 waves x 64 keys, one wave per SIMD, fenced in-wave interleave --------------------
+// profiles/r2/stamp_dkdv.md: the 8-wave kernel spends ~4,070 cycles per 32-row slice on 2,048 cycles of
+// MFMA work per SIMD because its 8 waves each re-read the slice's Q / dO from LDS (~1,280 LDS-array
+// cycles per slice interval at 256 B/clk).  Here each wave owns 64 keys as two 32-key halves, so every
+// Q / dO fragment it reads feeds both halves (half the LDS bytes per MFMA), and the softmax VALU that
+// the second wave of a SIMD used to hide is interleaved by hand with the wave's OWN MFMAs
+// (sched_barrier fences; values pinned so the compiler cannot sink them past the fences):
+//
+//   sync(it)  A(it): S, dP' of both halves (32 MFMAs, next k-step's reads between them;
+//                    the row constants -lse/scale, -delta are the first MFMA's C operand, with -inf
+//                    at masked positions on diagonal / window / document slices)
+//   X:  dV, dK += B2(it - 1, half 1)  (16 MFMAs)  x  P, dS of (it, half 0)   (exp / mul / pack)
+//   Y:  dV, dK += B2(it,     half 0)  (16 MFMAs)  x  P, dS of (it, half 1)   (carried to slice it + 1)
+//
+// The transposed dO^T / Q^T reads of each d tile go out one d tile ahead.  Slice it - 1 is still read in
+// X of slice it, so the Q / dO ring has 4 slots (DMA two slices ahead into the slot of slice it - 2).
+// The DMA is inline asm (common.h lds_dma16) and counted with explicit vmcnt waits.  Slice 0's X runs
+// its 16 MFMAs on zero P / dS carried from "slice -1" (exact: K rows x 0 adds 0).
+FTC_DEV void lds_dma4(__amdgpu_buffer_rsrc_t r, const void* lds, int voff, int soff) {
+  const unsigned dst = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)lds;
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "buffer_load_dword %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(r), "s"(dst), "s"(soff)
+      : "memory");
+}
+
+template <int D>
+__global__ __launch_bounds__(256, 1) void bwd_dkdv_il_kernel(BwdArgs a) {
+  static_assert(D == 128, "IL dK/dV: head_dim 128");
+  constexpr int NCH = D / 8, DSTEPS = D / 16, DT = D / 32;
+  constexpr int BKV = 256, BQ2 = 32, WAVES = 4;
+  constexpr int KBYTES = BKV * D * 2, QBYTES = BQ2 * D * 2;
+  constexpr int SLICE = 2 * QBYTES + 2 * BQ2 * 4;  // Q | dO | -lse/scale | -delta
+  constexpr int NG = QBYTES / 1024 / WAVES;         // 1 KiB pieces per matrix per wave per slice
+  constexpr int RPG = 1024 / (D * 2);
+  constexpr int PER_SLICE = 2 * NG + 1;             // DMA instructions per wave per slice
+  __shared__ __attribute__((aligned(16))) char Ks[KBYTES];
+  __shared__ __attribute__((aligned(16))) char ring[4 * SLICE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = lane >> 5, lr = lane & 31;
+  const int S = a.S, G = a.H / a.KV;
+  const int npairs = a.B * a.KV;
+  int kb, pair;
+  {
+    const int bid = blockIdx.x;
+    if ((npairs & 7) == 0) {
+      const int xcd = bid & 7, slot = bid >> 3, ppx = npairs >> 3;
+      kb = slot / ppx;
+      pair = (slot % ppx) * 8 + xcd;
+    } else {
+      kb = bid / npairs;
+      pair = bid % npairs;
+    }
+  }
+  const int kvh = pair % a.KV, b = pair / a.KV;
+  const int kv0 = kb * BKV;
+  const int wkey0 = kv0 + wave * 64;
+
+  const uint16_t* kbase = a.k + ((long long)b * S) * a.kv_rs + (long long)kvh * D;
+  {
+    constexpr int RPP = 256 / NCH;
+    const int lrow = tid / NCH, lch = tid % NCH;
+    const auto krs = make_rsrc(kbase + (long long)kv0 * a.kv_rs);
+    const int voff = (lrow * (int)a.kv_rs + lch * 8) * 2;
+#pragma unroll
+    for (int p = 0; p < BKV / RPP; ++p)
+      *reinterpret_cast<u32x4*>(Ks + lds_off<D>(p * RPP + lrow, lch)) = buf_load16(krs, voff, p * RPP * (int)a.kv_rs * 2);
+  }
+  bf16x8 vf[2][DSTEPS];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const uint16_t* vp = a.v + ((long long)b * S + wkey0 + 32 * j + lr) * a.kv_rs + (long long)kvh * D + 8 * hh;
+#pragma unroll
+    for (int st = 0; st < DSTEPS; ++st) vf[j][st] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(vp + 16 * st));
+  }
+
+  int qbeg = a.causal ? kv0 : 0;
+  int qend = S;
+  if (a.window > 0) qend = min(S, kv0 + BKV - 1 + a.window);
+  int dmin[2] = {0x3fffffff, 0x3fffffff};
+  const int* de_row = a.doc_end ? a.doc_end + (long long)b * S : nullptr;
+  if (de_row) {
+    qend = min(qend, de_row[kv0 + BKV - 1]);
+    dmin[0] = de_row[wkey0];
+    dmin[1] = de_row[wkey0 + 32];
+  }
+  qbeg = (qbeg / BQ2) * BQ2;
+  const int nqt = (qend - qbeg + BQ2 - 1) / BQ2;
+  const int total = G * nqt;
+
+  const auto qrsrc = make_rsrc(a.q + (long long)b * S * a.q_rs);
+  const auto drsrc = make_rsrc(a.dout + (long long)b * S * a.do_rs);
+  const auto crsrc = make_rsrc(a.delta);
+  int qvo[NG], dvo[NG];
+#pragma unroll
+  for (int i = 0; i < NG; ++i) {
+    const int row = (wave * NG + i) * RPG + lane / NCH, pc = lane % NCH;
+    const int lc = (pc ^ swz(row)) & (NCH - 1);
+    qvo[i] = (row * (int)a.q_rs + lc * 8) * 2;
+    dvo[i] = (row * (int)a.do_rs + lc * 8) * 2;
+  }
+  const int cvo = (lr + (hh ? 0 : a.B * a.H * S)) * 4;  // lanes 0-31: -lse/scale rows, 32-63: -delta rows
+  auto slot = [&](int it_) __attribute__((always_inline)) -> char* { return ring + (it_ & 3) * SLICE; };
+  auto issue = [&](int it_) __attribute__((always_inline)) {
+    const int g_ = it_ / nqt, qt_ = qbeg + (it_ % nqt) * BQ2;
+    const int hq_ = kvh * G + g_;
+    char* base = slot(it_);
+    const int qso = (hq_ * D + qt_ * (int)a.q_rs) * 2, dso = (hq_ * D + qt_ * (int)a.do_rs) * 2;
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {
+      const int r0 = (wave * NG + i) * RPG;
+      lds_dma16(qrsrc, base + r0 * D * 2, qvo[i], qso);
+      lds_dma16(drsrc, base + QBYTES + r0 * D * 2, dvo[i], dso);
+    }
+    lds_dma4(crsrc, base + 2 * QBYTES, cvo, ((b * a.H + hq_) * S + qt_) * 4);
+  };
+  constexpr int VM_ONE = 0x0F70 | (PER_SLICE & 15) | ((PER_SLICE >> 4) << 14);  // vmcnt(PER_SLICE)
+
+  f32x16 dv[2][DT], dk[2][DT];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { dv[j][t][i] = 0.f; dk[j][t][i] = 0.f; }
+
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // K staging, V fragments, doc bounds retired (vmcnt(0))
+  __syncthreads();
+  if (total > 0) issue(0);
+  if (total > 1) issue(1);
+
+  auto fence = []() __attribute__((always_inline)) { __builtin_amdgcn_sched_barrier(0); };
+  const int2 to[DT] = {tr_offsets<D>(0, lane), tr_offsets<D>(32, lane), tr_offsets<D>(64, lane), tr_offsets<D>(96, lane)};
+  f32x16 s[2], dp[2];
+  bf16x8 pb0[2], sb0[2];  // P / dS of half 0 of the current slice
+  bf16x8 pbc[2], sbc[2];  // P / dS of half 1, carried into the next slice's X
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    pbc[k] = __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0));
+    sbc[k] = pbc[k];
+  }
+  // one element e (0..15) of half j: P = exp2(c S), dS = P dP'; packs after elements 7 and 15
+  auto b1_elem = [&](int j, int e, bf16x8* pbo, bf16x8* sbo) __attribute__((always_inline)) {
+    const float p = __builtin_amdgcn_exp2f(a.c * s[j][e]);
+    const float d = p * dp[j][e];
+    asm volatile("" ::"v"(p), "v"(d));  // pin: pure arithmetic would otherwise sink past the fences
+    s[j][e] = p;
+    dp[j][e] = d;
+    if ((e & 7) == 7) {
+      pbo[e >> 3] = pack8_bf(s[j], e & 8);
+      sbo[e >> 3] = pack8_bf(dp[j], e & 8);
+    }
+  };
+  // the four transposed operands of a d tile (dO^T rows 0-15 / 16-31, Q^T rows 0-15 / 16-31), ONE register
+  // set: operand m of d tile dt + 1 is read right after the MFMA that consumed operand m of d tile dt
+  // (three MFMAs of latency cover; a second set would not fit next to 320 accumulator registers)
+  bf16x8 tv[4];
+  auto tr_op = [&](const char* Qs, int dt, int m) __attribute__((always_inline)) {
+    tv[m] = tr_read<D>((m < 2 ? Qs + QBYTES : Qs), 16 * (m & 1), to[dt]);
+  };
+  // B2 of half j on d tile dt, MFMA m (0..3) of its four.  The dV / dK accumulators (256 registers) are
+  // pinned to the AGPR half by inline asm ("+a"): left to itself the compiler spreads them and the S / dP'
+  // chains over both halves and pays ~220 v_accvgpr moves per slice to feed the softmax VALU.  Wait
+  // states (guide §5.7 item 2): an MFMA's D feeding the next MFMA's C is 0 states; the operands are LDS
+  // reads (lgkmcnt-waited by the compiler) or packs made a region earlier; s_nop 1 covers a VALU-written
+  // operand anyway; the epilogue's readers follow a padding statement after the loop.
+  auto b2_mfma = [&](int j, int dt, int m, const bf16x8* pbs, const bf16x8* sbs) __attribute__((always_inline)) {
+    if (m < 2)
+      asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(dv[j][dt]) : "v"(tv[m]), "v"(pbs[m]));
+    else
+      asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(dk[j][dt]) : "v"(tv[m]), "v"(sbs[m - 2]));
+  };
+  // X / Y region: B2 of half j from slice image Qs (pbs / sbs), with B1 of half jv of the current slice
+  // (into pbo / sbo) one element per MFMA, and after each MFMA the re-read of its operand for the next
+  // d tile (for d tile 0 of Qnext after the last one).  Operands of d tile 0 are read by the caller.
+  auto region = [&](int j, const char* Qs, const bf16x8* pbs, const bf16x8* sbs, int jv, bf16x8* pbo, bf16x8* sbo,
+                    const char* Qnext) __attribute__((always_inline)) {
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        b2_mfma(j, dt, m, pbs, sbs);
+        fence();
+        b1_elem(jv, dt * 4 + m, pbo, sbo);
+        if (dt + 1 < DT) tr_op(Qs, dt + 1, m);
+        else if (Qnext) tr_op(Qnext, 0, m);
+        fence();
+      }
+  };
+
+  for (int it = 0; it < total; ++it) {
+    // ---- sync: slice it landed (it + 1 may fly), every wave is past slice it - 1's Y; DMA it + 2
+    if (it + 1 < total) __builtin_amdgcn_s_waitcnt(VM_ONE);
+    else __builtin_amdgcn_s_waitcnt(0x0F70);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    if (it + 2 < total) issue(it + 2);
+    fence();
+    const char* Qs = slot(it);
+    const char* Ds = Qs + QBYTES;
+    const char* Qprev = it > 0 ? slot(it - 1) : Ks;  // slice -1: K rows x zero P / dS
+    // ---- A: S = Q K^T - lse/scale, dP' = dO V^T - delta for both halves
+    {
+      const float* cst = reinterpret_cast<const float*>(Qs + 2 * QBYTES);
+      f32x16 cs, cd;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 lv = *reinterpret_cast<const float4*>(cst + 8 * g4 + 4 * hh);
+        const float4 dv4 = *reinterpret_cast<const float4*>(cst + BQ2 + 8 * g4 + 4 * hh);
+        cs[4 * g4 + 0] = lv.x; cs[4 * g4 + 1] = lv.y; cs[4 * g4 + 2] = lv.z; cs[4 * g4 + 3] = lv.w;
+        cd[4 * g4 + 0] = dv4.x; cd[4 * g4 + 1] = dv4.y; cd[4 * g4 + 2] = dv4.z; cd[4 * g4 + 3] = dv4.w;
+      }
+      // masks (diagonal / window / document slices; wave-uniform branches) go into the S chains' start
+      // values: -inf there, so P = exp2(c S) = 0 and dS = 0 -- on the 16-register constant tiles before
+      // the chains start, not on the live S accumulators
+      f32x16 cs0 = cs, cs1 = cs;
+      {
+        const int qt = qbeg + (it % nqt) * BQ2;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int kmin = wkey0 + 32 * j;
+          const bool need_mask = (a.causal && qt < kmin + 31) || (a.window > 0 && qt + 31 - kmin >= a.window) ||
+                                 qt + 31 >= dmin[j];
+          if (need_mask) {
+            const int key = kmin + lr;
+            const int base = qt + 4 * hh;
+            const int lo = (a.causal ? key : -0x3fffffff) - base;
+            const int dend = de_row ? de_row[key] : 0x40000000;
+            const int hi = min(a.window > 0 ? key + a.window - 1 : 0x3fffffff, dend - 1) - base;
+            f32x16& t = j ? cs1 : cs0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const int off = (i & 3) + 8 * (i >> 2);
+              t[i] = (off >= lo && off <= hi) ? t[i] : -INFINITY;
+            }
+          }
+        }
+      }
+      // one register set [qa, da, k0, k1]: each fragment of k-step st + 1 is read right after the last MFMA
+      // of k-step st that uses it (k0 after s0, qa / k1 after s1, da after dP'1)
+      u32x4 fr[4];
+      auto rd = [&](int st, int which) __attribute__((always_inline)) {
+        if (which == 0) fr[0] = *reinterpret_cast<const u32x4*>(Qs + lds_off<D>(lr, 2 * st + hh));
+        if (which == 1) fr[1] = *reinterpret_cast<const u32x4*>(Ds + lds_off<D>(lr, 2 * st + hh));
+        if (which == 2) fr[2] = *reinterpret_cast<const u32x4*>(Ks + lds_off<D>(wave * 64 + lr, 2 * st + hh));
+        if (which == 3) fr[3] = *reinterpret_cast<const u32x4*>(Ks + lds_off<D>(wave * 64 + 32 + lr, 2 * st + hh));
+      };
+#pragma unroll
+      for (int w = 0; w < 4; ++w) rd(0, w);
+      fence();
+#pragma unroll
+      for (int st = 0; st < DSTEPS; ++st) {
+        const bool more = st + 1 < DSTEPS;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const bf16x8 qa = __builtin_bit_cast(bf16x8, fr[0]), da = __builtin_bit_cast(bf16x8, fr[1]);
+          // S / dP' chains pinned to VGPRs (asm "v"): the softmax VALU reads them in place
+          const bf16x8 bop = m == 0 ? __builtin_bit_cast(bf16x8, fr[2]) : m == 1 ? __builtin_bit_cast(bf16x8, fr[3]) : vf[m - 2][st];
+          f32x16& acc = m == 0 ? s[0] : m == 1 ? s[1] : m == 2 ? dp[0] : dp[1];
+          if (st == 0) {
+            const f32x16& c0 = m == 0 ? cs0 : m == 1 ? cs1 : cd;
+            asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %3"
+                         : "=&v"(acc) : "v"(m < 2 ? qa : da), "v"(bop), "v"(c0));
+          } else {
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(m < 2 ? qa : da), "v"(bop));
+          }
+          fence();
+          if (more && m == 0) rd(st + 1, 2);
+          if (more && m == 1) { rd(st + 1, 0); rd(st + 1, 3); }
+          if (more && m == 3) rd(st + 1, 1);
+          if (st == DSTEPS - 1) tr_op(Qprev, 0, m);  // X's first d tile
+          fence();
+        }
+      }
+    }
+    // the S / dP' results (8-pass XDL, asm: not padded by the compiler) before the first VALU reader
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    fence();
+    // ---- X: B2(it - 1, half 1) x B1(it, half 0);  Y: B2(it, half 0) x B1(it, half 1)
+    region(1, Qprev, pbc, sbc, 0, pb0, sb0, Qs);
+    region(0, Qs, pb0, sb0, 1, pbc, sbc, nullptr);
+  }
+  // ---- the last slice's half 1
+  if (total > 0) {
+    const char* Ql = slot(total - 1);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) tr_op(Ql, 0, m);
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        b2_mfma(1, dt, m, pbc, sbc);
+        if (dt + 1 < DT) tr_op(Ql, dt + 1, m);
+      }
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // no DMA outlives the workgroup
+  asm volatile("s_nop 15" ::: "memory");  // the last asm MFMAs' results before any reader (16-pass XDL)
+
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int key = wkey0 + 32 * j + lr;
+    uint16_t* dkp = a.dk + ((long long)b * S + key) * a.dkv_rs + (long long)kvh * D;
+    uint16_t* dvp = a.dv + ((long long)b * S + key) * a.dkv_rs + (long long)kvh * D;
+    const bool wide = (a.dkv_rs & 7) == 0;
+    if (a.rcos) rope_inv_rows<DT>(dk[j], a, (long long)b * S + key, hh);
+    store_rows<DT>(dkp, dk[j], a.scale, hh, wide);
+    store_rows<DT>(dvp, dv[j], 1.0f, hh, wide);
+  }
+}
+
 // ---------------------------------------------------------------- 3. dQ
 #ifndef DQ_CINIT
 #define DQ_CINIT 1
@@ -889,11 +1204,25 @@ void launch_dkdv(const BwdArgs& a, int grid, int waves, bool pp, bool dist3, hip
     hipLaunchKernelGGL((bwd_dkdv_kernel<D, 1, true>), dim3(grid), dim3(512), 0, stream, a);
   else if (waves == 8)
     hipLaunchKernelGGL((bwd_dkdv_kernel<D, 1>), dim3(grid), dim3(512), 0, stream, a);
+  else if (D == 128 && waves == 1)
+    hipLaunchKernelGGL((bwd_dkdv_il_kernel<128>), dim3(grid), dim3(256), 0, stream, a);
   else
     hipLaunchKernelGGL((bwd_dkdv_kernel<D, 2>), dim3(grid), dim3(256), 0, stream, a);
 }
 
+// dK/dV variant: 8 (8 waves x 32 keys, ping-pong), 4 (4 waves x 64 keys), 1 (IL: 4 waves x 64 keys,
+// fenced interleave, D = 128); FTC_FLASH_DKDV_WAVES=8|4|il, or ftc_flash_dkdv_config (tests / tools)
+int& dkdv_variant() {
+  static int v = [] {
+    const char* e = getenv("FTC_FLASH_DKDV_WAVES");
+    return (e && e[0] == '4') ? 4 : (e && e[0] == 'i') ? 1 : 8;
+  }();
+  return v;
+}
+
 }  // namespace
+
+extern "C" void ftc_flash_dkdv_config(int waves) { dkdv_variant() = (waves == 4 || waves == 1) ? waves : 8; }
 
 extern "C" int ftc_flash_bwd_workspace(int B, int S, int H, int D, long long* bytes) {
   (void)D;
@@ -932,10 +1261,8 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
   }();
   // dK/dV workgroup shape at D=128: 8 waves x 32 keys (2 waves/SIMD, default: 1.20 vs 1.52 ms at the
   // Llama-3-8B layer shape, profiles/) or 4 waves x 64 keys (1 wave/SIMD); FTC_FLASH_DKDV_WAVES=8|4
-  static const int dkdv_waves = [] {
-    const char* e = getenv("FTC_FLASH_DKDV_WAVES");
-    return (e && e[0] == '4') ? 4 : 8;
-  }();
+  // FTC_FLASH_DKDV_WAVES=il: the round-4 interleaved 4-wave kernel (bwd_dkdv_il_kernel, D = 128)
+  const int dkdv_waves = dkdv_variant();
   // ping-pong phase order for the two waves of a SIMD (default; FTC_FLASH_DKDV_PP=0 turns it off):
   // bwd 2.00 -> 1.97 ms at the Llama-3-8B layer shape (profiles/r1_attn_dkdv_pp.log)
   static const bool pp = [] {

@@ -427,13 +427,16 @@ def test_lora_merge(C):
     torch.testing.assert_close(W.float(), ref, atol=3e-2, rtol=1e-2)
 
 
-@pytest.fixture(params=[1, 2], ids=["qb1", "qb2"])
+@pytest.fixture(params=[(1, 8), (2, 8), (1, 1)], ids=["qb1", "qb2", "il"])
 def fwd_qb(C, request):
-    """Both flash-forward variants: 32 query rows per wave (two workgroups per CU) and two 32-row blocks
-    per wave (one workgroup per CU, csrc/kernels/flash_attn_fwd.hip QB2)."""
-    C.flash_fwd_config(request.param)
-    yield request.param
+    """The flash variants: forward with 32 query rows per wave (two workgroups per CU) or two 32-row blocks
+    per wave (one workgroup per CU, csrc/kernels/flash_attn_fwd.hip QB2); dK/dV with 8 waves x 32 keys
+    (ping-pong) or the interleaved 4 waves x 64 keys (flash_attn_bwd.hip IL, head_dim 128)."""
+    C.flash_fwd_config(request.param[0])
+    C.flash_dkdv_config(request.param[1])
+    yield request.param[0]
     C.flash_fwd_config(1)
+    C.flash_dkdv_config(8)
 
 
 @pytest.mark.parametrize("B,S,H,KV,D,causal,window", [
