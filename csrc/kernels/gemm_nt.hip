@@ -476,7 +476,8 @@ struct Config {
 
 Config& config() {
   static Config c = [] {
-    Config d{0, -8, 32, 0, 0};
+    // load policy sc0 (1): +0.1-2.4 % over the default policy on the headline shapes (profiles/r4/gemm_nt/policy.log)
+    Config d{0, -8, 32, 0, 1};
     if (const char* e = getenv("FTC_GEMM_NT_ORDER"))
       sscanf(e, "%d,%d,%d,%d,%d", &d.grid_cap, &d.group, &d.xcc, &d.nt_store, &d.load_policy);
     return d;

@@ -400,8 +400,11 @@ def dw_splits(M: int, N: int, K: int, mode: str | None = None) -> int:
     if mode != "auto":
         s = int(mode)
         return s if s > 1 and K % (64 * s) == 0 else 1
+    # measured (profiles/r4/dw_split/): only the wide-input shape gains -- down dW [4096, 14336] 1.90 ->
+    # 1.68 ms (hipBLASLt's 3.5 waves of 256 x 256 tiles -> 7); qkv [6144, 4096] runs 1,240 TF/s unsplit
+    # (the library's own tiling is not 1.5 waves there) and loses 3 % split; o / gate-up are whole waves
     tiles = -(-M // 256) * -(-N // 256)
-    if tiles % _WAVE == 0 or tiles > 8 * _WAVE:
+    if N < 2 * M or tiles % _WAVE == 0 or tiles > 8 * _WAVE:
         return 1
     for s in (2, 4):
         if (tiles * s) % _WAVE == 0 and K % (64 * s) == 0:

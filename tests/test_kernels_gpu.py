@@ -268,14 +268,15 @@ def test_gemm_tn_rejects(C):
 def test_wgrad_split(C, cdtype, splits, beta):
     """Split-K weight gradient (ops.linear.wgrad_mm: batched GEMM into fp32 partials + splitk_sum_) on the
     operands of the production paths (dy^T as a transposed view, x transposed or as stored) vs fp32.
-    768 x 512 = 6 tiles: "auto" splits it 2 ways only at _WAVE = 4 (patched), as qkv dW is at 256."""
+    256 x 768 = 3 tiles of a wide-input shape: "auto" splits it 2 ways at _WAVE = 2 (patched), as down dW
+    is split at 256."""
     from finetune_controller_amd.ops import linear as L
     torch.manual_seed(5)
-    T, M, N = 1024, 768, 512
+    T, M, N = 1024, 256, 768
     dy = (torch.rand(T, M, device=DEV) * 2 - 1).to(torch.bfloat16)
     x = (torch.rand(T, N, device=DEV) * 2 - 1).to(torch.bfloat16)
     old = L._WAVE
-    L._WAVE = 4
+    L._WAVE = 2
     try:
         assert L.dw_splits(M, N, T, splits) == (2 if splits == "auto" else int(splits))
         L._DW_SPLIT = splits
@@ -323,7 +324,7 @@ def test_gemm_nt(C, cdtype, M, N, K, pad, beta):
 def nt_config(C):
     """Restores the projection GEMM's default launch configuration after a test that changes it."""
     yield C
-    C.gemm_nt_config(0, -8, 32, 0)
+    C.gemm_nt_config(0, -8, 32, 0, 1)
 
 
 @pytest.mark.parametrize("cfg", [(1, 1, 1, 0), (3, 4, 1, 0), (8, -2, 1, 1), (16, 2, 2, 0), (5, -16, 1, 0),

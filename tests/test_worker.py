@@ -654,12 +654,12 @@ def test_rslora_scale_and_adapter_config(tmp_path):
 
 
 def test_dw_split_choices_on_llama3_8b_shapes():
-    """Split-K weight gradients (ops.linear.dw_splits, FTC_DW_SPLIT=auto): only the wave-quantised
-    Llama-3-8B shapes split (qkv 384 tiles -> 2 x, down 896 -> 2 x); whole-wave and huge grids do not."""
+    """Split-K weight gradients (ops.linear.dw_splits, FTC_DW_SPLIT=auto): only the wave-quantised wide-input
+    shape splits (down 896 tiles -> 2 x); qkv (measured faster unsplit), whole-wave and huge grids do not."""
     from finetune_controller_amd.ops.linear import dw_splits
 
     T = 16384
-    assert dw_splits(6144, 4096, T, "auto") == 2   # qkv
+    assert dw_splits(6144, 4096, T, "auto") == 1   # qkv
     assert dw_splits(4096, 14336, T, "auto") == 2  # down
     assert dw_splits(4096, 4096, T, "auto") == 1   # o: one whole wave
     assert dw_splits(28672, 4096, T, "auto") == 1  # gate | up: seven whole waves

@@ -30,7 +30,7 @@ SHAPES = {  # name: (k, n)
     "down_fwd": (14336 + 64, 4096), "down_dx": (4096 + 64, 14336), "gu_dx": (28672 + 64, 4096),
     "o_dx": (4096 + 64, 4096), "qkv_dx": (6144 + 64, 4096), "lm_head": (4096, 4096 * 8),
 }
-DEFAULT_CONFIGS = "0,-8,32,0"
+DEFAULT_CONFIGS = "0,-8,32,0,1"
 
 
 def timeit(fn, iters):
