@@ -710,6 +710,12 @@ FTC_DEV void lds_dma4(__amdgpu_buffer_rsrc_t r, const void* lds, int voff, int s
       : "memory");
 }
 
+#ifndef IL_TV2
+#define IL_TV2 1
+#endif
+#ifndef IL_PIPE
+#define IL_PIPE 1
+#endif
 template <int D>
 __global__ __launch_bounds__(256, 1) void bwd_dkdv_il_kernel(BwdArgs a) {
   static_assert(D == 128, "IL dK/dV: head_dim 128");
@@ -827,40 +833,64 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_il_kernel(BwdArgs a) {
     pbc[k] = __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0));
     sbc[k] = pbc[k];
   }
-  // one element e (0..15) of half j: P = exp2(c S), dS = P dP'; packs after elements 7 and 15
-  auto b1_elem = [&](int j, int e, bf16x8* pbo, bf16x8* sbo) __attribute__((always_inline)) {
-    const float p = __builtin_amdgcn_exp2f(a.c * s[j][e]);
-    const float d = p * dp[j][e];
-    asm volatile("" ::"v"(p), "v"(d));  // pin: pure arithmetic would otherwise sink past the fences
-    s[j][e] = p;
-    dp[j][e] = d;
-    if ((e & 7) == 7) {
-      pbo[e >> 3] = pack8_bf(s[j], e & 8);
-      sbo[e >> 3] = pack8_bf(dp[j], e & 8);
+  // B1 of half j, software-pipelined over the 16 MFMA gaps of a region so no VALU waits on a fresh
+  // exponential: gap g computes P_g = exp2(c S_g) and dS_(g-1) = P_(g-1) dP'_(g-1); P's first 8 elements
+  // pack in gap 8, dS's in gap 9; the tail (dS_15, the second packs) follows the region's last MFMA
+  auto b1_gap = [&](int j, int g, bf16x8* pbo, bf16x8* sbo) __attribute__((always_inline)) {
+    if (!IL_PIPE) {  // unpipelined: P and dS of element g in gap g, packs after elements 7 / 15
+      if (g < 16) {
+        const float p = __builtin_amdgcn_exp2f(a.c * s[j][g]);
+        const float d = p * dp[j][g];
+        asm volatile("" ::"v"(p), "v"(d));
+        s[j][g] = p;
+        dp[j][g] = d;
+        if ((g & 7) == 7) {
+          pbo[g >> 3] = pack8_bf(s[j], g & 8);
+          sbo[g >> 3] = pack8_bf(dp[j], g & 8);
+        }
+      }
+      return;
+    }
+    if (g < 16) {
+      const float p = __builtin_amdgcn_exp2f(a.c * s[j][g]);
+      asm volatile("" ::"v"(p));  // pin: pure arithmetic would otherwise sink past the fences
+      s[j][g] = p;
+    }
+    if (g >= 1) {
+      const float d = s[j][g - 1] * dp[j][g - 1];
+      asm volatile("" ::"v"(d));
+      dp[j][g - 1] = d;
+    }
+    if (g == 8) pbo[0] = pack8_bf(s[j], 0);
+    if (g == 9) sbo[0] = pack8_bf(dp[j], 0);
+    if (g == 16) {
+      pbo[1] = pack8_bf(s[j], 8);
+      sbo[1] = pack8_bf(dp[j], 8);
     }
   };
-  // the four transposed operands of a d tile (dO^T rows 0-15 / 16-31, Q^T rows 0-15 / 16-31), ONE register
-  // set: operand m of d tile dt + 1 is read right after the MFMA that consumed operand m of d tile dt
-  // (three MFMAs of latency cover; a second set would not fit next to 320 accumulator registers)
-  bf16x8 tv[4];
+  // the four transposed operands of a d tile (dO^T rows 0-15 / 16-31, Q^T rows 0-15 / 16-31), two register
+  // sets by d-tile parity: d tile dt + 1 is read during the first two MFMAs of d tile dt (>= 6 MFMAs of
+  // latency cover)
+  bf16x8 tv[2][4];
+  constexpr int TVM = IL_TV2 ? 1 : 0;
   auto tr_op = [&](const char* Qs, int dt, int m) __attribute__((always_inline)) {
-    tv[m] = tr_read<D>((m < 2 ? Qs + QBYTES : Qs), 16 * (m & 1), to[dt]);
+    tv[dt & TVM][m] = tr_read<D>((m < 2 ? Qs + QBYTES : Qs), 16 * (m & 1), to[dt]);
   };
   // B2 of half j on d tile dt, MFMA m (0..3) of its four.  The dV / dK accumulators (256 registers) are
   // pinned to the AGPR half by inline asm ("+a"): left to itself the compiler spreads them and the S / dP'
   // chains over both halves and pays ~220 v_accvgpr moves per slice to feed the softmax VALU.  Wait
   // states (guide §5.7 item 2): an MFMA's D feeding the next MFMA's C is 0 states; the operands are LDS
-  // reads (lgkmcnt-waited by the compiler) or packs made a region earlier; s_nop 1 covers a VALU-written
-  // operand anyway; the epilogue's readers follow a padding statement after the loop.
+  // reads (lgkmcnt-waited by the compiler) or packs made at least one MFMA earlier, covered by the
+  // s_nop 1; the epilogue's readers follow a padding statement after the loop.
   auto b2_mfma = [&](int j, int dt, int m, const bf16x8* pbs, const bf16x8* sbs) __attribute__((always_inline)) {
     if (m < 2)
-      asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(dv[j][dt]) : "v"(tv[m]), "v"(pbs[m]));
+      asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(dv[j][dt]) : "v"(tv[dt & TVM][m]), "v"(pbs[m]));
     else
-      asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(dk[j][dt]) : "v"(tv[m]), "v"(sbs[m - 2]));
+      asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(dk[j][dt]) : "v"(tv[dt & TVM][m]), "v"(sbs[m - 2]));
   };
-  // X / Y region: B2 of half j from slice image Qs (pbs / sbs), with B1 of half jv of the current slice
-  // (into pbo / sbo) one element per MFMA, and after each MFMA the re-read of its operand for the next
-  // d tile (for d tile 0 of Qnext after the last one).  Operands of d tile 0 are read by the caller.
+  // X / Y region: B2 of half j from slice image Qs (pbs / sbs) with B1 of half jv of the current slice
+  // (into pbo / sbo), one gap per MFMA; the next d tile's operands (d tile 0 of Qnext after the last)
+  // are read in the first two gaps of each d tile.  Operands of d tile 0 are read by the caller.
   auto region = [&](int j, const char* Qs, const bf16x8* pbs, const bf16x8* sbs, int jv, bf16x8* pbo, bf16x8* sbo,
                     const char* Qnext) __attribute__((always_inline)) {
 #pragma unroll
@@ -869,14 +899,45 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_il_kernel(BwdArgs a) {
       for (int m = 0; m < 4; ++m) {
         b2_mfma(j, dt, m, pbs, sbs);
         fence();
-        b1_elem(jv, dt * 4 + m, pbo, sbo);
-        if (dt + 1 < DT) tr_op(Qs, dt + 1, m);
-        else if (Qnext) tr_op(Qnext, 0, m);
+        b1_gap(jv, dt * 4 + m, pbo, sbo);
+        const char* src = dt + 1 < DT ? Qs : Qnext;
+        if (IL_TV2 && m < 2 && src) {
+          tr_op(src, (dt + 1) & 3, 2 * m);
+          tr_op(src, (dt + 1) & 3, 2 * m + 1);
+        }
+        if (!IL_TV2 && src) tr_op(src, (dt + 1) & 3, m);
         fence();
       }
+    b1_gap(jv, 16, pbo, sbo);
+    fence();
   };
 
+#ifdef FTC_STAMPS  // diagnostic build (tools/stamp_dkdv.hip with FTC_FLASH_DKDV_WAVES=il): segments sync / A / X / Y
+  const bool stamping = blockIdx.x == g_stamp_block;
+  unsigned long long st_acc[4] = {0, 0, 0, 0}, st_prev = 0, st_now = 0, st_t0 = 0, st_t1 = 0;
+  if (stamping) FTC_STAMP(st_t0);
+#define IL_SEG_START()              \
+  do {                              \
+    if (stamping) FTC_STAMP(st_prev); \
+  } while (0)
+#define IL_SEG_END(i)                \
+  do {                               \
+    if (stamping) {                  \
+      FTC_STAMP(st_now);             \
+      st_acc[i] += st_now - st_prev; \
+      st_prev = st_now;              \
+    }                                \
+  } while (0)
+#else
+#define IL_SEG_START() \
+  do {                 \
+  } while (0)
+#define IL_SEG_END(i) \
+  do {                \
+  } while (0)
+#endif
   for (int it = 0; it < total; ++it) {
+    IL_SEG_START();
     // ---- sync: slice it landed (it + 1 may fly), every wave is past slice it - 1's Y; DMA it + 2
     if (it + 1 < total) __builtin_amdgcn_s_waitcnt(VM_ONE);
     else __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -884,24 +945,28 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_il_kernel(BwdArgs a) {
     __builtin_amdgcn_s_barrier();
     if (it + 2 < total) issue(it + 2);
     fence();
+    IL_SEG_END(0);
     const char* Qs = slot(it);
     const char* Ds = Qs + QBYTES;
     const char* Qprev = it > 0 ? slot(it - 1) : Ks;  // slice -1: K rows x zero P / dS
     // ---- A: S = Q K^T - lse/scale, dP' = dO V^T - delta for both halves
     {
+      // the chains start from the row constants (-lse/scale for S, -delta for dP'), read from the slice's
+      // LDS image straight into the accumulators (one copy per half: no separate start tile whose
+      // registers an in-flight MFMA would still be reading as C); masks (diagonal / window / document
+      // slices, wave-uniform branches) put -inf into S's start values, so P = exp2(c S) = 0 and dS = 0
       const float* cst = reinterpret_cast<const float*>(Qs + 2 * QBYTES);
-      f32x16 cs, cd;
+      auto ld_const = [&](f32x16& t, const float* src) __attribute__((always_inline)) {
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const float4 lv = *reinterpret_cast<const float4*>(cst + 8 * g4 + 4 * hh);
-        const float4 dv4 = *reinterpret_cast<const float4*>(cst + BQ2 + 8 * g4 + 4 * hh);
-        cs[4 * g4 + 0] = lv.x; cs[4 * g4 + 1] = lv.y; cs[4 * g4 + 2] = lv.z; cs[4 * g4 + 3] = lv.w;
-        cd[4 * g4 + 0] = dv4.x; cd[4 * g4 + 1] = dv4.y; cd[4 * g4 + 2] = dv4.z; cd[4 * g4 + 3] = dv4.w;
-      }
-      // masks (diagonal / window / document slices; wave-uniform branches) go into the S chains' start
-      // values: -inf there, so P = exp2(c S) = 0 and dS = 0 -- on the 16-register constant tiles before
-      // the chains start, not on the live S accumulators
-      f32x16 cs0 = cs, cs1 = cs;
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const float4 v4 = *reinterpret_cast<const float4*>(src + 8 * g4 + 4 * hh);
+          t[4 * g4 + 0] = v4.x; t[4 * g4 + 1] = v4.y; t[4 * g4 + 2] = v4.z; t[4 * g4 + 3] = v4.w;
+        }
+      };
+      ld_const(s[0], cst);
+      ld_const(s[1], cst);
+      ld_const(dp[0], cst + BQ2);
+      ld_const(dp[1], cst + BQ2);
       {
         const int qt = qbeg + (it % nqt) * BQ2;
 #pragma unroll
@@ -915,48 +980,44 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_il_kernel(BwdArgs a) {
             const int lo = (a.causal ? key : -0x3fffffff) - base;
             const int dend = de_row ? de_row[key] : 0x40000000;
             const int hi = min(a.window > 0 ? key + a.window - 1 : 0x3fffffff, dend - 1) - base;
-            f32x16& t = j ? cs1 : cs0;
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
               const int off = (i & 3) + 8 * (i >> 2);
-              t[i] = (off >= lo && off <= hi) ? t[i] : -INFINITY;
+              s[j][i] = (off >= lo && off <= hi) ? s[j][i] : -INFINITY;
             }
           }
         }
       }
-      // one register set [qa, da, k0, k1]: each fragment of k-step st + 1 is read right after the last MFMA
-      // of k-step st that uses it (k0 after s0, qa / k1 after s1, da after dP'1)
-      u32x4 fr[4];
-      auto rd = [&](int st, int which) __attribute__((always_inline)) {
-        if (which == 0) fr[0] = *reinterpret_cast<const u32x4*>(Qs + lds_off<D>(lr, 2 * st + hh));
-        if (which == 1) fr[1] = *reinterpret_cast<const u32x4*>(Ds + lds_off<D>(lr, 2 * st + hh));
-        if (which == 2) fr[2] = *reinterpret_cast<const u32x4*>(Ks + lds_off<D>(wave * 64 + lr, 2 * st + hh));
-        if (which == 3) fr[3] = *reinterpret_cast<const u32x4*>(Ks + lds_off<D>(wave * 64 + 32 + lr, 2 * st + hh));
+      // k-step fragments [qa, da, k0, k1], double-buffered: k-step st + 1 is read under k-step st's MFMAs
+      u32x4 fr[2][4];
+      auto rd = [&](int st) __attribute__((always_inline)) {
+        fr[st & 1][0] = *reinterpret_cast<const u32x4*>(Qs + lds_off<D>(lr, 2 * st + hh));
+        fr[st & 1][1] = *reinterpret_cast<const u32x4*>(Ds + lds_off<D>(lr, 2 * st + hh));
+        fr[st & 1][2] = *reinterpret_cast<const u32x4*>(Ks + lds_off<D>(wave * 64 + lr, 2 * st + hh));
+        fr[st & 1][3] = *reinterpret_cast<const u32x4*>(Ks + lds_off<D>(wave * 64 + 32 + lr, 2 * st + hh));
       };
-#pragma unroll
-      for (int w = 0; w < 4; ++w) rd(0, w);
+      rd(0);
       fence();
 #pragma unroll
       for (int st = 0; st < DSTEPS; ++st) {
         const bool more = st + 1 < DSTEPS;
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
-          const bf16x8 qa = __builtin_bit_cast(bf16x8, fr[0]), da = __builtin_bit_cast(bf16x8, fr[1]);
-          // S / dP' chains pinned to VGPRs (asm "v"): the softmax VALU reads them in place
-          const bf16x8 bop = m == 0 ? __builtin_bit_cast(bf16x8, fr[2]) : m == 1 ? __builtin_bit_cast(bf16x8, fr[3]) : vf[m - 2][st];
+          const u32x4* f = fr[st & 1];
+          const bf16x8 qa = __builtin_bit_cast(bf16x8, f[0]), da = __builtin_bit_cast(bf16x8, f[1]);
+          const bf16x8 bop = m == 0 ? __builtin_bit_cast(bf16x8, f[2]) : m == 1 ? __builtin_bit_cast(bf16x8, f[3]) : vf[m - 2][st];
           f32x16& acc = m == 0 ? s[0] : m == 1 ? s[1] : m == 2 ? dp[0] : dp[1];
-          if (st == 0) {
-            const f32x16& c0 = m == 0 ? cs0 : m == 1 ? cs1 : cd;
-            asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %3"
-                         : "=&v"(acc) : "v"(m < 2 ? qa : da), "v"(bop), "v"(c0));
-          } else {
+          // (s_nop 1 at k-step 0: the start values may come from the mask's VALU selects)
+          if (st == 0)
+            asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(m < 2 ? qa : da), "v"(bop));
+          else
             asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(m < 2 ? qa : da), "v"(bop));
-          }
           fence();
-          if (more && m == 0) rd(st + 1, 2);
-          if (more && m == 1) { rd(st + 1, 0); rd(st + 1, 3); }
-          if (more && m == 3) rd(st + 1, 1);
-          if (st == DSTEPS - 1) tr_op(Qprev, 0, m);  // X's first d tile
+          if (more && m == 0) rd(st + 1);
+          if (st == DSTEPS - 1 && m < 2) {  // X's first d tile
+            tr_op(Qprev, 0, 2 * m);
+            tr_op(Qprev, 0, 2 * m + 1);
+          }
           fence();
         }
       }
@@ -964,22 +1025,39 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_il_kernel(BwdArgs a) {
     // the S / dP' results (8-pass XDL, asm: not padded by the compiler) before the first VALU reader
     asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
     fence();
+    IL_SEG_END(1);
     // ---- X: B2(it - 1, half 1) x B1(it, half 0);  Y: B2(it, half 0) x B1(it, half 1)
     region(1, Qprev, pbc, sbc, 0, pb0, sb0, Qs);
+    IL_SEG_END(2);
     region(0, Qs, pb0, sb0, 1, pbc, sbc, nullptr);
+    IL_SEG_END(3);
   }
+#ifdef FTC_STAMPS
+  if (stamping) {
+    FTC_STAMP(st_t1);
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) g_stamps[wave][i] = st_acc[i];
+      g_stamps[wave][4] = st_t1 - st_t0;
+      g_stamps[wave][5] = (unsigned long long)total;
+    }
+  }
+#endif
+#undef IL_SEG_START
+#undef IL_SEG_END
   // ---- the last slice's half 1
   if (total > 0) {
     const char* Ql = slot(total - 1);
 #pragma unroll
     for (int m = 0; m < 4; ++m) tr_op(Ql, 0, m);
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
+    for (int dt = 0; dt < DT; ++dt) {
+      if (dt + 1 < DT)
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        b2_mfma(1, dt, m, pbc, sbc);
-        if (dt + 1 < DT) tr_op(Ql, dt + 1, m);
-      }
+        for (int m = 0; m < 4; ++m) tr_op(Ql, dt + 1, m);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) b2_mfma(1, dt, m, pbc, sbc);
+    }
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // no DMA outlives the workgroup
   asm volatile("s_nop 15" ::: "memory");  // the last asm MFMAs' results before any reader (16-pass XDL)

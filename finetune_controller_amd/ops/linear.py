@@ -386,8 +386,8 @@ def accum_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, alpha: float =
 # 256 CUs (qkv: 384 tiles = 1.5 waves, down: 896 = 3.5).  Split along the tokens into S slices so that
 # S x tiles is a whole number of waves: ONE batched hipBLASLt GEMM writes the S fp32 partials, one HIP
 # pass (csrc/kernels/elementwise.hip splitk_sum_kernel) folds them into the gradient (beta C + sum).
-# FTC_DW_SPLIT: "0" off, "auto" (wave-quantised shapes only), or a fixed S.
-_DW_SPLIT = os.environ.get("FTC_DW_SPLIT", "0")
+# FTC_DW_SPLIT: "auto" (default: the measured winning shapes), "0" off, or a fixed S.
+_DW_SPLIT = os.environ.get("FTC_DW_SPLIT", "auto")  # full FT +0.9 % (profiles/r4/dw_split/full_ab)
 _DW_PARTS: dict = {}  # (device, stream) -> flat fp32 scratch for the partials
 _WAVE = 256  # workgroups per wave: one 256 x 256 tile per CU
 

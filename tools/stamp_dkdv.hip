@@ -7,6 +7,8 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DFTC_STAMPS -Icsrc/kernels tools/stamp_dkdv.hip -o tools/stamp_dkdv
 //   tools/stamp_dkdv [block ...]        (default: blocks 0 (heaviest key block) and 256)
+// FTC_FLASH_DKDV_WAVES=il stamps the interleaved 4-wave kernel instead: its columns are sync / A (S, dP'
+// MFMAs) / X (B2 of the previous slice's half 1 + B1 of half 0) / Y (B2 of half 0 + B1 of half 1).
 #include "../csrc/kernels/flash_attn_bwd.hip"
 
 #include <cstdio>
@@ -75,11 +77,17 @@ int main(int argc, char** argv) {
   for (int blk : blocks) {
     if (blk < 0 || blk >= g_kv) continue;
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_block), &blk, sizeof(int)));
+    {
+      unsigned long long z[8][6];
+      memset(z, 0, sizeof(z));
+      CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)));
+    }
     float ms = 0.f;
     for (int rep = 0; rep < 3; ++rep) {
       CK(hipEventRecord(e0, 0));
       const int rc = ftc_flash_bwd(q, k, v, o, dout, lse, dq, dk, dv, ws, B, S, H, KV, D, H * D, KV * D, H * D, H * D,
-                                   H * D, KV * D, 0.08838834764831845f, 1, 0, nullptr, nullptr, 0);
+                                   H * D, KV * D, 0.08838834764831845f, 1, 0, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
+                                   0);
       CK(hipEventRecord(e1, 0));
       CK(hipEventSynchronize(e1));
       if (rc != 0) {
@@ -95,6 +103,7 @@ int main(int argc, char** argv) {
     printf("|---:|---:|---:|---:|---:|---:|---:|---:|\n");
     for (int w = 0; w < 8; ++w) {
       const double tot = (double)st[w][4], n = (double)st[w][5];
+      if (tot <= 0) continue;
       if (n <= 0) continue;
       printf("| %d | %.0f | %.0f | %.0f | %.1f %% | %.1f %% | %.1f %% | %.1f %% |\n", w, n, tot, tot / n,
              100.0 * st[w][0] / tot, 100.0 * st[w][1] / tot, 100.0 * st[w][2] / tot, 100.0 * st[w][3] / tot);
