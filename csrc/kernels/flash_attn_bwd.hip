@@ -226,32 +226,41 @@ __global__ __launch_bounds__(256) void bwd_delta_kernel(BwdArgs a) {
 // piece -- waves [0, P) a piece of Q, waves [P, 2P) the same piece of dO -- so every wave still issues
 // the same number of DMA instructions per slice (the counted vmcnt stays wave-uniform).
 // QR = 2 (64-row slices): the row constants are two 256-byte pieces (-lse/scale rows, then -delta rows).
+// one 4-byte-per-lane LDS-DMA piece (the row constants), inline asm like common.h lds_dma16
+FTC_DEV void lds_dma4(__amdgpu_buffer_rsrc_t r, const void* lds, int voff, int soff) {
+  const unsigned dst = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)lds;
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "buffer_load_dword %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(r), "s"(dst), "s"(soff)
+      : "memory");
+}
+
 template <int D, int NG, int RPG, int QBYTES, bool SPLIT = false, int QR = 1>
 FTC_DEV void dkdv_dma(__amdgpu_buffer_rsrc_t qr, __amdgpu_buffer_rsrc_t dr, __amdgpu_buffer_rsrc_t cr, const int* qvo,
                       const int* dvo, int cvo, int cvo2, int qso, int dso, int cso, char* base, int wave) {
+  // inline asm (lds_dma16 / lds_dma4), not the builtin: hipcc tracks builtin LDS-DMA and, unable to prove
+  // the ring slots disjoint from the row-constant reads, drained every in-flight slice (vmcnt(0)) at the
+  // start of each phase A -- the counted waits in sync_slice are the only ones the ring needs
   if constexpr (SPLIT) {
     constexpr int P = QBYTES / 1024;
     if (wave < P)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (__attribute__((address_space(3))) void*)(base + wave * 1024), 16,
-                                               qvo[0], qso, 0, 0);
+      lds_dma16(qr, base + wave * 1024, qvo[0], qso);
     else
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          dr, (__attribute__((address_space(3))) void*)(base + QBYTES + (wave - P) * 1024), 16, dvo[0], dso, 0, 0);
+      lds_dma16(dr, base + QBYTES + (wave - P) * 1024, dvo[0], dso);
   } else {
 #pragma unroll
     for (int i = 0; i < NG; ++i) {
       const int r0 = (wave * NG + i) * RPG;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (__attribute__((address_space(3))) void*)(base + r0 * D * 2), 16,
-                                               qvo[i], qso, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          dr, (__attribute__((address_space(3))) void*)(base + QBYTES + r0 * D * 2), 16, dvo[i], dso, 0, 0);
+      lds_dma16(qr, base + r0 * D * 2, qvo[i], qso);
+      lds_dma16(dr, base + QBYTES + r0 * D * 2, dvo[i], dso);
     }
   }
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(cr, (__attribute__((address_space(3))) void*)(base + 2 * QBYTES), 4, cvo,
-                                           cso, 0, 0);
+  lds_dma4(cr, base + 2 * QBYTES, cvo, cso);
   if constexpr (QR == 2)  // second piece: -delta of the 64 rows (cvo addressed the -lse/scale rows)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(cr, (__attribute__((address_space(3))) void*)(base + 2 * QBYTES + 256), 4,
-                                             cvo2, cso, 0, 0);
+    lds_dma4(cr, base + 2 * QBYTES + 256, cvo2, cso);
 }
 
 // HW = 32-key halves per wave: HW = 2 -> 4 waves x 64 keys, one wave per SIMD (512-register budget);
@@ -699,19 +708,17 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
 // X of slice it, so the Q / dO ring has 4 slots (DMA two slices ahead into the slot of slice it - 2).
 // The DMA is inline asm (common.h lds_dma16) and counted with explicit vmcnt waits.  Slice 0's X runs
 // its 16 MFMAs on zero P / dS carried from "slice -1" (exact: K rows x 0 adds 0).
-FTC_DEV void lds_dma4(__amdgpu_buffer_rsrc_t r, const void* lds, int voff, int soff) {
-  const unsigned dst = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)lds;
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-      "buffer_load_dword %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(r), "s"(dst), "s"(soff)
-      : "memory");
-}
 
 #ifndef IL_TV2
 #define IL_TV2 1
+#endif
+// timing-only ablations of the stamp build (tools/stamp_dkdv.hip -DIL_DIAG=N; wrong results): 1 no softmax
+// VALU in X / Y, 2 no transposed reads in X / Y, 3 no fragment reads in A, 4 = 3 + no row-constant loads /
+// masks, 5 = 4 + no A MFMAs
+#if defined(FTC_STAMPS) && defined(IL_DIAG)
+constexpr int kIlDiag = IL_DIAG;
+#else
+constexpr int kIlDiag = 0;
 #endif
 #ifndef IL_PIPE
 #define IL_PIPE 1
@@ -772,11 +779,16 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_il_kernel(BwdArgs a) {
   int qend = S;
   if (a.window > 0) qend = min(S, kv0 + BKV - 1 + a.window);
   int dmin[2] = {0x3fffffff, 0x3fffffff};
+  // the lane's own keys' document ends, loaded once: a global load inside the loop's mask branch made
+  // the compiler drain every in-flight DMA (vmcnt(0)) at the branch join on every slice
+  int dend[2] = {0x40000000, 0x40000000};
   const int* de_row = a.doc_end ? a.doc_end + (long long)b * S : nullptr;
   if (de_row) {
     qend = min(qend, de_row[kv0 + BKV - 1]);
     dmin[0] = de_row[wkey0];
     dmin[1] = de_row[wkey0 + 32];
+    dend[0] = de_row[wkey0 + lr];
+    dend[1] = de_row[wkey0 + 32 + lr];
   }
   qbeg = (qbeg / BQ2) * BQ2;
   const int nqt = (qend - qbeg + BQ2 - 1) / BQ2;
@@ -795,9 +807,16 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_il_kernel(BwdArgs a) {
   }
   const int cvo = (lr + (hh ? 0 : a.B * a.H * S)) * 4;  // lanes 0-31: -lse/scale rows, 32-63: -delta rows
   auto slot = [&](int it_) __attribute__((always_inline)) -> char* { return ring + (it_ & 3) * SLICE; };
+  // slices in order it = g nqt + i (query head g of the group, 32-row block i): the DMA cursor walks them
+  // with counters (no integer division per slice)
+  int dg = 0, di = 0;
   auto issue = [&](int it_) __attribute__((always_inline)) {
-    const int g_ = it_ / nqt, qt_ = qbeg + (it_ % nqt) * BQ2;
-    const int hq_ = kvh * G + g_;
+    const int qt_ = qbeg + di * BQ2;
+    const int hq_ = kvh * G + dg;
+    if (++di == nqt) {
+      di = 0;
+      ++dg;
+    }
     char* base = slot(it_);
     const int qso = (hq_ * D + qt_ * (int)a.q_rs) * 2, dso = (hq_ * D + qt_ * (int)a.do_rs) * 2;
 #pragma unroll
@@ -837,6 +856,7 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_il_kernel(BwdArgs a) {
   // exponential: gap g computes P_g = exp2(c S_g) and dS_(g-1) = P_(g-1) dP'_(g-1); P's first 8 elements
   // pack in gap 8, dS's in gap 9; the tail (dS_15, the second packs) follows the region's last MFMA
   auto b1_gap = [&](int j, int g, bf16x8* pbo, bf16x8* sbo) __attribute__((always_inline)) {
+    if (kIlDiag == 1) return;
     if (!IL_PIPE) {  // unpipelined: P and dS of element g in gap g, packs after elements 7 / 15
       if (g < 16) {
         const float p = __builtin_amdgcn_exp2f(a.c * s[j][g]);
@@ -874,6 +894,7 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_il_kernel(BwdArgs a) {
   bf16x8 tv[2][4];
   constexpr int TVM = IL_TV2 ? 1 : 0;
   auto tr_op = [&](const char* Qs, int dt, int m) __attribute__((always_inline)) {
+    if (kIlDiag == 2) return;
     tv[dt & TVM][m] = tr_read<D>((m < 2 ? Qs + QBYTES : Qs), 16 * (m & 1), to[dt]);
   };
   // B2 of half j on d tile dt, MFMA m (0..3) of its four.  The dV / dK accumulators (256 registers) are
@@ -936,6 +957,7 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_il_kernel(BwdArgs a) {
   do {                \
   } while (0)
 #endif
+  int ci = 0;  // 32-row block of the current slice
   for (int it = 0; it < total; ++it) {
     IL_SEG_START();
     // ---- sync: slice it landed (it + 1 may fly), every wave is past slice it - 1's Y; DMA it + 2
@@ -956,19 +978,27 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_il_kernel(BwdArgs a) {
       // registers an in-flight MFMA would still be reading as C); masks (diagonal / window / document
       // slices, wave-uniform branches) put -inf into S's start values, so P = exp2(c S) = 0 and dS = 0
       const float* cst = reinterpret_cast<const float*>(Qs + 2 * QBYTES);
-      auto ld_const = [&](f32x16& t, const float* src) __attribute__((always_inline)) {
+      // a second, opaque copy of the address: the S / dP' chains of both halves get their own LDS reads
+      // of the row constants (4 ds_read each) instead of one read + 32 v_mov copies
+      typedef __attribute__((address_space(3))) const float lds_f32;
+      unsigned cst_off = (unsigned)(uintptr_t)(lds_f32*)cst;  // (an opaque generic pointer would turn into
+      asm volatile("" : "+v"(cst_off));                      //  flat loads, counted by vmcnt: DMA drain)
+      lds_f32* cst_b = (lds_f32*)(uintptr_t)cst_off;
+      auto ld_const = [&](f32x16& t, auto src) __attribute__((always_inline)) {
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-          const float4 v4 = *reinterpret_cast<const float4*>(src + 8 * g4 + 4 * hh);
-          t[4 * g4 + 0] = v4.x; t[4 * g4 + 1] = v4.y; t[4 * g4 + 2] = v4.z; t[4 * g4 + 3] = v4.w;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) t[4 * g4 + e] = src[8 * g4 + 4 * hh + e];
         }
       };
-      ld_const(s[0], cst);
-      ld_const(s[1], cst);
-      ld_const(dp[0], cst + BQ2);
-      ld_const(dp[1], cst + BQ2);
-      {
-        const int qt = qbeg + (it % nqt) * BQ2;
+      if (kIlDiag < 4) {
+        ld_const(s[0], (lds_f32*)cst);
+        ld_const(dp[0], (lds_f32*)cst + BQ2);
+        ld_const(s[1], cst_b);
+        ld_const(dp[1], cst_b + BQ2);
+      }
+      if (kIlDiag < 4) {
+        const int qt = qbeg + ci * BQ2;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int kmin = wkey0 + 32 * j;
@@ -978,8 +1008,7 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_il_kernel(BwdArgs a) {
             const int key = kmin + lr;
             const int base = qt + 4 * hh;
             const int lo = (a.causal ? key : -0x3fffffff) - base;
-            const int dend = de_row ? de_row[key] : 0x40000000;
-            const int hi = min(a.window > 0 ? key + a.window - 1 : 0x3fffffff, dend - 1) - base;
+            const int hi = min(a.window > 0 ? key + a.window - 1 : 0x3fffffff, dend[j] - 1) - base;
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
               const int off = (i & 3) + 8 * (i >> 2);
@@ -991,6 +1020,7 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_il_kernel(BwdArgs a) {
       // k-step fragments [qa, da, k0, k1], double-buffered: k-step st + 1 is read under k-step st's MFMAs
       u32x4 fr[2][4];
       auto rd = [&](int st) __attribute__((always_inline)) {
+        if (kIlDiag >= 3 && st > 0) return;
         fr[st & 1][0] = *reinterpret_cast<const u32x4*>(Qs + lds_off<D>(lr, 2 * st + hh));
         fr[st & 1][1] = *reinterpret_cast<const u32x4*>(Ds + lds_off<D>(lr, 2 * st + hh));
         fr[st & 1][2] = *reinterpret_cast<const u32x4*>(Ks + lds_off<D>(wave * 64 + lr, 2 * st + hh));
@@ -1008,7 +1038,9 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_il_kernel(BwdArgs a) {
           const bf16x8 bop = m == 0 ? __builtin_bit_cast(bf16x8, f[2]) : m == 1 ? __builtin_bit_cast(bf16x8, f[3]) : vf[m - 2][st];
           f32x16& acc = m == 0 ? s[0] : m == 1 ? s[1] : m == 2 ? dp[0] : dp[1];
           // (s_nop 1 at k-step 0: the start values may come from the mask's VALU selects)
-          if (st == 0)
+          if (kIlDiag == 5)
+            asm volatile("" : "+v"(acc) : "v"(m < 2 ? qa : da), "v"(bop));
+          else if (st == 0)
             asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(m < 2 ? qa : da), "v"(bop));
           else
             asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(m < 2 ? qa : da), "v"(bop));
@@ -1031,6 +1063,7 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_il_kernel(BwdArgs a) {
     IL_SEG_END(2);
     region(0, Qs, pb0, sb0, 1, pbc, sbc, nullptr);
     IL_SEG_END(3);
+    if (++ci == nqt) ci = 0;
   }
 #ifdef FTC_STAMPS
   if (stamping) {
