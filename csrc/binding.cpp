@@ -58,7 +58,6 @@ int ftc_adamw(void* param_bf16, float* master, float* m, float* v, const void* g
 int ftc_sumsq_partials();
 int ftc_sumsq(const void* x, int is_fp32, long long n, float* partial, float* out, float* coef, float max_norm,
               float scale, hipStream_t stream);
-void ftc_flash_fwd_config(int qb);
 void ftc_flash_dkdv_config(int waves);
 int ftc_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H, int KV, int D,
                   long long q_row_stride, long long kv_row_stride, long long o_row_stride, float scale, int causal,
@@ -860,7 +859,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_nt_ok", &gemm_nt_ok);
   m.def("gemm_nt_rope_", &gemm_nt_rope_, py::arg("c"), py::arg("a"), py::arg("b"), py::arg("cos"), py::arg("sin"),
         py::arg("positions"), py::arg("seq_len"), py::arg("rot_heads"));
-  m.def("flash_fwd_config", [](int64_t qb) { ftc_flash_fwd_config((int)qb); }, py::arg("qb"));
   m.def("flash_dkdv_config", [](int64_t waves) { ftc_flash_dkdv_config((int)waves); }, py::arg("waves"));
   m.def("gemm_nt_config", &gemm_nt_config, py::arg("grid_cap"), py::arg("group"), py::arg("xcc"), py::arg("nt_store"),
         py::arg("load_policy") = 0);

@@ -714,7 +714,7 @@ __global__ __launch_bounds__(64 * (8 / HW), 1) void bwd_dkdv_kernel(BwdArgs a) {
 #endif
 // timing-only ablations of the stamp build (tools/stamp_dkdv.hip -DIL_DIAG=N; wrong results): 1 no softmax
 // VALU in X / Y, 2 no transposed reads in X / Y, 3 no fragment reads in A, 4 = 3 + no row-constant loads /
-// masks, 5 = 4 + no A MFMAs
+// masks, 5 = 4 + no A MFMAs, 6 = 3 + no masks, 7 = 3 + no row-constant loads
 #if defined(FTC_STAMPS) && defined(IL_DIAG)
 constexpr int kIlDiag = IL_DIAG;
 #else
@@ -991,13 +991,13 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_il_kernel(BwdArgs a) {
           for (int e = 0; e < 4; ++e) t[4 * g4 + e] = src[8 * g4 + 4 * hh + e];
         }
       };
-      if (kIlDiag < 4) {
+      if (kIlDiag < 4 || kIlDiag == 6) {
         ld_const(s[0], (lds_f32*)cst);
         ld_const(dp[0], (lds_f32*)cst + BQ2);
         ld_const(s[1], cst_b);
         ld_const(dp[1], cst_b + BQ2);
       }
-      if (kIlDiag < 4) {
+      if (kIlDiag < 4 || kIlDiag == 7) {
         const int qt = qbeg + ci * BQ2;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -1020,7 +1020,7 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_il_kernel(BwdArgs a) {
       // k-step fragments [qa, da, k0, k1], double-buffered: k-step st + 1 is read under k-step st's MFMAs
       u32x4 fr[2][4];
       auto rd = [&](int st) __attribute__((always_inline)) {
-        if (kIlDiag >= 3 && st > 0) return;
+        if (kIlDiag >= 3 && st > 0) return;  // (6, 7: as 3)
         fr[st & 1][0] = *reinterpret_cast<const u32x4*>(Qs + lds_off<D>(lr, 2 * st + hh));
         fr[st & 1][1] = *reinterpret_cast<const u32x4*>(Ds + lds_off<D>(lr, 2 * st + hh));
         fr[st & 1][2] = *reinterpret_cast<const u32x4*>(Ks + lds_off<D>(wave * 64 + lr, 2 * st + hh));

@@ -445,372 +445,22 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
   }
 }
 
-// ---- QB2: two 32-row query blocks per wave, one wave per SIMD (round 4) -------------------------------
-// 4 waves x 64 rows = 256 query rows per workgroup, one workgroup per CU (512-register budget).  Every K
-// fragment and V^T fragment read from LDS feeds BOTH blocks (half the LDS read bytes per FLOP), and the
-// two blocks' independent chains let one wave overlap its own softmax VALU with matrix work (no partner
-// wave on the SIMD): per tile the program order is
-//     A0 (S of block 0)  |  m0  |  A1 (S of block 1) x P0 (exp / row sum / pack of block 0)
-//                        |  m1  |  PV0 x P1  |  PV1
-// where m = mask + row max + deferred rescale (branches: between the interleaved regions) and "x" = one
-// two-element exp chunk after every MFMA, placed by sched_barrier fences (a sched_group_barrier pattern
-// left the compiler clustering all 32 exponentials ahead of the MFMAs); the V^T reads are A0's fillers.  K / V tiles
-// arrive by LDS-DMA two tiles ahead into a 3-slot ring (counted vmcnt, one barrier per tile); a wave
-// past its last visible tile (causal diagonal) keeps joining the DMA / barrier only.
-template <int D>
-__global__ __launch_bounds__(256, 1) void flash_fwd_qb2_kernel(FwdArgs a) {
-  constexpr int QB = 2, BQ = 32 * QB * WAVES;
-  constexpr int NCH = D / 8, DSTEPS = D / 16, DT = D / 32;
-  constexpr int TILE_BYTES = BK * D * 2;
-  constexpr int NGT = TILE_BYTES / 1024 / WAVES;
-  constexpr int RPG = 1024 / (D * 2);
-  constexpr int PER_TILE = 2 * NGT;  // DMA instructions per wave per tile
-  static_assert(NGT >= 1, "tile too small for the wave count");
-  __shared__ __attribute__((aligned(16))) char K0[TILE_BYTES];
-  __shared__ __attribute__((aligned(16))) char V0[TILE_BYTES];
-  __shared__ __attribute__((aligned(16))) char K1[TILE_BYTES];
-  __shared__ __attribute__((aligned(16))) char V1[TILE_BYTES];
-  __shared__ __attribute__((aligned(16))) char K2[TILE_BYTES];
-  __shared__ __attribute__((aligned(16))) char V2[TILE_BYTES];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int hh = lane >> 5, lr = lane & 31;
-  int qb, b, hq, kvh;
-  decode_block(a, qb, b, hq, kvh);
-  const int S = a.S;
-  const int q0 = qb * BQ;
-  const int wq0 = q0 + wave * 64;  // this wave's first row; block j = rows wq0 + 32 j + [0, 32)
-  int qrow[QB];
-  bool qvalid[QB];
-#pragma unroll
-  for (int j = 0; j < QB; ++j) {
-    qrow[j] = wq0 + 32 * j + lr;
-    qvalid[j] = qrow[j] < S;
-  }
-
-  bf16x8 qf[QB][DSTEPS];
-#pragma unroll
-  for (int j = 0; j < QB; ++j) {
-    const uint16_t* qp = a.q + ((long long)b * S + (qvalid[j] ? qrow[j] : 0)) * a.q_rs + (long long)hq * D + 8 * hh;
-#pragma unroll
-    for (int s2 = 0; s2 < DSTEPS; ++s2) {
-      uint4 v = qvalid[j] ? *reinterpret_cast<const uint4*>(qp + 16 * s2) : make_uint4(0, 0, 0, 0);
-      qf[j][s2] = as_bf8(v);
-    }
-  }
-
-  // ---- key range: the workgroup's (DMA / barriers) and this wave's (compute)
-  const int q_last = min(S, q0 + BQ) - 1;
-  const int kv_end = min(a.causal ? q_last + 1 : S, a.kv_valid);
-  int kv_begin = 0;
-  if (a.window > 0) kv_begin = (max(0, q0 - a.window + 1) / BK) * BK;
-  int dlo[QB], wdmax[QB];
-#pragma unroll
-  for (int j = 0; j < QB; ++j) dlo[j] = wdmax[j] = -0x3fffffff;
-  if (a.doc_start) {
-    const int* ds = a.doc_start + (long long)b * S;
-#pragma unroll
-    for (int j = 0; j < QB; ++j) {
-      dlo[j] = ds[qvalid[j] ? qrow[j] : S - 1];
-      wdmax[j] = ds[min(S - 1, wq0 + 32 * j + 31)];
-    }
-    kv_begin = max(kv_begin, (ds[q0] / BK) * BK);
-  }
-  const int ntiles = kv_end > kv_begin ? (kv_end - kv_begin + BK - 1) / BK : 0;
-  const int w_end = min(a.causal ? min(S, wq0 + 64) : S, a.kv_valid);  // keys this wave can see end here
-  const int wtiles = w_end > kv_begin ? min(ntiles, (w_end - kv_begin + BK - 1) / BK) : 0;
-
-  const uint16_t* kbase = a.k + (long long)b * S * a.kv_rs + (long long)kvh * D;
-  const uint16_t* vbase = a.v + (long long)b * S * a.kv_rs + (long long)kvh * D;
-  const auto krs = make_rsrc(kbase), vrs = make_rsrc(vbase);
-  int voff[NGT];
-#pragma unroll
-  for (int i = 0; i < NGT; ++i) {
-    const int row = (wave * NGT + i) * RPG + lane / NCH, pc = lane % NCH;
-    voff[i] = (row * (int)a.kv_rs + ((pc ^ swz(row)) & (NCH - 1)) * 8) * 2;
-  }
-
-  f32x16 o[QB][DT];
-#pragma unroll
-  for (int j = 0; j < QB; ++j)
-#pragma unroll
-    for (int t = 0; t < DT; ++t)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) o[j][t][i] = 0.f;
-  float m[QB] = {-INFINITY, -INFINITY}, l[QB] = {0.f, 0.f};
-  const float c = a.scale_log2;
-
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // Q fragments (plain loads) retired before any DMA: vmcnt(0)
-  // the DMA as inline asm (common.h lds_dma16): the compiler's own waits would otherwise treat every
-  // later LDS read as possibly aliasing the in-flight tile and drain it (vmcnt) ahead of the V^T reads;
-  // the counted waits below are the only ones the pipeline needs
-  auto dma = [&](int t, char* Kd, char* Vd) __attribute__((always_inline)) {
-    const int toff = (kv_begin + t * BK) * (int)a.kv_rs * 2;
-#pragma unroll
-    for (int i = 0; i < NGT; ++i) {
-      const int r0 = (wave * NGT + i) * RPG;
-      lds_dma16(krs, Kd + r0 * D * 2, voff[i], toff);
-      lds_dma16(vrs, Vd + r0 * D * 2, voff[i], toff);
-    }
-  };
-  // prologue: tiles 0 and 1 in flight (a missing tile is replaced by a repeat of tile 0 into its slot,
-  // so every wave always has the same number of DMA instructions outstanding)
-  if (ntiles > 0) {
-    dma(0, K0, V0);
-    dma(ntiles > 1 ? 1 : 0, K1, V1);
-  }
-
-  const int gi = lane >> 4, li = lane & 15;
-  const int trq = li >> 2, trp = li & 3;
-  int vto[DT][2];
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt) {
-    const int col = dt * 32 + 16 * (gi & 1) + 4 * trp;
-    const int chunk = col >> 3, half8 = (col & 7) ? 8 : 0;
-    vto[dt][0] = lds_off<D>(4 * hh + trq, chunk) + half8;
-    vto[dt][1] = lds_off<D>(4 * hh + trq + 8, chunk) + half8;
-  }
-
-  f32x16 s[QB][2];
-  bf16x8 pf[QB][4];
-  uint4 kf[2][DSTEPS];
-  s16x4 vt[DT][8];
-
-  // mask + row max + deferred rescale of block j (branches; before its interleaved exp region)
-  auto rowmax = [&](int j, int t) __attribute__((always_inline)) -> float {
-    const int kv0 = kv_begin + t * BK;
-    const int qmin = wq0 + 32 * j;
-    const bool need_mask = (a.causal && kv0 + BK - 1 > qmin) || (a.window > 0 && qmin + 31 - kv0 >= a.window) ||
-                           kv0 + BK > a.kv_valid || kv0 < wdmax[j];
-    if (need_mask) {
-      const int base = kv0 + 4 * hh;
-      const int hi = min(a.causal ? qrow[j] : 0x3fffffff, a.kv_valid - 1) - base;
-      const int lo = max(a.window > 0 ? qrow[j] - a.window + 1 : -0x3fffffff, dlo[j]) - base;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int off = kt * 32 + (i & 3) + 8 * (i >> 2);
-          s[j][kt][i] = (off >= lo && off <= hi) ? s[j][kt][i] : -INFINITY;
-        }
-    }
-    float mt = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[j][kt][i]);
-    mt = xhalf_max(mt) * c;
-    if (__builtin_amdgcn_ballot_w64(mt > m[j] + 8.0f) != 0) {
-      const float mn = fmaxf(m[j], mt);
-      const float alpha = __builtin_amdgcn_exp2f(m[j] - ((mn == -INFINITY) ? 0.f : mn));
-      m[j] = mn;
-      l[j] *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[j][dt][i] *= alpha;
-    }
-    return (m[j] == -INFINITY) ? 0.f : m[j];
-  };
-  // exponentials / row sum / bf16 packing of block j in 16 chunks of two elements (element e = 16 kt + i of
-  // s[j]); chunk idx packs P fragment ks once its 8 elements are done
-  float rs[QB] = {0.f, 0.f};
-  auto exp_chunk = [&](int j, int idx, float mref) __attribute__((always_inline)) {
-#pragma unroll
-    for (int e = 2 * idx; e < 2 * idx + 2; ++e) {
-      const int kt = e >> 4, i = e & 15;
-      const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[j][kt][i], c, -mref));
-      s[j][kt][i] = pv;
-      rs[j] += pv;
-      asm volatile("" ::"v"(pv));  // pin: pure arithmetic would otherwise sink past the fences (IR level)
-    }
-    if ((idx & 3) == 3) pf[j][idx >> 2] = pack_p(s[j][idx >> 3], 8 * ((idx >> 2) & 1));
-  };
-  auto fence = []() __attribute__((always_inline)) { __builtin_amdgcn_sched_barrier(0); };
-  auto mfma_s = [&](int j, int kt, int st, f32x16& acc) __attribute__((always_inline)) {
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(kf[kt][st]), qf[j][st], acc, 0, 0, 0);
-  };
-  auto mfma_pv = [&](int j, int dt, int ks) __attribute__((always_inline)) {
-    const s16x4 v1 = vt[dt][2 * ks], v2 = vt[dt][2 * ks + 1];
-    s16x8 va = {v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
-    o[j][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, va), pf[j][ks], o[j][dt], 0, 0, 0);
-  };
-  auto read_vt = [&](const char* Vc, int r) __attribute__((always_inline)) {  // transposed V read r of 8 * DT
-    const int dt = r >> 3, q = r & 7, ks = q >> 1;
-    vt[dt][q] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(Vc + vto[dt][q & 1] + ks * 16 * D * 2));
-  };
-
-  // one tile, hand-interleaved (sched_barrier fences fix the order the compiler would otherwise cluster):
-  //   A0: S of block 0; K fragments of 32-key half 1 read under half 0's MFMAs, V^T d-tile 0 under half 1's
-  //   mask / max / rescale of block 0
-  //   A1: S of block 1, one exp chunk of block 0 after every MFMA
-  //   mask / max / rescale of block 1
-  //   PV0: O0 += V^T P0, per d tile dt: an exp chunk of block 1 and the V^T reads of d tile dt + 1
-  //   PV1: O1 += V^T P1 (every V^T fragment already in registers)
-  auto compute = [&](const int t, const char* Kc, const char* Vc) __attribute__((always_inline)) {
-    auto read_k = [&](int kt, int st) __attribute__((always_inline)) {
-      kf[kt][st] = *reinterpret_cast<const uint4*>(Kc + lds_off<D>(kt * 32 + lr, 2 * st + hh));
-    };
-#pragma unroll
-    for (int st = 0; st < DSTEPS; ++st) read_k(0, st);
-    constexpr int RV = 8 / DSTEPS;  // V^T reads per A0 half-1 MFMA (d tile 0: 8 reads)
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      f32x16 acc;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-#pragma unroll
-      for (int st = 0; st < DSTEPS; ++st) {
-        mfma_s(0, kt, st, acc);
-        fence();
-        if (kt == 0) {
-          read_k(1, st);
-        } else {
-#pragma unroll
-          for (int r = st * RV; r < (st + 1) * RV; ++r) read_vt(Vc, r);
-        }
-        fence();
-      }
-      s[0][kt] = acc;
-    }
-    const float mref0 = rowmax(0, t);
-    rs[0] = 0.f;
-    fence();
-    constexpr int NS = 2 * DSTEPS;  // S MFMAs per block
-    constexpr int CH = 16 / NS;     // exp chunks per S MFMA (D = 128: 1; D = 64: 2)
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      f32x16 acc;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-#pragma unroll
-      for (int st = 0; st < DSTEPS; ++st) {
-        mfma_s(1, kt, st, acc);
-        fence();
-#pragma unroll
-        for (int c2 = 0; c2 < CH; ++c2) exp_chunk(0, (kt * DSTEPS + st) * CH + c2, mref0);
-        fence();
-      }
-      s[1][kt] = acc;
-    }
-    l[0] += rs[0];
-    const float mref1 = rowmax(1, t);
-    rs[1] = 0.f;
-    fence();
-    constexpr int NP = 4 * DT;   // PV MFMAs per block
-    constexpr int CP = 16 / NP;  // exp chunks per PV MFMA (D = 128: 1; D = 64: 2)
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        mfma_pv(0, dt, ks);
-        fence();
-#pragma unroll
-        for (int c2 = 0; c2 < CP; ++c2) exp_chunk(1, (dt * 4 + ks) * CP + c2, mref1);
-        if (dt + 1 < DT) {
-          read_vt(Vc, 8 * (dt + 1) + 2 * ks);
-          read_vt(Vc, 8 * (dt + 1) + 2 * ks + 1);
-        }
-        fence();
-      }
-    l[1] += rs[1];
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) mfma_pv(1, dt, ks);
-  };
-  // tile t: wait for it (tile t+1 may still fly: vmcnt(PER_TILE)), barrier, DMA tile t+2 into the slot
-  // tile t-1 used; compute when this wave sees tile t
-  auto tile = [&](const int t, const char* Kc, const char* Vc, char* Kn, char* Vn) __attribute__((always_inline)) {
-    __builtin_amdgcn_s_waitcnt(0x0F70 | (PER_TILE & 15) | ((PER_TILE >> 4) << 14));
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
-    dma(t + 2 < ntiles ? t + 2 : 0, Kn, Vn);  // past the end: a repeat into a slot nobody reads again
-    if (t < wtiles) compute(t, Kc, Vc);
-  };
-  for (int t = 0; t < ntiles; t += 3) {
-    tile(t, K0, V0, K2, V2);
-    if (t + 1 < ntiles) tile(t + 1, K1, V1, K0, V0);
-    if (t + 2 < ntiles) tile(t + 2, K2, V2, K1, V1);
-  }
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // no LDS-DMA may outlive the workgroup
-
-  // ---- epilogue per block: normalise, store O (bf16, 16-byte stores) and LSE (natural log)
-#pragma unroll
-  for (int j = 0; j < QB; ++j) {
-    const float ltot = l[j] + __shfl_xor(l[j], 32, 64);
-    const float inv = ltot > 0.f ? 1.0f / ltot : 0.f;
-    uint16_t* op = a.o + ((long long)b * S + (qvalid[j] ? qrow[j] : 0)) * a.o_rs + (long long)hq * D;
-    if ((a.o_rs & 7) == 0) {
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        uint32_t w[4][2];
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          w[g4][0] = pack_bf2(o[j][dt][4 * g4 + 0] * inv, o[j][dt][4 * g4 + 1] * inv);
-          w[g4][1] = pack_bf2(o[j][dt][4 * g4 + 2] * inv, o[j][dt][4 * g4 + 3] * inv);
-        }
-        const auto a0 = __builtin_amdgcn_permlane32_swap(w[0][0], w[2][0], false, false);
-        const auto a1 = __builtin_amdgcn_permlane32_swap(w[0][1], w[2][1], false, false);
-        const auto b0 = __builtin_amdgcn_permlane32_swap(w[1][0], w[3][0], false, false);
-        const auto b1 = __builtin_amdgcn_permlane32_swap(w[1][1], w[3][1], false, false);
-        if (qvalid[j]) {
-          const int d = dt * 32 + 16 * hh;
-          *reinterpret_cast<uint4*>(op + d) = make_uint4(a0[0], a1[0], a0[1], a1[1]);
-          *reinterpret_cast<uint4*>(op + d + 8) = make_uint4(b0[0], b1[0], b0[1], b1[1]);
-        }
-      }
-    } else if (qvalid[j]) {
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          uint2 w;
-          w.x = pack_bf2(o[j][dt][4 * g4 + 0] * inv, o[j][dt][4 * g4 + 1] * inv);
-          w.y = pack_bf2(o[j][dt][4 * g4 + 2] * inv, o[j][dt][4 * g4 + 3] * inv);
-          *reinterpret_cast<uint2*>(op + dt * 32 + 8 * g4 + 4 * hh) = w;
-        }
-    }
-    if (qvalid[j] && hh == 0) {
-      const float lse2 = (m[j] == -INFINITY) ? -INFINITY : m[j] + __log2f(ltot);
-      a.lse[((long long)b * a.H + hq) * S + qrow[j]] = lse2 * LN2;
-    }
-  }
-}
-
 }  // namespace
 
-// Forward variant of every later call: 1 = 32 query rows per wave (two workgroups per CU), 2 = two 32-row
-// blocks per wave (one workgroup per CU); tests and tools/bench_attention.py switch it in one process.
-namespace {
-int& fwd_qb() {
-  static int v = [] {
-    const char* e = getenv("FTC_FLASH_FWD_QB");
-    return (e && e[0] == '2') ? 2 : 1;
-  }();
-  return v;
-}
-}  // namespace
-
-extern "C" void ftc_flash_fwd_config(int qb) { fwd_qb() = qb == 2 ? 2 : 1; }
+// (Removed in round 4: QB2 -- two 32-row query blocks per wave, one wave per SIMD, the softmax of one
+// block fenced between the other block's MFMAs, asm-DMA 3-slot ring: 0.740 vs 0.554 ms at the Llama-3-8B
+// layer, profiles/r4/attn/fwd_qb6.log; git history has the kernel.)
 
 extern "C" int ftc_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H,
                              int KV, int D, long long q_rs, long long kv_rs, long long o_rs, float scale, int causal,
                              int window, const int* doc_start, int kv_valid, hipStream_t stream) {
   if (S % BK != 0 || H % KV != 0 || (D != 128 && D != 64)) return -1;
   if (kv_valid <= 0 || kv_valid > S) kv_valid = S;
-  const int qb = fwd_qb();
-  const int BQ = 32 * 4 * qb;
+  constexpr int BQ = 32 * WAVES;
   FwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, q_rs, kv_rs, o_rs,
             B, S, H, KV, (S + BQ - 1) / BQ, scale * LOG2E, causal, window, doc_start, kv_valid};
   const int nblocks = a.nqb * B * H;
-  if (qb == 2) {
-    if (D == 128)
-      hipLaunchKernelGGL((flash_fwd_qb2_kernel<128>), dim3(nblocks), dim3(256), 0, stream, a);
-    else
-      hipLaunchKernelGGL((flash_fwd_qb2_kernel<64>), dim3(nblocks), dim3(256), 0, stream, a);
-  } else if (D == 128) {
+  if (D == 128) {
     hipLaunchKernelGGL((flash_fwd_kernel<128>), dim3(nblocks), dim3(256), 0, stream, a);
   } else {
     hipLaunchKernelGGL((flash_fwd_kernel<64>), dim3(nblocks), dim3(256), 0, stream, a);

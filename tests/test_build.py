@@ -26,7 +26,7 @@ def test_extension_has_no_diagnostic_hooks():
     # one production projection-GEMM kernel template (bf16 / fp32 C x epilogue x store policy x beta)
     assert "gemm_nt_kernel<" in syms
     for old in ("gemm_nt_v5_kernel", "gemm_nt_w4d_kernel", "gemm_nt_pb_kernel", "gemm_nt_pp_kernel",
-                "flash_fwd_pipe_kernel"):
+                "flash_fwd_pipe_kernel", "flash_fwd_qb2_kernel"):
         assert old not in syms, old
 
 

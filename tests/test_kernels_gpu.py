@@ -428,15 +428,12 @@ def test_lora_merge(C):
     torch.testing.assert_close(W.float(), ref, atol=3e-2, rtol=1e-2)
 
 
-@pytest.fixture(params=[(1, 8), (2, 8), (1, 1)], ids=["qb1", "qb2", "il"])
-def fwd_qb(C, request):
-    """The flash variants: forward with 32 query rows per wave (two workgroups per CU) or two 32-row blocks
-    per wave (one workgroup per CU, csrc/kernels/flash_attn_fwd.hip QB2); dK/dV with 8 waves x 32 keys
-    (ping-pong) or the interleaved 4 waves x 64 keys (flash_attn_bwd.hip IL, head_dim 128)."""
-    C.flash_fwd_config(request.param[0])
-    C.flash_dkdv_config(request.param[1])
-    yield request.param[0]
-    C.flash_fwd_config(1)
+@pytest.fixture(params=[8, 1], ids=["dkdv8", "il"])
+def dkdv_variant(C, request):
+    """The dK/dV variants: 8 waves x 32 keys (ping-pong, the default) and the interleaved 4 waves x 64 keys
+    (csrc/kernels/flash_attn_bwd.hip IL, head_dim 128; other head dims take the 4-wave kernel)."""
+    C.flash_dkdv_config(request.param)
+    yield request.param
     C.flash_dkdv_config(8)
 
 
@@ -450,7 +447,7 @@ def fwd_qb(C, request):
     (1, 512, 8, 2, 64, False, 0),
     (1, 768, 8, 4, 64, True, 320),
 ])
-def test_flash_attention_fwd_bwd(C, fwd_qb, B, S, H, KV, D, causal, window):
+def test_flash_attention_fwd_bwd(C, dkdv_variant, B, S, H, KV, D, causal, window):
     from finetune_controller_amd.ops.attention import _FlashPacked, attention_reference
 
     torch.manual_seed(0)
@@ -571,7 +568,7 @@ def test_llama_rope_grad_handoff(C, monkeypatch, method):
     (2, 700, 4, 2, 128, 0, True),
 ])
 @pytest.mark.parametrize("causal", [True, False])
-def test_flash_tail_lengths(C, fwd_qb, B, S, H, KV, D, window, docs, causal):
+def test_flash_tail_lengths(C, dkdv_variant, B, S, H, KV, D, window, docs, causal):
     """S not a multiple of the 256-row tile: attention_packed takes the tail-padded flash path (not
     SDPA) and matches the fp32 reference, forward and backward -- causal (pads never visible) and
     non-causal (pad keys masked in the kernels through kv_valid)."""
@@ -612,7 +609,7 @@ def test_flash_tail_lengths(C, fwd_qb, B, S, H, KV, D, window, docs, causal):
     (2, 300, 4, 2, 96, 0, False),
     (1, 256, 4, 2, 32, 0, True),
 ])
-def test_flash_head_dim_padded(C, fwd_qb, B, S, H, KV, D, window, causal):
+def test_flash_head_dim_padded(C, dkdv_variant, B, S, H, KV, D, window, causal):
     """head_dim outside the kernels' {64, 128} (80 / 96 / 112 / 32): attention_packed zero-pads every head
     to the next kernel head_dim and runs the flash kernels (not SDPA), forward and backward equal to the
     fp32 reference at the real D's softmax scale."""
@@ -638,7 +635,7 @@ def test_flash_head_dim_padded(C, fwd_qb, B, S, H, KV, D, window, causal):
         assert rel < 1.5e-2, (lo, rel)
 
 
-def test_flash_lse(C, fwd_qb):
+def test_flash_lse(C, dkdv_variant):
     torch.manual_seed(1)
     B, S, H, KV, D = 1, 256, 4, 2, 128
     qkv = bf(torch.randn(B * S, (H + 2 * KV) * D, device=DEV))
@@ -1163,7 +1160,7 @@ def _doc_ids(B, S, lens_per_row, eos=2):
 
 
 @pytest.mark.parametrize("D,H,KV,window", [(128, 8, 2, 0), (64, 8, 2, 0), (128, 4, 4, 200), (64, 4, 2, 0)])
-def test_flash_attention_packed_documents(C, fwd_qb, D, H, KV, window):
+def test_flash_attention_packed_documents(C, dkdv_variant, D, H, KV, window):
     """Document-masked flash attention (doc_start / doc_end bounds, tile skipping, boundary masks)
     against the fp32 reference: documents shorter than a tile, spanning several 256-key blocks, and a
     row that is one document."""
