@@ -158,6 +158,13 @@ class _Prefetch:
         self.pending: dict = {}    # key -> event of a prefetched decode
         self.stream = None
         self.device = None
+        self.stats = {"passes": 0, "prefetched": 0, "hits": 0, "inline": 0, "deviations": 0}
+
+    def reset(self) -> None:
+        """Forget the recorded plan (its closures hold the model's scratch and adapter tensors)."""
+        if self.stream is not None and self.device is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
+        self.order, self.rec, self.pending, self.pos, self.ok = [], [], {}, 0, True
 
     def begin_pass(self, device) -> None:
         if not self.enabled or not torch.cuda.is_available() or device.type != "cuda":
@@ -171,6 +178,7 @@ class _Prefetch:
             self.rec = []  # the last pass deviated: record again
         self.pos, self.ok = 0, True
         self.device = device
+        self.stats["passes"] += 1
 
     def decode(self, key, buf, fn) -> None:
         """Make the operand ``key`` (written into scratch ``buf`` by ``fn()``) ready on the current stream."""
@@ -183,15 +191,22 @@ class _Prefetch:
             fn()
             return
         if not (self.ok and self.pos < len(self.order) and self.order[self.pos][0] == key):
-            if self.ok and self.stream is not None:
-                main.wait_stream(self.stream)
+            if self.ok:
+                self.stats["deviations"] += 1
+                if self.stream is not None:
+                    main.wait_stream(self.stream)
+                self.pending.clear()
+                self.order = []  # re-recorded by the next pass; drop the stale closures now
             self.ok = False
+            self.stats["inline"] += 1
             fn()
             return
         ev = self.pending.pop(key, None)
         if ev is not None:
             main.wait_event(ev)
+            self.stats["hits"] += 1
         else:
+            self.stats["inline"] += 1
             fn()
         self.pos += 1
         if self.pos < len(self.order):
@@ -205,6 +220,7 @@ class _Prefetch:
                     e = torch.cuda.Event()
                     e.record(self.stream)
                 self.pending[nkey] = e
+                self.stats["prefetched"] += 1
 
 
 prefetch = _Prefetch()
@@ -333,6 +349,7 @@ def quantize_model_(model) -> int:
     Returns bytes saved.  Embeddings, norms and lm_head stay bf16 (QLoRA convention)."""
     if model.cfg.family != "llama":
         raise ValueError("QLoRA quantisation is implemented for the Llama/Mistral trunk")
+    prefetch.reset()  # a new set of NF4 operands: the recorded decode plan no longer applies
     saved = 0
     for layer in model.layers:
         for name, attr in (("qkv", "wqkv"), ("o", "wo"), ("gu", "wgu"), ("down", "wdown")):
