@@ -31,7 +31,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=6)
     ap.add_argument("--labels", default="gpurun_out/pmc_gemm_labels.json")
+    ap.add_argument("--ours", action="store_true",
+                    help="also run the hand-written NT GEMM (csrc/kernels/gemm_nt.hip) on every shape, after the "
+                         "library: its own kernel row in the counter table")
     a = ap.parse_args()
+    C = None
+    if a.ours:
+        from finetune_controller_amd.ops._backend import ext
+        C = ext()
     bf = torch.bfloat16
     torch.manual_seed(0)
     labels = []
@@ -49,6 +56,17 @@ def main():
         en.record()
         torch.cuda.synchronize()
         ms = st.elapsed_time(en) / a.iters
+        if C is not None and C.gemm_nt_ok(y, x, w):
+            C.gemm_nt_(y, x, w, 1.0, 0.0)
+            torch.cuda.synchronize()
+            st.record()
+            for _ in range(a.iters):
+                C.gemm_nt_(y, x, w, 1.0, 0.0)
+            en.record()
+            torch.cuda.synchronize()
+            mo = st.elapsed_time(en) / a.iters
+            print(json.dumps({"gemm": name, "kernel": "ours", "ms": round(mo, 3),
+                              "tflops": round(2.0 * T * n * k / mo / 1e9, 1)}), flush=True)
         fl = 2.0 * T * n * (k - 64 if k % 256 == 64 else k)  # model FLOPs exclude the LoRA pad columns
         labels.append({"label": name, "M": T, "N": n, "K": k, "flops": 2.0 * T * n * k, "model_flops": fl})
         print(json.dumps({"gemm": name, "M": T, "N": n, "K": k, "ms": round(ms, 3),

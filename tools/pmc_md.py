@@ -80,12 +80,12 @@ def group(disp, labels, match):
         if shapes is not None and "FillFunctor<unsigned char>" in name:
             cur += 1
             continue
-        if match and match not in name:
+        if match and not any(m in name for m in match.split(",")):
             continue
         if shapes is not None:
             if cur < 0 or cur >= len(shapes):
                 continue
-            key = shapes[cur]["label"]
+            key = shapes[cur]["label"] + (" [ours]" if "gemm_nt" in name else "")
         else:
             key = _short(name)
         a = agg[key]
@@ -100,7 +100,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--labels", default=None)
-    ap.add_argument("--match", default=None, help="only kernels whose name contains this")
+    ap.add_argument("--match", default=None, help="only kernels whose name contains this (comma: any of)")
     ap.add_argument("--title", default="rocprofv3 PMC summary")
     ap.add_argument("--raw", action="store_true", help="every counter's mean per dispatch (custom passes)")
     ap.add_argument("--hbm", default=None, metavar="CALIB_MATCH",
@@ -148,10 +148,11 @@ def main():
                if c.get("SQ_LDS_IDX_ACTIVE") and "SQ_LDS_BANK_CONFLICT" in c else None)
         hbm = 2 * c["FETCH_SIZE"] / 1e6 if "FETCH_SIZE" in c else None  # FETCH_SIZE is in KB
         tf = share = None
-        if key in flops and us:
-            tf = flops[key]["flops"] / (us * 1e-6) / 1e12
+        fk = key.replace(" [ours]", "")
+        if fk in flops and us:
+            tf = flops[fk]["flops"] / (us * 1e-6) / 1e12
             if cyc:
-                share = flops[key]["flops"] / (cyc * SIMDS * BF16_FLOP_PER_CLK_SIMD)
+                share = flops[fk]["flops"] / (cyc * SIMDS * BF16_FLOP_PER_CLK_SIMD)
 
         def f(v, p=3):
             return "" if v is None else f"{v:.{p}f}"
