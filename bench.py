@@ -205,12 +205,6 @@ def _bucket_busbw(info, mb: float, native=None, iters: int = 10) -> dict:
             "busbw_GBps": round(numel * 2 / sec / 1e9 * 2 * (n - 1) / n, 1)}
 
 
-def _nf4_stats() -> dict:
-    from finetune_controller_amd.ops import nf4
-
-    return dict(nf4.prefetch.stats, enabled=nf4.prefetch.enabled, plan_len=len(nf4.prefetch.order))
-
-
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     a = _parse(argv)
@@ -375,7 +369,6 @@ def main(argv=None) -> int:
             "dist_backend": info.backend,
             "rccl_version": rccl,
             "p2p_peers": p2p,
-            **({"nf4_prefetch": _nf4_stats()} if a.method == "qlora" else {}),
             "rank_ms_per_step": {"max": round(ms, 2), "min": round(fastest / a.steps * 1000, 2)},
             **({"allreduce_bucket": comm} if comm else {}),
             "comm": {

@@ -281,9 +281,6 @@ class LlamaForCausalLM(nn.Module):
     def forward(self, input_ids: torch.Tensor, labels: torch.Tensor | None = None, positions=None,
                 n_valid: int | None = None, segments=None):
         B, S = input_ids.shape
-        if self.layers and self.layers[0].qweights:  # QLoRA: a new pass of the NF4 decode-prefetch plan
-            from ..ops.nf4 import prefetch
-            prefetch.begin_pass(input_ids.device)
         if self.sp is not None:  # S = this rank's 1/P of each sequence (attention pads the full one itself)
             if segments is not None:
                 raise ValueError("packed documents are not supported with sequence parallelism")

@@ -73,32 +73,22 @@ class NF4Proj:
         self.sc = _QScratch.get(self.N, self.K, self.Rp, pair.A.device)
 
     def fwd_weight(self) -> torch.Tensor:
-        from .nf4 import _dequant_into, prefetch
+        from .nf4 import _dequant_into
 
         N, K, R = self.N, self.K, self.R
-        qw, sc, B = self.qw, self.sc, self.B
-
-        def fn():
-            _dequant_into(qw, sc.fwd[:N, :K], False)
-            sc.fwd[:N, K:K + R].copy_(B)
-
-        prefetch.decode((id(qw), "fwd"), (id(sc), "fwd"), fn)  # side-stream decode under the previous GEMMs
+        _dequant_into(self.qw, self.sc.fwd[:N, :K], False)
+        self.sc.fwd[:N, K:K + R].copy_(self.B)
         return self.sc.fwd[:N]
 
     def fwd_tail(self) -> torch.Tensor:
         return self.tails.fwd_tail_operand(self.A, self.B, self.s)
 
     def bwd_weight(self) -> torch.Tensor:
-        from .nf4 import _dequant_into, prefetch
+        from .nf4 import _dequant_into
 
         N, R = self.N, self.R
-        qw, sc = self.qw, self.sc
-
-        def fn():
-            _dequant_into(qw, sc.bwdT[:, :N], True)
-            sc.bwdT[:, N:N + R].copy_(self.fwd_tail()[:R].t())
-
-        prefetch.decode((id(qw), "bwd"), (id(sc), "bwd"), fn)
+        _dequant_into(self.qw, self.sc.bwdT[:, :N], True)
+        self.sc.bwdT[:, N:N + R].copy_(self.fwd_tail()[:R].t())
         return self.sc.bwdT.t()
 
     def bwd_tail(self) -> torch.Tensor:

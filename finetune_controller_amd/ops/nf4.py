@@ -134,96 +134,11 @@ def _dequant_into(qw: NF4Weight, out: torch.Tensor, transpose: bool):
                               qw.shape[1], qw.block, qw.block2, transpose)
 
 
-class _Prefetch:
-    """NF4 decode of the NEXT operand on a side HIP stream, under the current projection's GEMMs.
-
-    The decode is HBM-bound (~4.5 B per parameter, 33 us per Llama-3-8B projection) and the GEMM that
-    consumes the previous operand is MFMA-bound, so on one stream the decodes sit in series with the
-    GEMMs (8.5 ms of a Mistral-7B QLoRA step).  The decode calls of a training pass come in a fixed order
-    (forward: each layer's qkv, o, gate|up, down; backward: the transposed operands in reverse, plus any
-    checkpoint recompute), so the first pass records the order and later passes replay it: when operand k
-    is consumed, operand k + 1 is decoded on the side stream into its own per-shape scratch (a different
-    buffer from k's -- otherwise no prefetch), ordered after everything the main stream has enqueued so
-    far (the previous users of that scratch), and the main stream waits for it before use.
-    Never across a pass boundary (index 0: the optimizer may have moved B / A in between), never when the
-    order deviates (then the pass falls back to inline decodes and the next pass re-records).
-    ``FTC_NF4_PREFETCH=0`` decodes inline on the main stream."""
-
-    def __init__(self):
-        self.enabled = os.environ.get("FTC_NF4_PREFETCH", "1") != "0"
-        self.order: list = []      # [(key, buffer id, decode fn)] of the recorded pass
-        self.rec: list | None = []  # recording in progress (None: replaying)
-        self.pos = 0
-        self.ok = True
-        self.pending: dict = {}    # key -> event of a prefetched decode
-        self.stream = None
-        self.device = None
-        self.stats = {"passes": 0, "prefetched": 0, "hits": 0, "inline": 0, "deviations": 0}
-
-    def reset(self) -> None:
-        """Forget the recorded plan (its closures hold the model's scratch and adapter tensors)."""
-        if self.stream is not None and self.device is not None:
-            torch.cuda.current_stream(self.device).wait_stream(self.stream)
-        self.order, self.rec, self.pending, self.pos, self.ok = [], [], {}, 0, True
-
-    def begin_pass(self, device) -> None:
-        if not self.enabled or not torch.cuda.is_available() or device.type != "cuda":
-            return
-        if self.stream is not None:
-            torch.cuda.current_stream(self.device).wait_stream(self.stream)  # nothing stale may still write
-        self.pending.clear()
-        if self.rec is not None and self.rec:
-            self.order, self.rec = self.rec, None  # the first pass's order is the plan from now on
-        elif self.rec is None and not self.ok:
-            self.rec = []  # the last pass deviated: record again
-        self.pos, self.ok = 0, True
-        self.device = device
-        self.stats["passes"] += 1
-
-    def decode(self, key, buf, fn) -> None:
-        """Make the operand ``key`` (written into scratch ``buf`` by ``fn()``) ready on the current stream."""
-        if not self.enabled or self.device is None:
-            fn()
-            return
-        main = torch.cuda.current_stream(self.device)
-        if self.rec is not None:
-            self.rec.append((key, buf, fn))
-            fn()
-            return
-        if not (self.ok and self.pos < len(self.order) and self.order[self.pos][0] == key):
-            if self.ok:
-                self.stats["deviations"] += 1
-                if self.stream is not None:
-                    main.wait_stream(self.stream)
-                self.pending.clear()
-                self.order = []  # re-recorded by the next pass; drop the stale closures now
-            self.ok = False
-            self.stats["inline"] += 1
-            fn()
-            return
-        ev = self.pending.pop(key, None)
-        if ev is not None:
-            main.wait_event(ev)
-            self.stats["hits"] += 1
-        else:
-            self.stats["inline"] += 1
-            fn()
-        self.pos += 1
-        if self.pos < len(self.order):
-            nkey, nbuf, nfn = self.order[self.pos]
-            if nbuf != buf:
-                if self.stream is None:
-                    self.stream = torch.cuda.Stream(device=self.device)
-                self.stream.wait_stream(main)  # the previous users of that scratch are all enqueued before
-                with torch.cuda.stream(self.stream):
-                    nfn()
-                    e = torch.cuda.Event()
-                    e.record(self.stream)
-                self.pending[nkey] = e
-                self.stats["prefetched"] += 1
-
-
-prefetch = _Prefetch()
+# (Removed in round 4: decoding the next NF4 operand on a side HIP stream under the current projection's
+# GEMMs.  It engaged on every call (1,270 prefetches, 0 fallbacks) and measured -0.3 % on Mistral-7B QLoRA
+# (37,181 / 37,229 / 37,240 vs 37,365 / 37,305 / 37,344 tok/s inline, profiles/r4/qlora_pf2/): the
+# library's persistent GEMMs hold every CU, so the HBM-bound decode has nothing to run beside and only
+# contends.  git history keeps it.)
 
 
 # 0: the separate copy / scale kernels.  Mistral-7B QLoRA, interleaved on one box (profiles/r3/qlora_aug/):
@@ -265,11 +180,8 @@ class _QLoRALinearFn(torch.autograd.Function):
         if use_aug:
             R = A.shape[0]
             sc = _QScratch.get(N, K, Rp, x2.device)
-            # W, B and s A into [[W | B 0], [s A ; 0 | 0]] in one launch (csrc/kernels/nf4.hip AugTail),
-            # prefetched on the side stream under the previous projection's GEMMs (_Prefetch)
-            prefetch.decode((id(qw), "fwd"), (id(sc), "fwd"),
-                            lambda: _dequant_aug(qw, sc.fwd[:N, :K], False, B, sc.fwd[:N, K:K + R], A,
-                                                 sc.fwd[N:N + R, :K], scale))
+            # W, B and s A into [[W | B 0], [s A ; 0 | 0]] in one launch (csrc/kernels/nf4.hip AugTail)
+            _dequant_aug(qw, sc.fwd[:N, :K], False, B, sc.fwd[:N, K:K + R], A, sc.fwd[N:N + R, :K], scale)
             # the producer kernel (fused SwiGLU) may already have formed s x A^T in the spare columns
             if tails is None or not take_prefilled("fwd", x2, tails):
                 _mm_into(x2, sc.fwd[N:, :K].t(), _tail(x2, K, Rp))
@@ -302,13 +214,8 @@ class _QLoRALinearFn(torch.autograd.Function):
                 sc = _QScratch.get(N, K, Rp, dy2.device)
                 prefilled = ctx.tails is not None and take_prefilled("bwd", dy2, ctx.tails)
                 # W^T, (s A)^T and (unless the producer formed dy B already) B for the tail product, one launch
-                if prefilled:
-                    prefetch.decode((id(qw), "bwd"), (id(sc), "bwd"),
-                                    lambda: _dequant_aug(qw, sc.bwdT[:, :N], True, None, None, A, sc.bwdT[:, N:N + R], s))
-                else:
-                    prefetch.decode((id(qw), "bwd+B"), (id(sc), "bwd"),
-                                    lambda: _dequant_aug(qw, sc.bwdT[:, :N], True, B, sc.Bp[:, :R], A,
-                                                         sc.bwdT[:, N:N + R], s))
+                _dequant_aug(qw, sc.bwdT[:, :N], True, None if prefilled else B, None if prefilled else sc.Bp[:, :R],
+                             A, sc.bwdT[:, N:N + R], s)
                 if not prefilled:
                     _mm_into(dy2, sc.Bp, _tail(dy2, N, Rp))
                 dyb = _tail(dy2, N, R)
@@ -349,7 +256,6 @@ def quantize_model_(model) -> int:
     Returns bytes saved.  Embeddings, norms and lm_head stay bf16 (QLoRA convention)."""
     if model.cfg.family != "llama":
         raise ValueError("QLoRA quantisation is implemented for the Llama/Mistral trunk")
-    prefetch.reset()  # a new set of NF4 operands: the recorded decode plan no longer applies
     saved = 0
     for layer in model.layers:
         for name, attr in (("qkv", "wqkv"), ("o", "wo"), ("gu", "wgu"), ("down", "wdown")):

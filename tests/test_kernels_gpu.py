@@ -1555,52 +1555,3 @@ def test_gpt2_steps_hip_match_torch_path(C, monkeypatch, method):
         assert abs(a - b) < 2e-2 * abs(b), (lh, lt)
     assert lh[2] < lh[0]
     assert (ph - pt).abs().max().item() < 1e-2
-
-
-@pytest.mark.parametrize("mlp_seq", [1024, 512])  # ffn width
-def test_qlora_decode_prefetch_bitwise(C, mlp_seq):
-    """ops.nf4 _Prefetch: NF4 decodes of the next operand on a side stream (recorded order replayed from the
-    second pass on), including an optimizer step between passes, are bit-identical to inline decodes --
-    losses and every adapter gradient of three training passes."""
-    from finetune_controller_amd.models import LoRAConfig, build_model
-    from finetune_controller_amd.models.config import ModelConfig
-    from finetune_controller_amd.ops import nf4
-    from finetune_controller_amd.ops.nf4 import quantize_model_
-    from finetune_controller_amd.train.optim import FlatAdamW
-
-    cfg = ModelConfig("llama", 512, 256, 2, 4, 2, mlp_seq, 512, 10000.0, name="llama-test")
-    ids = torch.randint(0, cfg.vocab_size, (2, 256), device=DEV)
-    labels = torch.roll(ids, -1, 1)
-    res = {}
-    saved = nf4.prefetch
-    try:
-        for on in (True, False):
-            nf4.prefetch = nf4._Prefetch()
-            nf4.prefetch.enabled = on
-            torch.manual_seed(0)
-            m = build_model(cfg, LoRAConfig(r=16, alpha=32), device=DEV, dtype=torch.bfloat16)
-            m.init_weights(seed=5)
-            m.freeze_base()
-            quantize_model_(m)
-            g = torch.Generator(device=DEV).manual_seed(1)
-            for layer in m.layers:
-                for p in layer.lora.values():
-                    for _, _, B_s in p.segment_tensors():
-                        B_s.data.normal_(0, 0.05, generator=g)
-            opt = FlatAdamW([p for p in m.parameters() if p.requires_grad], lr=1e-3)
-            out = []
-            for _ in range(3):
-                opt.zero_grad()
-                loss = m(ids, labels)
-                loss.backward()
-                out.append((loss.float().item(), opt.grad_flat.float().clone()))
-                opt.step()
-            torch.cuda.synchronize()
-            if on:
-                assert nf4.prefetch.rec is None and len(nf4.prefetch.order) > 0 and nf4.prefetch.ok
-            res[on] = out
-    finally:
-        nf4.prefetch = saved
-    for (l1, g1), (l0, g0) in zip(res[True], res[False]):
-        assert l1 == l0
-        assert torch.equal(g1, g0)
