@@ -203,9 +203,10 @@ def test_cross_entropy_inplace(C, V):
 
 
 @pytest.mark.parametrize("gdtype", [torch.bfloat16, torch.float32])
-def test_adamw_flat(C, gdtype):
+@pytest.mark.parametrize("n", [3, 10_003, 1_000_001])
+def test_adamw_flat(C, gdtype, n):
+    """One-shot grid: tail-only (n < 4), one partial workgroup, many workgroups; tails n % 4 = 3 / 1."""
     torch.manual_seed(0)
-    n = 10_003
     master = torch.randn(n, device=DEV)
     param = bf(master)
     m = torch.zeros(n, device=DEV)
