@@ -1,6 +1,7 @@
 // K4 RoPE (in place, forward and inverse rotation) and K9 SwiGLU forward/backward.
 // Memory-bound: 16-byte vector loads per lane, cos/sin from host-precomputed fp32 tables
-// (no on-device trig: guide Appendix B "Element-wise"), grid-stride capped at 2048 blocks.
+// (no on-device trig: guide Appendix B "Element-wise"); grid-stride loops launched one-shot
+// (common.h oneshot_grid: one work item per thread).
 #include "common.h"
 
 #include <algorithm>
@@ -55,7 +56,7 @@ extern "C" int ftc_rope(void* qkv, const float* cosT, const float* sinT, const i
                         hipStream_t stream) {
   if (head_dim % 16 != 0 || ld % 8 != 0) return -1;
   const long long total = rows * n_rot_heads * (head_dim / 16);
-  const int grid = ftc::stream_grid(total, 256);
+  const int grid = ftc::oneshot_grid(total, 256);
   hipLaunchKernelGGL(rope_kernel, dim3(grid), dim3(256), 0, stream, (uint16_t*)qkv, cosT, sinT, positions, rows, ld,
                      n_rot_heads, head_dim, seq_len, inverse ? -1.0f : 1.0f, max_pos);
   return (int)hipGetLastError();
@@ -110,7 +111,7 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const uint16_t* __restr
 // a / dgu may be padded row views (row strides a_rs >= F, dgu_rs >= 2F; multiples of 8)
 extern "C" int ftc_swiglu_fwd(const void* gu, void* a, long long rows, int F, long long a_rs, hipStream_t stream) {
   if (F % 8 != 0 || a_rs % 8 != 0) return -1;
-  const int grid = ftc::stream_grid(rows * (F / 8), 256);
+  const int grid = ftc::oneshot_grid(rows * (F / 8), 256);
   hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(grid), dim3(256), 0, stream, (const uint16_t*)gu, (uint16_t*)a, rows, F,
                      a_rs);
   return (int)hipGetLastError();
@@ -119,7 +120,7 @@ extern "C" int ftc_swiglu_fwd(const void* gu, void* a, long long rows, int F, lo
 extern "C" int ftc_swiglu_bwd(const void* da, const void* gu, void* dgu, long long rows, int F, long long dgu_rs,
                               hipStream_t stream) {
   if (F % 8 != 0 || dgu_rs % 8 != 0) return -1;
-  const int grid = ftc::stream_grid(rows * (F / 8), 256);
+  const int grid = ftc::oneshot_grid(rows * (F / 8), 256);
   hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid), dim3(256), 0, stream, (const uint16_t*)da, (const uint16_t*)gu,
                      (uint16_t*)dgu, rows, F, dgu_rs);
   return (int)hipGetLastError();
@@ -213,7 +214,7 @@ extern "C" int ftc_splitk_sum(const float* parts, int nsplit, long long pstride,
   if (nsplit < 1 || cols % 8 != 0 || ldc % 8 != 0 || (reinterpret_cast<uintptr_t>(parts) & 15) ||
       (reinterpret_cast<uintptr_t>(c) & 15) || pstride % 8 != 0)
     return -1;
-  const int grid = ftc::stream_grid(rows * (cols / 8), 256);
+  const int grid = ftc::oneshot_grid(rows * (cols / 8), 256);
   if (c_fp32)
     hipLaunchKernelGGL(splitk_sum_kernel<true>, dim3(grid), dim3(256), 0, stream, parts, nsplit, pstride, c, rows, cols,
                        ldc, beta);

@@ -253,7 +253,7 @@ extern "C" int ftc_nf4_dequant_aug(const uint8_t* packed, const uint8_t* absmax_
                        packed, absmax_q, absmax_scale, absmax_offset, (uint16_t*)out, rows, cols, ldo, block2, t);
   } else {
     const long long n = (long long)rows * cols;
-    const int grid = ftc::stream_grid(n / 16, 256);
+    const int grid = ftc::oneshot_grid(n / 16, 256);
     hipLaunchKernelGGL(nf4_dequant_rows_kernel, dim3(grid + (has_tail ? kTailBlocks : 0)), dim3(256), 0, stream,
                        packed, absmax_q, absmax_scale, absmax_offset, (uint16_t*)out, n, cols, ldo, block, block2, grid,
                        t);
@@ -274,7 +274,7 @@ extern "C" int ftc_nf4_dequant(const uint8_t* packed, const uint8_t* absmax_q, c
                                float absmax_offset, void* out, long long n, int block, int block2,
                                hipStream_t stream) {
   if (n % 16 != 0 || block % 16 != 0) return -1;
-  const int grid = ftc::stream_grid(n / 16, 256);
+  const int grid = ftc::oneshot_grid(n / 16, 256);
   hipLaunchKernelGGL(nf4_dequant_kernel, dim3(grid), dim3(256), 0, stream, packed, absmax_q, absmax_scale,
                      absmax_offset, (uint16_t*)out, n, block, block2);
   return (int)hipGetLastError();
