@@ -1361,7 +1361,7 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
             lse, (float*)workspace, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, q_rs, kv_rs, o_rs, dq_rs, dkv_rs, do_rs,
             B, S, H, KV, scale, scale * LOG2E, causal, window, doc_start, doc_end, kv_valid,
             rope_cos, rope_sin, rope_pos};
-  const int grid_d = ftc::stream_grid((long long)B * S, 4);
+  const int grid_d = ftc::oneshot_grid((long long)B * S, 4);
   const int g_kv = B * KV * (S / 256);
   const int g_q = B * H * (S / 128);
   // occupancy variant of the two main kernels: 2 waves/SIMD (256-VGPR budget, spills a few staging

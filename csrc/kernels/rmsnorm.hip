@@ -324,6 +324,10 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p
   if (wv == 0 && c < d) out[c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
+// frozen-weight launches: one row group per workgroup (common.h oneshot_grid); bwd 0.097 vs 0.101 ms,
+// fwd equal (profiles/r4/oneshot/rms.log).  The dw backward keeps its capped grid (partials per block).
+static int rms_grid(long long rows, int per_block) { return ftc::oneshot_grid(rows, per_block); }
+
 static int pick_nv(int d) {
   const int per_lane = (d / 8 + 63) / 64;
   int nv = 1;
@@ -337,7 +341,7 @@ extern "C" int ftc_rmsnorm_fwd(const void* x, const void* res, const void* w, vo
                                int rows, int d, float eps, long long y_rs, hipStream_t stream) {
   if (d % 8 != 0 || d > 16 * 512) return -1;
   const int nv = pick_nv(d);
-  const int grid = ftc::stream_grid(rows, 4);
+  const int grid = rms_grid(rows, 4);
   auto X = (const uint16_t*)x;
   auto R = (const uint16_t*)res;
   auto W = (const uint16_t*)w;
@@ -355,7 +359,7 @@ extern "C" int ftc_rmsnorm_fwd(const void* x, const void* res, const void* w, vo
     return !(e && e[0] == '0');
   }();
   if (two && nv >= 2) {
-    const int g2 = ftc::stream_grid(rows, 2);
+    const int g2 = rms_grid(rows, 2);
 #define FTC_LAUNCH_FWD2(NV2)                                                                                     \
   if (res)                                                                                                       \
     hipLaunchKernelGGL((rmsnorm_fwd2_kernel<NV2, true>), dim3(g2), dim3(256), 0, stream, X, R, W, H, Y, rstd, rows, \
@@ -395,7 +399,7 @@ extern "C" int ftc_rmsnorm_bwd(const void* dy, const void* h, const void* w, con
   const int nv = pick_nv(d);
   const bool need_dw = dw != nullptr;
   // the dw path keeps per-wave accumulators: fewer, longer-lived blocks
-  const int grid = need_dw ? ftc_rmsnorm_bwd_grid(rows) : ftc::stream_grid(rows, 4);
+  const int grid = need_dw ? ftc_rmsnorm_bwd_grid(rows) : rms_grid(rows, 4);
   const size_t lds = need_dw ? (size_t)4 * d * sizeof(float) : 0;
   auto DY = (const uint16_t*)dy;
   auto Hh = (const uint16_t*)h;
@@ -419,7 +423,7 @@ extern "C" int ftc_rmsnorm_bwd(const void* dy, const void* h, const void* w, con
     return !(e && e[0] == '0');
   }();
   if (!need_dw && two && nv >= 2) {
-    const int g2 = ftc::stream_grid(rows, 2);
+    const int g2 = rms_grid(rows, 2);
     const size_t l2 = (size_t)(d / 8) * 16 + 4 * sizeof(float);
 #define FTC_LAUNCH_BWD2(NV2)                                                                                  \
   if (dres)                                                                                                   \
