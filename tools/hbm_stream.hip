@@ -173,6 +173,76 @@ __global__ __launch_bounds__(256) void fwd_rowtile(const uint4* __restrict__ gu,
   }
 }
 
+__device__ __forceinline__ void bwd_math(uint4 g, uint4 u, uint4 d, uint4& dg, uint4& du) {
+  const unsigned* gp = reinterpret_cast<const unsigned*>(&g);
+  const unsigned* up = reinterpret_cast<const unsigned*>(&u);
+  const unsigned* dp = reinterpret_cast<const unsigned*>(&d);
+  unsigned* o1 = reinterpret_cast<unsigned*>(&dg);
+  unsigned* o2 = reinterpret_cast<unsigned*>(&du);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float gg[2] = {lo(gp[k]), hi(gp[k])}, uu[2] = {lo(up[k]), hi(up[k])}, dd[2] = {lo(dp[k]), hi(dp[k])};
+    float a[2], b[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const float sg = 1.0f / (1.0f + __expf(-gg[e]));
+      b[e] = dd[e] * gg[e] * sg;
+      a[e] = dd[e] * uu[e] * sg * (1.0f + gg[e] * (1.0f - sg));
+    }
+    o1[k] = pk(a[0], a[1]);
+    o2[k] = pk(b[0], b[1]);
+  }
+}
+
+// Backward structure of the production fused kernel: a workgroup owns 512 columns (wave: 128) and RB
+// rows walked in 16-row sub-tiles.  PFG: g/u of sub-tile s+1 issued before s is computed; PFD: da too.
+template <bool PFG, bool PFD, bool NT>
+__global__ __launch_bounds__(256, 2) void bwd_colwalk(const uint4* __restrict__ gu, const uint4* __restrict__ da,
+                                                      uint4* __restrict__ dgu, long long T, int nc, long long ds16,
+                                                      int RB, int ncb) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int cb = blockIdx.x % ncb, rb = blockIdx.x / ncb;
+  const int cw = cb * 64 + 16 * wave;  // chunk index of this wave's first 8-column chunk
+  const int cq = lane & 15, rq = lane >> 4;
+  const long long rbeg = (long long)rb * RB, rend = rbeg + RB < T ? rbeg + RB : T;
+  uint4 g[4], u[4], d[4];
+  auto ld_gu = [&](long long r) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const long long row = r + 4 * i + rq;
+      g[i] = gu[row * 2 * nc + cw + cq];
+      u[i] = gu[row * 2 * nc + nc + cw + cq];
+    }
+  };
+  auto ld_d = [&](long long r) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) d[i] = da[(r + 4 * i + rq) * nc + cw + cq];
+  };
+  if (PFG) ld_gu(rbeg);
+  if (PFD) ld_d(rbeg);
+  for (long long r0 = rbeg; r0 < rend; r0 += 16) {
+    if (!PFG) ld_gu(r0);
+    if (!PFD) ld_d(r0);
+    uint4 gc[4], uc[4], dc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      gc[i] = g[i];
+      uc[i] = u[i];
+      dc[i] = d[i];
+    }
+    if (PFG && r0 + 16 < rend) ld_gu(r0 + 16);
+    if (PFD && r0 + 16 < rend) ld_d(r0 + 16);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const long long row = r0 + 4 * i + rq;
+      uint4 a, b;
+      bwd_math(gc[i], uc[i], dc[i], a, b);
+      st16<NT>(dgu + row * ds16 + cw + cq, a);
+      st16<NT>(dgu + row * ds16 + nc + cw + cq, b);
+    }
+  }
+}
+
 int main(int argc, char** argv) {
   const long long T = argc > 1 ? atoll(argv[1]) : 16384;
   const int F = 14336, Rp = 64;
@@ -264,6 +334,69 @@ int main(int argc, char** argv) {
   run("fwd_rowtile_pf", [&] { hipLaunchKernelGGL((fwd_rowtile<true, false>), dim3(rt), dim3(256), 0, 0, G, H, T, nc, hs16); }, fwd_bytes, true);
   run("fwd_rowtile_nt", [&] { hipLaunchKernelGGL((fwd_rowtile<false, true>), dim3(rt), dim3(256), 0, 0, G, H, T, nc, hs16); }, fwd_bytes, true);
   run("fwd_rowtile_pf_nt", [&] { hipLaunchKernelGGL((fwd_rowtile<true, true>), dim3(rt), dim3(256), 0, 0, G, H, T, nc, hs16); }, fwd_bytes, true);
+  // ---- backward: da [T][F], dgu [T][2F + Rp]
+  const long long ds = 2LL * F + Rp, ds16 = ds / 8;
+  const size_t da_bytes = (size_t)T * F * 2, dgu_bytes = (size_t)T * ds * 2;
+  void *da, *dgu, *dgu0;
+  CK(hipMalloc(&da, da_bytes));
+  CK(hipMalloc(&dgu, dgu_bytes));
+  CK(hipMalloc(&dgu0, dgu_bytes));
+  CK(hipMemcpy(da, gu, da_bytes, hipMemcpyDeviceToDevice));  // any finite bf16 values
+  CK(hipMemset(dgu, 0, dgu_bytes));
+  CK(hipMemset(dgu0, 0, dgu_bytes));
+  const double bwd_bytes = (double)T * 2 * F * 2 + (double)T * F * 2 + (double)T * 2 * F * 2;
+  const int ncb = F / 512;
+  auto bwd_run = [&](const char* name, auto kern, int wgs, bool ref) {
+    long long nrb = wgs / ncb, rb = (T + nrb - 1) / nrb;
+    rb = (rb + 15) / 16 * 16;
+    nrb = (T + rb - 1) / rb;
+    const dim3 grid((unsigned)(ncb * nrb));
+    void* out = ref ? dgu0 : dgu;
+    auto launch = [&] {
+      hipLaunchKernelGGL(kern, grid, dim3(256), 0, 0, (const uint4*)gu, (const uint4*)da, (uint4*)out, T, nc, ds16,
+                         (int)rb, ncb);
+    };
+    if (ref) {
+      launch();
+      CK(hipDeviceSynchronize());
+      return;
+    }
+    for (int i = 0; i < 3; ++i) launch();
+    CK(hipDeviceSynchronize());
+    float best = 1e30f, sum = 0.f;
+    const int reps = 20;
+    for (int r = 0; r < reps; ++r) {
+      CK(hipEventRecord(e0));
+      launch();
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      best = ms < best ? ms : best;
+      sum += ms;
+    }
+    std::vector<unsigned short> a(dgu_bytes / 2), b(dgu_bytes / 2);
+    CK(hipMemcpy(a.data(), dgu, dgu_bytes, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(b.data(), dgu0, dgu_bytes, hipMemcpyDeviceToHost));
+    int ok = 1;
+    for (long long t = 0; t < T && ok; ++t)
+      if (memcmp(&a[t * ds], &b[t * ds], (size_t)F * 4)) ok = 0;
+    CK(hipMemset(dgu, 0, dgu_bytes));
+    printf("{\"variant\": \"%s_wgs%d\", \"us_best\": %.1f, \"us_mean\": %.1f, \"TBps_best\": %.3f, \"match\": %d}\n", name,
+           wgs, best * 1e3, sum / reps * 1e3, bwd_bytes / (best * 1e-3) / 1e12, ok);
+    fflush(stdout);
+  };
+  bwd_run("ref", bwd_colwalk<false, false, false>, 512, true);
+  for (int wgs : {512, 1024}) {
+    bwd_run("bwd_nopf", bwd_colwalk<false, false, false>, wgs, false);
+    bwd_run("bwd_pfgu", bwd_colwalk<true, false, false>, wgs, false);
+    bwd_run("bwd_pfall", bwd_colwalk<true, true, false>, wgs, false);
+    bwd_run("bwd_pfgu_nt", bwd_colwalk<true, false, true>, wgs, false);
+    bwd_run("bwd_pfall_nt", bwd_colwalk<true, true, true>, wgs, false);
+  }
+  CK(hipFree(da));
+  CK(hipFree(dgu));
+  CK(hipFree(dgu0));
   CK(hipFree(gu));
   CK(hipFree(h));
   CK(hipFree(h0));
