@@ -54,6 +54,11 @@ def main():
     ms = timeit(lambda: N._dequant_into(qw, out, False))
     print(json.dumps({"op": "nf4_dequant_rows", "tag": tag, "ms": round(ms, 4),
                       "TBps": round((F * d // 2 + F * d * 2) / ms / 1e9, 3)}), flush=True)
+    outT = torch.empty(d, F, device=dev, dtype=bf)
+    ms = timeit(lambda: N._dequant_into(qw, outT, True))
+    print(json.dumps({"op": "nf4_dequant_t", "tag": tag, "ms": round(ms, 4),
+                      "TBps": round((F * d // 2 + F * d * 2) / ms / 1e9, 3)}), flush=True)
+    assert torch.equal(outT, out.t()), "transposed dequant != rows dequant transposed"
 
 
 if __name__ == "__main__":
