@@ -1,5 +1,6 @@
 #!/bin/bash
 # AdamW wide kernel: bitwise tests + A/B at 2e9 elements
+# (historical record of a measurement: the A/B switch or worktree it used was removed afterwards; see profiles/r4/)
 set -o pipefail
 mkdir -p gpurun_out/adamw
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "adamw" > gpurun_out/adamw/pytest.log 2>&1; rc=$?; tail -3 gpurun_out/adamw/pytest.log; [ $rc -eq 0 ] || exit $rc

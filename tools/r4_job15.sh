@@ -1,5 +1,6 @@
 #!/bin/bash
 # one-shot grids for the element-wise stream kernels: tests, per-op A/B, full-FT A/B
+# (historical record of a measurement: the A/B switch or worktree it used was removed afterwards; see profiles/r4/)
 set -o pipefail
 mkdir -p gpurun_out/oneshot
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "swiglu or rope or splitk or nf4 or wgrad_split or adamw" > gpurun_out/oneshot/pytest.log 2>&1; rc=$?; tail -3 gpurun_out/oneshot/pytest.log; [ $rc -eq 0 ] || exit $rc

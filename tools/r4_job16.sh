@@ -1,5 +1,6 @@
 #!/bin/bash
 # one-shot RMSNorm / delta launches: tests, RMSNorm A/B, LoRA step kernel table
+# (historical record of a measurement: the A/B switch or worktree it used was removed afterwards; see profiles/r4/)
 set -o pipefail
 mkdir -p gpurun_out/oneshot2
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "rmsnorm or flash or norm" > gpurun_out/oneshot2/pytest.log 2>&1; rc=$?; tail -3 gpurun_out/oneshot2/pytest.log; [ $rc -eq 0 ] || exit $rc

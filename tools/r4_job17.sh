@@ -1,5 +1,6 @@
 #!/bin/bash
 # same-box A/B: LoRA headline step, tree before today's stream-kernel changes (.ab_base) vs HEAD
+# (historical record of a measurement: the A/B switch or worktree it used was removed afterwards; see profiles/r4/)
 set -o pipefail
 mkdir -p gpurun_out/ab17
 for r in 1 2; do

@@ -1,5 +1,6 @@
 #!/bin/bash
 # full FT: W^T refresh eager (after AdamW) vs lazy (inside the next backward), same box, two rounds
+# (historical record of a measurement: the A/B switch or worktree it used was removed afterwards; see profiles/r4/)
 set -o pipefail
 mkdir -p gpurun_out/wt_eager
 for r in 1 2; do

@@ -1,5 +1,6 @@
 #!/bin/bash
 # NF4 row dequant: coalesced 8-codes-per-thread mapping; tests, op A/B and Mistral-7B QLoRA A/B vs the base tree
+# (historical record of a measurement: the A/B switch or worktree it used was removed afterwards; see profiles/r4/)
 set -o pipefail
 mkdir -p gpurun_out/nf4c
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "nf4 or qlora" > gpurun_out/nf4c/pytest.log 2>&1; rc=$?; tail -3 gpurun_out/nf4c/pytest.log; [ $rc -eq 0 ] || exit $rc
