@@ -18,7 +18,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from finetune_controller_amd.ops._backend import ext  # noqa: E402
 
-VARIANTS = {"8": 8, "il": 1}
+VARIANTS = {"8": 8, "4": 4, "il": 1}
 
 
 def timeit(fn, iters):
