@@ -134,12 +134,12 @@ def _parse(argv):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--method", default="lora", choices=["lora", "qlora", "full"])
-    ap.add_argument("--batch-size", type=int, default=int(os.environ.get("FTC_BENCH_MICRO", "4")))
-    ap.add_argument("--seq-len", type=int, default=int(os.environ.get("FTC_BENCH_SEQ", "4096")))
+    ap.add_argument("--batch-size", type=int, default=4)
+    ap.add_argument("--seq-len", type=int, default=4096)
     ap.add_argument("--lora-r", type=int, default=16)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
-    ap.add_argument("--comm-engine", default=os.environ.get("FTC_COMM_ENGINE", "torch"), choices=["torch", "native"])
-    ap.add_argument("--comm-ab", action="store_true", default=os.environ.get("FTC_BENCH_COMM_AB") == "1",
+    ap.add_argument("--comm-engine", default="torch", choices=["torch", "native"])
+    ap.add_argument("--comm-ab", action="store_true",
                     help="after the timed region, also time the native RCCL engine's bucket all-reduce")
     ap.add_argument("--grad-dtype", default="auto", choices=["auto", "fp32", "bf16"],
                     help="gradient buffer / reduction dtype (full FT; auto: fp32 when accumulating)")
@@ -151,7 +151,7 @@ def _parse(argv):
                     help="Ulysses sequence parallelism: groups of SP ranks share each sequence (1/SP of the tokens "
                          "per rank); --seq-len is the FULL sequence length")
     ap.add_argument("--checkpoint-layers", action="store_true")
-    ap.add_argument("--ce-chunk-rows", type=int, default=int(os.environ.get("FTC_CE_CHUNK", "4096")),
+    ap.add_argument("--ce-chunk-rows", type=int, default=4096,
                     help="rows per lm_head + cross-entropy chunk (the only vocab-sized buffer)")
     ap.add_argument("--kernels", default=None, choices=["hip", "torch"],
                     help="torch = stock PyTorch-ROCm ops (the 'before' row)")
@@ -161,7 +161,7 @@ def _parse(argv):
     ap.add_argument("--doc-len", type=int, default=0,
                     help="packed documents of this many tokens (document-masked attention; 0: one per row)")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (not timed)")
-    ap.add_argument("--launcher-timeout", type=float, default=float(os.environ.get("FTC_BENCH_TIMEOUT", "0")),
+    ap.add_argument("--launcher-timeout", type=float, default=0.0,
                     help="launcher mode: give up after this many seconds (0: never)")
     return ap.parse_args(argv)
 

@@ -41,7 +41,7 @@ int ftc_gemm_nt_ok(const void* a, long long lda, const void* b, long long ldb, c
                    int M, int N, int K);
 int ftc_gemm_nt(const void* a, long long lda, const void* b, long long ldb, void* c, long long ldc, int c_fp32, int M,
                 int N, int K, float alpha, float beta, hipStream_t stream);
-void ftc_gemm_nt_config(int grid_cap, int group, int xcc, int nt_store, int load_policy);
+void ftc_gemm_nt_config(int grid_cap, int group, int xcc);
 int ftc_gemm_nt_rope(const void* a, long long lda, const void* b, long long ldb, void* c, long long ldc, int M, int N,
                      int K, const float* cos_t, const float* sin_t, const int* positions, int seq_len, int rot_heads,
                      hipStream_t stream);
@@ -58,7 +58,6 @@ int ftc_adamw(void* param_bf16, float* master, float* m, float* v, const void* g
 int ftc_sumsq_partials();
 int ftc_sumsq(const void* x, int is_fp32, long long n, float* partial, float* out, float* coef, float max_norm,
               float scale, hipStream_t stream);
-void ftc_flash_dkdv_config(int waves);
 int ftc_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H, int KV, int D,
                   long long q_row_stride, long long kv_row_stride, long long o_row_stride, float scale, int causal,
                   int window, const int* doc_start, int kv_valid, hipStream_t stream);
@@ -477,9 +476,8 @@ void gemm_nt_rope_(at::Tensor& c, const at::Tensor& a, const at::Tensor& b, cons
 
 // launch configuration of the projection GEMM (persistent grid cap, tile order, store policy); the
 // defaults are the measured best (profiles/r4/gemm_nt.md) -- tools/bench_gemm_nt.py sweeps it
-void gemm_nt_config(int64_t grid_cap, int64_t group, int64_t xcc, int64_t nt_store, int64_t load_policy) {
-  TORCH_CHECK(load_policy >= 0 && load_policy <= 4, "gemm_nt_config: load_policy 0..4");
-  ftc_gemm_nt_config((int)grid_cap, (int)group, (int)xcc, nt_store ? 1 : 0, (int)load_policy);
+void gemm_nt_config(int64_t grid_cap, int64_t group, int64_t xcc) {
+  ftc_gemm_nt_config((int)grid_cap, (int)group, (int)xcc);
 }
 
 // ---------------- cross entropy (in place on logits) ----------------
@@ -859,9 +857,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_nt_ok", &gemm_nt_ok);
   m.def("gemm_nt_rope_", &gemm_nt_rope_, py::arg("c"), py::arg("a"), py::arg("b"), py::arg("cos"), py::arg("sin"),
         py::arg("positions"), py::arg("seq_len"), py::arg("rot_heads"));
-  m.def("flash_dkdv_config", [](int64_t waves) { ftc_flash_dkdv_config((int)waves); }, py::arg("waves"));
-  m.def("gemm_nt_config", &gemm_nt_config, py::arg("grid_cap"), py::arg("group"), py::arg("xcc"), py::arg("nt_store"),
-        py::arg("load_policy") = 0);
+  m.def("gemm_nt_config", &gemm_nt_config, py::arg("grid_cap"), py::arg("group"), py::arg("xcc"));
   m.def("gemm_nt_", &gemm_nt_, py::arg("c"), py::arg("a"), py::arg("b"), py::arg("alpha") = 1.0, py::arg("beta") = 0.0);
   m.def("ce_fwd_bwd_", &ce_fwd_bwd_);
   m.def("adamw_", &adamw_, py::arg("param"), py::arg("master"), py::arg("m"), py::arg("v"), py::arg("grad"),

@@ -13,7 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define FTC_DEV __device__ __forceinline__
+#define DEV_INLINE __device__ __forceinline__
 
 namespace ftc {
 
@@ -28,10 +28,10 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 
 // Raw buffer resource over a wave-uniform base pointer (guide T8): loads then take one 32-bit VGPR
 // offset + an SGPR offset instead of a 64-bit VGPR address per row.
-FTC_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
+DEV_INLINE __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
 }
-FTC_DEV u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, int voff_bytes, int soff_bytes) {
+DEV_INLINE u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, int voff_bytes, int soff_bytes) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, voff_bytes, soff_bytes, 0);
 }
 
@@ -41,7 +41,7 @@ FTC_DEV u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, int voff_bytes, int soff_byte
 // completion with explicit vmcnt waits.  M0 is saved / restored inside the statement (compiler-
 // reserved).  The operands must come from SALU (kernel arguments, blockIdx / readfirstlane-derived
 // values computed well before): no VALU-written SGPR hazard is padded here.
-FTC_DEV void lds_dma16(__amdgpu_buffer_rsrc_t r, const void* lds, int voff, int soff) {
+DEV_INLINE void lds_dma16(__amdgpu_buffer_rsrc_t r, const void* lds, int voff, int soff) {
   const unsigned dst = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)lds;
   unsigned keep;
   asm volatile(
@@ -52,29 +52,29 @@ FTC_DEV void lds_dma16(__amdgpu_buffer_rsrc_t r, const void* lds, int voff, int 
       : "memory");
 }
 
-FTC_DEV float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
-FTC_DEV float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
-FTC_DEV float bf2f(uint16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
+DEV_INLINE float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
+DEV_INLINE float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+DEV_INLINE float bf2f(uint16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
 
-FTC_DEV uint16_t f2bf(float x) {
+DEV_INLINE uint16_t f2bf(float x) {
   __bf16 b = (__bf16)x;
   return __builtin_bit_cast(uint16_t, b);
 }
 // pack two floats into one dword of 2 x bf16 (lo in bits 0..15)
-FTC_DEV uint32_t pack_bf2(float lo, float hi) {
+DEV_INLINE uint32_t pack_bf2(float lo, float hi) {
   f32x2 v = {lo, hi};
   bf16x2 b = __builtin_convertvector(v, bf16x2);
   return __builtin_bit_cast(uint32_t, b);
 }
 
 // 8 bf16 <-> 8 floats
-FTC_DEV void unpack8(const uint4& v, float* f) {
+DEV_INLINE void unpack8(const uint4& v, float* f) {
   f[0] = bf_lo(v.x); f[1] = bf_hi(v.x);
   f[2] = bf_lo(v.y); f[3] = bf_hi(v.y);
   f[4] = bf_lo(v.z); f[5] = bf_hi(v.z);
   f[6] = bf_lo(v.w); f[7] = bf_hi(v.w);
 }
-FTC_DEV uint4 pack8(const float* f) {
+DEV_INLINE uint4 pack8(const float* f) {
   uint4 v;
   v.x = pack_bf2(f[0], f[1]);
   v.y = pack_bf2(f[2], f[3]);
@@ -83,12 +83,12 @@ FTC_DEV uint4 pack8(const float* f) {
   return v;
 }
 
-FTC_DEV float wave_sum(float v) {
+DEV_INLINE float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
   return v;
 }
-FTC_DEV float wave_max(float v) {
+DEV_INLINE float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
   return v;
@@ -96,7 +96,7 @@ FTC_DEV float wave_max(float v) {
 
 // Block-wide sum for blockDim.x == NT (multiple of 64). `red` needs NT/64 floats of LDS.
 template <int NT>
-FTC_DEV float block_sum(float v, float* red) {
+DEV_INLINE float block_sum(float v, float* red) {
   v = wave_sum(v);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (lane == 0) red[w] = v;
@@ -108,7 +108,7 @@ FTC_DEV float block_sum(float v, float* red) {
   return r;
 }
 template <int NT>
-FTC_DEV float block_max(float v, float* red) {
+DEV_INLINE float block_max(float v, float* red) {
   v = wave_max(v);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (lane == 0) red[w] = v;

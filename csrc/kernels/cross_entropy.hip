@@ -15,7 +15,7 @@
 
 using namespace ftc;
 
-FTC_DEV void ms_merge(float& m, float& s, float m2, float s2) {
+DEV_INLINE void ms_merge(float& m, float& s, float m2, float s2) {
   const float mn = fmaxf(m, m2);
   if (mn == -INFINITY) return;
   s = s * __expf(m - mn) + s2 * __expf(m2 - mn);

@@ -62,7 +62,7 @@ extern "C" int ftc_rope(void* qkv, const float* cosT, const float* sinT, const i
   return (int)hipGetLastError();
 }
 
-FTC_DEV float silu_f(float g) { return g / (1.0f + __expf(-g)); }
+DEV_INLINE float silu_f(float g) { return g / (1.0f + __expf(-g)); }
 
 // gu: [rows, 2F] (gate | up), a: [rows, F]
 __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ a,

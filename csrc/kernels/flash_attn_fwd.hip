@@ -64,26 +64,26 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
-FTC_DEV int swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+DEV_INLINE int swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
 
 template <int D>
-FTC_DEV int lds_off(int r, int chunk) {  // byte offset of 16-byte chunk `chunk` of row r
+DEV_INLINE int lds_off(int r, int chunk) {  // byte offset of 16-byte chunk `chunk` of row r
   constexpr int NCH = D / 8;
   return r * (D * 2) + 16 * ((chunk ^ swz(r)) & (NCH - 1));
 }
 
-FTC_DEV bf16x8 as_bf8(const uint4& v) { return __builtin_bit_cast(bf16x8, v); }
+DEV_INLINE bf16x8 as_bf8(const uint4& v) { return __builtin_bit_cast(bf16x8, v); }
 
 // max over lanes l and l ^ 32: v_permlane32_swap (gfx950 VALU, one instruction) instead of
 // ds_bpermute -- the row max sits on the softmax's dependency chain every tile, and the LDS permute's
 // round trip was part of it.
-FTC_DEV float xhalf_max(float v) {
+DEV_INLINE float xhalf_max(float v) {
   const auto pr = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   const float a = __uint_as_float(pr[0]), b = __uint_as_float(pr[1]);
   return a > b ? a : b;  // lane l holds {v_l, v_(l^32)} in some order
 }
 
-FTC_DEV bf16x8 pack_p(const f32x16& p, int base) {
+DEV_INLINE bf16x8 pack_p(const f32x16& p, int base) {
   f32x4 lo = {p[base + 0], p[base + 1], p[base + 2], p[base + 3]};
   f32x4 hi = {p[base + 4], p[base + 5], p[base + 6], p[base + 7]};
   uint4 u;
@@ -109,7 +109,7 @@ struct FwdArgs {
 };
 
 // logical block -> (qb, b, kvh, g) with heavy-first order and GQA groups co-located on one XCD
-FTC_DEV void decode_block(const FwdArgs& a, int& qb, int& b, int& hq, int& kvh) {
+DEV_INLINE void decode_block(const FwdArgs& a, int& qb, int& b, int& hq, int& kvh) {
   const int G = a.H / a.KV;
   const int bid = blockIdx.x;
   const int ngroups = a.nqb * a.B * a.KV;
@@ -135,7 +135,7 @@ FTC_DEV void decode_block(const FwdArgs& a, int& qb, int& b, int& hq, int& kvh) 
 // XOR-swizzled one; toff = the tile's first row (scalar).  A device-only function: the host pass of
 // hipcc cannot instantiate these builtins inside a kernel lambda.
 template <int D, int NGT, int RPG>
-FTC_DEV void fwd_dma(__amdgpu_buffer_rsrc_t kr, __amdgpu_buffer_rsrc_t vr, const int* voff, int toff, char* kdst,
+DEV_INLINE void fwd_dma(__amdgpu_buffer_rsrc_t kr, __amdgpu_buffer_rsrc_t vr, const int* voff, int toff, char* kdst,
                      char* vdst, int wave) {
 #pragma unroll
   for (int i = 0; i < NGT; ++i) {

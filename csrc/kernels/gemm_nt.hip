@@ -81,10 +81,10 @@ struct NTArgs {
   int seq_len, rot_heads;
 };
 
-FTC_DEV int f5(int r) { return (r & 1) | (r & 2) | ((r >> 1) & 4); }
+DEV_INLINE int f5(int r) { return (r & 1) | (r & 2) | ((r >> 1) & 4); }
 
 // logical tile id -> (M block, N block)
-FTC_DEV void tile_of(const NTArgs& p, int l, int& mb, int& nb) {
+DEV_INLINE void tile_of(const NTArgs& p, int l, int& mb, int& nb) {
   const bool mfast = p.group > 0;
   const int g = mfast ? p.group : -p.group;
   const int nf = mfast ? p.nm : p.nn, ns = mfast ? p.nn : p.nm;  // fast / slow block counts
@@ -96,49 +96,25 @@ FTC_DEV void tile_of(const NTArgs& p, int l, int& mb, int& nb) {
 }
 
 // hardware workgroup id -> first logical tile id (bijective on [0, gridDim.x))
-FTC_DEV int xmap(int w, int xcc) {
+DEV_INLINE int xmap(int w, int xcc) {
   const int run = 8 * xcc, within = w & (run - 1);
   return (w - within) + (within & 7) * xcc + (within >> 3);
 }
 
-FTC_DEV bf16x8 rd(const char* s, int off) { return *reinterpret_cast<const bf16x8*>(s + off); }
+DEV_INLINE bf16x8 rd(const char* s, int off) { return *reinterpret_cast<const bf16x8*>(s + off); }
 
-FTC_DEV void barrier() {
+DEV_INLINE void barrier() {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
-}
-
-// Diagnostic build only (tools/gemm_lab/build_stamp.sh defines FTC_GEMM_STAMP; the extension build never
-// does): per-wave cycle sums of the K loop's wait segments for the first 8 workgroups (guide "In-kernel
-// stamps": s_memtime + lgkmcnt(0), placed only where no LDS read is outstanding or right before the
-// lgkmcnt wait that follows anyway -- shares, not exact lengths).
-#ifdef FTC_GEMM_STAMP
-__device__ unsigned long long g_gemm_stamps[8][4][8];  // [block][wave][lgkm1, bar1, lgkm2, bar2, vm, bar3, loop, iters]
-FTC_DEV unsigned long long stamp() {
-  unsigned long long t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-#define FTC_GS(...) __VA_ARGS__
-#else
-#define FTC_GS(...)
-#endif
-
-template <bool NTS, typename T>
-FTC_DEV void st(T* p, const T& v) {
-  if constexpr (NTS) __builtin_nontemporal_store(v, p);
-  else *p = v;
 }
 
 // Epilogue of one wave's 128 x 128: lane holds C[row0 + 16 mt + (lane & 15)][c0 + 32 pr + 8 kc + 0..7] in
 // acc[mt][2 pr] (columns +0..3) and acc[mt][2 pr + 1] (+4..7), kc = lane >> 4: one 16-byte (bf16) / two
 // (fp32) stores per (mt, pr).  With c0 % 128 == 0 the wave's columns are a whole 128-wide head, so
 // RoPE's rotate_half partners (d, d + 64) are pairs pr / pr + 2 of the same lane.
-template <bool F32C, int EPI, bool NTS, bool BETA>
-FTC_DEV void store_w128(const NTArgs& p, const f32x4 (&acc)[8][8], long long row0, long long c0) {
+template <bool F32C, int EPI, bool BETA>
+DEV_INLINE void store_w128(const NTArgs& p, const f32x4 (&acc)[8][8], long long row0, long long c0) {
   // the lane index is re-derived here behind an opaque statement, so the per-lane epilogue addresses
   // are computed at the epilogue instead of being kept live (and spilled) across the K loop
   int lane;
@@ -166,8 +142,8 @@ FTC_DEV void store_w128(const NTArgs& p, const f32x4 (&acc)[8][8], long long row
               v[4 + j] += p.beta * o1[j];
             }
           }
-          st<NTS>(cp, f32x4{v[0], v[1], v[2], v[3]});
-          st<NTS>(cp + 1, f32x4{v[4], v[5], v[6], v[7]});
+          *cp = f32x4{v[0], v[1], v[2], v[3]};
+          cp[1] = f32x4{v[4], v[5], v[6], v[7]};
         } else {
           u32x4* cp = reinterpret_cast<u32x4*>(reinterpret_cast<uint16_t*>(p.c) + off);
           if constexpr (BETA) {
@@ -178,7 +154,7 @@ FTC_DEV void store_w128(const NTArgs& p, const f32x4 (&acc)[8][8], long long row
             for (int j = 0; j < 8; ++j) v[j] += p.beta * f[j];
           }
           const uint4 q = pack8(v);
-          st<NTS>(cp, u32x4{q.x, q.y, q.z, q.w});
+          *cp = u32x4{q.x, q.y, q.z, q.w};
         }
         __builtin_amdgcn_sched_barrier(0);  // one store at a time: no register pile-up beside the live X set
       }
@@ -216,8 +192,8 @@ FTC_DEV void store_w128(const NTArgs& p, const f32x4 (&acc)[8][8], long long row
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           const uint4 w = pack8(v[q]);
-          st<NTS>(reinterpret_cast<u32x4*>(reinterpret_cast<uint16_t*>(p.c) + row * p.ldc + c0 + 64 * q + 32 * h + 8 * kc),
-                  u32x4{w.x, w.y, w.z, w.w});
+          *reinterpret_cast<u32x4*>(reinterpret_cast<uint16_t*>(p.c) + row * p.ldc + c0 + 64 * q + 32 * h + 8 * kc) =
+              u32x4{w.x, w.y, w.z, w.w};
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -229,7 +205,7 @@ FTC_DEV void store_w128(const NTArgs& p, const f32x4 (&acc)[8][8], long long row
 template <bool F32C>
 constexpr int kEpiStores = F32C ? 64 : 32;
 
-template <bool F32C, int EPI, bool NTS, bool BETA, int LP = 0>
+template <bool F32C, int EPI, bool BETA>
 __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(NTArgs p) {
   __shared__ __attribute__((aligned(16))) char S[2 * SS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -269,29 +245,16 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(NTArgs p) {
   // loop never writes M0 right before a DMA (MFMAs separate them: the SALU-write -> LDS-DMA hazard) and
   // needs one SALU per piece.  NOP: a wait state before the load (back-to-back pieces, prologue only).
   // M0 has no other user in this kernel (tests/test_build.py checks the ISA).
-  // LP: the pieces' cache policy (0 default, 1 sc0, 2 sc1, 3 sc0 sc1, 4 nt; Config::load_policy)
-#define FTC_NT_PIECE(POL)                                                                          \
-  if (j < 7)                                                                                       \
-    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen " POL "lds\n\ts_add_u32 m0, m0, 0x400"    \
-                 ::"v"(vo[op][j & 1]), "s"(r), "s"(so[op][j]) : "memory");                       \
-  else                                                                                             \
-    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen " POL "lds\n\ts_mov_b32 m0, %3"            \
-                 ::"v"(vo[op][1]), "s"(r), "s"(so[op][7]), "s"(next) : "memory");
+  // `sc0` cache policy on the pieces (profiles/r4/gemm_nt/policy.log)
   auto dma = [&](int op, __amdgpu_buffer_rsrc_t r, int j, unsigned next, bool nop) __attribute__((always_inline)) {
     if (nop) asm volatile("s_nop 0" ::: "memory");
-    if constexpr (LP == 1) {
-      FTC_NT_PIECE("sc0 ")
-    } else if constexpr (LP == 2) {
-      FTC_NT_PIECE("sc1 ")
-    } else if constexpr (LP == 3) {
-      FTC_NT_PIECE("sc0 sc1 ")
-    } else if constexpr (LP == 4) {
-      FTC_NT_PIECE("nt ")
-    } else {
-      FTC_NT_PIECE("")
-    }
+    if (j < 7)
+      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen sc0 lds\n\ts_add_u32 m0, m0, 0x400"
+                   ::"v"(vo[op][j & 1]), "s"(r), "s"(so[op][j]) : "memory");
+    else
+      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen sc0 lds\n\ts_mov_b32 m0, %3"
+                   ::"v"(vo[op][1]), "s"(r), "s"(so[op][7]), "s"(next) : "memory");
   };
-#undef FTC_NT_PIECE
   static_assert(PSTRIDE == 0x400, "the M0 walk adds one 1 KiB piece");
 
   // prefetch cursor: global stage pg = (tile pi, stage ps); pa / pb = the operands at stage ps of tile pi
@@ -357,7 +320,6 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(NTArgs p) {
     }
   };
   auto nop = [](int) __attribute__((always_inline)) {};
-  FTC_GS(unsigned long long gs[8] = {}; unsigned long long t_a, t_b;)
 
   // one super-stage.  first: the tile's first stage (zero accumulators); after_epi: an epilogue's
   // stores were issued between the DMA of stage g+1 and this iteration's pieces, so the wait for stage
@@ -377,11 +339,8 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(NTArgs p) {
         ya[4 * gi + k] = rd(cur, a_off[1] + (4 * gi + k) * 2048);
       });
     group(xa, xb, 2, first, nop);
-    FTC_GS(t_a = stamp();)
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-    FTC_GS(t_b = stamp(); gs[0] += t_b - t_a;)
     barrier();
-    FTC_GS(t_a = stamp(); gs[1] += t_a - t_b;)
 #pragma unroll
     for (int gi = 3; gi < 7; ++gi)
       group(xa, xb, gi, first, [&](int k) __attribute__((always_inline)) {
@@ -390,11 +349,8 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(NTArgs p) {
         else dma(0, ras, i, dB, false);
       });
     group(xa, xb, 7, first, nop);
-    FTC_GS(t_a = stamp();)
     __builtin_amdgcn_s_waitcnt(0xC07F);
-    FTC_GS(t_b = stamp(); gs[2] += t_b - t_a;)
     barrier();
-    FTC_GS(t_a = stamp(); gs[3] += t_a - t_b;)
     // half 1 on Y: B pieces in groups 0-3, wait for stage g+1, X of g+1 in groups 4-5 (A first: the
     // next iteration's first group needs all of X.A but only X.B[0])
 #pragma unroll
@@ -402,16 +358,13 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(NTArgs p) {
       group(ya, yb, gi, std::false_type{}, [&](int k) __attribute__((always_inline)) {
         if (!(k & 1)) dma(1, rbs, 2 * gi + (k >> 1), dA_next, false);
       });
-    FTC_GS(t_a = stamp();)
     if (after_epi) {
       constexpr int n = 16 + kEpiStores<F32C> > 63 ? 63 : 16 + kEpiStores<F32C>;
       __builtin_amdgcn_s_waitcnt(0x0F70 | (n & 15) | ((n >> 4) << 14));
     } else {
       __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16): the 16 pieces of g+1 landed
     }
-    FTC_GS(t_b = stamp(); gs[4] += t_b - t_a;)
     barrier();
-    FTC_GS(t_a = stamp(); gs[5] += t_a - t_b; gs[7] += 1;)
     group(ya, yb, 4, std::false_type{}, [&](int k) __attribute__((always_inline)) {
       xa[2 * k] = rd(nxt, a_off[0] + 2 * k * 2048);
       xa[2 * k + 1] = rd(nxt, a_off[0] + (2 * k + 1) * 2048);
@@ -448,40 +401,30 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_kernel(NTArgs p) {
     xb[i] = rd(S, b_off[0] + bnt(i));
   }
 
-  FTC_GS(const unsigned long long t_loop = stamp();)
   int g = 0;
   for (int ti = 0; ti < my; ++ti) {
     iteration(g++, std::true_type{}, ti > 0);
     for (int s = 1; s < ns; ++s) iteration(g++, std::false_type{}, false);
     int mb, nb;
     tile_of(p, lw + ti * G, mb, nb);
-    store_w128<F32C, EPI, NTS, BETA>(p, acc, (long long)mb * BM + wm * 128, (long long)nb * BN + wn * 128);
+    store_w128<F32C, EPI, BETA>(p, acc, (long long)mb * BM + wm * 128, (long long)nb * BN + wn * 128);
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no LDS-DMA may outlive the workgroup
-#ifdef FTC_GEMM_STAMP
-  gs[6] = stamp() - t_loop;
-  if (blockIdx.x < 8 && lane == 0)
-    for (int i = 0; i < 8; ++i) g_gemm_stamps[blockIdx.x][wave][i] = gs[i];
-#endif
 }
 
 // ---- launch configuration ----------------------------------------------------------------------------
+// Measured and fixed (profiles/r4/gemm_nt.md, gemm_nt/policy.log): one persistent workgroup per CU, N-fast
+// groups of 8 blocks, XCD runs of 32 logical ids, plain C stores (non-temporal: no gain), `sc0` on the
+// operand DMA (+0.1-2.4 % over the default policy; sc1 / sc0 sc1 equal, nt -20-30 %).  The grid cap / order
+// stay settable for tools/bench_gemm_nt.py and the multi-tile tests (ftc_gemm_nt_config).
 struct Config {
   int grid_cap;  // persistent grid: min(tiles, grid_cap) workgroups (0: number of CUs)
   int group;     // tile order, see NTArgs
   int xcc;
-  int nt_store;     // non-temporal C stores
-  int load_policy;  // cache policy of the operand DMA: 0 default, 1 sc0, 2 sc1, 3 sc0 sc1, 4 nt
 };
 
 Config& config() {
-  static Config c = [] {
-    // load policy sc0 (1): +0.1-2.4 % over the default policy on the headline shapes (profiles/r4/gemm_nt/policy.log)
-    Config d{0, -8, 32, 0, 1};
-    if (const char* e = getenv("FTC_GEMM_NT_ORDER"))
-      sscanf(e, "%d,%d,%d,%d,%d", &d.grid_cap, &d.group, &d.xcc, &d.nt_store, &d.load_policy);
-    return d;
-  }();
+  static Config c{0, -8, 32};
   return c;
 }
 
@@ -504,40 +447,20 @@ int launch(NTArgs& p, hipStream_t stream) {
   int xcc = c.xcc > 0 ? c.xcc : 1;
   while (xcc > 1 && grid % (8 * xcc)) xcc >>= 1;  // xmap must be a bijection on [0, grid)
   if (grid % 8) xcc = 1;
-  int grp = c.group == 0 ? 1 : c.group;
-  p.group = grp;
+  p.group = c.group == 0 ? 1 : c.group;
   p.xcc = xcc;
-  const bool beta = EPI == EPI_STORE && p.beta != 0.f;
-  if (beta)  // (accumulating calls: tests / rare paths -- default store policy)
-    hipLaunchKernelGGL((gemm_nt_kernel<F32C, EPI, false, EPI == EPI_STORE>), dim3(grid), dim3(256), 0, stream, p);
-  else if (c.nt_store)
-    hipLaunchKernelGGL((gemm_nt_kernel<F32C, EPI, true, false>), dim3(grid), dim3(256), 0, stream, p);
-  else if (c.load_policy == 1)
-    hipLaunchKernelGGL((gemm_nt_kernel<F32C, EPI, false, false, 1>), dim3(grid), dim3(256), 0, stream, p);
-  else if (c.load_policy == 2)
-    hipLaunchKernelGGL((gemm_nt_kernel<F32C, EPI, false, false, 2>), dim3(grid), dim3(256), 0, stream, p);
-  else if (c.load_policy == 3)
-    hipLaunchKernelGGL((gemm_nt_kernel<F32C, EPI, false, false, 3>), dim3(grid), dim3(256), 0, stream, p);
-  else if (c.load_policy == 4)
-    hipLaunchKernelGGL((gemm_nt_kernel<F32C, EPI, false, false, 4>), dim3(grid), dim3(256), 0, stream, p);
+  if (EPI == EPI_STORE && p.beta != 0.f)  // accumulating calls: tests / rare paths
+    hipLaunchKernelGGL((gemm_nt_kernel<F32C, EPI, true>), dim3(grid), dim3(256), 0, stream, p);
   else
-    hipLaunchKernelGGL((gemm_nt_kernel<F32C, EPI, false, false>), dim3(grid), dim3(256), 0, stream, p);
+    hipLaunchKernelGGL((gemm_nt_kernel<F32C, EPI, false>), dim3(grid), dim3(256), 0, stream, p);
   return (int)hipGetLastError();
 }
 
 }  // namespace
 
-// Launch configuration of every later call (tools/bench_gemm_nt.py sweeps it in one process):
-// grid_cap (0 = CU count), group (> 0 M-fast, < 0 N-fast), xcc, nt_store, load_policy.
-extern "C" void ftc_gemm_nt_config(int grid_cap, int group, int xcc, int nt_store, int load_policy) {
-  config() = Config{grid_cap, group, xcc, nt_store, load_policy};
-}
-
-#ifdef FTC_GEMM_STAMP
-extern "C" int ftc_gemm_nt_stamps(unsigned long long* host) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_stamps), sizeof(g_gemm_stamps));
-}
-#endif
+// Launch configuration of every later call (tools/bench_gemm_nt.py, tests): grid_cap (0 = CU count),
+// group (> 0 M-fast, < 0 N-fast), xcc.
+extern "C" void ftc_gemm_nt_config(int grid_cap, int group, int xcc) { config() = Config{grid_cap, group, xcc}; }
 
 // C[M, N] (ldc) = alpha A B^T + beta C; A [M, K] (lda), B [N, K] (ldb) bf16 row-major, K contiguous.
 // Returns 0 when the shape / alignment is outside the kernel's contract.

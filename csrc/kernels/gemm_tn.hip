@@ -48,20 +48,20 @@ constexpr int STAGE = 4 * IMG;     // A lo | A hi | B lo | B hi
 // spreads the 4 rows a 32-lane half reads over the 4 quarters of the bank row -- conflict-free -- and
 // rows r and r + 8 (the two reads of a fragment) share one swizzle, so a fragment costs ONE address
 // register (+2048 immediate) and a DMA piece's source columns do not depend on its row block.
-FTC_DEV int swz(int r) { return (r & 3) << 2; }
-FTC_DEV int img_off(int r, int chunk) { return r * 256 + 16 * ((chunk ^ swz(r)) & 15); }
+DEV_INLINE int swz(int r) { return (r & 3) << 2; }
+DEV_INLINE int img_off(int r, int chunk) { return r * 256 + 16 * ((chunk ^ swz(r)) & 15); }
 
 // A/B fragment (32 cols x 16 k, permuted k) by two transposed reads: lane l gets column colbase +
 // (l & 31), k = kb + 4 (l >> 5) + {0..3} from the first read and + 8 + {0..3} from the second; both
 // operands use the same permutation, so the MFMA's k-sum is unchanged.
-FTC_DEV int tr_offset(int colbase, int lane) {
+DEV_INLINE int tr_offset(int colbase, int lane) {
   const int hh = lane >> 5, gi = (lane >> 4) & 3, li = lane & 15;
   const int trq = li >> 2, trp = li & 3;
   const int col = colbase + 16 * (gi & 1) + 4 * trp;
   const int chunk = col >> 3, half8 = (col & 7) ? 8 : 0;
   return img_off(4 * hh + trq, chunk) + half8;  // row r1; row r1 + 8 is +2048 (same swizzle)
 }
-FTC_DEV bf16x8 tr_read(const char* img, int kb, int off) {
+DEV_INLINE bf16x8 tr_read(const char* img, int kb, int off) {
   s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + off + kb * 256));
   s16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + off + kb * 256 + 2048));
   s16x8 va = {v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
@@ -75,8 +75,6 @@ struct GemmTNArgs {
   long long lda, ldb, ldc;
   int K, nm, nn;
   float alpha, beta;
-  int mode;  // diagnostics (FTC_GEMM_TN_MODE in an FTC_EXPERIMENTS build only; 0 in the extension): 1 no DMA wait, 2 no DMA,
-             // 8 every DMA re-reads K-step 0 (L2-resident operands)
   int group_m;  // M-blocks per tile group (XCD-local operand reuse)
   long long cstride;  // split-K: elements between the splits' C (fp32 partial) matrices; K = one split's rows
 };
@@ -87,7 +85,7 @@ struct GemmTNArgs {
 // draining the DMA that is meant to fly under the MFMAs; here the one explicit vmcnt(0) before each
 // barrier is the only wait.  M0 is saved / restored inside the statement (guide: compiler-reserved);
 // s_nop 4 covers an SGPR operand written by v_readfirstlane just before.
-FTC_DEV void glds16(__amdgpu_buffer_rsrc_t r, const char* lds, int voff, int soff) {
+DEV_INLINE void glds16(__amdgpu_buffer_rsrc_t r, const char* lds, int voff, int soff) {
   const unsigned dst = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)lds;
   unsigned keep;
   asm volatile(
@@ -100,7 +98,7 @@ FTC_DEV void glds16(__amdgpu_buffer_rsrc_t r, const char* lds, int voff, int sof
 
 // The same piece without the leading s_nop 4 (its operands are SALU-computed long before: no
 // readfirstlane -> SGPR hazard to cover); used inside the K loop of the spread schedule.
-FTC_DEV void glds16_fast(__amdgpu_buffer_rsrc_t r, const char* lds, int voff, int soff) {
+DEV_INLINE void glds16_fast(__amdgpu_buffer_rsrc_t r, const char* lds, int voff, int soff) {
   const unsigned dst = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)lds;
   unsigned keep;
   asm volatile(
@@ -116,7 +114,7 @@ FTC_DEV void glds16_fast(__amdgpu_buffer_rsrc_t r, const char* lds, int voff, in
 // (r & 3) << 2 swizzle every lane's row phase is lane >> 4 whatever the piece, so one source offset
 // per matrix serves all PW pieces (+ 4 j rows as the scalar offset).
 template <int NW>
-FTC_DEV void tn_dma(__amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int voa, int vob, int sa4, int sb4,
+DEV_INLINE void tn_dma(__amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int voa, int vob, int sa4, int sb4,
                     char* stage, int wave) {
   constexpr int PW = 32 / NW;
   const int c0 = wave * PW;
@@ -128,19 +126,19 @@ FTC_DEV void tn_dma(__amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int vo
   }
 }
 
-// NW = 8: 2 (M) x 4 (N) waves of 128 x 64, two waves per SIMD (256 registers each).
-// NW = 4: 2 x 2 waves of 128 x 128, one wave per SIMD (512 registers; the 256 accumulator registers
-//         live in AGPRs): per MFMA a wave reads 1 fragment instead of 1.5, which takes the LDS array
-//         (tr reads + the DMA's writes) from ~90 % to ~60 % of the MFMA time per K-step.
-// SCHED = 1 (NW = 4, the default since round 3): the K-step's DMA is spread over its four 16-deep
-// phases.  Rows 16 q .. 16 q + 15 of an image feed only k-step q, so once every wave has read k-step q
+// 2 x 2 waves of 128 x 128, one wave per SIMD (512 registers; the 256 accumulator registers live in
+// AGPRs): per MFMA a wave reads 1 fragment instead of 1.5 for 8 waves of 128 x 64 (measured slower and
+// removed), which takes the LDS array (tr reads + the DMA's writes) from ~90 % to ~60 % of the MFMA
+// time per K-step.  The K-step's DMA is spread over its four 16-deep phases (the round-2 schedule -- one
+// 16-piece burst behind the step's single barrier -- is in git history).  Rows 16 q .. 16 q + 15 of an image feed only k-step q, so once every wave has read k-step q
 // (lgkmcnt(0) + a barrier at the start of phase q + 1) the pieces covering those rows may be refilled
 // with step kt + 2: 4 pieces at phase 1 (k-step 0's rows), 4 at phase 2, 8 at phase 3, each one
 // between MFMAs instead of a 16-piece burst behind the step's single barrier (whose issue cost -- M0
 // save / restore, s_nop -- left the matrix pipe idle); the next step's buffer is waited for with a
 // counted vmcnt (this step's pieces stay in flight) before the last phase reads its k-step 0.
-template <bool F32C, int NW, int SCHED = 0>
-__global__ __launch_bounds__(NW * 64, 1) void gemm_tn_kernel(GemmTNArgs p) {
+template <bool F32C>
+__global__ __launch_bounds__(256, 1) void gemm_tn_kernel(GemmTNArgs p) {
+  constexpr int NW = 4;
   constexpr int WN = NW / 2;         // waves along N
   constexpr int WNC = BN / WN;       // columns per wave: 64 or 128
   constexpr int NT = WNC / 32;       // 32-wide accumulator tiles along N: 2 or 4
@@ -186,7 +184,6 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_tn_kernel(GemmTNArgs p) {
   const uint16_t* abase = p.a + m0 + (long long)ks * p.K * p.lda;
   const uint16_t* bbase = p.b + n0 + (long long)ks * p.K * p.ldb;
   auto issue = [&](int kt, char* stage) {
-    if (p.mode & 8) kt = 0;
     const auto ra = make_rsrc(abase + (long long)kt * BK * p.lda);
     const auto rb = make_rsrc(bbase + (long long)kt * BK * p.ldb);
     tn_dma<NW>(ra, rb, voa, vob, sa4, sb4, stage, wave);
@@ -236,31 +233,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_tn_kernel(GemmTNArgs p) {
   };
   const int nk = p.K / BK;
   bf16x8 pa[4], pb[NT], qa[4], qb[NT];
-  // step kt (tile kt in `cur`, its k-step 0 already in P):
-  //   [read 1 -> Q | MFMA P] [read 2 -> P | MFMA Q] [read 3 -> Q | MFMA P]
-  //   vmcnt(0) barrier [DMA kt+2 -> cur | read 0 of kt+1 -> P | MFMA Q]
-  // The barrier sits before the last phase: every wave's reads of `cur` are complete (lgkmcnt(0)), so
-  // tile kt + 2 may be DMA'd into it, and tile kt + 1 (DMA'd one step earlier, vmcnt(0)) is visible.
-  auto step = [&](int kt, char* cur, const char* nxt) __attribute__((always_inline)) {
-    lgkm0();
-    read_k(cur, 1, qa, qb);
-    mfma_k(pa, pb);
-    lgkm0();
-    read_k(cur, 2, pa, pb);
-    mfma_k(qa, qb);
-    lgkm0();
-    read_k(cur, 3, qa, qb);
-    mfma_k(pa, pb);
-    lgkm0();
-    if (!(p.mode & 1)) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (kt + 2 < nk && !(p.mode & 2)) issue(kt + 2, cur);
-    if (kt + 1 < nk) read_k(nxt, 0, pa, pb);
-    mfma_k(qa, qb);
-  };
-  if constexpr (SCHED == 1) {
-    static_assert(NW == 4, "spread schedule: one wave per SIMD");
+  {
     // refill mapping: the 8 pieces (4 rows each) of k-step q's 16 rows across both half images are
     // split 2 per wave -- wave w takes half image w >> 1, rows 16 q + 8 (w & 1) + 4 e (e = 0, 1) -- so
     // every wave issues the same pieces in the same phase (no wave-dependent branch around the
@@ -275,8 +248,8 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_tn_kernel(GemmTNArgs p) {
     const int dst2 = (wave >> 1) * IMG + 2 * (wave & 1) * 1024;
     // piece (q, e) of step kt2 into `stage`
     auto piece = [&](int kt2, char* stage, int q, int e) __attribute__((always_inline)) {
-      if (kt2 >= nk || (p.mode & 2)) return;
-      const int kk = (p.mode & 8) ? 0 : kt2;
+      if (kt2 >= nk) return;
+      const int kk = kt2;
       const auto ra = make_rsrc(abase + (long long)kk * BK * p.lda);
       const auto rb = make_rsrc(bbase + (long long)kk * BK * p.ldb);
       const int off = (4 * q + e) * 1024;
@@ -343,26 +316,14 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_tn_kernel(GemmTNArgs p) {
         piece(kt + 2, cur, q23b[1], e23b[1]);
       }
       __builtin_amdgcn_sched_barrier(0);
-      if (!(p.mode & 1)) {
-        if (kt + 2 < nk && !(p.mode & 2)) __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
-        else __builtin_amdgcn_s_waitcnt(0x0F70);                             // vmcnt(0)
-      }
+      if (kt + 2 < nk) __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
+      else __builtin_amdgcn_s_waitcnt(0x0F70);             // vmcnt(0)
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       if (kt + 1 < nk) read_k(nxt, 0, pa, pb);
       mfma_pieces(qa, qb, 2, 4, kt + 2, cur, q23, e23, 0);
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // no DMA may land after the workgroup ends
-  } else {
-    issue(0, S);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    __builtin_amdgcn_s_barrier();
-    if (nk > 1) issue(1, S + STAGE);
-    read_k(S, 0, pa, pb);
-    for (int kt = 0; kt < nk; ++kt) {
-      const int so = (kt & 1) * STAGE;
-      step(kt, S + so, S + (STAGE - so));
-    }
   }
 
   // ---- epilogue: lane holds C[m0 + wm 128 + mt 32 + 8 (r >> 2) + 4 hh + (r & 3)][n0 + wn WNC + nt 32 + lr];
@@ -416,49 +377,12 @@ extern "C" int ftc_gemm_tn_ok(const void* a, long long lda, const void* b, long 
 extern "C" int ftc_gemm_tn(const void* a, long long lda, const void* b, long long ldb, void* c, long long ldc,
                            int c_fp32, int M, int N, int K, float alpha, float beta, hipStream_t stream) {
   if (!ftc_gemm_tn_ok(a, lda, b, ldb, c, ldc, M, N, K)) return -1;
-#ifdef FTC_EXPERIMENTS  // timing-only modes with wrong results: tools builds only, never the extension
-  static const int mode = [] {
-    const char* e = getenv("FTC_GEMM_TN_MODE");
-    return e ? atoi(e) : 0;
-  }();
-#else
-  constexpr int mode = 0;
-#endif
-  static const int group_m = [] {
-    const char* e = getenv("FTC_GEMM_TN_GROUP");
-    return e ? atoi(e) : 4;
-  }();
-  GemmTNArgs p{(const uint16_t*)a, (const uint16_t*)b, c, lda, ldb, ldc, K, M / BM, N / BN, alpha, beta, mode,
-               group_m > 0 ? group_m : 4, 0};
+  GemmTNArgs p{(const uint16_t*)a, (const uint16_t*)b, c, lda, ldb, ldc, K, M / BM, N / BN, alpha, beta, 4, 0};
   const int grid = p.nm * p.nn;
-  // FTC_GEMM_TN_WAVES=8: the two-waves-per-SIMD variant (A/B only)
-  static const int waves = [] {
-    const char* e = getenv("FTC_GEMM_TN_WAVES");
-    return (e && e[0] == '8') ? 8 : 4;
-  }();
-  if (waves == 8) {
-    if (c_fp32)
-      hipLaunchKernelGGL((gemm_tn_kernel<true, 8>), dim3(grid), dim3(512), 0, stream, p);
-    else
-      hipLaunchKernelGGL((gemm_tn_kernel<false, 8>), dim3(grid), dim3(512), 0, stream, p);
-  } else {
-    // FTC_GEMM_TN_SCHED=0: the round-2 schedule (one 16-piece DMA burst behind one barrier per step)
-    static const int sched = [] {
-      const char* e = getenv("FTC_GEMM_TN_SCHED");
-      return (e && e[0] == '0') ? 0 : 1;
-    }();
-    if (sched == 1) {
-      if (c_fp32)
-        hipLaunchKernelGGL((gemm_tn_kernel<true, 4, 1>), dim3(grid), dim3(256), 0, stream, p);
-      else
-        hipLaunchKernelGGL((gemm_tn_kernel<false, 4, 1>), dim3(grid), dim3(256), 0, stream, p);
-    } else {
-      if (c_fp32)
-        hipLaunchKernelGGL((gemm_tn_kernel<true, 4>), dim3(grid), dim3(256), 0, stream, p);
-      else
-        hipLaunchKernelGGL((gemm_tn_kernel<false, 4>), dim3(grid), dim3(256), 0, stream, p);
-    }
-  }
+  if (c_fp32)
+    hipLaunchKernelGGL((gemm_tn_kernel<true>), dim3(grid), dim3(256), 0, stream, p);
+  else
+    hipLaunchKernelGGL((gemm_tn_kernel<false>), dim3(grid), dim3(256), 0, stream, p);
   return (int)hipGetLastError();
 }
 
@@ -469,14 +393,10 @@ extern "C" int ftc_gemm_tn(const void* a, long long lda, const void* b, long lon
 extern "C" int ftc_gemm_tn_split(const void* a, long long lda, const void* b, long long ldb, float* parts, int M, int N,
                                  int K, int splits, hipStream_t stream) {
   if (splits < 1 || K % splits || !ftc_gemm_tn_ok(a, lda, b, ldb, parts, N, M, N, K / splits)) return -1;
-  static const int group_m = [] {
-    const char* e = getenv("FTC_GEMM_TN_GROUP");
-    return e ? atoi(e) : 4;
-  }();
-  GemmTNArgs p{(const uint16_t*)a, (const uint16_t*)b, parts, lda, ldb, N, K / splits, M / BM, N / BN, 1.0f, 0.0f, 0,
-               group_m > 0 ? group_m : 4, (long long)M * N};
+  GemmTNArgs p{(const uint16_t*)a, (const uint16_t*)b, parts, lda, ldb, N, K / splits, M / BM, N / BN, 1.0f, 0.0f, 4,
+               (long long)M * N};
   const long long grid = (long long)p.nm * p.nn * splits;
   if (grid > 0x7fffffffLL) return -1;
-  hipLaunchKernelGGL((gemm_tn_kernel<true, 4, 1>), dim3((unsigned)grid), dim3(256), 0, stream, p);
+  hipLaunchKernelGGL((gemm_tn_kernel<true>), dim3((unsigned)grid), dim3(256), 0, stream, p);
   return (int)hipGetLastError();
 }

@@ -26,9 +26,9 @@ constexpr int MB = 128;  // X columns per workgroup (32 per wave)
 constexpr int TT = 64;   // rows per LDS tile
 constexpr int RW = 64;   // Y image width (r padded to 64, zero-filled past r)
 
-FTC_DEV int swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+DEV_INLINE int swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
 template <int W>
-FTC_DEV int img_off(int row, int chunk) {  // byte offset of 16-byte chunk `chunk` of image row `row`
+DEV_INLINE int img_off(int row, int chunk) {  // byte offset of 16-byte chunk `chunk` of image row `row`
   constexpr int NCH = W / 8;
   return row * (W * 2) + 16 * ((chunk ^ swz(row)) & (NCH - 1));
 }
@@ -36,7 +36,7 @@ FTC_DEV int img_off(int row, int chunk) {  // byte offset of 16-byte chunk `chun
 // lane l gets column colbase + (l & 31), rows {4h..4h+3} then {4h+8..4h+11} (h = l >> 5).  The
 // swizzle depends on row & 15 only, so a k base that is a multiple of 16 is a plain row offset.
 template <int W>
-FTC_DEV int2 tr_offsets(int colbase, int lane) {
+DEV_INLINE int2 tr_offsets(int colbase, int lane) {
   const int hh = lane >> 5, gi = (lane >> 4) & 3, li = lane & 15;
   const int col = colbase + 16 * (gi & 1) + 4 * (li & 3);
   const int chunk = col >> 3, half8 = (col & 7) ? 8 : 0;
@@ -44,7 +44,7 @@ FTC_DEV int2 tr_offsets(int colbase, int lane) {
   return make_int2(img_off<W>(r1, chunk) + half8, img_off<W>(r1 + 8, chunk) + half8);
 }
 template <int W>
-FTC_DEV bf16x8 tr_read(const char* img, int kb, int2 off) {
+DEV_INLINE bf16x8 tr_read(const char* img, int kb, int2 off) {
   s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + off.x + kb * W * 2));
   s16x4 v2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + off.y + kb * W * 2));
   s16x8 va = {v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
@@ -60,7 +60,7 @@ struct Segs {
   int ycol[4];
   int ocol[4];
 };
-FTC_DEV int seg_of(const Segs& sg, int m) {
+DEV_INLINE int seg_of(const Segs& sg, int m) {
   int i = 0;
 #pragma unroll
   for (int k = 0; k < 3; ++k) i += (k + 1 < sg.n && m >= sg.m_end[k]) ? 1 : 0;
@@ -225,15 +225,15 @@ extern "C" int ftc_lora_wgrad(const void* x, long long ldx, const void* y, long 
   const long long n = (long long)M * R;
   const dim3 rg((unsigned)((n / 4 + 255) / 256));
   auto out16 = (uint16_t*)out;
-#define FTC_RED(SP)                                                                                       \
+#define RED_CASE(SP)                                                                                       \
   case SP:                                                                                                \
     hipLaunchKernelGGL(lora_wgrad_reduce_kernel<SP>, rg, dim3(256), 0, stream, ws, M, R, out16, out_sm, out_sr, \
                        alpha, beta, sg);                                                                  \
     break;
   switch (splits) {
-    FTC_RED(1) FTC_RED(2) FTC_RED(4) FTC_RED(8) FTC_RED(16) FTC_RED(32) FTC_RED(64)
+    RED_CASE(1) RED_CASE(2) RED_CASE(4) RED_CASE(8) RED_CASE(16) RED_CASE(32) RED_CASE(64)
     default: return -1;
   }
-#undef FTC_RED
+#undef RED_CASE
   return (int)hipGetLastError();
 }

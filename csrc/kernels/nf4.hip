@@ -30,12 +30,12 @@ __constant__ float kNF4[16] = {-1.0f,
 // The codebook indexed per lane from __constant__ memory compiles to one global load per element (16
 // vector-memory loads per 8 bytes of codes: the dequant kernels ran at 2.5 TB/s).  Each workgroup
 // copies it to LDS once; a lookup is then one conflict-free ds_read (16 entries, 16 banks).
-FTC_DEV void nf4_lut_load(float* lut) {
+DEV_INLINE void nf4_lut_load(float* lut) {
   if (threadIdx.x < 16) lut[threadIdx.x] = kNF4[threadIdx.x];
   __syncthreads();
 }
 
-FTC_DEV int nf4_encode(float x) {
+DEV_INLINE int nf4_encode(float x) {
   // nearest codebook entry (midpoints between consecutive codes)
   int best = 0;
   float bd = fabsf(x - kNF4[0]);
@@ -66,7 +66,7 @@ struct AugTail {
   int N, R, K, a_t;
 };
 
-FTC_DEV void aug_tail_fill(const AugTail& t, long long i0, long long stride) {
+DEV_INLINE void aug_tail_fill(const AugTail& t, long long i0, long long stride) {
   const long long nb = t.B ? (long long)t.N * t.R : 0;
   const long long na = t.A ? (long long)t.R * t.K : 0;
   for (long long i = i0; i < nb + na; i += stride) {

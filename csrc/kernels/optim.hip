@@ -14,29 +14,29 @@
 using namespace ftc;
 
 template <typename G>
-FTC_DEV void load_grad4(const G* g, long long i, float* o);
+DEV_INLINE void load_grad4(const G* g, long long i, float* o);
 template <>
-FTC_DEV void load_grad4<float>(const float* g, long long i, float* o) {
+DEV_INLINE void load_grad4<float>(const float* g, long long i, float* o) {
   const float4 v = reinterpret_cast<const float4*>(g)[i];
   o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
 }
 template <>
-FTC_DEV void load_grad4<uint16_t>(const uint16_t* g, long long i, float* o) {
+DEV_INLINE void load_grad4<uint16_t>(const uint16_t* g, long long i, float* o) {
   const uint2 v = reinterpret_cast<const uint2*>(g)[i];
   o[0] = bf_lo(v.x); o[1] = bf_hi(v.x); o[2] = bf_lo(v.y); o[3] = bf_hi(v.y);
 }
 template <typename G>
-FTC_DEV float load_grad1(const G* g, long long i);
+DEV_INLINE float load_grad1(const G* g, long long i);
 template <>
-FTC_DEV float load_grad1<float>(const float* g, long long i) { return g[i]; }
+DEV_INLINE float load_grad1<float>(const float* g, long long i) { return g[i]; }
 template <>
-FTC_DEV float load_grad1<uint16_t>(const uint16_t* g, long long i) { return bf2f(g[i]); }
+DEV_INLINE float load_grad1<uint16_t>(const uint16_t* g, long long i) { return bf2f(g[i]); }
 
 struct AdamHP {
   float lr, b1, b2, eps, wd, bc1, bc2;  // bc = 1 - beta^t
 };
 
-FTC_DEV void adam_elem(float& p, float& m, float& v, float g, const AdamHP& hp) {
+DEV_INLINE void adam_elem(float& p, float& m, float& v, float g, const AdamHP& hp) {
   m = hp.b1 * m + (1.f - hp.b1) * g;
   v = hp.b2 * v + (1.f - hp.b2) * g * g;
   const float mh = m / hp.bc1;
@@ -59,9 +59,12 @@ __global__ __launch_bounds__(256) void adamw_kernel(uint16_t* __restrict__ param
   // one 4-element group per thread over a one-shot grid: 5.91 vs 5.62 TB/s for the grid-stride loop
   // (2048 workgroups) at 8.03 B elements, 38.1 vs 40.0 ms (profiles/r4/adamw/; an 8-wide group read
   // 5.67)
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  // one pass when the launch covers the tensor (the usual case); the loop keeps a capped grid correct
+  // (ftc_adamw caps it so grid x 256 stays below HIP's 2^32 work items per launch)
+  const long long i0 = (long long)blockIdx.x * 256 + threadIdx.x;
   const long long n4 = n >> 2;
-  if (i < n4) {
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long i = i0; i < n4; i += stride) {
     float g[4];
     load_grad4<G>(grad, i, g);
     float4 P = reinterpret_cast<float4*>(master)[i];
@@ -81,7 +84,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(uint16_t* __restrict__ param
       reinterpret_cast<uint2*>(param)[i] = o;
     }
   }
-  const long long t = (n4 << 2) + i;  // tail (n % 4): the first threads of the grid
+  const long long t = (n4 << 2) + i0;  // tail (n % 4): the first threads of the grid
   if (t < n) {
     float P = master[t], M = m[t], Vv = v[t];
     adam_elem(P, M, Vv, load_grad1<G>(grad, t) * sc, hp);
@@ -95,7 +98,9 @@ extern "C" int ftc_adamw(void* param_bf16, float* master, float* m, float* v, co
                          const float* gscale, const float* hpdev, hipStream_t stream) {
   AdamHP hp{lr, b1, b2, eps, wd, bc1, bc2};
   const long long groups = n >> 2 > 0 ? n >> 2 : 1;
-  const dim3 grid((unsigned)((groups + 255) / 256));
+  long long blocks = (groups + 255) / 256;
+  if (blocks > (1LL << 24) - 1) blocks = (1LL << 24) - 1;  // grid x 256 < 2^32: larger tensors loop
+  const dim3 grid((unsigned)blocks);
   if (grad_is_fp32)
     hipLaunchKernelGGL((adamw_kernel<float>), dim3(grid), dim3(256), 0, stream, (uint16_t*)param_bf16, master, m, v,
                        (const float*)grad, n, hp, gscale, hpdev);
@@ -108,7 +113,7 @@ extern "C" int ftc_adamw(void* param_bf16, float* master, float* m, float* v, co
 // ---- sum of squares (grad-norm) : deterministic two-stage reduction ----
 // 16-byte loads (8 bf16 / 4 fp32 per lane), two independent loads in flight per lane per iteration:
 // the full-FT gradient (16 GB bf16) streams at HBM rate (the 8-byte-per-lane version read 3.7 TB/s).
-FTC_DEV float sumsq16(const uint4 v, const uint16_t*) {
+DEV_INLINE float sumsq16(const uint4 v, const uint16_t*) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
   float s = 0.f;
 #pragma unroll
@@ -118,7 +123,7 @@ FTC_DEV float sumsq16(const uint4 v, const uint16_t*) {
   }
   return s;
 }
-FTC_DEV float sumsq16(const uint4 v, const float*) {
+DEV_INLINE float sumsq16(const uint4 v, const float*) {
   const float a = __uint_as_float(v.x), b = __uint_as_float(v.y), c = __uint_as_float(v.z),
               d = __uint_as_float(v.w);
   return a * a + b * b + c * c + d * d;

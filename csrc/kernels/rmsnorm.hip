@@ -347,20 +347,17 @@ extern "C" int ftc_rmsnorm_fwd(const void* x, const void* res, const void* w, vo
   auto W = (const uint16_t*)w;
   auto H = (uint16_t*)h_out;
   auto Y = (uint16_t*)y;
-#define FTC_LAUNCH_FWD(NV)                                                                                    \
+#define LAUNCH_FWD(NV)                                                                                    \
   if (res)                                                                                                    \
     hipLaunchKernelGGL((rmsnorm_fwd_kernel<NV, true>), dim3(grid), dim3(256), 0, stream, X, R, W, H, Y, rstd, \
                        rows, d, eps, y_rs);                                                                         \
   else                                                                                                        \
     hipLaunchKernelGGL((rmsnorm_fwd_kernel<NV, false>), dim3(grid), dim3(256), 0, stream, X, R, W, H, Y,     \
                        rstd, rows, d, eps, y_rs);
-  static const bool two = [] {
-    const char* e = getenv("FTC_RMSNORM_FWD2");
-    return !(e && e[0] == '0');
-  }();
-  if (two && nv >= 2) {
+  // two waves per row wherever a row has >= 2 vectors per lane (the one-wave kernel: d <= 512)
+  if (nv >= 2) {
     const int g2 = rms_grid(rows, 2);
-#define FTC_LAUNCH_FWD2(NV2)                                                                                     \
+#define LAUNCH_FWD2(NV2)                                                                                     \
   if (res)                                                                                                       \
     hipLaunchKernelGGL((rmsnorm_fwd2_kernel<NV2, true>), dim3(g2), dim3(256), 0, stream, X, R, W, H, Y, rstd, rows, \
                        d, eps, y_rs);                                                                            \
@@ -368,24 +365,24 @@ extern "C" int ftc_rmsnorm_fwd(const void* x, const void* res, const void* w, vo
     hipLaunchKernelGGL((rmsnorm_fwd2_kernel<NV2, false>), dim3(g2), dim3(256), 0, stream, X, R, W, H, Y, rstd,     \
                        rows, d, eps, y_rs);
     switch (nv) {
-      case 2: FTC_LAUNCH_FWD2(1); break;
-      case 4: FTC_LAUNCH_FWD2(2); break;
-      case 8: FTC_LAUNCH_FWD2(4); break;
-      case 16: FTC_LAUNCH_FWD2(8); break;
+      case 2: LAUNCH_FWD2(1); break;
+      case 4: LAUNCH_FWD2(2); break;
+      case 8: LAUNCH_FWD2(4); break;
+      case 16: LAUNCH_FWD2(8); break;
       default: return -1;
     }
-#undef FTC_LAUNCH_FWD2
+#undef LAUNCH_FWD2
     return (int)hipGetLastError();
   }
   switch (nv) {
-    case 1: FTC_LAUNCH_FWD(1); break;
-    case 2: FTC_LAUNCH_FWD(2); break;
-    case 4: FTC_LAUNCH_FWD(4); break;
-    case 8: FTC_LAUNCH_FWD(8); break;
-    case 16: FTC_LAUNCH_FWD(16); break;
+    case 1: LAUNCH_FWD(1); break;
+    case 2: LAUNCH_FWD(2); break;
+    case 4: LAUNCH_FWD(4); break;
+    case 8: LAUNCH_FWD(8); break;
+    case 16: LAUNCH_FWD(16); break;
     default: return -1;
   }
-#undef FTC_LAUNCH_FWD
+#undef LAUNCH_FWD
   return (int)hipGetLastError();
 }
 
@@ -406,26 +403,22 @@ extern "C" int ftc_rmsnorm_bwd(const void* dy, const void* h, const void* w, con
   auto W = (const uint16_t*)w;
   auto DR = (const uint16_t*)dres;
   auto DX = (uint16_t*)dx;
-#define FTC_LAUNCH_BWD(NV, DWB, DRB)                                                                       \
+#define LAUNCH_BWD(NV, DWB, DRB)                                                                       \
   hipLaunchKernelGGL((rmsnorm_bwd_kernel<NV, DWB, DRB>), dim3(grid), dim3(256), lds, stream, DY, Hh, W, rstd, \
                      DR, DX, dw_part, rows, d, dres_rs, dx_rs)
-#define FTC_LAUNCH_BWD_NV(NV)                     \
+#define LAUNCH_BWD_NV(NV)                     \
   if (need_dw) {                                  \
-    if (dres) FTC_LAUNCH_BWD(NV, true, true);     \
-    else FTC_LAUNCH_BWD(NV, true, false);         \
+    if (dres) LAUNCH_BWD(NV, true, true);     \
+    else LAUNCH_BWD(NV, true, false);         \
   } else {                                        \
-    if (dres) FTC_LAUNCH_BWD(NV, false, true);    \
-    else FTC_LAUNCH_BWD(NV, false, false);        \
+    if (dres) LAUNCH_BWD(NV, false, true);    \
+    else LAUNCH_BWD(NV, false, false);        \
   }
-  // frozen norms: the two-waves-per-row variant (FTC_RMSNORM_BWD2=0 selects the one-wave kernel)
-  static const bool two = [] {
-    const char* e = getenv("FTC_RMSNORM_BWD2");
-    return !(e && e[0] == '0');
-  }();
-  if (!need_dw && two && nv >= 2) {
+  // frozen norms: the two-waves-per-row kernel (the weight-gradient path keeps per-wave accumulators)
+  if (!need_dw && nv >= 2) {
     const int g2 = rms_grid(rows, 2);
     const size_t l2 = (size_t)(d / 8) * 16 + 4 * sizeof(float);
-#define FTC_LAUNCH_BWD2(NV2)                                                                                  \
+#define LAUNCH_BWD2(NV2)                                                                                  \
   if (dres)                                                                                                   \
     hipLaunchKernelGGL((rmsnorm_bwd2_kernel<NV2, true>), dim3(g2), dim3(256), l2, stream, DY, Hh, W, rstd, DR, DX, \
                        rows, d, dres_rs, dx_rs);                                                              \
@@ -433,25 +426,25 @@ extern "C" int ftc_rmsnorm_bwd(const void* dy, const void* h, const void* w, con
     hipLaunchKernelGGL((rmsnorm_bwd2_kernel<NV2, false>), dim3(g2), dim3(256), l2, stream, DY, Hh, W, rstd, DR,  \
                        DX, rows, d, dres_rs, dx_rs);
     switch (nv) {
-      case 2: FTC_LAUNCH_BWD2(1); break;
-      case 4: FTC_LAUNCH_BWD2(2); break;
-      case 8: FTC_LAUNCH_BWD2(4); break;
-      case 16: FTC_LAUNCH_BWD2(8); break;
+      case 2: LAUNCH_BWD2(1); break;
+      case 4: LAUNCH_BWD2(2); break;
+      case 8: LAUNCH_BWD2(4); break;
+      case 16: LAUNCH_BWD2(8); break;
       default: return -1;
     }
-#undef FTC_LAUNCH_BWD2
+#undef LAUNCH_BWD2
     return (int)hipGetLastError();
   }
   switch (nv) {
-    case 1: FTC_LAUNCH_BWD_NV(1); break;
-    case 2: FTC_LAUNCH_BWD_NV(2); break;
-    case 4: FTC_LAUNCH_BWD_NV(4); break;
-    case 8: FTC_LAUNCH_BWD_NV(8); break;
-    case 16: FTC_LAUNCH_BWD_NV(16); break;
+    case 1: LAUNCH_BWD_NV(1); break;
+    case 2: LAUNCH_BWD_NV(2); break;
+    case 4: LAUNCH_BWD_NV(4); break;
+    case 8: LAUNCH_BWD_NV(8); break;
+    case 16: LAUNCH_BWD_NV(16); break;
     default: return -1;
   }
-#undef FTC_LAUNCH_BWD_NV
-#undef FTC_LAUNCH_BWD
+#undef LAUNCH_BWD_NV
+#undef LAUNCH_BWD
   if (need_dw) {
     hipLaunchKernelGGL(colsum_kernel, dim3((d + 63) / 64), dim3(256), 0, stream, dw_part, dw, grid, d);
   }

@@ -33,17 +33,17 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int kRows = 16;
 constexpr int kWaves = 4;
 
-FTC_DEV float silu_f(float g) { return g / (1.0f + __expf(-g)); }
+DEV_INLINE float silu_f(float g) { return g / (1.0f + __expf(-g)); }
 
-FTC_DEV bf16x8 as_frag(const uint4& v) { return __builtin_bit_cast(bf16x8, v); }
+DEV_INLINE bf16x8 as_frag(const uint4& v) { return __builtin_bit_cast(bf16x8, v); }
 
-FTC_DEV f32x4 mfma16(const uint4& a, const uint4& b, f32x4 c) {
+DEV_INLINE f32x4 mfma16(const uint4& a, const uint4& b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a), as_frag(b), c, 0, 0, 0);
 }
 
 // Sum the four waves' [16 x 16] partials per column tile and write the bf16 tail (+ zero padding).
 template <int NCT>
-FTC_DEV void write_tail(f32x4 (&acc)[NCT], float* red, uint16_t* base, long long rs, long long r0, long long rows,
+DEV_INLINE void write_tail(f32x4 (&acc)[NCT], float* red, uint16_t* base, long long rs, long long r0, long long rows,
                         int col0, int Rp) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #pragma unroll
@@ -71,19 +71,19 @@ FTC_DEV void write_tail(f32x4 (&acc)[NCT], float* red, uint16_t* base, long long
 // Wave-private LDS tile [RT*16 rows][128 cols] bf16 with the 16-byte chunk index XOR-swizzled by
 // (row & 15): the coalesced row writes (16 lanes x 16 B per row) and the MFMA fragment reads (16 rows
 // x one chunk per quarter-wave) are both conflict-free.
-FTC_DEV __amdgpu_buffer_rsrc_t make_rsrc_n(const void* base, unsigned bytes) {
+DEV_INLINE __amdgpu_buffer_rsrc_t make_rsrc_n(const void* base, unsigned bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
-FTC_DEV uint4 bload16(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+DEV_INLINE uint4 bload16(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
   const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
   return make_uint4(v[0], v[1], v[2], v[3]);
 }
-FTC_DEV void bstore16(const uint4& v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
+DEV_INLINE void bstore16(const uint4& v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
   const u32x4 d = {v.x, v.y, v.z, v.w};
   __builtin_amdgcn_raw_buffer_store_b128(d, r, voff, soff, 0);
 }
 
-FTC_DEV int tile_off(int row, int chunk) { return row * 256 + ((chunk ^ (row & 15)) << 4); }
+DEV_INLINE int tile_off(int row, int chunk) { return row * 256 + ((chunk ^ (row & 15)) << 4); }
 
 // Coalesced layout of a [RT*16, 128] chunk: load i of a lane covers row 4 i + (lane >> 4), columns
 // 8 (lane & 15) .. +8 -- 256 contiguous bytes per row per instruction.
@@ -288,11 +288,11 @@ namespace {
 typedef short s16x4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4v lds_s16x4v;
 
-FTC_DEV f32x4 mfma16k16(const s16x4v& a, const s16x4v& b, f32x4 c) {
+DEV_INLINE f32x4 mfma16k16(const s16x4v& a, const s16x4v& b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
 }
 // transposed 4-row x 16-column read: lane 4q+p of each 16-lane group addresses row q, columns 4p..4p+3
-FTC_DEV s16x4v tr4(const char* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4v*)p); }
+DEV_INLINE s16x4v tr4(const char* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4v*)p); }
 
 struct WgArgs {
   const uint16_t* gu;
@@ -315,10 +315,10 @@ struct WgArgs {
 constexpr int kCB = 512;  // gate|up column pairs per workgroup (128 per wave)
 
 // byte offset of (row, col) in a wave tile [16][128] bf16 with the 16-byte chunk swizzle of tile_off
-FTC_DEV int tcol_off(int row, int col) { return row * 256 + ((((col >> 3) ^ (row & 15)) & 15) << 4) + (col & 7) * 2; }
+DEV_INLINE int tcol_off(int row, int col) { return row * 256 + ((((col >> 3) ^ (row & 15)) & 15) << 4) + (col & 7) * 2; }
 
-// PF = false: the previous schedule (loads at the top of each sub-tile, __syncthreads), FTC_WGRAD_PF=0 (A/B)
-template <bool PF>
+// The next 16-row sub-tile's loads are issued before the current one is consumed (0.517 vs 0.528 ms at the
+// Llama-3-8B MLP shape, profiles/r3/swiglu_pf*.log; the load-at-the-top schedule is in git history).
 __global__ __launch_bounds__(256, 2) void swiglu_bwd_wgrad_kernel(WgArgs a) {
   __shared__ __attribute__((aligned(16))) char tiles[kWaves][3][16 * 256];  // dg, du, h
   __shared__ __attribute__((aligned(16))) char xat[kWaves][16 * 64];       // xa sub-tile [16][32]
@@ -367,10 +367,9 @@ __global__ __launch_bounds__(256, 2) void swiglu_bwd_wgrad_kernel(WgArgs a) {
       uv[i] = bload16(rg, (int)((row * 2LL * F + F + cw + 8 * cq) * 2), 0);
     }
   };
-  if (PF && rbeg < rend) issue(rbeg);
+  if (rbeg < rend) issue(rbeg);
   int sub = 0;
   for (long long r0 = rbeg; r0 < rend; r0 += 16, ++sub) {
-    if (!PF) issue(r0);
     const long long nrows = rend - r0 < 16 ? rend - r0 : 16;
     // stores past the block's rows are dropped
     const __amdgpu_buffer_rsrc_t ro = make_rsrc_n(a.dgu + r0 * a.dgu_rs, (unsigned)(nrows * a.dgu_rs * 2));
@@ -410,7 +409,7 @@ __global__ __launch_bounds__(256, 2) void swiglu_bwd_wgrad_kernel(WgArgs a) {
       *reinterpret_cast<uint4*>(my + 16 * 256 + off) = uq;
       *reinterpret_cast<uint4*>(my + 2 * 16 * 256 + off) = hq;
     }
-    if (PF && r0 + 16 < rend) issue(r0 + 16);
+    if (r0 + 16 < rend) issue(r0 + 16);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // wave-private tiles complete
 
     // ---- row tail: [16 rows] x (gate tile 0, up tile 1)
@@ -442,13 +441,9 @@ __global__ __launch_bounds__(256, 2) void swiglu_bwd_wgrad_kernel(WgArgs a) {
       rbuf[((wave * 2 + 1) * 4 + i) * 64 + lane] = tu[i];
     }
     // LDS-only barrier: __syncthreads' release fence would also drain the prefetch loads (vmcnt(0))
-    if constexpr (PF) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    } else {
-      __syncthreads();
-    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     for (int idx = tid; idx < 2 * 4 * 64; idx += 256) {  // (tile, i, lane) -> row 4 (ln >> 4) + i, col tile*16 + (ln & 15)
       const int t = idx >> 8, i = (idx >> 6) & 3, ln = idx & 63;
       float s = 0.f;
@@ -531,11 +526,8 @@ extern "C" int ftc_swiglu_wgrad_plan(long long T, int F, int* rb, long long* ws_
   if (F % kCB != 0 || T <= 0) return -1;
   const int ncb = F / kCB;
   // workgroup target: partial traffic grows with ncb + nrb, balance wants whole rounds of the
-  // 2-per-CU residency (FTC_WGRAD_WGS, default 512 = one round on 256 CUs)
-  static const int target = [] {
-    const char* e = getenv("FTC_WGRAD_WGS");
-    return e ? atoi(e) : 512;
-  }();
+  // 2-per-CU residency (512 = one round on 256 CUs; profiles/r3/wgrad_wgs/)
+  constexpr int target = 512;
   long long nrb = target / ncb > 0 ? target / ncb : 1;
   long long r = (T + nrb - 1) / nrb;
   r = (r + 15) / 16 * 16;
@@ -562,14 +554,7 @@ extern "C" int ftc_swiglu_bwd_wgrad(const void* da, long long da_rs, const void*
   WgArgs a{(const uint16_t*)gu, (const uint16_t*)da, da_rs, (uint16_t*)dgu, dgu_rs, (const uint16_t*)bt, ldb,
            (const uint16_t*)xa, xa_rs, (const uint16_t*)dyb, dyb_rs, ws, ws + (long long)ncb * T * 32,
            ws + (long long)ncb * T * 32 + (long long)nrb * 2 * F * 16, (int)T, F, RB, ncb};
-  static const bool pf = [] {
-    const char* e = getenv("FTC_WGRAD_PF");
-    return !(e && e[0] == '0');
-  }();
-  if (pf)
-    hipLaunchKernelGGL(swiglu_bwd_wgrad_kernel<true>, dim3(ncb * nrb), dim3(256), 0, stream, a);
-  else
-    hipLaunchKernelGGL(swiglu_bwd_wgrad_kernel<false>, dim3(ncb * nrb), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(swiglu_bwd_wgrad_kernel, dim3(ncb * nrb), dim3(256), 0, stream, a);
   const long long nt = T * (Rp / 8);
   hipLaunchKernelGGL(wgrad_tail_reduce_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, stream, a.p_tail,
                      ncb, (int)T, (uint16_t*)dgu, dgu_rs, 2 * F, Rp);

@@ -20,7 +20,7 @@ per GPU, RCCL over xGMI inside each node).
 """
 from __future__ import annotations
 
-from typing import ClassVar, Literal
+from typing import Annotated, ClassVar, Literal
 
 from pydantic import Field
 
@@ -101,7 +101,9 @@ class MNIST_MI355X(MNIST):
 class LMTrainingArguments(TrainingArguments):
     """Flags of ``finetune_controller_amd.train.cli`` exposed to the UI form."""
 
-    batch_size: int | Literal["auto"] = Field(
+    # the int branch keeps its lower bound: 0 / negative values are rejected by the API, not by the
+    # worker's argparse inside a restarting pod
+    batch_size: Annotated[int, Field(ge=1)] | Literal["auto"] = Field(
         default=4, description="Micro-batch (sequences) per GPU, or auto: the largest that fits 90 % of the GPU's "
                                "HBM (utils/memplan.py), capped at 16k tokens")
     seq_len: int = Field(default=4096, ge=16, description="Tokens per sequence")
@@ -197,14 +199,18 @@ class _WorkerSpec(BaseFineTuneModel):
         t = self.training_arguments
         vals = t.model_dump()
         if vals.get("batch_size") == "auto" or vals.get("checkpoint_layers") == "auto":
-            p = self.memory_plan()  # the pod command carries the chosen numbers (the worker re-checks them)
-            if p is not None:
-                vals["batch_size"], vals["checkpoint_layers"] = p.batch_size, p.checkpoint_layers
+            # validated here against the spec's accelerator_memory_gb (memplan raises when nothing fits,
+            # so an impossible job is refused at submission), but "auto" itself goes to the pod: the
+            # worker re-plans against the real device's total_memory (Trainer._plan_memory), so a
+            # spec that overstates the accelerator cannot render a micro-batch that OOMs
+            self.memory_plan()
         args = [f"--model={self.model_preset}", f"--method={self.method}"]
         for k, v in vals.items():
             if isinstance(v, bool):
                 if v:
                     args.append(f"--{k.replace('_', '-')}")
+            elif k == "checkpoint_layers":  # "auto" (bool handled above)
+                args.append("--checkpoint-layers=auto")
             else:
                 args.append(f"--{k.replace('_', '-')}={v}")
         cmd = list(self.command)

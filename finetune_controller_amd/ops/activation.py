@@ -7,7 +7,6 @@ augmented GEMMs (``ops.linear``) from the values they produce, saving a full re-
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn.functional as F
@@ -15,7 +14,7 @@ import torch.nn.functional as F
 from ._backend import ext, use_hip
 from .linear import LoRATail, mark_prefilled
 
-_FUSED_OFF = os.environ.get("FTC_FUSED_TAIL", "1") == "0"  # A/B switch: separate tail GEMMs
+_FUSED_OFF = False  # True: separate tail GEMMs (A/B by patching; profiles/r1_bench_fused_swiglu_tail*.log)
 
 
 class _SwiGLUHip(torch.autograd.Function):

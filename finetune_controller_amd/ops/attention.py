@@ -21,7 +21,6 @@ from __future__ import annotations
 
 import logging
 import math
-import os
 from dataclasses import dataclass
 
 import torch
@@ -164,8 +163,8 @@ def _sdpa_packed(qkv, B, S, H, KV, D, causal, window, scale, docs: Segments | No
     return o.transpose(1, 2).reshape(B * S, H * D)
 
 
-# kill switch of the RoPE-backward handoff (FTC_ROPE_BWD_FUSE=0: the producer runs the separate pass)
-ROPE_BWD_FUSE = os.environ.get("FTC_ROPE_BWD_FUSE", "1") != "0"
+# RoPE-backward handoff to the flash epilogues (False: the producer runs the separate pass; tests patch it)
+ROPE_BWD_FUSE = True
 
 
 class RopeGrad:

@@ -4,7 +4,7 @@ Every base GEMM of a LoRA / QLoRA step has the "NT" form ``C[T, n] = A[T, k] . B
 operands K-contiguous (ops/linear.py: the augmented forward ``[x | s x A^T] . [W | B]^T`` and the
 input-gradient ``[dy | dy B] . [W ; s A]`` through the transposed frozen weight).  The hand-written
 kernel is a persistent 256 x 256-tile MFMA GEMM with LDS-DMA staging (see the .hip header);
-``ext().gemm_nt_config`` sets its launch configuration (persistent grid cap, tile order, store policy).
+``ext().gemm_nt_config`` sets its launch configuration (persistent grid cap, tile order).
 """
 from __future__ import annotations
 

@@ -61,7 +61,7 @@ def _refresh_key(A: torch.Tensor, B: torch.Tensor, scale: float) -> tuple:
 # copies (s A, B, and the transposed s A^T / B^T where kept) refreshed: ~16 small copy / scale launches
 # per layer.  The first refresh of a parameter generation refreshes EVERY bound operand set in one
 # launch (csrc/kernels/elementwise.hip ``copy2d_batched``); the later calls find their key current.
-_BATCH_REFRESH = os.environ.get("FTC_BATCH_REFRESH", "1") != "0"
+_BATCH_REFRESH = True
 _BOUND: list = []  # weakrefs to AugWeight / TailOperands bound to their (A, B, scale)
 _JOB_TABLES: dict = {}  # packed job table bytes -> device int64 tensor (addresses are stable per model)
 
@@ -333,7 +333,7 @@ class TrainableTransposed(FrozenTransposed):
 
 
 param_t = TrainableTransposed()
-_TN_DW = os.environ.get("FTC_TN_DW", "1") != "0"  # weight gradients with the activation transposed
+_TN_DW = True  # weight gradients with the activation transposed (14-24 % faster, profiles/r1_dw_gemm_layouts.log)
 
 
 def transpose2d(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
@@ -388,7 +388,6 @@ def accum_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, alpha: float =
 # pass (csrc/kernels/elementwise.hip splitk_sum_kernel) folds them into the gradient (beta C + sum).
 # FTC_DW_SPLIT: "auto" (default: the measured winning shapes), "0" off, or a fixed S.
 _DW_SPLIT = os.environ.get("FTC_DW_SPLIT", "auto")  # full FT +0.9 % (profiles/r4/dw_split/full_ab)
-_DW_PARTS: dict = {}  # (device, stream) -> flat fp32 scratch for the partials
 _WAVE = 256  # workgroups per wave: one 256 x 256 tile per CU
 
 
@@ -430,11 +429,10 @@ def wgrad_mm(out: torch.Tensor, a: torch.Tensor, b: torch.Tensor, beta: float = 
 
 
 def _dw_parts(device, s: int, M: int, N: int) -> torch.Tensor:
-    key = (device, torch.cuda.current_stream(device).cuda_stream)
-    buf = _DW_PARTS.get(key)
-    if buf is None or buf.numel() < s * M * N:
-        buf = _DW_PARTS[key] = torch.empty(s * M * N, dtype=torch.float32, device=device)
-    return buf[:s * M * N].view(s, M, N)
+    """fp32 split-K partials, from the caching allocator per call: the block goes back to the pool of the
+    stream it was taken on after the fold (no per-stream buffer pinned for the life of the process;
+    ``utils.memplan`` counts one per dW stream in the full-FT peak)."""
+    return torch.empty((s, M, N), dtype=torch.float32, device=device)
 
 
 def wgrad_tn(out: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, beta: float = 1.0) -> torch.Tensor:
@@ -456,10 +454,10 @@ def wgrad_tn(out: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, beta: float
 # beta = 1 GEMM per micro-batch, so the optimizer skips their slices (FlatAdamW.zero_grad) and marks them
 # "fresh": their first GEMM of the step runs with beta = 0 instead.  A weight joins the set only after a
 # step in which it was zeroed and written by that GEMM; one that a step leaves fresh (never written) is
-# zeroed by ``flush_fresh`` before the gradients are used.  Default on (``FTC_GRAD_FIRST_WRITE=0``: zero
+# zeroed by ``flush_fresh`` before the gradients are used.  Default on (``_FIRST_WRITE = False``: zero
 # the whole buffer): Llama-3-8B full FT, interleaved on one box (profiles/r3/first_write/), 690.1 / 692.0 ms
 # vs 693.7 / 694.4 ms/step (+0.4 %).
-_FIRST_WRITE = os.environ.get("FTC_GRAD_FIRST_WRITE", "1") != "0"
+_FIRST_WRITE = True
 # id(param) -> weakref(param): weights only a projection GEMM writes.  Entries are identity-checked (a dead
 # parameter's id can be reused by a new tensor of another trainer) and hold no reference to the gradient
 # buffer (a main_grad view would keep a whole flat fp32 buffer alive after its optimizer is gone)
@@ -597,7 +595,7 @@ class LoRATail:
                           and blocks[1][1] == aug.N)
 
 
-_HIP_TAIL = os.environ.get("FTC_TAIL_GEMM", "1") != "0"  # A/B switch: hipBLASLt for the skinny tail GEMMs
+_HIP_TAIL = True  # False: hipBLASLt for the skinny tail GEMMs (A/B by patching; profiles/r1_tail_gemm_ab.log)
 
 
 def tail_product(x2: torch.Tensor, width: int, Rp: int, operand: torch.Tensor, nct: int) -> None:
@@ -702,7 +700,7 @@ def direct_grad_params(A, B, blocks):
     return None
 
 
-_HIP_WGRAD = os.environ.get("FTC_LORA_WGRAD", "1") != "0"
+_HIP_WGRAD = True
 
 
 def _accum_xty(out: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, alpha: float, blocks=None):

@@ -24,7 +24,6 @@ optimizers without flat gradient buffers).
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -33,7 +32,7 @@ from . import linear as _L
 from .gemm import mm as gemm_mm
 from .linear import _accum_xty, _grad_ready, _spare_cols, _tail, _wide, tail_product, tn_backward
 
-_OFF = os.environ.get("FTC_FUSED_MLP", "1") == "0"  # A/B switch: unfused composition
+_OFF = False  # True: the unfused composition (A/B by patching; profiles/r1_bench_fused_mlp*.log)
 
 
 class AugProj:

@@ -19,7 +19,6 @@ The backward needs ``W`` again for ``dx = dy W`` and re-decodes it (nothing weig
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -144,7 +143,7 @@ def _dequant_into(qw: NF4Weight, out: torch.Tensor, transpose: bool):
 # 0: the separate copy / scale kernels.  Mistral-7B QLoRA, interleaved on one box (profiles/r3/qlora_aug/):
 # 439.88 / 439.70 ms fused vs 439.85 / 439.67 separate -- neutral (the 5 us copies it removes were hidden
 # between launches); kept for the 4 fewer launches per projection call (hipGraph capture size)
-_NF4_AUG = os.environ.get("FTC_NF4_AUG", "1") != "0"
+_NF4_AUG = True  # W / B / s A in one decode launch (the three-launch path: tests / A/B by patching)
 
 
 def _dequant_aug(qw: NF4Weight, out: torch.Tensor, transpose: bool, B, out_b, A, out_a, s: float):

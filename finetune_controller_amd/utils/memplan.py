@@ -5,7 +5,8 @@ spec (``controlplane/spec/models/builtin.py``) and the worker CLI (``train/cli.p
 The reference leaves batch sizing to the user's form (``/root/reference/app/models/base/finetuning.py:
 28-34`` training arguments, ``:83-93`` resources / ``accelerator_count``); BASELINE.json's north star asks
 for micro-batches sized for the 288 GB of HBM3E per MI355X.  Pure Python (no torch): the control plane
-renders the chosen values into the pod command, the worker re-plans with the real ``total_memory``.
+plans against the spec's ``accelerator_memory_gb`` to refuse a job that cannot fit, and passes ``auto``
+on to the pod, where the worker plans against the real device's ``total_memory``.
 
 Memory model (bytes), per GPU -- what the runtime of this repository allocates:
 
@@ -135,6 +136,9 @@ def estimate(dims: Dims, method: str, batch_size: int, seq_len: int, device_gb: 
         shard = max(1, world // max(1, sp)) if zero else 1
         parts["grads"] = g * P + (g * P / shard if zero else 0)
         parts["optimizer"] = 12.0 * P / shard  # fp32 master + exp_avg + exp_avg_sq
+        # split-K fp32 partials of the down-projection dW (ops.linear.wgrad_mm, 2 token halves), one live
+        # block per dW stream (main + side)
+        parts["dw_split_scratch"] = 2 * (2 * 4.0 * dims.dim * dims.ffn_dim)
     else:
         A = dims.lora_params(lora_r)
         parts["adapters"] = 16.0 * A  # bf16 param + grad, fp32 master / m / v

@@ -1,13 +1,18 @@
-"""The shipped extension: built for gfx950 only, and free of diagnostic code (timing-only modes with wrong
-results and cycle stamps exist only in the tools' diagnostic builds: FTC_EXPERIMENTS, FTC_GEMM_STAMP,
-FTC_STAMPS -- never set by finetune_controller_amd/tools/build.py)."""
+"""The shipped extension: built for gfx950 only, carrying only the kernel variants that won their
+measurements (no diagnostic code, no losing variants selectable at run time), and every runtime switch
+the sources read is documented ("Ship only winners")."""
 import os
+import re
 import subprocess
 
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SO = os.path.join(ROOT, "finetune_controller_amd", "_C.so")
+SOURCES = [os.path.join(ROOT, "bench.py")]
+for top in ("finetune_controller_amd", "csrc"):
+    for dp, _, fs in os.walk(os.path.join(ROOT, top)):
+        SOURCES += [os.path.join(dp, f) for f in fs if f.endswith((".py", ".hip", ".cpp", ".h"))]
 
 
 def _strings(path):
@@ -15,16 +20,33 @@ def _strings(path):
     return r.stdout
 
 
+def _switch_names():
+    names = set()
+    for p in SOURCES:
+        names |= set(re.findall(r"\bFTC_[A-Z0-9_]+", open(p, errors="replace").read()))
+    return names
+
+
 @pytest.mark.skipif(not os.path.exists(SO), reason="extension not built (python -m finetune_controller_amd.tools.build)")
-def test_extension_has_no_diagnostic_hooks():
+def test_extension_ships_only_the_winning_variants():
     text = _strings(SO)
-    for name in ("FTC_GEMM_TN_MODE", "FTC_GEMM_NT_MODE", "FTC_GEMM_NT_V5_MODE", "FTC_GEMM_NT_V7_MODE",
-                 "FTC_GEMM_NT_PB_MODE", "FTC_FLASH_FWD_PIPE", "FTC_FLASH_FWD_PP", "FTC_FLASH_DKDV_PP2",
-                 "g_gemm_stamps", "g_stamps", "ftc_gemm_nt_stamps"):
+    for name in ("FTC_GEMM_TN_MODE", "FTC_GEMM_TN_WAVES", "FTC_GEMM_TN_SCHED", "FTC_GEMM_TN_GROUP",
+                 "FTC_GEMM_NT_ORDER", "FTC_FLASH_DKDV_WAVES", "FTC_FLASH_DKDV_PP", "FTC_FLASH_DKDV_DIST",
+                 "FTC_FLASH_DKDV_QR", "FTC_FLASH_BWD_OCC", "FTC_WGRAD_WGS", "FTC_WGRAD_PF", "FTC_RMSNORM_FWD2",
+                 "FTC_RMSNORM_BWD2", "g_gemm_stamps", "g_stamps", "ftc_gemm_nt_stamps", "ftc_flash_dkdv_config"):
         assert name not in text, name
     syms = subprocess.run(["nm", "-C", SO], capture_output=True, text=True, check=True).stdout
-    # one production projection-GEMM kernel template (bf16 / fp32 C x epilogue x store policy x beta)
-    assert "gemm_nt_kernel<" in syms
+    # flash backward: the 8-wave ping-pong dK/dV (QR 1 at D = 128, 2 at D = 64) and the 2-wave/SIMD dQ only
+    assert "bwd_dkdv8_kernel<128, 1>" in syms and "bwd_dkdv8_kernel<64, 2>" in syms
+    for gone in ("bwd_dkdv_il_kernel", "bwd_dkdv_kernel<", "bwd_dq_kernel<128, 1>", "bwd_dq_kernel<64, 1>"):
+        assert gone not in syms, gone
+    # projection GEMM: one kernel template (bf16 / fp32 C x epilogue x beta), no store / DMA-policy variants
+    nt = set(re.findall(r"gemm_nt_kernel<[^>]*>", syms))
+    assert nt and all(len(t.split(",")) == 3 for t in nt), nt
+    # TN weight-gradient GEMM: the 4-wave spread-DMA schedule only (bf16 / fp32 C)
+    tn = set(re.findall(r"gemm_tn_kernel<[^>]*>", syms))
+    assert tn and tn <= {"gemm_tn_kernel<true>", "gemm_tn_kernel<false>"}, tn
+    assert "swiglu_bwd_wgrad_kernel<" not in syms  # one schedule, no template switch
     for old in ("gemm_nt_v5_kernel", "gemm_nt_w4d_kernel", "gemm_nt_pb_kernel", "gemm_nt_pp_kernel",
                 "flash_fwd_pipe_kernel", "flash_fwd_qb2_kernel"):
         assert old not in syms, old
@@ -32,5 +54,14 @@ def test_extension_has_no_diagnostic_hooks():
 
 def test_build_script_sets_no_diagnostic_define():
     src = open(os.path.join(ROOT, "finetune_controller_amd", "tools", "build.py")).read()
-    for d in ("FTC_EXPERIMENTS", "FTC_GEMM_STAMP", "FTC_STAMPS"):
+    for d in ("EXPERIMENTS", "STAMP"):
         assert d not in src
+
+
+def test_runtime_switches_are_documented():
+    names = _switch_names()
+    assert len(names) <= 25, sorted(names)
+    doc = open(os.path.join(ROOT, "docs", "kernels.md")).read()
+    table = doc[doc.index("## Runtime switches"):doc.index("## Counter evidence")]
+    missing = sorted(n for n in names if f"`{n}`" not in table)
+    assert not missing, missing

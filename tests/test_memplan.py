@@ -68,18 +68,30 @@ def test_plan_choices_on_the_baseline_configs():
     assert memplan.plan(L8, "full", 4096, world=8).peak_gb < memplan.plan(L8, "full", 4096).peak_gb
 
 
-def test_spec_renders_planned_values_into_the_command():
+def test_spec_passes_auto_to_the_worker_and_validates_it():
+    """"auto" reaches the pod (the worker plans against the real total_memory); the control plane
+    only checks that some plan fits the spec's accelerator, and rejects 0 / negative micro-batches."""
+    from pydantic import ValidationError
+
     from finetune_controller_amd.controlplane.spec.models.builtin import Llama3_8B_LoRA
+    from finetune_controller_amd.train.cli import build_parser
 
     spec = Llama3_8B_LoRA(training_arguments={"batch_size": "auto", "seq_len": 32768, "checkpoint_layers": "auto"})
     cmd = spec.run_cmd()[-1].split()
-    assert "--batch-size=1" in cmd and "--checkpoint-layers" not in cmd
-    assert not [t for t in cmd if t.startswith(("--batch-size", "--checkpoint-layers")) and "auto" in t]
-    spec = Llama3_8B_LoRA(training_arguments={"batch_size": "auto", "seq_len": 131072, "checkpoint_layers": "auto"})
-    cmd = spec.run_cmd()[-1].split()
-    assert "--batch-size=1" in cmd and "--checkpoint-layers" in cmd
+    assert "--batch-size=auto" in cmd and "--checkpoint-layers=auto" in cmd
+    # the rendered flags parse in the worker CLI
+    flags = [t for t in cmd if t.startswith("--") and not t.startswith(("--standalone", "--nproc"))]
+    a = build_parser().parse_args(flags)
+    assert a.batch_size == 0 and a.checkpoint_layers == "auto"
     spec = Llama3_8B_LoRA(training_arguments={"batch_size": 2})  # explicit values pass through untouched
     assert "--batch-size=2" in spec.run_cmd()[-1].split()
+    for bad in (0, -1):
+        with pytest.raises(ValidationError):
+            Llama3_8B_LoRA(training_arguments={"batch_size": bad})
+    # a job no plan can fit is refused when the command is rendered (submission), not in the pod
+    huge = Llama3_8B_LoRA(training_arguments={"batch_size": "auto", "seq_len": 1 << 22, "checkpoint_layers": "auto"})
+    with pytest.raises(ValueError):
+        huge.run_cmd()
 
 
 def test_control_plane_plans_without_torch():

@@ -4,12 +4,11 @@ one Llama-3-8B LoRA step: ``C[T, n] = A[T, k] . B[n, k]^T`` with T = 16384 token
 augmented LoRA forms of ops/linear.py (k = K + 64 forward, the transposed frozen weight backward).
 
     python tools/bench_gemm_nt.py [--iters 20] [--rounds 5] [--shapes qkv_fwd,o_fwd] \
-        [--configs "0,8,32,0;0,16,2,1"]
+        [--configs "0,-8,32;0,16,2"]
 
-Each config is ``grid_cap,group,xcc,nt_store[,load_policy]`` (ext().gemm_nt_config: grid_cap 0 = one persistent
-workgroup per CU, a large cap = one workgroup per tile; group > 0 M-fast / < 0 N-fast tile groups; xcc
-logical ids per XCD slot; nt_store non-temporal C stores; load_policy the operand DMA's cache bits:
-0 default, 1 sc0, 2 sc1, 3 sc0 sc1, 4 nt).  Every config and the library are timed in
+Each config is ``grid_cap,group,xcc`` (ext().gemm_nt_config: grid_cap 0 = one persistent workgroup per CU,
+a large cap = one workgroup per tile; group > 0 M-fast / < 0 N-fast tile groups; xcc logical ids per XCD
+slot).  Every config and the library are timed in
 INTERLEAVED rounds on the same uniform random [-1, 1) operands (zeros read fast: DVFS), so box-to-box
 clock differences cancel; one JSON line per (shape, config) with the median / min ms, TF/s on the
 median, the speed-up over the library and the max |ours - lib| / max |lib| of one product."""
@@ -30,7 +29,7 @@ SHAPES = {  # name: (k, n)
     "down_fwd": (14336 + 64, 4096), "down_dx": (4096 + 64, 14336), "gu_dx": (28672 + 64, 4096),
     "o_dx": (4096 + 64, 4096), "qkv_dx": (6144 + 64, 4096), "lm_head": (4096, 4096 * 8),
 }
-DEFAULT_CONFIGS = "0,-8,32,0,1"
+DEFAULT_CONFIGS = "0,-8,32"
 
 
 def timeit(fn, iters):
