@@ -143,6 +143,10 @@ def _parse(argv):
                     help="after the timed region, also time the native RCCL engine's bucket all-reduce")
     ap.add_argument("--grad-dtype", default="auto", choices=["auto", "fp32", "bf16"],
                     help="gradient buffer / reduction dtype (full FT; auto: fp32 when accumulating)")
+    ap.add_argument("--grad-wire", default="auto", choices=["auto", "bf16"],
+                    help="gradient reduction dtype on the wire (bf16 over an fp32 buffer: half the bytes)")
+    ap.add_argument("--rccl-channels", type=int, default=0,
+                    help="> 0: NCCL_MIN/MAX_NCHANNELS for RCCL's communicators (set before the first GPU call)")
     ap.add_argument("--grad-accum", type=int, default=1)
     ap.add_argument("--zero-stage", type=int, default=-1, choices=[-1, 0, 1],
                     help="1: ZeRO-1 -- AdamW state sharded over the data-parallel ranks (reduce-scatter + all-gather); "
@@ -166,7 +170,43 @@ def _parse(argv):
     return ap.parse_args(argv)
 
 
-def _bucket_busbw(info, mb: float, native=None, iters: int = 10) -> dict:
+def _rccl_channels(path: str | None) -> list[int] | None:
+    """Channel counts RCCL chose for this rank's communicators, from its INIT log lines
+    (``Channel 00/16 : 0 1 ...`` -> 16); None when there is no log (1 rank, CPU, a user NCCL_DEBUG)."""
+    import re
+
+    if not path or not os.path.exists(path):
+        return None
+    found = set()
+    with open(path, errors="replace") as f:
+        for ln in f:
+            m = re.search(r"Channel \d+/(\d+)", ln)
+            if m:
+                found.add(int(m.group(1)))
+    return sorted(found)
+
+
+def _channel_sweep(info, mb: float, counts=(2, 4, 8, 16)) -> dict:
+    """Bus bandwidth of the ``mb``-MB bucket all-reduce on fresh RCCL communicators pinned to each channel
+    count (ncclConfig_t min/maxCTAs through ProcessGroupNCCL.Options): tells channel starvation from link
+    bandwidth in the first 8-GPU record.  Errors are reported, never raised."""
+    import torch.distributed as dist
+
+    out = {}
+    for c in counts:
+        try:
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.config.min_ctas = c
+            opts.config.max_ctas = c
+            g = dist.new_group(backend="nccl", pg_options=opts)
+            out[str(c)] = _bucket_busbw(info, mb, iters=5, group=g)["busbw_GBps"]
+            dist.destroy_process_group(g)
+        except Exception as e:  # noqa: BLE001 -- a diagnostic
+            out[str(c)] = f"error: {type(e).__name__}: {e}"[:160]
+    return out
+
+
+def _bucket_busbw(info, mb: float, native=None, iters: int = 10, group=None) -> dict:
     """Bus bandwidth (GB/s) of one ``mb``-MB bf16 SUM all-reduce, the DDP bucket size: algbw x
     2(n-1)/n, the per-link rate a ring moves (nccl-tests convention)."""
     import torch
@@ -183,7 +223,7 @@ def _bucket_busbw(info, mb: float, native=None, iters: int = 10) -> dict:
         if native is not None:
             native.all_reduce_async(t).wait()
         else:
-            dist.all_reduce(t)
+            dist.all_reduce(t, group=group)
 
     for _ in range(3):
         run()
@@ -220,6 +260,16 @@ def main(argv=None) -> int:
     # RCCL's intra-node buffers travel by dmabuf IPC on these hosts; the legacy IPC handle path fails
     # (hipIpcGetMemHandle: invalid argument).  Read by the HIP runtime at its first call, i.e. after here.
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    # RCCL reads these at communicator creation, i.e. after here
+    if a.rccl_channels > 0:
+        os.environ["NCCL_MIN_NCHANNELS"] = os.environ["NCCL_MAX_NCHANNELS"] = str(a.rccl_channels)
+    rccl_log = None
+    if a.device == "cuda" and a.gpus > 1 and "NCCL_DEBUG" not in os.environ:
+        # the channel count RCCL picks is in its INIT log lines: to a per-rank file (never stdout)
+        import tempfile
+
+        rccl_log = os.path.join(tempfile.gettempdir(), f"ftc_rccl_{os.getpid()}.log")
+        os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT", NCCL_DEBUG_FILE=rccl_log)
 
     import torch
     import torch.distributed as dist
@@ -232,7 +282,8 @@ def main(argv=None) -> int:
     tc = TrainConfig(model=a.model, method=a.method, lora_r=a.lora_r, lora_alpha=2.0 * a.lora_r,
                      batch_size=a.batch_size, seq_len=a.seq_len, synthetic=True, max_steps=a.warmup + a.steps,
                      warmup_steps=0, schedule="constant", lr=1e-4, bucket_mb=a.bucket_mb, comm_engine=a.comm_engine,
-                     zero_stage=a.zero_stage, grad_accum=a.grad_accum, grad_dtype=a.grad_dtype, sp=a.sp,
+                     zero_stage=a.zero_stage, grad_accum=a.grad_accum, grad_dtype=a.grad_dtype,
+                     grad_wire=a.grad_wire, sp=a.sp,
                      checkpoint_layers=a.checkpoint_layers, ce_chunk_rows=a.ce_chunk_rows, save_model=False,
                      resume=False, device=a.device, pack_documents=a.doc_len > 0, eos_id=2,
                      synthetic_doc_len=a.doc_len, graph=a.graph, comm_probe=a.gpus > 1)
@@ -283,11 +334,13 @@ def main(argv=None) -> int:
 
     # ---- after the timed region: transport diagnostics (never part of the metric)
     comm = {}
+    channels = _rccl_channels(rccl_log) if info.is_main else None  # before the sweep adds communicators
     if n > 1:
         comm["torch"] = _bucket_busbw(info, a.bucket_mb)
         if cuda:  # bucket-size sweep on the same process group: xGMI data for tuning bucket_mb
             comm["sweep_busbw_GBps"] = {str(mb): _bucket_busbw(info, mb, iters=5)["busbw_GBps"]
                                         for mb in (4, 16, 64, 256)}
+            comm["channel_sweep_busbw_GBps"] = _channel_sweep(info, a.bucket_mb)
         if cuda and (a.comm_ab or a.comm_engine == "native"):
             try:
                 native = tr.ddp._native
@@ -368,6 +421,7 @@ def main(argv=None) -> int:
             "world_size_pg": pg_world,
             "dist_backend": info.backend,
             "rccl_version": rccl,
+            "rccl_channels": channels,
             "p2p_peers": p2p,
             "rank_ms_per_step": {"max": round(ms, 2), "min": round(fastest / a.steps * 1000, 2)},
             **({"allreduce_bucket": comm} if comm else {}),
@@ -375,9 +429,10 @@ def main(argv=None) -> int:
                 "comm_exposed_ms": None if exposed is None else round(exposed, 3),
                 "param_sync_exposed_ms": None if psync is None else round(psync, 3),
                 "zero_gather_overlap": bool(tr.zero_stage and getattr(tr.opt, "_stage_buckets", None) is not None),
-                "wire_GB_per_step": round(tr.ddp.wire_bytes_per_step() / 1e9, 4),
+                "wire_GB_per_step": round(tr.ddp.wire_bytes_per_step() / 1e9, 6),
                 "n_buckets": tr.ddp.n_collectives(),
                 "bucket_mb": a.bucket_mb,
+                "grad_wire": str(tr.ddp.wire_dtype or tr.opt.grad_flat.dtype).replace("torch.", ""),
                 "env": {k: v for k, v in sorted(os.environ.items())
                         if k.startswith(("NCCL_", "RCCL_")) or k in ("HSA_ENABLE_IPC_MODE_LEGACY", "FTC_SHARE_GPU")},
             },

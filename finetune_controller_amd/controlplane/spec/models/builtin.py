@@ -129,6 +129,9 @@ class LMTrainingArguments(TrainingArguments):
                                 "(long context; must divide the GPU count and the model's head counts)")
     grad_dtype: Literal["auto", "fp32", "bf16"] = Field(
         default="auto", description="Gradient buffer / all-reduce dtype (auto: fp32 for full FT with accumulation or DP)")
+    grad_wire: Literal["auto", "bf16"] = Field(
+        default="auto", description="Gradient reduction dtype on the wire (bf16: an fp32 buffer reduced as bf16, half "
+                                    "the bytes on xGMI; auto: the buffer's dtype)")
     eval_every: int = Field(default=0, ge=0, description="Held-out loss every N steps (0 = off)")
     eval_batches: int = Field(default=4, ge=1, description="Micro-batches per GPU per evaluation")
     eval_holdout: float = Field(default=0.01, gt=0, description="Held-out share of the dataset (>= 1: windows)")

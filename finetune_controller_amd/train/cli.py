@@ -50,6 +50,9 @@ def build_parser() -> argparse.ArgumentParser:
                          "-1 (auto): ZeRO-1 for full fine-tuning on > 1 GPU")
     ap.add_argument("--grad-dtype", default="auto", choices=["auto", "fp32", "bf16"],
                     help="gradient buffer / all-reduce dtype (auto: fp32 for full FT with accumulation or DP)")
+    ap.add_argument("--grad-wire", default="auto", choices=["auto", "bf16"],
+                    help="gradient reduction dtype on the wire (bf16: an fp32 gradient buffer reduced as bf16, "
+                         "half the bytes; auto: the buffer's dtype)")
     ap.add_argument("--init-from", default="", help="HF safetensors checkpoint dir to fine-tune from")
     ap.add_argument("--synthetic", action="store_true", help="ignore the dataset; synthetic tokens")
     ap.add_argument("--no-resume", action="store_true")
@@ -94,7 +97,7 @@ def config_from_args(a) -> TrainConfig:
                        weight_decay=a.weight_decay, max_grad_norm=a.max_grad_norm, seed=a.seed,
                        dataset_path=a.dataset_path, checkpoint_path=a.checkpoint_path, log_interval=a.log_interval,
                        save_every=a.save_every, resume=not a.no_resume, synthetic=a.synthetic, bucket_mb=a.bucket_mb,
-                       comm_engine=a.comm_engine, zero_stage=a.zero_stage, grad_dtype=a.grad_dtype, sp=a.sp,
+                       comm_engine=a.comm_engine, zero_stage=a.zero_stage, grad_dtype=a.grad_dtype, grad_wire=a.grad_wire, sp=a.sp,
                        checkpoint_layers="auto" if a.checkpoint_layers == "auto" else a.checkpoint_layers == "1",
                        init_from=a.init_from,
                        dtype=a.dtype, device=a.device, timers=a.timers, profile_steps=a.profile_steps,

@@ -80,6 +80,9 @@ class TrainConfig:
     # gradient buffer / reduction dtype: fp32 | bf16 | auto (fp32 for full fine-tuning with gradient
     # accumulation or data parallelism -- summing 4+ bf16 micro-batch / rank gradients loses mantissa)
     grad_dtype: str = "auto"
+    # the gradient reduction's dtype on the wire: "auto" = the gradient buffer's; "bf16" = an fp32 buffer
+    # (exact local accumulation) reduced / reduce-scattered as bf16 (parallel.ddp: half the wire bytes)
+    grad_wire: str = "auto"
     checkpoint_layers: bool | str = False  # "auto": only when the planned micro-batch needs it
     init_from: str = ""
     dtype: str = "auto"  # auto: bf16 on GPU, fp32 on CPU
@@ -182,7 +185,10 @@ class Trainer:
                 pdist.broadcast_params_([p for p in self.model.parameters() if not p.requires_grad], self.info)
         self._overlap_update()
         tied = [self.model.lm_head] if self.cfg.tie_embeddings and tc.method == "full" else []
-        self.ddp = GradBucketer(self.opt, tc.bucket_mb, engine=tc.comm_engine, multi_use_params=tied)
+        if tc.grad_wire not in ("auto", "bf16", "bfloat16"):
+            raise ValueError(f"grad_wire must be auto or bf16, not {tc.grad_wire!r}")
+        wire = torch.bfloat16 if tc.grad_wire in ("bf16", "bfloat16") and self.opt.grad_flat.dtype == torch.float32 else None
+        self.ddp = GradBucketer(self.opt, tc.bucket_mb, engine=tc.comm_engine, multi_use_params=tied, wire_dtype=wire)
         self._data = None
         self._eval_synth = None
         self.step = 0
