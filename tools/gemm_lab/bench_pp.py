@@ -5,7 +5,7 @@ reference on small and production shapes, then interleaved timing rounds (same u
 operands) of hipBLASLt (torch.mm), the shipped 4-wave kernel (ext().gemm_nt_) and the ping-pong kernel on
 the Llama-3-8B LoRA-step shapes (T = 16384).  One JSON line per shape.
 
-    python tools/gemm_lab/bench_pp.py [--shapes qkv_fwd,o_fwd] [--iters 20] [--rounds 5] [--check-only]
+    python tools/gemm_lab/bench_pp.py [--variants d0,d3,m1] [--shapes qkv_fwd,o_fwd] [--iters 20] [--rounds 5]
 """
 import argparse
 import ctypes
@@ -28,7 +28,7 @@ SHAPES = {  # name: (k, n) -- as tools/bench_gemm_nt.py
 }
 
 def _load(mode):
-    lib = ctypes.CDLL(os.path.join(HERE, "libgemm_pp.so" if mode == 0 else f"libgemm_pp_m{mode}.so"))
+    lib = ctypes.CDLL(os.path.join(HERE, f"libgemm_pp_{mode}.so"))
     lib.ftc_gemm_pp.restype = ctypes.c_int
     lib.ftc_gemm_pp.argtypes = [ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_longlong,
                                 ctypes.c_void_p, ctypes.c_longlong, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -36,10 +36,10 @@ def _load(mode):
     return lib
 
 
-_libs = {0: _load(0)}
+_libs = {}
 
 
-def pp(c, a, b, alpha=1.0, grid_cap=0, group=-8, xcc=32, mode=0):
+def pp(c, a, b, alpha=1.0, grid_cap=0, group=-8, xcc=32, mode="d0"):
     M, K = a.shape
     N = b.shape[0]
     rc = _libs[mode].ftc_gemm_pp(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0), M, N, K,
@@ -48,7 +48,7 @@ def pp(c, a, b, alpha=1.0, grid_cap=0, group=-8, xcc=32, mode=0):
         raise RuntimeError(f"ftc_gemm_pp rc={rc} for {M}x{N}x{K}")
 
 
-def check():
+def check(mode):
     torch.manual_seed(3)
     cases = [(256, 256, 64, 0, 0), (512, 768, 192, 0, 0), (1024, 1280, 448, 8, 3), (768, 512, 128, 0, 1),
              (2048, 2048, 4160, 0, 0), (1024, 768, 64, 0, 5)]
@@ -57,15 +57,15 @@ def check():
         a = abuf[:, :K]
         b = (torch.arange(N * K, device="cuda").reshape(N, K) % 7 - 3).to(torch.bfloat16)
         c = torch.full((M, N), 7.0, device="cuda", dtype=torch.bfloat16)
-        pp(c, a, b, grid_cap=cap)
+        pp(c, a, b, grid_cap=cap, mode=mode)
         exact = (a.double() @ b.double().t()).to(torch.bfloat16)
         ok = torch.equal(c, exact)
         a = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
         b = (torch.rand(N, K, device="cuda") * 2 - 1).to(torch.bfloat16)
-        pp(c, a, b, alpha=0.5, grid_cap=cap)
+        pp(c, a, b, alpha=0.5, grid_cap=cap, mode=mode)
         ref = 0.5 * (a.float() @ b.float().t())
         err = ((c.float() - ref).abs().max() / ref.abs().max()).item()
-        print(json.dumps({"check": [M, N, K, pad, cap], "exact_int": ok, "max_rel_err": float(f"{err:.2e}")}), flush=True)
+        print(json.dumps({"check": [M, N, K, pad, cap], "variant": mode, "exact_int": ok, "max_rel_err": float(f"{err:.2e}")}), flush=True)
         if not ok or err > 2e-2:
             raise SystemExit("ping-pong GEMM mismatch")
 
@@ -86,12 +86,16 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--shapes", default="qkv_fwd,o_fwd,gu_fwd,down_dx,down_fwd")
     ap.add_argument("--check-only", action="store_true")
-    ap.add_argument("--modes", default="0", help="ping-pong builds to time: 0 the kernel, 1-3 lab ablations")
+    ap.add_argument("--no-check", action="store_true", help="skip the correctness cases (counter runs)")
+    ap.add_argument("--variants", default="d0",
+                    help="ping-pong builds to time (tools/gemm_lab/build.sh): d0-d3 DMA placements, m1-m3 ablations of d0")
     a = ap.parse_args()
-    modes = [int(m) for m in a.modes.split(",")]
+    modes = a.variants.split(",")
     for m in modes:
         _libs.setdefault(m, _load(m))
-    check()
+    for m in modes:
+        if m.startswith("d") and not a.no_check:
+            check(m)
     if a.check_only:
         return
     C = ext()
@@ -105,15 +109,17 @@ def main():
         y2 = torch.empty_like(y0)
         y3 = torch.empty_like(y0)
         torch.mm(x, w.t(), out=y0)
-        pp(y2, x, w)
         C.gemm_nt_(y1, x, w)
-        torch.cuda.synchronize()
-        err = ((y2.float() - y0.float()).abs().max() / y0.float().abs().max()).item()
-        arms = {"lib": lambda: torch.mm(x, w.t(), out=y0), "nt4": lambda: C.gemm_nt_(y1, x, w),
-                "pp8": lambda: pp(y2, x, w)}
+        errs = {}
         for m in modes:
-            if m:
-                arms[f"pp8m{m}"] = (lambda m_: (lambda: pp(y3, x, w, mode=m_)))(m)
+            if m.startswith("d"):
+                y2.zero_()
+                pp(y2, x, w, mode=m)
+                torch.cuda.synchronize()
+                errs[m] = float(f"{((y2.float() - y0.float()).abs().max() / y0.float().abs().max()).item():.2e}")
+        arms = {"lib": lambda: torch.mm(x, w.t(), out=y0), "nt4": lambda: C.gemm_nt_(y1, x, w)}
+        for m in modes:
+            arms[m] = (lambda m_: (lambda: pp(y2 if m_.startswith("d") else y3, x, w, mode=m_)))(m)
         t = {k_: [] for k_ in arms}
         for _ in range(a.rounds):
             for k_, f in arms.items():
@@ -123,8 +129,8 @@ def main():
         print(json.dumps({"gemm": name, "M": T, "N": n, "K": k,
                           **{f"{k_}_ms": round(v, 4) for k_, v in med.items()},
                           **{f"{k_}_tf": round(fl / v / 1e9) for k_, v in med.items()},
-                          "pp8_vs_lib": round(med["lib"] / med["pp8"], 4), "nt4_vs_lib": round(med["lib"] / med["nt4"], 4),
-                          "pp8_max_rel_err_vs_lib": float(f"{err:.2e}")}), flush=True)
+                          **{f"{k_}_vs_lib": round(med["lib"] / v, 4) for k_, v in med.items() if k_ != "lib"},
+                          "max_rel_err_vs_lib": errs}), flush=True)
         del x, w, y0, y1, y2, y3
         torch.cuda.empty_cache()
 

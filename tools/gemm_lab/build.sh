@@ -1,12 +1,12 @@
 #!/bin/bash
-# Build the GEMM lab kernels (CPU-side, in-tree; the .so files travel to the GPU box with the snapshot):
-# libgemm_pp.so (the kernel) and libgemm_pp_m{1,2,3}.so (timing-only ablations, wrong results: no loop DMA /
-# no loop DMA + fragment reads / no counted waits) -- each in its own library (no co-compiled variants).
+# Build the GEMM lab kernels (CPU-side, in-tree; the .so files travel to the GPU box with the snapshot), each
+# variant in its own library (no co-compiled variants): libgemm_pp_d{0..3}.so -- the ping-pong kernel with
+# its DMA pieces after / before the fragment reads, half / all of them inside the next compute phase;
+# libgemm_pp_m{1,2,3}.so -- timing-only ablations of d0 (wrong results): no loop DMA / no loop DMA + reads /
+# no counted waits.
 set -e
 cd "$(dirname "$0")/../.."
-for m in 0 1 2 3; do
-  out=tools/gemm_lab/libgemm_pp.so; [ $m -gt 0 ] && out=tools/gemm_lab/libgemm_pp_m$m.so
-  hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Icsrc/kernels -ffp-contract=fast -DPPM=$m \
-    tools/gemm_lab/gemm_pp.hip -o $out &
-done
+build() { hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Icsrc/kernels -ffp-contract=fast "$@"; }
+for d in 0 1 2 3; do build -DPPM=0 -DDMAP=$d tools/gemm_lab/gemm_pp.hip -o tools/gemm_lab/libgemm_pp_d$d.so & done
+for m in 1 2 3; do build -DPPM=$m -DDMAP=0 tools/gemm_lab/gemm_pp.hip -o tools/gemm_lab/libgemm_pp_m$m.so & done
 wait

@@ -32,6 +32,13 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #define PPM 0  // lab ablations (wrong results, timing only): 1 no loop DMA / waits, 2 + no loop reads, 3 no waits
 #endif
 constexpr bool kLoopDma = PPM == 0 || PPM == 3, kLoopRead = PPM != 2, kLoopWait = PPM == 0;
+// where a wave's 4 DMA pieces per load phase go: 0 after its fragment reads, 1 before them, 2 two before
+// them + two inside its next compute phase, 3 all four inside its next compute phase (spread over the MFMAs)
+#ifndef DMAP
+#define DMAP 0
+#endif
+constexpr int kLoadPieces = DMAP == 2 ? 2 : DMAP == 3 ? 0 : 4;  // pieces issued in the load phase
+constexpr int kG1P2Wait = DMAP == 2 ? 6 : DMAP == 3 ? 4 : 8;     // G1's count at the end of P2
 constexpr int BM = 256, BN = 256, BK = 64;
 constexpr int SLOT = 256 * BK * 2;  // 32 KiB
 constexpr int NSLOT = 5;
@@ -90,7 +97,10 @@ struct Cursor {
   const uint16_t* pb;
 };
 
-__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(PPArgs p) {
+#define PP_CAT2(a, b) a##b
+#define PP_CAT(a, b) PP_CAT2(a, b)
+#define PP_KERNEL PP_CAT(PP_CAT(gemm_pp_kernel_m, PPM), PP_CAT(_d, DMAP))
+__global__ __launch_bounds__(512, 1) void PP_KERNEL(PPArgs p) {
   __shared__ __attribute__((aligned(16))) char S[NSLOT * SLOT];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -147,13 +157,36 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(PPArgs p) {
   const unsigned lds_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)S;
   // one job share: 4 pieces (8 rows x 128 B each) of rows [row0 + 32 ws, +32) of operand A (op 0) or B
   // (op 1) of cursor c's stage, into slot `slot`
-  auto job = [&](const Cursor& c, int op, int row0, int slot) __attribute__((always_inline)) {
+  // one job share: 4 pieces (8 rows x 128 B each) of rows [row0 + 32 ws, +32) of operand A (op 0) or B
+  // (op 1) of cursor c's stage, into slot `slot`; described first (jobd), issued later (pieces j0..j1-1)
+  struct JobD {
+    __amdgpu_buffer_rsrc_t rs;
+    int s0, st, v0, v1;
+    unsigned dst;
+  };
+  auto jobd = [&](const Cursor& c, int op, int row0, int slot) __attribute__((always_inline)) {
     const long long ld = op == 0 ? p.lda : p.ldb;
     const int r0 = row0 + 32 * ws;
-    const auto rs = make_rsrc(op == 0 ? c.pa : c.pb);
-    const int s0 = (int)(r0 * ld * 2), st = (int)(8 * ld * 2);
-    const int v0 = op == 0 ? voa[0] : vob[0], v1 = op == 0 ? voa[1] : vob[1];
-    const unsigned dst = lds_base + (unsigned)(slot * SLOT + r0 * 128);
+    JobD d;
+    d.rs = make_rsrc(op == 0 ? c.pa : c.pb);
+    d.s0 = (int)(r0 * ld * 2);
+    d.st = (int)(8 * ld * 2);
+    d.v0 = op == 0 ? voa[0] : vob[0];
+    d.v1 = op == 0 ? voa[1] : vob[1];
+    d.dst = lds_base + (unsigned)(slot * SLOT + r0 * 128);
+    return d;
+  };
+  auto piece = [&](const JobD& d, int j) __attribute__((always_inline)) {
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %3, %4 offen sc0 lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"((j & 1) ? d.v1 : d.v0), "s"(d.dst + 1024u * j), "s"(d.rs), "s"(d.s0 + j * d.st)
+        : "memory");
+  };
+  auto job = [&](const Cursor& c, int op, int row0, int slot) __attribute__((always_inline)) {
+    const JobD d = jobd(c, op, row0, slot);
     unsigned keep;
     asm volatile(
         "s_mov_b32 %0, m0\n\t"
@@ -167,7 +200,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(PPArgs p) {
         "buffer_load_dwordx4 %2, %4, %8 offen sc0 lds\n\t"
         "s_mov_b32 m0, %0"
         : "=&s"(keep)
-        : "v"(v0), "v"(v1), "s"(dst), "s"(rs), "s"(s0), "s"(s0 + st), "s"(s0 + 2 * st), "s"(s0 + 3 * st)
+        : "v"(d.v0), "v"(d.v1), "s"(d.dst), "s"(d.rs), "s"(d.s0), "s"(d.s0 + d.st), "s"(d.s0 + 2 * d.st),
+          "s"(d.s0 + 3 * d.st)
         : "memory");
   };
 
@@ -207,6 +241,23 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(PPArgs p) {
 #pragma unroll
       for (int mt = 0; mt < 8; ++mt)
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nt], fa[mt], acc[mt][nt], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // the same 32 MFMAs with n pieces of a deferred job (j0 ..) spread over them
+  auto compute_dma = [&](const JobD& d, int j0, int n) __attribute__((always_inline)) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt) {
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nt], fa[mt], acc[mt][nt], 0, 0, 0);
+        const int idx = nt * 8 + mt;
+        if (n > 0 && idx % (32 / (n > 0 ? n : 1)) == 16 / (n > 0 ? n : 1) - 1) {
+          __builtin_amdgcn_sched_barrier(0);
+          if (kLoopDma) piece(d, j0 + idx / (32 / n));
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
     __builtin_amdgcn_s_setprio(0);
   };
   // a new tile: clear the accumulators in a load phase (128 v_mov once per tile; ONE loop body keeps the
@@ -279,16 +330,31 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(PPArgs p) {
   }
 
   clear();
+  constexpr int kDef = 4 - kLoadPieces;  // pieces deferred into the next compute phase
+  auto load_pieces = [&](const JobD& d) __attribute__((always_inline)) {
+    if (!kLoopDma) return;
+#pragma unroll
+    for (int j = 0; j < kLoadPieces; ++j) piece(d, j);
+  };
   if (grp == 0) {
     int s = 0, ti = 0;
+    JobD dA = jobd(c2, 0, 0, slotA(1));  // (no deferred pieces before stage 0: the prologue loaded stage 1)
     for (int t = 0; t < total; ++t) {
-      compute();                             // P0: (t, h0)
+      if (kDef > 0 && t > 0) compute_dma(dA, kLoadPieces, kDef);  // P0: (t, h0)
+      else compute();
       barrier();
-      if (kLoopRead) read(t, 1);                            // P1
-      if (kLoopDma) job(c2, 1, 0, slotB(t + 2));
+      const JobD dB = jobd(c2, 1, 0, slotB(t + 2));  // P1
+      if (DMAP == 0) {
+        if (kLoopRead) read(t, 1);
+        if (kLoopDma) job(c2, 1, 0, slotB(t + 2));
+      } else {
+        load_pieces(dB);
+        if (kLoopRead) read(t, 1);
+      }
       lgkm0();
       barrier();
-      compute();                             // P2: (t, h1)
+      if (kDef > 0) compute_dma(dB, kLoadPieces, kDef);  // P2: (t, h1)
+      else compute();
       if (kLoopWait) vmcnt<4>();
       barrier();
       if (s == ns - 1) {                     // P3
@@ -299,8 +365,14 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(PPArgs p) {
       } else {
         ++s;
       }
-      if (kLoopRead && t + 1 < total) read(t + 1, 0);
-      if (kLoopDma) job(c2, 0, 0, slotA(t + 2));
+      dA = jobd(c2, 0, 0, slotA(t + 2));
+      if (DMAP == 0) {
+        if (kLoopRead && t + 1 < total) read(t + 1, 0);
+        if (kLoopDma) job(c2, 0, 0, slotA(t + 2));
+      } else {
+        load_pieces(dA);
+        if (kLoopRead && t + 1 < total) read(t + 1, 0);
+      }
       lgkm0();
       barrier();
       cur_adv(c1);
@@ -319,18 +391,32 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(PPArgs p) {
         clear();
       }
       if (t == total) break;
-      if (kLoopRead) read(t, 0);
-      if (kLoopDma) job(c1, 0, 128, slotA(t + 1));
+      const JobD dA = jobd(c1, 0, 128, slotA(t + 1));
+      if (DMAP == 0) {
+        if (kLoopRead) read(t, 0);
+        if (kLoopDma) job(c1, 0, 128, slotA(t + 1));
+      } else {
+        load_pieces(dA);
+        if (kLoopRead) read(t, 0);
+      }
       lgkm0();
       barrier();
-      compute();                             // P1: (t, h0)
+      if (kDef > 0) compute_dma(dA, kLoadPieces, kDef);  // P1: (t, h0)
+      else compute();
       barrier();
-      if (kLoopRead) read(t, 1);                            // P2
-      if (kLoopDma) job(c2, 1, 128, slotB(t + 2));
+      const JobD dB = jobd(c2, 1, 128, slotB(t + 2));  // P2
+      if (DMAP == 0) {
+        if (kLoopRead) read(t, 1);
+        if (kLoopDma) job(c2, 1, 128, slotB(t + 2));
+      } else {
+        load_pieces(dB);
+        if (kLoopRead) read(t, 1);
+      }
       lgkm0();
-      if (kLoopWait) vmcnt<8>();
+      if (kLoopWait) vmcnt<kG1P2Wait>();
       barrier();
-      compute();                             // P3: (t, h1)
+      if (kDef > 0) compute_dma(dB, kLoadPieces, kDef);  // P3: (t, h1)
+      else compute();
       if (kLoopWait) vmcnt<4>();
       barrier();
       cur_adv(c1);
@@ -373,6 +459,6 @@ extern "C" int ftc_gemm_pp(const void* a, long long lda, const void* b, long lon
   while (x > 1 && grid % (8 * x)) x >>= 1;
   if (grid % 8) x = 1;
   p.xcc = x;
-  hipLaunchKernelGGL(gemm_pp_kernel, dim3(grid), dim3(512), 0, stream, p);
+  hipLaunchKernelGGL(PP_KERNEL, dim3(grid), dim3(512), 0, stream, p);
   return (int)hipGetLastError();
 }
