@@ -264,8 +264,10 @@ def main(argv=None) -> int:
     if a.rccl_channels > 0:
         os.environ["NCCL_MIN_NCHANNELS"] = os.environ["NCCL_MAX_NCHANNELS"] = str(a.rccl_channels)
     rccl_log = None
-    if a.device == "cuda" and a.gpus > 1 and "NCCL_DEBUG" not in os.environ:
-        # the channel count RCCL picks is in its INIT log lines: to a per-rank file (never stdout)
+    if (a.device == "cuda" and a.gpus > 1 and "NCCL_DEBUG_FILE" not in os.environ
+            and os.environ.get("NCCL_DEBUG", "").upper() in ("", "VERSION", "WARN", "NONE")):
+        # the channel count RCCL picks is in its INIT log lines: to a per-rank file (never stdout); a
+        # launcher's NCCL_DEBUG=VERSION / WARN is raised to INIT-subsystem INFO for this file only
         import tempfile
 
         rccl_log = os.path.join(tempfile.gettempdir(), f"ftc_rccl_{os.getpid()}.log")

@@ -61,8 +61,7 @@ int ftc_sumsq(const void* x, int is_fp32, long long n, float* partial, float* ou
 int ftc_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H, int KV, int D,
                   long long q_row_stride, long long kv_row_stride, long long o_row_stride, float scale, int causal,
                   int window, const int* doc_start, int kv_valid, hipStream_t stream);
-int ftc_flash_bwd_workspace2(int B, int S, int H, int D, int causal, int window, int docs, int kv_valid,
-                             long long* bytes);
+int ftc_flash_bwd_workspace(int B, int S, int H, int D, long long* bytes);
 long long ftc_decode_workspace_floats(int B, int H, int KV, int D, int max_len);
 int ftc_decode_attention(const void* q, void* kc, void* vc, const void* knew, const void* vnew, long long new_rs,
                          const int* lens, void* out, float* workspace, int B, int H, int KV, int D, int max_len,
@@ -618,9 +617,7 @@ void flash_bwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, co
   TORCH_CHECK(dk.stride(0) == dv.stride(0) && k.stride(0) == v.stride(0), "flash_bwd: k/v strides");
   TORCH_CHECK(lse.numel() == B * H * S, "flash_bwd: lse size");
   long long ws = 0;
-  check(ftc_flash_bwd_workspace2((int)B, (int)S, (int)H, (int)D, causal ? 1 : 0, (int)window, doc_start.has_value() ? 1 : 0,
-                                 (int)kv_valid, &ws),
-        "flash_bwd_workspace");
+  check(ftc_flash_bwd_workspace((int)B, (int)S, (int)H, (int)D, &ws), "flash_bwd_workspace");
   auto work = at::empty({ws}, q.options().dtype(at::kByte));
   check(ftc_flash_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
                       dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), work.data_ptr(), (int)B, (int)S, (int)H, (int)KV,

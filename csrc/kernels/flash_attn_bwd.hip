@@ -135,10 +135,6 @@ struct BwdArgs {
   const float* rcos;
   const float* rsin;
   const int* rpos;
-  // dS spill (causal, no window / documents / padding, D = 128): the dK/dV kernel stores dS^T[b][hq][key][q]
-  // (bf16, q contiguous, S x S per head) and bwd_dq_ds_kernel forms dQ = scale dS K from it; null = dQ
-  // recomputes S and dP itself (bwd_dq_kernel)
-  uint16_t* dsT;
 };
 
 // Inverse rotation of one row's gradient held as store_rows' accumulators: element i of tile dt is
@@ -167,59 +163,10 @@ DEV_INLINE void rope_inv_rows(f32x16* acc, const BwdArgs& a, long long token, in
     }
 }
 
-// ---------------------------------------------------------------- 1. delta (dS-spill path only)
-// The recomputing path forms delta inside bwd_dq_kernel (it runs first there); the dS-spill path runs
-// dK/dV first (it produces dS), so delta comes from this separate row-dot pass.
-template <int D>
-__global__ __launch_bounds__(256) void bwd_delta_kernel(BwdArgs a) {
-  constexpr int CPH = D / 8;  // 16-byte chunks per head
-  const int lane = threadIdx.x & 63;
-  const long long rows = (long long)a.B * a.S;
-  const int nch = a.H * CPH;
-  for (long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += (long long)gridDim.x * 4) {
-    const uint16_t* orow = a.o + row * a.o_rs;
-    const uint16_t* drow = a.dout + row * a.do_rs;
-    const int b = (int)(row / a.S), s = (int)(row % a.S);
-    for (int c0 = 0; c0 < nch; c0 += 64) {
-      const int c = c0 + lane;
-      float acc = 0.f;
-      if (c < nch) {
-        float x[8], y[8];
-        unpack8(reinterpret_cast<const uint4*>(orow)[c], x);
-        unpack8(reinterpret_cast<const uint4*>(drow)[c], y);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc += x[j] * y[j];
-      }
-#pragma unroll
-      for (int off = CPH / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-      if (c < nch && (c % CPH) == 0) {
-        const int h = c / CPH;
-        // workspace rows: [-delta | -lse/scale] -- the dK/dV kernel's accumulator start values, DMA'd as is
-        const long long ri = ((long long)b * a.H + h) * a.S + s;
-        a.delta[ri] = -acc;
-        a.delta[rows * a.H + ri] = -a.lse[ri] / a.scale;
-      }
-    }
-  }
-}
+// (Removed in round 5: the separate delta = rowsum(dO * O) pass -- bwd_dq_kernel forms delta from the
+// operands it already loads and runs first; 1.892 vs 1.933 ms per layer backward, profiles/r5/attn_ab2/.)
 
-template <int N>
-DEV_INLINE void vmwait() {
-  static_assert(N >= 0 && N < 64, "vmcnt field");
-  __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 15) | ((N >> 4) << 14));
-}
-// s_waitcnt vmcnt(n) for a wave-uniform runtime n in [0, 32): a scalar branch to the immediate form
-template <int N = 0>
-DEV_INLINE void vmwait_rt(int n) {
-  if constexpr (N < 32) {
-    if (n == N) vmwait<N>();
-    else vmwait_rt<N + 1>(n);
-  } else {
-    vmwait<0>();
-  }
-}
-
-// ---------------------------------------------------------------- 2. dK / dV
+// ---------------------------------------------------------------- 1. dK / dV
 // One workgroup = 4 waves = 256 keys of one (batch, kv head); each wave owns 64 keys as two 32-key
 // halves and keeps their dK^T / dV^T accumulators (2 x 2 x D/32 tiles = 256 VGPRs at D=128) for the
 // whole sweep over the G query heads x 32-row query slices, so the 512-register single-wave budget
@@ -285,7 +232,7 @@ DEV_INLINE void dkdv_dma(__amdgpu_buffer_rsrc_t qr, __amdgpu_buffer_rsrc_t dr, _
 // vs 1.788 ms), the round-4 in-wave interleaved 4-wave kernel "IL" (1.890 ms, profiles/r4/attn_final/),
 // no ping-pong (2.00 vs 1.97 ms), DMA distance 2 (1.99 vs 1.96 ms), 32-row slices at D = 64, and a
 // B1 B2 A order for half 1 carrying the raw S / dP' across the barrier (2.03 vs 1.96 ms).
-template <int D, int QR = 1, bool DSOUT = false>
+template <int D, int QR = 1>
 __global__ __launch_bounds__(512, 1) void bwd_dkdv8_kernel(BwdArgs a) {
   constexpr int HW = 1, DIST = 3;
   static_assert(QR == 1 || QR == 2, "one or two 32-row query blocks per slice");
@@ -482,10 +429,6 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv8_kernel(BwdArgs a) {
   };
   // phase B1: P, dS (bf16 B operands of the accumulating products) -- exp / mask / pack VALU work
   bf16x8 pb[QR][HW][2], sb[QR][HW][2];
-  // dS spill: lane (key, hh) stores at dS^T[key][qt + 4 hh + 8 g] -> per-lane byte offset in the head's plane
-  int dso[HW];
-#pragma unroll
-  for (int j = 0; j < HW; ++j) dso[j] = ((wkey0 + 32 * j + lr) * S + 4 * hh) * 2;
   auto phaseB1 = [&](const int it) __attribute__((always_inline)) {
 #pragma unroll
     for (int r = 0; r < QR; ++r) {
@@ -515,20 +458,6 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv8_kernel(BwdArgs a) {
         pb[r][j][1] = pack8_bf(s[r][j], 8);
         sb[r][j][0] = pack8_bf(dp[r][j], 0);
         sb[r][j][1] = pack8_bf(dp[r][j], 8);
-        if constexpr (DSOUT) {
-          // dS^T[key][qt + 4 hh + 8 g + 0..3] (g = 0..3) = this lane's packed dS, four 8-byte stores; inline
-          // asm so hipcc keeps them out of its waits (sync_slice counts them with the DMA pieces)
-          const auto rs = make_rsrc(a.dsT + ((long long)(b * a.H + kvh * G + it / nqt) * S) * S);
-          const uint4 lo = __builtin_bit_cast(uint4, sb[r][j][0]), hi = __builtin_bit_cast(uint4, sb[r][j][1]);
-          asm volatile(
-              "buffer_store_dwordx2 %0, %4, %5, %6 offen\n\t"
-              "buffer_store_dwordx2 %1, %4, %5, %6 offen offset:16\n\t"
-              "buffer_store_dwordx2 %2, %4, %5, %6 offen offset:32\n\t"
-              "buffer_store_dwordx2 %3, %4, %5, %6 offen offset:48"
-              ::"v"(make_uint2(lo.x, lo.y)), "v"(make_uint2(lo.z, lo.w)), "v"(make_uint2(hi.x, hi.y)),
-                "v"(make_uint2(hi.z, hi.w)), "v"(dso[j]), "s"(rs), "s"(qt * 2)
-              : "memory");
-        }
       }
     }
   };
@@ -557,14 +486,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv8_kernel(BwdArgs a) {
   };
   // one barrier per slice: slice it is in LDS for every wave, the DMA of slice it + 2 goes out
   auto sync_slice = [&](const int it, char* dma_slot) __attribute__((always_inline)) {
-    if constexpr (DSOUT) {
-      // the dS stores (STORES per slice, issued after that slice's DMA of slice + 3) count in vmcnt too:
-      // younger than slice it's pieces are the pieces of slices it+1, it+2 already issued and the stores of
-      // the (up to) 3 slices since slice it's DMA went out
-      constexpr int STORES = 4 * QR * HW;
-      const int ahead = min(total - 1, it + 2) - it;
-      vmwait_rt((ahead > 0 ? ahead : 0) * PER_SLICE + min(it, 3) * STORES);
-    } else if (it + 2 < total) {
+    if (it + 2 < total) {
       __builtin_amdgcn_s_waitcnt(VM_TWO);  // slices it+1, it+2 may fly on
     } else if (it + 1 < total) {
       __builtin_amdgcn_s_waitcnt(VM_ONE);  // slice it landed, it+1 may fly on
@@ -581,12 +503,21 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv8_kernel(BwdArgs a) {
   // ... [B2(it-1) A(it) B1(it)] ...; the halves run separate straight-line loops (one branch outside the
   // loop, not one per slice: the register allocator then sees two independent paths) with the same
   // barrier count
+  // causal: a slice whose last query row is above this wave's first key is masked out entirely for this
+  // wave (P = dS = 0) -- the wave skips its MFMAs and VALU there (wave-uniform) but keeps the barriers and
+  // its share of the DMA; its SIMD partner runs alone meanwhile.  On the diagonal key block that is slice
+  // w of 8 for wave w.
+  auto masked = [&](const int it) __attribute__((always_inline)) {
+    return a.causal && qbeg + (it % nqt) * BQ2 + BQ2 - 1 < wkey0;
+  };
   if (wave < 4) {  // waves w and w + 4 share a SIMD
     auto body = [&](const int it, const char* Qs, char* dma_slot) __attribute__((always_inline)) {
       sync_slice(it, dma_slot);
-      phaseA(Qs);
-      phaseB1(it);
-      phaseB2(Qs);
+      if (!masked(it)) {
+        phaseA(Qs);
+        phaseB1(it);
+        phaseB2(Qs);
+      }
     };
     for (int it = 0; it < total; it += 5) {
       body(it, slot0, slot3);
@@ -598,9 +529,11 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv8_kernel(BwdArgs a) {
   } else {
     auto body = [&](const int it, const char* Qs, const char* Qprev, char* dma_slot) __attribute__((always_inline)) {
       sync_slice(it, dma_slot);
-      if (it > 0) phaseB2(Qprev);
-      phaseA(Qs);
-      phaseB1(it);
+      if (it > 0 && !masked(it - 1)) phaseB2(Qprev);
+      if (!masked(it)) {
+        phaseA(Qs);
+        phaseB1(it);
+      }
     };
     for (int it = 0; it < total; it += 5) {
       body(it, slot0, slot4, slot3);
@@ -609,7 +542,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv8_kernel(BwdArgs a) {
       if (it + 3 < total) body(it + 3, slot3, slot2, slot1);
       if (it + 4 < total) body(it + 4, slot4, slot3, slot2);
     }
-    if (total > 0) {
+    if (total > 0 && !masked(total - 1)) {
       const int r = (total - 1) % 5;
       phaseB2(r == 0 ? slot0 : r == 1 ? slot1 : r == 2 ? slot2 : r == 3 ? slot3 : slot4);
     }
@@ -648,7 +581,7 @@ DEV_INLINE void kv_dma(__amdgpu_buffer_rsrc_t kr, __amdgpu_buffer_rsrc_t vr, con
   }
 }
 
-template <int D, int OCC, bool FDELTA = true>
+template <int D, int OCC>
 __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
   constexpr int NCH = D / 8, DSTEPS = D / 16, DT = D / 32;
   constexpr int BQ = 128, BK = 64;
@@ -692,9 +625,7 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
   // pass over dO and O is gone.  The row constants the dK/dV kernel DMAs ([-delta | -lse/scale] in the
   // workspace) are written here too: this kernel runs first.
   float dsum = 0.f;
-  if constexpr (!FDELTA) {
-    dsum = -a.delta[sidx];
-  } else {
+  {
     const uint16_t* op = a.o + ((long long)b * S + qrow) * a.o_rs + (long long)hq * D + 8 * hh;
 #pragma unroll
     for (int s = 0; s < DSTEPS; ++s) {
@@ -705,9 +636,9 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
       for (int j = 0; j < 8; ++j) dsum += fo[j] * fd[j];
     }
   }
-  if constexpr (FDELTA) dsum += __shfl_xor(dsum, 32, 64);
+  dsum += __shfl_xor(dsum, 32, 64);
   const float ndlt = -dsum;
-  if (FDELTA && hh == 0) {
+  if (hh == 0) {
     a.delta[sidx] = ndlt;
     a.delta[(long long)a.B * S * a.H + sidx] = -lse / a.scale;
   }
@@ -760,6 +691,7 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     __builtin_amdgcn_s_barrier();        // ... everyone's; and tile t-1's buffers are free
     if (t + 1 < ntiles) issue(kv0 + BK, Kn, Vn);  // flies under this tile's compute
+    if (a.causal && kv0 > q0 + wave * 32 + 31) return;  // tile above this wave's rows: dS = 0 (wave-uniform)
     f32x16 s[2], dp[2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
@@ -845,105 +777,14 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
 }
 
 
-// ---------------------------------------------------------------- dQ from the spilled dS (D = 128)
-// dQ^T[d][q] = scale sum_k K^T[d][k] dS^T[k][q]: one workgroup = 128 query rows of one (b, q head), key tiles
-// of 64 up to the diagonal (causal; the dK/dV kernel wrote zeros where the mask applies).  Both operands
-// by ds_read_b64_tr_b16 from [64 keys][128] LDS images (the K tile and the dS^T tile share the swizzled
-// 256-byte-row geometry), filled by LDS-DMA one tile ahead: a third of the recomputing kernel's MFMAs,
-// no softmax, the dS^T tile streamed once from HBM.
-__global__ __launch_bounds__(256, 2) void bwd_dq_ds_kernel(BwdArgs a) {
-  constexpr int D = 128, NCH = D / 8, DT = D / 32;
-  constexpr int BQ = 128, BK = 64;
-  constexpr int TILE = BK * D * 2;  // 16 KiB: K [64][128] or dS^T [64][128 q]
-  __shared__ __attribute__((aligned(16))) char Kt0[TILE];
-  __shared__ __attribute__((aligned(16))) char Dt0[TILE];
-  __shared__ __attribute__((aligned(16))) char Kt1[TILE];
-  __shared__ __attribute__((aligned(16))) char Dt1[TILE];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int hh = lane >> 5, lr = lane & 31;
-  const int S = a.S, G = a.H / a.KV;
-  const int nqb = S / BQ;
-  const int qr = blockIdx.x / (a.B * a.H);
-  const int rem = blockIdx.x % (a.B * a.H);
-  const int b = rem / a.H, hq = rem % a.H;
-  const int kvh = hq / G;
-  const int qb = nqb - 1 - qr;  // heaviest (latest) query blocks first
-  const int q0 = qb * BQ;
-  const int qrow = q0 + wave * 32 + lr;
-  const int ntiles = (q0 + BQ) / BK;
-
-  constexpr int NGT = TILE / 1024 / 4;  // 1 KiB pieces per wave per matrix
-  constexpr int RPG = 1024 / (D * 2);   // rows per piece
-  const auto krs = make_rsrc(a.k + (long long)b * S * a.kv_rs + (long long)kvh * D);
-  const auto drs = make_rsrc(a.dsT + ((long long)(b * a.H + hq) * S) * S + q0);
-  int kvo[NGT], dvo[NGT];
-#pragma unroll
-  for (int i = 0; i < NGT; ++i) {
-    const int row = (wave * NGT + i) * RPG + lane / NCH, pc = lane % NCH;
-    const int lc = (pc ^ swz(row)) & (NCH - 1);
-    kvo[i] = (row * (int)a.kv_rs + lc * 8) * 2;
-    dvo[i] = (row * S + lc * 8) * 2;
-  }
-  auto issue = [&](int kv0_, char* kdst, char* ddst) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < NGT; ++i) {
-      const int r0 = (wave * NGT + i) * RPG;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (__attribute__((address_space(3))) void*)(kdst + r0 * D * 2), 16,
-                                               kvo[i], kv0_ * (int)a.kv_rs * 2, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, (__attribute__((address_space(3))) void*)(ddst + r0 * D * 2), 16,
-                                               dvo[i], kv0_ * S * 2, 0, 0);
-    }
-  };
-
-  f32x16 dq[DT];
-#pragma unroll
-  for (int t = 0; t < DT; ++t)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) dq[t][i] = 0.f;
-  const int2 tq = tr_offsets<D>(wave * 32, lane);  // this wave's 32 query columns of the dS^T image
-  if (ntiles > 0) issue(0, Kt0, Dt0);
-  auto tile = [&](const int t, const char* Kc, const char* Dc, char* Kn, char* Dn) __attribute__((always_inline)) {
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's pieces of tile t landed (vmcnt(0))
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();  // everyone's; tile t-1's buffers are free
-    if (t + 1 < ntiles) issue((t + 1) * BK, Kn, Dn);
-    bf16x8 sb[4];
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) sb[ks] = tr_read<D>(Dc, 16 * ks, tq);
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      bf16x8 ka[4];
-      const int2 to = tr_offsets<D>(dt * 32, lane);
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) ka[ks] = tr_read<D>(Kc, 16 * ks, to);
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) dq[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[ks], sb[ks], dq[dt], 0, 0, 0);
-    }
-  };
-  for (int t = 0; t < ntiles; t += 2) {
-    tile(t, Kt0, Dt0, Kt1, Dt1);
-    if (t + 1 < ntiles) tile(t + 1, Kt1, Dt1, Kt0, Dt0);
-  }
-  uint16_t* op = a.dq + ((long long)b * S + qrow) * a.dq_rs + (long long)hq * D;
-  if (a.rcos) rope_inv_rows<DT>(dq, a, (long long)b * S + qrow, hh);
-  store_rows<DT>(op, dq, a.scale, hh, (a.dq_rs & 7) == 0);
-}
-
 }  // namespace
 
-// the dS-spill path: the causal, full-sequence, D = 128 shape of every training step (dK/dV stores dS^T,
-// bwd_dq_ds_kernel reads it); windows, packed documents and padded tails keep the recomputing dQ
-static bool ds_spill(int S, int D, int causal, int window, bool docs, int kv_valid) {
-  return D == 128 && causal && window <= 0 && !docs && (kv_valid <= 0 || kv_valid >= S);
-}
-
-extern "C" int ftc_flash_bwd_workspace2(int B, int S, int H, int D, int causal, int window, int docs, int kv_valid,
-                                        long long* bytes) {
+// (Removed in round 5: a dS spill -- dK/dV stores dS^T (bf16), a third kernel forms dQ = scale dS K from
+// it instead of recomputing S and dP.  dK/dV 1.435 vs 1.119 ms (2.15 GB of dS stores at the Llama-3-8B
+// layer, B4 S4096) and the dS-reading dQ 0.586 vs 0.773: 2.079 vs 1.892 ms per layer, memory bound on both
+// sides, profiles/r5/attn_ab2/; git history has the kernels.)
+extern "C" int ftc_flash_bwd_workspace(int B, int S, int H, int D, long long* bytes) {
   *bytes = 2LL * B * H * S * sizeof(float);  // -delta, -lse/scale
-  if (ds_spill(S, D, causal, window, docs != 0, kv_valid))
-    *bytes += 2LL * B * H * S * S + 256;  // dS^T [B][H][S][S] bf16, 256-byte aligned after the row constants
   return 0;
 }
 
@@ -966,27 +807,11 @@ extern "C" int ftc_flash_bwd(const void* q, const void* k, const void* v, const 
   BwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (const uint16_t*)o, (const uint16_t*)dout,
             lse, (float*)workspace, (uint16_t*)dq, (uint16_t*)dk, (uint16_t*)dv, q_rs, kv_rs, o_rs, dq_rs, dkv_rs, do_rs,
             B, S, H, KV, scale, scale * LOG2E, causal, window, doc_start, doc_end, kv_valid,
-            rope_cos, rope_sin, rope_pos, nullptr};
+            rope_cos, rope_sin, rope_pos};
   const int g_kv = B * KV * (S / 256);
   const int g_q = B * H * (S / 128);
-  const char* lab = getenv("FTC_FLASH_BWD_MODE");  // LAB A/B (removed after measurement): sep | ds | fused
-  if (lab && lab[0] == 's' && lab[1] == 'e' && D == 128) {
-    hipLaunchKernelGGL(bwd_delta_kernel<128>, dim3(ftc::oneshot_grid((long long)B * S, 4)), dim3(256), 0, stream, a);
-    hipLaunchKernelGGL((bwd_dkdv8_kernel<128, 1>), dim3(g_kv), dim3(512), 0, stream, a);
-    hipLaunchKernelGGL((bwd_dq_kernel<128, 2, false>), dim3(g_q), dim3(256), 0, stream, a);
-    return (int)hipGetLastError();
-  }
-  if (lab && lab[0] == 'd' && ds_spill(S, D, causal, window, doc_start != nullptr, kv_valid)) {
-    // delta pass, then dK/dV (also writes dS^T), then dQ = dS K as a plain GEMM over the spilled dS^T
-    a.dsT = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(workspace) +
-                                        ((2LL * B * H * S * sizeof(float) + 255) & ~255LL));
-    hipLaunchKernelGGL(bwd_delta_kernel<128>, dim3(ftc::oneshot_grid((long long)B * S, 4)), dim3(256), 0, stream, a);
-    hipLaunchKernelGGL((bwd_dkdv8_kernel<128, 1, true>), dim3(g_kv), dim3(512), 0, stream, a);
-    hipLaunchKernelGGL(bwd_dq_ds_kernel, dim3(g_q), dim3(256), 0, stream, a);
-    return (int)hipGetLastError();
-  }
   // dQ first: it forms delta for its rows and writes the workspace row constants the dK/dV kernel reads
-  // (the separate delta pass is gone).  dQ at 2 waves per SIMD (one wave per SIMD, 512 registers: +0.2 ms at
+  // (the separate delta pass is gone: -41 us per layer, profiles/r5/attn_ab2/).  dQ at 2 waves per SIMD (one wave per SIMD, 512 registers: +0.2 ms at
   // the Llama-3-8B layer shape, profiles/r4/attn_final/); D = 64 dK/dV takes two 32-row query blocks per slice
   if (D == 128) {
     hipLaunchKernelGGL((bwd_dq_kernel<128, 2>), dim3(g_q), dim3(256), 0, stream, a);

@@ -386,6 +386,9 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
   // wave passed this tile's barrier
   auto tile = [&](const int t, const char* Kc, const char* Vc, char* Kn, char* Vn) __attribute__((always_inline)) {
     sync_tile(t, Kn, Vn);
+    // causal: a tile entirely above this wave's 32 rows contributes nothing (its P is 0 and the running
+    // max does not move) -- skip it (wave-uniform; barriers and the DMA share stay)
+    if (a.causal && kv_begin + t * BK > q0 + wave * 32 + 31) return;
     if constexpr (FWD_PRIO) __builtin_amdgcn_s_setprio(1);  // S MFMA phase ahead of the partner wave's VALU
     phaseA(Kc);
     if constexpr (FWD_PRIO) __builtin_amdgcn_s_setprio(0);

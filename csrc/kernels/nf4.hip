@@ -137,7 +137,27 @@ __global__ __launch_bounds__(256) void nf4_dequant_kernel(const uint8_t* __restr
   }
 }
 
-// dequantise into a row view: out[n * ldo + k] (a column block of an augmented GEMM operand)
+// 8 codes (one 32-bit word, first element in the high nibble of each byte) -> 8 bf16 (one 16-byte chunk)
+DEV_INLINE uint4 nf4_decode8(uint32_t w, float a, const float* lut) {
+  float f[8];
+#pragma unroll
+  for (int bt = 0; bt < 4; ++bt) {
+    const uint32_t byte = (w >> (8 * bt)) & 0xffu;
+    f[2 * bt] = lut[byte >> 4] * a;
+    f[2 * bt + 1] = lut[byte & 0xf] * a;
+  }
+  return pack8(f);
+}
+DEV_INLINE float nf4_absmax(const uint8_t* aq, const float* s2, float off, long long bi, int block2) {
+  return off + ((float)aq[bi] - 128.0f) * (1.0f / 127.0f) * s2[bi / block2];
+}
+
+// dequantise into a row view: out[n * ldo + k] (a column block of an augmented GEMM operand).
+// Lane-contiguous chunks: chunk c = 8 elements; a wave's load instruction reads 64 consecutive 4-byte code
+// words and its store writes 64 consecutive 16-byte chunks (1 KiB, whole lines), NCH chunks per thread all
+// loaded before any is decoded.  (Round 4: 16 codes per thread, two 16-byte stores at a 32-byte lane stride:
+// 3.7 TB/s.)
+constexpr int kRowsNCH = 4;
 __global__ __launch_bounds__(256) void nf4_dequant_rows_kernel(const uint8_t* __restrict__ packed,
                                                                const uint8_t* __restrict__ aq,
                                                                const float* __restrict__ s2, float off,
@@ -151,74 +171,82 @@ __global__ __launch_bounds__(256) void nf4_dequant_rows_kernel(const uint8_t* __
   }
   __shared__ float lut[16];
   nf4_lut_load(lut);
-  const long long n16 = n >> 4;
-  const int c16 = cols >> 4;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long long)main_blocks * 256) {
-    const uint2 p = reinterpret_cast<const uint2*>(packed)[i];
-    const long long e0 = i << 4;
-    const long long bi = e0 / block;
-    const float a = off + ((float)aq[bi] - 128.0f) * (1.0f / 127.0f) * s2[bi / block2];
-    float f[16];
-    const uint32_t words[2] = {p.x, p.y};
+  const long long n8 = n >> 3;
+  const int c8 = cols >> 3;
+  const int per_block = block >> 3;  // chunks per absmax block
+  for (long long base = (long long)blockIdx.x * 256 * kRowsNCH; base < n8; base += (long long)main_blocks * 256 * kRowsNCH) {
+    uint32_t w[kRowsNCH];
+    float am[kRowsNCH];
 #pragma unroll
-    for (int wd = 0; wd < 2; ++wd)
+    for (int j = 0; j < kRowsNCH; ++j) {
+      const long long c = base + j * 256 + threadIdx.x;
+      w[j] = c < n8 ? reinterpret_cast<const uint32_t*>(packed)[c] : 0u;
+      am[j] = c < n8 ? nf4_absmax(aq, s2, off, c / per_block, block2) : 0.f;
+    }
 #pragma unroll
-      for (int bt = 0; bt < 4; ++bt) {
-        const uint32_t byte = (words[wd] >> (8 * bt)) & 0xffu;
-        f[wd * 8 + bt * 2] = lut[byte >> 4] * a;
-        f[wd * 8 + bt * 2 + 1] = lut[byte & 0xf] * a;
+    for (int j = 0; j < kRowsNCH; ++j) {
+      const long long c = base + j * 256 + threadIdx.x;
+      if (c < n8) {
+        const long long row = c / c8;
+        const int col = (int)(c - row * c8) * 8;
+        *reinterpret_cast<uint4*>(out + row * ldo + col) = nf4_decode8(w[j], am[j], lut);
       }
-    const long long row = i / c16;
-    const int c = (int)(i - row * c16) * 16;
-    uint4* o = reinterpret_cast<uint4*>(out + row * ldo + c);
-    o[0] = pack8(f);
-    o[1] = pack8(f + 8);
+    }
   }
 }
 
 // dequantise TRANSPOSED: outT[k * ldo + n] = W[n][k] -- the K-contiguous right operand of the backward
-// GEMM dx = dy . W (TN layout).  A 64 x 64 tile per workgroup, transposed through LDS; one NF4 block
-// (64 along k) per row of the tile, so one absmax per thread.
+// GEMM dx = dy . W (TN layout).  A 64 (n) x 128 (k) tile per workgroup through LDS as [k][n]:
+//   decode: thread (n pair 2m, 2m + 1; 16 k) loads the two rows' 8-byte code runs, and writes each k's
+//           (W[2m][k], W[2m+1][k]) pair as ONE 32-bit LDS word (16 ds_write_b32, not 32 ds_write_b16);
+//   store:  each output row segment (64 n = 128 bytes) is 8 lanes x 16 bytes of one store instruction, a wave
+//           instruction covers 8 whole rows (ds_read_b128 from a 16-byte-aligned padded LDS row).
+// (Round 4: 64 x 64 tiles, 16-bit LDS writes and reads, 3.6 TB/s.)
+constexpr int kTN = 64, kTK = 128, kTPad = 8;  // LDS row = kTN + kTPad bf16 = 144 bytes
 __global__ __launch_bounds__(256) void nf4_dequant_t_kernel(const uint8_t* __restrict__ packed,
                                                             const uint8_t* __restrict__ aq,
                                                             const float* __restrict__ s2, float off,
                                                             uint16_t* __restrict__ outT, int N, int K, long long ldo,
                                                             int block2, AugTail tail) {
-  if ((int)blockIdx.y == K / 64) {  // the extra row of workgroups: the rank-r operand parts
+  if ((int)blockIdx.y == (K + kTK - 1) / kTK) {  // the extra row of workgroups: the rank-r operand parts
     aug_tail_fill(tail, (long long)blockIdx.x * 256 + threadIdx.x, (long long)gridDim.x * 256);
     return;
   }
-  __shared__ uint16_t tile[64][64 + 2];
+  __shared__ __attribute__((aligned(16))) uint16_t tile[kTK][kTN + kTPad];
   __shared__ float lut[16];
   nf4_lut_load(lut);
-  const int n0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
+  const int n0 = blockIdx.x * kTN, k0 = blockIdx.y * kTK;
+  const int kvalid = min(kTK, K - k0);  // K % 128 == 64: a half tile at the end
   const int t = threadIdx.x;
-  {
-    const int nl = t >> 2, kq = (t & 3) * 16;
-    const long long e0 = (long long)(n0 + nl) * K + k0 + kq;
-    const uint2 p = *reinterpret_cast<const uint2*>(packed + (e0 >> 1));
-    const long long bi = e0 >> 6;  // block 64
-    const float a = off + ((float)aq[bi] - 128.0f) * (1.0f / 127.0f) * s2[bi / block2];
-    const uint32_t words[2] = {p.x, p.y};
+  if ((t >> 5) * 16 < kvalid) {
+    const int m = t & 31, seg = t >> 5;  // rows n0 + 2m, 2m + 1; k in [16 seg, 16 seg + 16)
+    const int kq = seg * 16;
+    const long long e0 = (long long)(n0 + 2 * m) * K + k0 + kq;  // first element of row 2m's run
+    const long long e1 = e0 + K;
+    const uint2 p0 = *reinterpret_cast<const uint2*>(packed + (e0 >> 1));
+    const uint2 p1 = *reinterpret_cast<const uint2*>(packed + (e1 >> 1));
+    const float a0 = nf4_absmax(aq, s2, off, e0 >> 6, block2), a1 = nf4_absmax(aq, s2, off, e1 >> 6, block2);
+    const uint32_t w0[2] = {p0.x, p0.y}, w1[2] = {p1.x, p1.y};
 #pragma unroll
     for (int wd = 0; wd < 2; ++wd)
 #pragma unroll
       for (int bt = 0; bt < 4; ++bt) {
-        const uint32_t byte = (words[wd] >> (8 * bt)) & 0xffu;
+        const uint32_t b0 = (w0[wd] >> (8 * bt)) & 0xffu, b1 = (w1[wd] >> (8 * bt)) & 0xffu;
         const int kk = kq + wd * 8 + bt * 2;
-        tile[kk][nl] = f2bf(lut[byte >> 4] * a);
-        tile[kk + 1][nl] = f2bf(lut[byte & 0xf] * a);
+        *reinterpret_cast<uint32_t*>(&tile[kk][2 * m]) = pack_bf2(lut[b0 >> 4] * a0, lut[b1 >> 4] * a1);
+        *reinterpret_cast<uint32_t*>(&tile[kk + 1][2 * m]) = pack_bf2(lut[b0 & 0xf] * a0, lut[b1 & 0xf] * a1);
       }
   }
   __syncthreads();
   {
-    const int kl = t >> 2, np = (t & 3) * 16;
-    uint32_t w[8];
+    const int lane = t & 63, wave = t >> 6, ch = lane & 7;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) w[j] = (uint32_t)tile[kl][np + 2 * j] | ((uint32_t)tile[kl][np + 2 * j + 1] << 16);
-    uint4* o = reinterpret_cast<uint4*>(outT + (long long)(k0 + kl) * ldo + n0 + np);
-    o[0] = make_uint4(w[0], w[1], w[2], w[3]);
-    o[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    for (int j = 0; j < kTK / 32; ++j) {
+      const int kr = wave * (kTK / 4) + j * 8 + (lane >> 3);
+      if (kr >= kvalid) break;
+      const uint4 v = *reinterpret_cast<const uint4*>(&tile[kr][ch * 8]);
+      *reinterpret_cast<uint4*>(outT + (long long)(k0 + kr) * ldo + n0 + ch * 8) = v;
+    }
   }
 }
 
@@ -248,12 +276,13 @@ extern "C" int ftc_nf4_dequant_aug(const uint8_t* packed, const uint8_t* absmax_
   const bool has_tail = R > 0 && (B || A);
   if (!has_tail) t.B = t.A = nullptr;
   if (transpose) {
-    if (rows % 64 != 0) return -1;
-    hipLaunchKernelGGL(nf4_dequant_t_kernel, dim3(rows / 64, cols / 64 + (has_tail ? 1 : 0)), dim3(256), 0, stream,
+    if (rows % kTN != 0) return -1;
+    const int ky = (cols + kTK - 1) / kTK;
+    hipLaunchKernelGGL(nf4_dequant_t_kernel, dim3(rows / kTN, ky + (has_tail ? 1 : 0)), dim3(256), 0, stream,
                        packed, absmax_q, absmax_scale, absmax_offset, (uint16_t*)out, rows, cols, ldo, block2, t);
   } else {
     const long long n = (long long)rows * cols;
-    const int grid = ftc::oneshot_grid(n / 16, 256);
+    const int grid = ftc::oneshot_grid(n / 8, 256 * kRowsNCH);
     hipLaunchKernelGGL(nf4_dequant_rows_kernel, dim3(grid + (has_tail ? kTailBlocks : 0)), dim3(256), 0, stream,
                        packed, absmax_q, absmax_scale, absmax_offset, (uint16_t*)out, n, cols, ldo, block, block2, grid,
                        t);

@@ -37,8 +37,10 @@ def test_extension_ships_only_the_winning_variants():
         assert name not in text, name
     syms = subprocess.run(["nm", "-C", SO], capture_output=True, text=True, check=True).stdout
     # flash backward: the 8-wave ping-pong dK/dV (QR 1 at D = 128, 2 at D = 64) and the 2-wave/SIMD dQ only
-    assert "bwd_dkdv8_kernel<128, 1, " in syms and "bwd_dkdv8_kernel<64, 2, false>" in syms
-    for gone in ("bwd_dkdv_il_kernel", "bwd_dkdv_kernel<", "bwd_dq_kernel<128, 1>", "bwd_dq_kernel<64, 1>"):
+    assert "bwd_dkdv8_kernel<128, 1>" in syms and "bwd_dkdv8_kernel<64, 2>" in syms
+    # round 5: delta fused into dQ (no separate pass); the dS-spill dQ lost (profiles/r5/attn_ab2/)
+    for gone in ("bwd_dkdv_il_kernel", "bwd_dkdv_kernel<", "bwd_dq_kernel<128, 1>", "bwd_dq_kernel<64, 1>",
+                 "bwd_delta_kernel", "bwd_dq_ds_kernel"):
         assert gone not in syms, gone
     # projection GEMM: one kernel template (bf16 / fp32 C x epilogue x beta), no store / DMA-policy variants
     nt = set(re.findall(r"gemm_nt_kernel<[^>]*>", syms))

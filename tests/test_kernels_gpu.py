@@ -875,11 +875,13 @@ def test_nf4_fused_gemm_matches_dequant(C, M):
     torch.testing.assert_close(nf4.nf4_matmul(x, qw).float(), ref, atol=2e-2, rtol=2e-2)
 
 
-def test_nf4_dequantize_into_rows_and_transposed(C):
+@pytest.mark.parametrize("N,K", [(192, 320), (512, 1408), (256, 4160)])
+def test_nf4_dequantize_into_rows_and_transposed(C, N, K):
+    """Row and transposed (64 x 128 LDS tile; K % 128 == 64 ends in a half tile) decodes, bitwise the
+    reference dequantisation, nothing written outside the views."""
     from finetune_controller_amd.ops import nf4
 
     torch.manual_seed(3)
-    N, K = 192, 320
     qw = nf4.NF4Weight.quantize(bf(torch.randn(N, K, device=DEV) * 0.05))
     ref = qw.dequantize()
     buf = torch.full((N, K + 64), 7.0, device=DEV, dtype=torch.bfloat16)

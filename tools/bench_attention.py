@@ -35,7 +35,6 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--window", type=int, default=0)
-    ap.add_argument("--ab", default="", help="LAB: comma list of FTC_FLASH_BWD_MODE values to time besides the default")
     ap.add_argument("--doc-len", type=int, default=0, help="packed documents of this many tokens (0: one per row)")
     a = ap.parse_args()
     from finetune_controller_amd.ops.attention import _FlashPacked, _sdpa_packed, segments_from_eos
@@ -71,9 +70,6 @@ def main():
         f()
     torch.cuda.synchronize()
     res = {"ours_fwd": [], "sdpa_fwd": [], "ours_fwdbwd": [], "sdpa_fwdbwd": []}
-    modes = [m for m in a.ab.split(",") if m]
-    for m in modes:
-        res[f"{m}_fwdbwd"] = []
     with torch.no_grad():
         pass
     for _ in range(a.rounds):
@@ -84,10 +80,6 @@ def main():
                                           a.iters))
         res["ours_fwdbwd"].append(timeit(ours_fb, a.iters))
         res["sdpa_fwdbwd"].append(timeit(sdpa_fb, a.iters))
-        for m in modes:
-            os.environ["FTC_FLASH_BWD_MODE"] = m
-            res[f"{m}_fwdbwd"].append(timeit(ours_fb, a.iters))
-            os.environ.pop("FTC_FLASH_BWD_MODE")
     out = {"shape": dict(B=B, S=S, H=H, KV=KV, D=D, causal=True, window=a.window, doc_len=a.doc_len)}
     for k, v in res.items():
         ms = min(v)
