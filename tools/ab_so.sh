@@ -1,6 +1,6 @@
 #!/bin/bash
-# A/B two builds of the kernel extension on one box: finetune_controller_amd/_C_a.so and _C_b.so (built
-# here beforehand) are copied in turn over _C.so and the same command runs against each, alternating
+# A/B builds of the kernel extension on one box: finetune_controller_amd/_C_a.so, _C_b.so, ... (VARIANTS,
+# default "a b"; built here beforehand) are copied in turn over _C.so and the same command runs against each, alternating
 # for ROUNDS rounds (box drift hits both arms).  Usage (from gpurun):
 #   ROUNDS=3 OUT=name bash tools/ab_so.sh 'python -u tools/bench_attention.py' 'python -u bench.py'
 # -> gpurun_out/OUT/{a,b}_<cmd index>_r<round>.log
@@ -10,7 +10,7 @@ export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
 O=gpurun_out/${OUT:-ab_so}; mkdir -p $O
 P=finetune_controller_amd
 for r in $(seq 1 ${ROUNDS:-2}); do
-  for v in a b; do
+  for v in ${VARIANTS:-a b}; do
     cp $P/_C_$v.so $P/_C.so || exit 1
     i=0
     for c in "$@"; do
