@@ -503,21 +503,12 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv8_kernel(BwdArgs a) {
   // ... [B2(it-1) A(it) B1(it)] ...; the halves run separate straight-line loops (one branch outside the
   // loop, not one per slice: the register allocator then sees two independent paths) with the same
   // barrier count
-  // causal: a slice whose last query row is above this wave's first key is masked out entirely for this
-  // wave (P = dS = 0) -- the wave skips its MFMAs and VALU there (wave-uniform) but keeps the barriers and
-  // its share of the DMA; its SIMD partner runs alone meanwhile.  On the diagonal key block that is slice
-  // w of 8 for wave w.
-  auto masked = [&](const int it) __attribute__((always_inline)) {
-    return a.causal && qbeg + (it % nqt) * BQ2 + BQ2 - 1 < wkey0;
-  };
   if (wave < 4) {  // waves w and w + 4 share a SIMD
     auto body = [&](const int it, const char* Qs, char* dma_slot) __attribute__((always_inline)) {
       sync_slice(it, dma_slot);
-      if (!masked(it)) {
-        phaseA(Qs);
-        phaseB1(it);
-        phaseB2(Qs);
-      }
+      phaseA(Qs);
+      phaseB1(it);
+      phaseB2(Qs);
     };
     for (int it = 0; it < total; it += 5) {
       body(it, slot0, slot3);
@@ -529,11 +520,9 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv8_kernel(BwdArgs a) {
   } else {
     auto body = [&](const int it, const char* Qs, const char* Qprev, char* dma_slot) __attribute__((always_inline)) {
       sync_slice(it, dma_slot);
-      if (it > 0 && !masked(it - 1)) phaseB2(Qprev);
-      if (!masked(it)) {
-        phaseA(Qs);
-        phaseB1(it);
-      }
+      if (it > 0) phaseB2(Qprev);
+      phaseA(Qs);
+      phaseB1(it);
     };
     for (int it = 0; it < total; it += 5) {
       body(it, slot0, slot4, slot3);
@@ -542,7 +531,7 @@ __global__ __launch_bounds__(512, 1) void bwd_dkdv8_kernel(BwdArgs a) {
       if (it + 3 < total) body(it + 3, slot3, slot2, slot1);
       if (it + 4 < total) body(it + 4, slot4, slot3, slot2);
     }
-    if (total > 0 && !masked(total - 1)) {
+    if (total > 0) {
       const int r = (total - 1) % 5;
       phaseB2(r == 0 ? slot0 : r == 1 ? slot1 : r == 2 ? slot2 : r == 3 ? slot3 : slot4);
     }
@@ -691,7 +680,6 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     __builtin_amdgcn_s_barrier();        // ... everyone's; and tile t-1's buffers are free
     if (t + 1 < ntiles) issue(kv0 + BK, Kn, Vn);  // flies under this tile's compute
-    if (a.causal && kv0 > q0 + wave * 32 + 31) return;  // tile above this wave's rows: dS = 0 (wave-uniform)
     f32x16 s[2], dp[2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
@@ -779,6 +767,9 @@ __global__ __launch_bounds__(256, OCC) void bwd_dq_kernel(BwdArgs a) {
 
 }  // namespace
 
+// (Removed in round 5: skipping the causal slices / tiles a wave sees fully masked, in dK/dV and dQ -- the
+// wave-uniform branch cost more than the diagonal work it saved: forward + backward 2.478 vs 2.437 ms,
+// headline -0.75 %, profiles/r5/attn_skip/.)
 // (Removed in round 5: a dS spill -- dK/dV stores dS^T (bf16), a third kernel forms dQ = scale dS K from
 // it instead of recomputing S and dP.  dK/dV 1.435 vs 1.119 ms (2.15 GB of dS stores at the Llama-3-8B
 // layer, B4 S4096) and the dS-reading dQ 0.586 vs 0.773: 2.079 vs 1.892 ms per layer, memory bound on both

@@ -60,11 +60,6 @@ constexpr int BK = 64;   // keys per tile
 #ifndef FWD_PK_SOFTMAX
 #define FWD_PK_SOFTMAX 0
 #endif
-// row sum l of the online softmax on the matrix pipe: one more O^T tile with an all-ones A operand
-// (4 MFMAs per tile, 16 accumulator registers) instead of 32 dependent f32 adds on the VALU
-#ifndef FWD_MFMA_ROWSUM
-#define FWD_MFMA_ROWSUM 1
-#endif
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
@@ -229,9 +224,6 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
 #pragma unroll
     for (int i = 0; i < 16; ++i) o[t][i] = 0.f;
   float m = -INFINITY, l = 0.f;
-  f32x16 osum;  // FWD_MFMA_ROWSUM: every element of lane q holds row q's sum of the bf16 P
-#pragma unroll
-  for (int i = 0; i < 16; ++i) osum[i] = 0.f;
   const float c = a.scale_log2;
 
   if constexpr (FWD_EARLY_DMA) {
@@ -331,10 +323,6 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
       const float alpha = __builtin_amdgcn_exp2f(m - ((mn == -INFINITY) ? 0.f : mn));
       m = mn;
       l *= alpha;
-      if constexpr (FWD_MFMA_ROWSUM) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) osum[i] *= alpha;
-      }
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -360,23 +348,16 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
       }
     l += rs2[0] + rs2[1];
 #else
-    if constexpr (FWD_MFMA_ROWSUM) {
+    float rs = 0.f;
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+    for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) s[kt][i] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kt][i], c, -mref));
-    } else {
-      float rs = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kt][i], c, -mref));
-          s[kt][i] = p;
-          rs += p;
-        }
-      l += rs;
-    }
+      for (int i = 0; i < 16; ++i) {
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kt][i], c, -mref));
+        s[kt][i] = p;
+        rs += p;
+      }
+    l += rs;
 #endif
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) pf[ks] = pack_p(s[ks >> 1], 8 * (ks & 1));
@@ -400,12 +381,6 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
         o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, va), pf[ks], o[dt], 0, 0, 0);
       }
     }
-    if constexpr (FWD_MFMA_ROWSUM) {
-      const s16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};  // bf16 1.0
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
-        osum = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ones), pf[ks], osum, 0, 0, 0);
-    }
   };
   // tile t reads (Kc, Vc); tile t+1 is DMA'd into (Kn, Vn), which held tile t-1 -- free once every
   // wave passed this tile's barrier
@@ -426,7 +401,7 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
   }
 
   // ---- epilogue: normalise, store O (bf16) and LSE (natural log)
-  const float ltot = FWD_MFMA_ROWSUM ? osum[0] : l + __shfl_xor(l, 32, 64);
+  const float ltot = l + __shfl_xor(l, 32, 64);
   const float inv = ltot > 0.f ? 1.0f / ltot : 0.f;
   uint16_t* op = a.o + ((long long)b * S + (qvalid ? qrow : 0)) * a.o_rs + (long long)hq * D;
   if (FWD_WIDE_STORE && (a.o_rs & 7) == 0) {
@@ -475,6 +450,8 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
 
 }  // namespace
 
+// (Removed in round 5: the row sum l on the matrix pipe -- a fifth O^T tile with an all-ones A operand,
+// 4 MFMAs per tile instead of 32 f32 adds: forward 0.570 vs 0.553 ms, profiles/r5/attn_skip/.)
 // (Removed in round 4: QB2 -- two 32-row query blocks per wave, one wave per SIMD, the softmax of one
 // block fenced between the other block's MFMAs, asm-DMA 3-slot ring: 0.740 vs 0.554 ms at the Llama-3-8B
 // layer, profiles/r4/attn/fwd_qb6.log; git history has the kernel.)
