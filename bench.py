@@ -190,6 +190,8 @@ def _channel_sweep(info, mb: float, counts=(2, 4, 8, 16)) -> dict:
     """Bus bandwidth of the ``mb``-MB bucket all-reduce on fresh RCCL communicators pinned to each channel
     count (ncclConfig_t min/maxCTAs through ProcessGroupNCCL.Options): tells channel starvation from link
     bandwidth in the first 8-GPU record.  Errors are reported, never raised."""
+    import datetime
+
     import torch.distributed as dist
 
     out = {}
@@ -198,7 +200,7 @@ def _channel_sweep(info, mb: float, counts=(2, 4, 8, 16)) -> dict:
             opts = dist.ProcessGroupNCCL.Options()
             opts.config.min_ctas = c
             opts.config.max_ctas = c
-            g = dist.new_group(backend="nccl", pg_options=opts)
+            g = dist.new_group(backend="nccl", pg_options=opts, timeout=datetime.timedelta(seconds=120))
             out[str(c)] = _bucket_busbw(info, mb, iters=5, group=g)["busbw_GBps"]
             dist.destroy_process_group(g)
         except Exception as e:  # noqa: BLE001 -- a diagnostic

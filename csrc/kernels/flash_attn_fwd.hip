@@ -386,9 +386,6 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
   // wave passed this tile's barrier
   auto tile = [&](const int t, const char* Kc, const char* Vc, char* Kn, char* Vn) __attribute__((always_inline)) {
     sync_tile(t, Kn, Vn);
-    // causal: a tile entirely above this wave's 32 rows contributes nothing (its P is 0 and the running
-    // max does not move) -- skip it (wave-uniform; barriers and the DMA share stay)
-    if (a.causal && kv_begin + t * BK > q0 + wave * 32 + 31) return;
     if constexpr (FWD_PRIO) __builtin_amdgcn_s_setprio(1);  // S MFMA phase ahead of the partner wave's VALU
     phaseA(Kc);
     if constexpr (FWD_PRIO) __builtin_amdgcn_s_setprio(0);
@@ -450,6 +447,8 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
 
 }  // namespace
 
+// (Removed in round 5: skipping a tile a wave sees fully masked (causal diagonal) -- 0.566 / 0.559 vs
+// 0.558 / 0.556 ms, profiles/r5/followup/.)
 // (Removed in round 5: the row sum l on the matrix pipe -- a fifth O^T tile with an all-ones A operand,
 // 4 MFMAs per tile instead of 32 f32 adds: forward 0.570 vs 0.553 ms, profiles/r5/attn_skip/.)
 // (Removed in round 4: QB2 -- two 32-row query blocks per wave, one wave per SIMD, the softmax of one

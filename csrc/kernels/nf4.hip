@@ -137,27 +137,13 @@ __global__ __launch_bounds__(256) void nf4_dequant_kernel(const uint8_t* __restr
   }
 }
 
-// 8 codes (one 32-bit word, first element in the high nibble of each byte) -> 8 bf16 (one 16-byte chunk)
-DEV_INLINE uint4 nf4_decode8(uint32_t w, float a, const float* lut) {
-  float f[8];
-#pragma unroll
-  for (int bt = 0; bt < 4; ++bt) {
-    const uint32_t byte = (w >> (8 * bt)) & 0xffu;
-    f[2 * bt] = lut[byte >> 4] * a;
-    f[2 * bt + 1] = lut[byte & 0xf] * a;
-  }
-  return pack8(f);
-}
 DEV_INLINE float nf4_absmax(const uint8_t* aq, const float* s2, float off, long long bi, int block2) {
   return off + ((float)aq[bi] - 128.0f) * (1.0f / 127.0f) * s2[bi / block2];
 }
 
-// dequantise into a row view: out[n * ldo + k] (a column block of an augmented GEMM operand).
-// Lane-contiguous chunks: chunk c = 8 elements; a wave's load instruction reads 64 consecutive 4-byte code
-// words and its store writes 64 consecutive 16-byte chunks (1 KiB, whole lines), NCH chunks per thread all
-// loaded before any is decoded.  (Round 4: 16 codes per thread, two 16-byte stores at a 32-byte lane stride:
-// 3.7 TB/s.)
-constexpr int kRowsNCH = 4;
+// dequantise into a row view: out[n * ldo + k] (a column block of an augmented GEMM operand).  (Measured
+// and kept over a lane-contiguous rewrite -- 4-byte code words, 16-byte stores, four chunks per thread in
+// flight: 14.3 / 74.7 vs 13.6 / 71.1 us at the qkv / gate_up shapes, profiles/r5/followup/.)
 __global__ __launch_bounds__(256) void nf4_dequant_rows_kernel(const uint8_t* __restrict__ packed,
                                                                const uint8_t* __restrict__ aq,
                                                                const float* __restrict__ s2, float off,
@@ -171,27 +157,28 @@ __global__ __launch_bounds__(256) void nf4_dequant_rows_kernel(const uint8_t* __
   }
   __shared__ float lut[16];
   nf4_lut_load(lut);
-  const long long n8 = n >> 3;
-  const int c8 = cols >> 3;
-  const int per_block = block >> 3;  // chunks per absmax block
-  for (long long base = (long long)blockIdx.x * 256 * kRowsNCH; base < n8; base += (long long)main_blocks * 256 * kRowsNCH) {
-    uint32_t w[kRowsNCH];
-    float am[kRowsNCH];
+  const long long n16 = n >> 4;
+  const int c16 = cols >> 4;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long long)main_blocks * 256) {
+    const uint2 p = reinterpret_cast<const uint2*>(packed)[i];
+    const long long e0 = i << 4;
+    const long long bi = e0 / block;
+    const float a = off + ((float)aq[bi] - 128.0f) * (1.0f / 127.0f) * s2[bi / block2];
+    float f[16];
+    const uint32_t words[2] = {p.x, p.y};
 #pragma unroll
-    for (int j = 0; j < kRowsNCH; ++j) {
-      const long long c = base + j * 256 + threadIdx.x;
-      w[j] = c < n8 ? reinterpret_cast<const uint32_t*>(packed)[c] : 0u;
-      am[j] = c < n8 ? nf4_absmax(aq, s2, off, c / per_block, block2) : 0.f;
-    }
+    for (int wd = 0; wd < 2; ++wd)
 #pragma unroll
-    for (int j = 0; j < kRowsNCH; ++j) {
-      const long long c = base + j * 256 + threadIdx.x;
-      if (c < n8) {
-        const long long row = c / c8;
-        const int col = (int)(c - row * c8) * 8;
-        *reinterpret_cast<uint4*>(out + row * ldo + col) = nf4_decode8(w[j], am[j], lut);
+      for (int bt = 0; bt < 4; ++bt) {
+        const uint32_t byte = (words[wd] >> (8 * bt)) & 0xffu;
+        f[wd * 8 + bt * 2] = lut[byte >> 4] * a;
+        f[wd * 8 + bt * 2 + 1] = lut[byte & 0xf] * a;
       }
-    }
+    const long long row = i / c16;
+    const int c = (int)(i - row * c16) * 16;
+    uint4* o = reinterpret_cast<uint4*>(out + row * ldo + c);
+    o[0] = pack8(f);
+    o[1] = pack8(f + 8);
   }
 }
 
@@ -282,7 +269,7 @@ extern "C" int ftc_nf4_dequant_aug(const uint8_t* packed, const uint8_t* absmax_
                        packed, absmax_q, absmax_scale, absmax_offset, (uint16_t*)out, rows, cols, ldo, block2, t);
   } else {
     const long long n = (long long)rows * cols;
-    const int grid = ftc::oneshot_grid(n / 8, 256 * kRowsNCH);
+    const int grid = ftc::oneshot_grid(n / 16, 256);
     hipLaunchKernelGGL(nf4_dequant_rows_kernel, dim3(grid + (has_tail ? kTailBlocks : 0)), dim3(256), 0, stream,
                        packed, absmax_q, absmax_scale, absmax_offset, (uint16_t*)out, n, cols, ldo, block, block2, grid,
                        t);
