@@ -177,10 +177,13 @@ def _rccl_channels(path: str | None) -> list[int] | None:
 
     if not path or not os.path.exists(path):
         return None
+    # the ring / tree layout lines ("Channel 03/16 :    0   1") -- not the per-connection transport lines
+    # ("Channel 00/0 : 0[0] -> 1[1] via P2P/IPC", whose number after the slash is a connection index)
+    ring = re.compile(r"Channel \d+/(\d+) :(?:\s+\d+)+\s*$")
     found = set()
     with open(path, errors="replace") as f:
         for ln in f:
-            m = re.search(r"Channel \d+/(\d+)", ln)
+            m = ring.search(ln)
             if m:
                 found.add(int(m.group(1)))
     return sorted(found)

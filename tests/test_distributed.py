@@ -604,3 +604,22 @@ def test_zero1_rccl_update_matches_ddp(tmp_path):
     print(f"zero1 vs ddp: {moved:.3f} of sampled weights moved, max |diff| {diff:.3g}")
     assert moved > 0.5
     torch.testing.assert_close(z[0]["after"], d[0]["after"], atol=1e-6, rtol=0)
+
+
+def test_rccl_channel_parse_reads_ring_lines_only(tmp_path):
+    """bench.py's channel report takes the ring / tree layout lines of RCCL's INIT log, not the per-peer
+    transport lines (whose number after the slash is a connection index)."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    log = tmp_path / "rccl.log"
+    log.write_text(
+        "host:1:1 [0] NCCL INFO Channel 00/04 :    0   1\n"
+        "host:1:1 [0] NCCL INFO Channel 03/04 :    0   1\n"
+        "host:1:1 [0] NCCL INFO Channel 00/0 : 0[0] -> 1[1] via P2P/IPC\n"
+        "host:1:1 [0] NCCL INFO Channel 01/0 : 0[0] -> 1[1] via P2P/IPC comm 0x1\n"
+        "host:1:1 [0] NCCL INFO Channel 00/16 :    0   1   2   3   4   5   6   7\n")
+    assert bench._rccl_channels(str(log)) == [4, 16]
+    assert bench._rccl_channels(str(tmp_path / "missing.log")) is None
