@@ -1,7 +1,6 @@
 #!/usr/bin/env python3
 """RMSNorm (+residual) forward / backward kernels at the Llama-3-8B shape (16384 x 4096, bf16):
-ms and effective HBM TB/s (bytes a streaming kernel must move).  FTC_RMSNORM_BWD2=0 selects the
-one-wave-per-row frozen-weight backward for A/B."""
+ms and effective HBM TB/s (bytes a streaming kernel must move)."""
 import json
 import os
 import sys
