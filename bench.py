@@ -449,6 +449,8 @@ def main(argv=None) -> int:
         }
         print(json.dumps(out), flush=True)
     tr.close()
+    if rccl_log and os.path.exists(rccl_log):  # this rank's RCCL INIT log: parsed above, not kept
+        os.remove(rccl_log)
     return 0
 
 
