@@ -4,6 +4,7 @@ the sources read is documented ("Ship only winners")."""
 import os
 import re
 import subprocess
+import sys
 
 import pytest
 
@@ -67,3 +68,16 @@ def test_runtime_switches_are_documented():
     table = doc[doc.index("## Runtime switches"):doc.index("## Counter evidence")]
     missing = sorted(n for n in names if f"`{n}`" not in table)
     assert not missing, missing
+
+
+def test_run_patched_sets_module_constants_before_the_script(tmp_path):
+    """tools/run_patched.py: the A/B arm of an "A/B by patching" toggle -- the constant is set before the
+    script runs, and the script sees its own argv."""
+    script = tmp_path / "probe.py"
+    script.write_text("import sys\nfrom finetune_controller_amd.ops import norm\n"
+                      "print('argv', sys.argv[1:])\nprint('val', getattr(norm, '_PROBE_X', None))\n")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "run_patched.py"),
+                        "finetune_controller_amd.ops.norm._PROBE_X=3", "--", str(script), "--steps", "2"],
+                       capture_output=True, text=True, cwd=ROOT, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "argv ['--steps', '2']" in r.stdout and "val 3" in r.stdout
