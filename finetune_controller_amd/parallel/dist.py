@@ -49,10 +49,7 @@ def init_distributed(device_type: str = "auto", timeout_s: int = 1800) -> DistIn
     share = os.environ.get("FTC_SHARE_GPU") == "1"
     if device_type == "cuda":
         # FTC_SHARE_GPU=1: several ranks on one card (rehearsing the multi-GPU path on a 1-GPU box)
-        count = torch.cuda.device_count()
-        if not share:
-            check_local_rank(local, count)
-        idx = local % count if share else local
+        idx = local_device_index(local, torch.cuda.device_count(), share)
         torch.cuda.set_device(idx)
         device = torch.device("cuda", idx)
     else:
@@ -100,6 +97,19 @@ def device_key(device: torch.device) -> str:
     if all(v is not None for v in pci):
         return "pci:%x:%x:%x/%s" % (pci[0], pci[1], pci[2], uuid)
     return uuid or f"index{device.index}"
+
+
+def local_device_index(local: int, count: int, share: bool = False) -> int:
+    """The visible-device index this rank binds to: ``LOCAL_RANK`` when every rank sees the node's GPUs
+    (torchrun), device 0 when the launcher narrowed each rank to ONE visible device (a per-rank
+    ``HIP_VISIBLE_DEVICES``; the distinct-device check after the rendezvous still refuses two ranks on
+    one card), ``LOCAL_RANK mod count`` for a shared-card rehearsal."""
+    if share:
+        return local % count
+    if count == 1:
+        return 0
+    check_local_rank(local, count)
+    return local
 
 
 def check_local_rank(local: int, count: int) -> None:

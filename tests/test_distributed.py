@@ -219,6 +219,11 @@ def test_distinct_device_binding_checks():
     pdist.check_local_rank(7, 8)
     with pytest.raises(RuntimeError, match="LOCAL_RANK 8"):
         pdist.check_local_rank(8, 8)
+    assert pdist.local_device_index(5, 8) == 5
+    assert pdist.local_device_index(5, 1) == 0  # launcher gave each rank one visible device
+    assert pdist.local_device_index(5, 2, share=True) == 1
+    with pytest.raises(RuntimeError, match="LOCAL_RANK 4"):
+        pdist.local_device_index(4, 4)
 
 
 def test_bench_refuses_mislabelled_world(tmp_path):
