@@ -596,6 +596,7 @@ class LoRATail:
 
 
 _HIP_TAIL = True  # False: hipBLASLt for the skinny tail GEMMs (A/B by patching; profiles/r1_tail_gemm_ab.log)
+_HIP_TAIL_MAX_NCT = 2  # widest tail (in 16-column tiles) the HIP kernel takes
 
 
 def tail_product(x2: torch.Tensor, width: int, Rp: int, operand: torch.Tensor, nct: int) -> None:
@@ -607,7 +608,7 @@ def tail_product(x2: torch.Tensor, width: int, Rp: int, operand: torch.Tensor, n
     # up to 32 live columns the kernel streams at 6.3 TB/s vs hipBLASLt's 5.4 in isolation; at 48
     # (packed q|k|v forward, nct = 3) its L2 fragment traffic loses (tools/bench_rmsnorm.py).  End to
     # end the difference is within box noise (profiles/r1_tail_gemm_ab.log)
-    if _HIP_TAIL and nct <= 2 and use_hip(x2) and ext().tail_gemm_ok(xv, Rp):
+    if _HIP_TAIL and nct <= _HIP_TAIL_MAX_NCT and use_hip(x2) and ext().tail_gemm_ok(xv, Rp):
         ext().tail_gemm_(xv, operand, nct, Rp)
     else:
         _mm_into(x2, operand.t(), _tail(x2, width, Rp))
