@@ -82,6 +82,9 @@ class JobMonitor:
             if prev.status == DatabaseStatusEnum.canceled:
                 continue
             if TrainingJobStatus.is_stopped(prev.status) and prev.status == mapped:
+                if status == KubeflowStatusEnum.succeeded.value:
+                    # already reconciled, yet still listed: an earlier pass's delete failed -- retry it
+                    await self.delete_job(job_id)
                 continue  # already reconciled
             if prev.status != mapped:
                 logger.info("job %s status %s -> %s", job_id, prev.status.value, mapped.value)

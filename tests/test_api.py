@@ -106,6 +106,26 @@ def test_submit_lifecycle_metrics_logs_cancel(env):
     assert item["meta_"]["data"]["promotion_path"] == "language/llama3-8b/lora" and item["index_"] >= 1
 
 
+def test_monitor_retries_a_failed_delete_of_a_succeeded_job(env, monkeypatch):
+    """The reference deletes a succeeded PyTorchJob once; if that call fails, the job is already
+    'completed' in the DB and a status-only reconciler would leave it on the cluster for good."""
+    ctx, c = env
+    jid = submit(c)
+    real = ctx.kube.delete_pytorchjob
+    calls = []
+
+    def flaky(ns, name):
+        calls.append(name)
+        if len(calls) == 1:
+            raise RuntimeError("apiserver unavailable")
+        return real(ns, name)
+
+    monkeypatch.setattr(ctx.kube, "delete_pytorchjob", flaky)
+    settle(ctx)
+    assert c.get(f"/api/v1/jobs/{jid}").json()["status"] == "completed"
+    assert calls[:2] == [jid, jid] and ctx.kube.list_pytorchjobs(ctx.namespace) == []
+
+
 def test_dataset_upload_reuse_url_and_delete(env, monkeypatch):
     ctx, c = env
     files = {"dataset": ("train.jsonl", io.BytesIO(b'{"text": "hello"}\n' * 10), "application/json")}
