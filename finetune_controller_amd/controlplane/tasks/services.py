@@ -32,8 +32,10 @@ class NotFound(Exception):
 
 
 def _http_client() -> httpx.Client:
-    """HTTP client used to stream dataset URLs (patched in tests)."""
-    return httpx.Client(timeout=None, follow_redirects=True)
+    """HTTP client used to stream dataset URLs (patched in tests).  No bound on the whole transfer (a
+    dataset may take long), but a server that stops answering fails the submission instead of holding its
+    worker thread forever: 30 s to connect, 300 s per read."""
+    return httpx.Client(timeout=httpx.Timeout(None, connect=30.0, read=300.0), follow_redirects=True)
 
 
 async def upload_dataset_file(ctx: AppContext, job: JobInput, upload, description: str) -> DatasetModel:
@@ -101,12 +103,22 @@ async def task_builder(ctx: AppContext, job: JobInput, dataset_input: DatasetInp
         raise ValueError(f"Invalid device '{job.device}'. Must be one of {ctx.devices.list_workers()}.")
     manifest = build_pytorchjob_manifest(job, worker, ctx.settings, ctx.namespace)
     result = await asyncio.to_thread(ctx.kube.create_pytorchjob, ctx.namespace, manifest)
-    await ctx.store.create_job(
-        user_id=job.user_id, job_id=job.job_id, job_name=job.job_name, model_name=job.model_name, device=job.device,
-        task=job.model.task.value, framework=job.model.framework.value, arguments=job.arguments,
-        dataset_id=dataset_doc.id if dataset_doc else None, atrifacts_uri=job.s3_artifacts_uri,
-        dataset_name=job.model.dataset_info.dataset_name or None,
-        metadata={"kubernetes_job_name": (result.get("metadata") or {}).get("name")})
+    k8s_name = (result.get("metadata") or {}).get("name")
+    try:
+        await ctx.store.create_job(
+            user_id=job.user_id, job_id=job.job_id, job_name=job.job_name, model_name=job.model_name, device=job.device,
+            task=job.model.task.value, framework=job.model.framework.value, arguments=job.arguments,
+            dataset_id=dataset_doc.id if dataset_doc else None, atrifacts_uri=job.s3_artifacts_uri,
+            dataset_name=job.model.dataset_info.dataset_name or None,
+            metadata={"kubernetes_job_name": k8s_name})
+    except Exception:
+        # no job document: the monitor would treat the PyTorchJob as another controller's and leave it
+        # holding its GPUs -- take it back before reporting the failure
+        try:
+            await asyncio.to_thread(ctx.kube.delete_pytorchjob, ctx.namespace, k8s_name or job.job_id)
+        except Exception as e:
+            logger.error("could not delete PyTorchJob %s after the job insert failed: %s", k8s_name, e)
+        raise
     return result
 
 

@@ -126,6 +126,20 @@ def test_monitor_retries_a_failed_delete_of_a_succeeded_job(env, monkeypatch):
     assert calls[:2] == [jid, jid] and ctx.kube.list_pytorchjobs(ctx.namespace) == []
 
 
+def test_failed_job_insert_takes_the_pytorchjob_back(env, monkeypatch):
+    """The PyTorchJob is created before the job document; when the insert fails the submission must
+    not leave a job on the cluster that no DB record (and so no monitor pass) will ever claim."""
+    ctx, c = env
+
+    async def broken(**kw):
+        raise RuntimeError("mongo write timeout")
+
+    monkeypatch.setattr(ctx.store, "create_job", broken)
+    r = c.post("/api/v1/jobs", data=FORM)
+    assert r.status_code == 500 and "mongo write timeout" in r.json()["detail"]
+    assert ctx.kube.list_pytorchjobs(ctx.namespace) == []
+
+
 def test_dataset_upload_reuse_url_and_delete(env, monkeypatch):
     ctx, c = env
     files = {"dataset": ("train.jsonl", io.BytesIO(b'{"text": "hello"}\n' * 10), "application/json")}
