@@ -91,8 +91,8 @@ class LogStreamManager:
         try:
             pod = await asyncio.to_thread(self.ctx.kube.read_pod, self.ctx.namespace, self.pod_name)
             return pod.get("status", {}).get("phase") in ("Running", "Pending")
-        except Exception as e:
-            return getattr(e, "status", None) not in (404,) and False
+        except Exception:
+            return False  # gone (404) or unreadable: stop following
 
     async def _process_and_send(self, lines: list[str]):
         out = []
@@ -139,6 +139,17 @@ class LogStreamManager:
             loop = asyncio.get_running_loop()
             stop = {"flag": False}
 
+            def put(item) -> bool:
+                # bounded hand-off that gives up once the consumer has left: a put blocked on a full
+                # queue nobody drains any more would pin this thread and the pod's log stream forever
+                while not stop["flag"]:
+                    try:
+                        asyncio.run_coroutine_threadsafe(asyncio.wait_for(q.put(item), 1.0), loop).result()
+                        return True
+                    except asyncio.TimeoutError:
+                        continue
+                return False
+
             def pump():
                 try:
                     it = kube.stream_pod_log(ns, self.pod_name, self.container_name, tail)
@@ -149,11 +160,12 @@ class LogStreamManager:
                         n += 1
                         if n <= skip:
                             continue
-                        asyncio.run_coroutine_threadsafe(q.put(raw), loop).result()
+                        if not put(raw):
+                            break
                 except Exception as e:
-                    asyncio.run_coroutine_threadsafe(q.put(e), loop).result()
+                    put(e)
                 finally:
-                    asyncio.run_coroutine_threadsafe(q.put(_END), loop).result()
+                    put(_END)
 
             fut = loop.run_in_executor(None, pump)
             try:
