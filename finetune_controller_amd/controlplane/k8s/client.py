@@ -71,29 +71,61 @@ class KubeClient:
         return [p["metadata"]["name"] for p in self.list_pods(namespace, sel)]
 
 
+class _TokenFileAuth(httpx.Auth):
+    """Bearer token read from a projected service-account token file.  The kubelet rotates bound
+    tokens (about hourly), so a controller that read the file once at start-up would begin failing
+    with 401 after the first rotation.  The file is re-read when its mtime changes, and once more
+    (then the request retried) on a 401."""
+
+    def __init__(self, path: str):
+        self.path, self._token, self._mtime = path, "", None
+
+    def _load(self, force: bool = False) -> str:
+        try:
+            m = os.stat(self.path).st_mtime_ns
+        except OSError:
+            return self._token
+        if force or m != self._mtime:
+            with open(self.path) as f:
+                self._token = f.read().strip()
+            self._mtime = m
+        return self._token
+
+    def auth_flow(self, request):
+        request.headers["Authorization"] = f"Bearer {self._load()}"
+        response = yield request
+        if response.status_code == 401:
+            request.headers["Authorization"] = f"Bearer {self._load(force=True)}"
+            yield request
+
+
 class HttpKubeClient(KubeClient):
     SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
 
     def __init__(self, server: str | None = None, token: str | None = None, verify=True, cert=None,
-                 kubeconfig: str | None = None, timeout: float = 30.0, transport: httpx.BaseTransport | None = None):
+                 kubeconfig: str | None = None, timeout: float = 30.0, transport: httpx.BaseTransport | None = None,
+                 token_file: str | None = None):
         if server is None:
-            server, token, verify, cert = self._discover(kubeconfig)
+            server, token, verify, cert, token_file = self._discover(kubeconfig)
         self.server = server.rstrip("/")
         self.verify, self.cert = verify, cert
-        headers = {"Authorization": f"Bearer {token}"} if token else {}
+        auth = _TokenFileAuth(token_file) if token_file else None
+        headers = {"Authorization": f"Bearer {token}"} if token and not token_file else {}
         if transport is not None:  # injected transport (tests replay API-server responses): no TLS setup
-            self.http = httpx.Client(base_url=self.server, headers=headers, timeout=timeout, transport=transport)
+            self.http = httpx.Client(base_url=self.server, headers=headers, timeout=timeout, transport=transport,
+                                     auth=auth)
         else:
-            self.http = httpx.Client(base_url=self.server, headers=headers, verify=verify, cert=cert, timeout=timeout)
+            self.http = httpx.Client(base_url=self.server, headers=headers, verify=verify, cert=cert, timeout=timeout,
+                                     auth=auth)
 
     # ---- configuration discovery (in-cluster first, then kubeconfig) ----
     @classmethod
     def _discover(cls, kubeconfig: str | None):
         host, port = os.environ.get("KUBERNETES_SERVICE_HOST"), os.environ.get("KUBERNETES_SERVICE_PORT")
         if host and port and os.path.exists(os.path.join(cls.SA_DIR, "token")):
-            with open(os.path.join(cls.SA_DIR, "token")) as f:
-                token = f.read().strip()
-            return f"https://{host}:{port}", token, os.path.join(cls.SA_DIR, "ca.crt"), None
+            # in-cluster: the token is read per request from the rotating file (_TokenFileAuth)
+            return f"https://{host}:{port}", None, os.path.join(cls.SA_DIR, "ca.crt"), None, \
+                os.path.join(cls.SA_DIR, "token")
         path = kubeconfig or os.environ.get("KUBECONFIG", os.path.expanduser("~/.kube/config"))
         import yaml
 
@@ -116,7 +148,7 @@ class HttpKubeClient(KubeClient):
                     cls._tmpfile(base64.b64decode(user["client-key-data"])))
         elif "client-certificate" in user:
             cert = (user["client-certificate"], user["client-key"])
-        return cluster["server"], user.get("token"), verify, cert
+        return cluster["server"], user.get("token"), verify, cert, None
 
     @staticmethod
     def _tmpfile(data: bytes) -> str:

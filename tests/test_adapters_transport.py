@@ -311,8 +311,8 @@ def test_kubeconfig_discovery(tmp_path, monkeypatch):
                         {"name": "dev", "context": {"cluster": "c2", "user": "bot"}}]}
     p = tmp_path / "config"
     p.write_text(yaml.safe_dump(cfg))
-    server, token, verify, cert = kc.HttpKubeClient._discover(str(p))
-    assert server == "https://10.0.0.1:6443" and token is None
+    server, token, verify, cert, token_file = kc.HttpKubeClient._discover(str(p))
+    assert server == "https://10.0.0.1:6443" and token is None and token_file is None
     assert open(verify, "rb").read() == ca
     assert open(cert[0], "rb").read() == crt and open(cert[1], "rb").read() == key
     import os
@@ -321,7 +321,7 @@ def test_kubeconfig_discovery(tmp_path, monkeypatch):
     cfg["current-context"] = "dev"
     p.write_text(yaml.safe_dump(cfg))
     monkeypatch.setenv("KUBECONFIG", str(p))
-    assert kc.HttpKubeClient._discover(None) == ("https://dev:6443", "tok-123", False, None)
+    assert kc.HttpKubeClient._discover(None) == ("https://dev:6443", "tok-123", False, None, None)
     # in-cluster service account wins when present
     sa = tmp_path / "sa"
     sa.mkdir()
@@ -330,7 +330,34 @@ def test_kubeconfig_discovery(tmp_path, monkeypatch):
     monkeypatch.setattr(kc.HttpKubeClient, "SA_DIR", str(sa))
     monkeypatch.setenv("KUBERNETES_SERVICE_HOST", "10.96.0.1")
     monkeypatch.setenv("KUBERNETES_SERVICE_PORT", "443")
-    assert kc.HttpKubeClient._discover(None) == ("https://10.96.0.1:443", "sa-token", str(sa / "ca.crt"), None)
+    # (the token itself is read per request from the rotating file)
+    assert kc.HttpKubeClient._discover(None) == ("https://10.96.0.1:443", None, str(sa / "ca.crt"), None,
+                                                 str(sa / "token"))
+
+
+def test_service_account_token_rotation(tmp_path):
+    """The kubelet rotates projected service-account tokens: every request carries the file's current
+    token, and a 401 re-reads the file and retries once."""
+    tok = tmp_path / "token"
+    tok.write_text("t1\n")
+    seen = []
+
+    def handler(request):
+        seen.append(request.headers.get("Authorization"))
+        if request.headers.get("Authorization") == "Bearer stale":
+            return httpx.Response(401, json={"kind": "Status", "code": 401})
+        return httpx.Response(200, json={"items": []})
+
+    k = kc.HttpKubeClient("https://api:6443", token_file=str(tok), transport=httpx.MockTransport(handler))
+    assert k.list_pytorchjobs("ft") == [] and seen[-1] == "Bearer t1"
+    import os
+    tok.write_text("t2\n")
+    os.utime(tok, ns=(1, 1))  # a new mtime, as the kubelet's atomic swap gives
+    k.list_pytorchjobs("ft")
+    assert seen[-1] == "Bearer t2"
+    # a token the server already rejects while the file looks unchanged: re-read on the 401 and retry
+    k.http.auth._token, n = "stale", len(seen)
+    assert k.list_pytorchjobs("ft") == [] and seen[n:] == ["Bearer stale", "Bearer t2"]
 
 
 def _rbac_allows(rules, group, resource, verb, name=None) -> bool:
