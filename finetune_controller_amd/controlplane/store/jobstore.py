@@ -12,13 +12,17 @@ Changes vs the reference:
   read-modify-write of the whole sub-document (concurrent monitor + API cancel were racy);
 * ``update_dataset`` appends the job reference with ``$addToSet``;
 * the datasets page reports the number of ITEMS as ``total`` (the reference returns the page count);
-* ``acquire_lock`` -- a TTL lease document used to keep a single active job monitor.
+* ``acquire_lock`` -- a TTL lease document used to keep a single active job monitor;
+* the name search of the jobs / datasets pages matches the user's text literally (``re.escape``): the
+  reference hands it to ``$regex`` as a pattern, so ``(`` or ``[`` fail the request and a crafted pattern
+  can make the server backtrack for a long time.
 """
 from __future__ import annotations
 
 import datetime as _dt
 import inspect
 import logging
+import re
 from typing import Any
 
 from bson import ObjectId
@@ -160,7 +164,7 @@ class JobStore:
         if model_name:
             q["model_name"] = model_name
         if query:
-            q["job_name"] = {"$regex": query, "$options": "i"}
+            q["job_name"] = {"$regex": re.escape(query), "$options": "i"}
         key, order = _sort_spec(sort or "-start_time")
         pipeline = [{"$match": q}] + self._job_pipeline_add_fields() + [
             {"$setWindowFields": {"sortBy": {key: order}, "output": {"index_": {"$documentNumber": {}}}}},
@@ -260,7 +264,7 @@ class JobStore:
         page, page_size = max(1, int(page)), max(1, int(page_size))
         q: dict[str, Any] = {"user_id": user_id}
         if query:
-            q["dataset_name"] = {"$regex": query, "$options": "i"}
+            q["dataset_name"] = {"$regex": re.escape(query), "$options": "i"}
         key, order = _sort_spec(sort or "-created_at")
         if key == "start_time":  # the reference's default key does not exist on datasets
             key = "created_at"

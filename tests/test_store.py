@@ -114,6 +114,12 @@ def test_user_jobs_pagination_sort_filter(store):
         assert [j.job_id for j in s.items] == ["job-5"]
         lim = await store.get_user_jobs("u1", sort="job_name", limit=[2, 4], page_size=10)
         assert [j.job_id for j in lim.items] == ["job-1", "job-3"]
+        # the search text is literal: regex metacharacters neither fail the query nor act as a pattern
+        await _mk(store, "job-x", name="run (v2) [final]")
+        s = await store.get_user_jobs("u1", query="(V2) [")
+        assert [j.job_id for j in s.items] == ["job-x"]
+        assert (await store.get_user_jobs("u1", query="run .")).total == 0
+        assert (await store.get_user_jobs("u1", query="(a+)+$")).total == 0
 
     run(go())
 
