@@ -66,7 +66,7 @@ from ..schemas.jobs import (Dataset, DatasetInput, DatasetMeta, Job, JobIdsReque
 from ..schemas.kubeflow import TrainingJobStatus
 from ..spec.finetuning import TrainingTask
 from ..tasks.services import NotFound, PromotionTask, task_builder
-from .forms import FormError, parse_form
+from .forms import FormError, discard_uploads, parse_form
 from .ratelimit import Limiter, RateLimitExceeded, remote_address
 
 logger = logging.getLogger("ftc.api")
@@ -289,6 +289,12 @@ def create_app(ctx: AppContext, run_monitor: bool | None = None, validator_facto
             fields, files = await parse_form(request)
         except FormError as e:
             raise HTTPException(status_code=422, detail=str(e)) from e
+        try:
+            return await submit_job(request, fields, files)
+        finally:
+            discard_uploads(files)  # a rejected request leaves no spooled upload behind
+
+    async def submit_job(request: Request, fields: dict, files: dict):
         user_id = fields.get("user_id") or DEFAULT_USER
         import re
 
@@ -316,6 +322,8 @@ def create_app(ctx: AppContext, run_monitor: bool | None = None, validator_facto
             model_arguments = json.loads(fields.get("arguments") or "{}")
         except json.JSONDecodeError as e:
             raise HTTPException(status_code=400, detail="Invalid JSON for arguments") from e
+        if not isinstance(model_arguments, dict):
+            raise HTTPException(status_code=400, detail="Invalid JSON for arguments: expected an object")
         job_id = make_job_id(model)
         if fields.get("dataset_id"):
             ds = DatasetInput(dataset_id=fields["dataset_id"])

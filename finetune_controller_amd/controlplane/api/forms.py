@@ -21,6 +21,16 @@ class FormError(ValueError):
     pass
 
 
+def discard_uploads(files: dict[str, UploadedFile]) -> None:
+    """Remove the spooled temp files of ``files`` that nothing consumed (the dataset ingest removes its
+    own after the upload to object storage)."""
+    for f in files.values():
+        try:
+            os.remove(f.path)
+        except FileNotFoundError:
+            pass
+
+
 def _boundary(ctype: str) -> bytes:
     for part in ctype.split(";"):
         part = part.strip()
@@ -40,6 +50,21 @@ def _parse_disposition(value: str) -> dict:
 
 
 async def parse_form(request) -> tuple[dict[str, str], dict[str, UploadedFile]]:
+    """Fields and spooled files of the request body.  On any failure (a bad part, an oversized field,
+    the client going away mid-upload) every temp file written so far is removed before re-raising."""
+    spooled: list[str] = []
+    try:
+        return await _parse_form(request, spooled)
+    except BaseException:
+        for path in spooled:
+            try:
+                os.remove(path)
+            except FileNotFoundError:
+                pass
+        raise
+
+
+async def _parse_form(request, spooled: list[str]) -> tuple[dict[str, str], dict[str, UploadedFile]]:
     ctype = request.headers.get("content-type", "")
     if ctype.startswith("application/x-www-form-urlencoded"):
         body = await request.body()
@@ -65,6 +90,8 @@ async def parse_form(request) -> tuple[dict[str, str], dict[str, UploadedFile]]:
             cur_fh.close()
             cur_file.size = os.path.getsize(cur_file.path)
             if cur_file.filename:
+                if cur_name in files:  # a repeated file field: the last one wins, the earlier is dropped
+                    os.remove(files[cur_name].path)
                 files[cur_name] = cur_file
             else:
                 os.remove(cur_file.path)
@@ -108,6 +135,7 @@ async def parse_form(request) -> tuple[dict[str, str], dict[str, UploadedFile]]:
                 if "filename" in disp:
                     fname = os.path.basename(disp["filename"])
                     fd, path = tempfile.mkstemp(prefix="upload-", dir=UPLOAD_DIR)
+                    spooled.append(path)
                     cur_fh = os.fdopen(fd, "wb")
                     cur_file = UploadedFile(filename=fname, path=path,
                                             content_type=headers.get("content-type", "application/octet-stream"))
@@ -130,6 +158,8 @@ async def parse_form(request) -> tuple[dict[str, str], dict[str, UploadedFile]]:
                     cur_fh.write(data)
                 else:
                     cur_val.extend(data)
+                    if len(cur_val) > MAX_FIELD_BYTES:  # (also when the whole field came in one chunk)
+                        raise FormError("form field too large")
                 finish_part()
                 state = "after_delim"
     if state not in ("after_delim", "preamble"):

@@ -140,6 +140,36 @@ def test_failed_job_insert_takes_the_pytorchjob_back(env, monkeypatch):
     assert ctx.kube.list_pytorchjobs(ctx.namespace) == []
 
 
+def test_rejected_submissions_leave_no_spooled_upload(env, monkeypatch, tmp_path):
+    """Dataset files are spooled to disk while the form streams in; a submission refused after that
+    (bad model, bad arguments, a form that breaks mid-upload) must not leave the file behind."""
+    from finetune_controller_amd.controlplane.api import forms
+
+    ctx, c = env
+    spool = tmp_path / "spool"
+    monkeypatch.setattr(forms, "UPLOAD_DIR", str(spool))
+
+    def upload(**over):
+        files = {"dataset": ("train.jsonl", io.BytesIO(b'{"text": "hi"}\n' * 1000), "application/json")}
+        return c.post("/api/v1/jobs", data=dict(FORM, **over), files=files)
+
+    assert upload(model="Nope").status_code == 404
+    r = upload(arguments="[1, 2]")
+    assert r.status_code == 400 and "expected an object" in r.json()["detail"]
+    assert list(spool.iterdir()) == []
+    # a field past the size bound AFTER the file part: the parser fails and removes what it spooled
+    monkeypatch.setattr(forms, "MAX_FIELD_BYTES", 64)
+    b = "ftcboundary"
+    parts = [f'--{b}\r\nContent-Disposition: form-data; name="dataset"; filename="t.jsonl"\r\n'
+             f"Content-Type: application/json\r\n\r\n{'x' * 5000}\r\n"]
+    for k, v in dict(FORM, dataset_description="d" * 4096).items():
+        parts.append(f'--{b}\r\nContent-Disposition: form-data; name="{k}"\r\n\r\n{v}\r\n')
+    body = ("".join(parts) + f"--{b}--\r\n").encode()
+    r = c.post("/api/v1/jobs", content=body, headers={"content-type": f"multipart/form-data; boundary={b}"})
+    assert r.status_code == 422 and "too large" in r.json()["detail"]
+    assert list(spool.iterdir()) == []
+
+
 def test_dataset_upload_reuse_url_and_delete(env, monkeypatch):
     ctx, c = env
     files = {"dataset": ("train.jsonl", io.BytesIO(b'{"text": "hello"}\n' * 10), "application/json")}
