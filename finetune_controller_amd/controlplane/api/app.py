@@ -177,6 +177,15 @@ def create_app(ctx: AppContext, run_monitor: bool | None = None, validator_facto
         logger.warning("user %s denied admin action %s", jwt.user_id, action)
         raise HTTPException(status_code=403, detail="Admin privileges required")
 
+    def parse_limit(limit: str | None) -> list[int] | None:
+        """``limit``: comma-separated row indices of the table view; anything else is the client's error."""
+        if not limit:
+            return None
+        try:
+            return [int(x) for x in limit.split(",")]
+        except ValueError as e:
+            raise HTTPException(status_code=422, detail="limit: comma-separated integers expected") from e
+
     def available_models(jwt=None) -> list[str]:
         return ctx.registry.available_for(jwt.available_models if jwt else None)
 
@@ -382,8 +391,8 @@ def create_app(ctx: AppContext, run_monitor: bool | None = None, validator_facto
         jwt_data, jwt = decode_request(request)
         if jwt_data and jwt:
             user_id = jwt.user_id
+        lim = parse_limit(limit)
         try:
-            lim = [int(x) for x in limit.split(",")] if limit else None
             data = await ctx.store.get_user_jobs(user_id, page, page_size, sort, query, lim, status, model_name)
             items = []
             for j in data.items:
@@ -543,8 +552,8 @@ def create_app(ctx: AppContext, run_monitor: bool | None = None, validator_facto
         jwt_data, jwt = decode_request(request)
         if jwt:
             user_id = jwt.user_id
+        lim = parse_limit(limit)
         try:
-            lim = [int(x) for x in limit.split(",")] if limit else None
             data = await ctx.store.get_user_datasets_page(user_id, page, page_size, sort, query, lim)
             items = []
             for d in data.items:

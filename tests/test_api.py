@@ -78,6 +78,11 @@ def test_submit_validation_errors(env):
     for bad in ("ftp://h/x.csv", "not a url", "http:///nohost"):  # (submit is rate limited to 10/min)
         r = c.post("/api/v1/jobs", data=dict(FORM, dataset_url=bad))
         assert r.status_code == 422 and "dataset_url" in r.json()["detail"], bad
+    # a malformed row-index filter is the client's error, not a server failure
+    for path in ("/api/v1/jobs", "/api/v1/datasets"):
+        r = c.get(path, params={"limit": "1,two"})
+        assert r.status_code == 422 and "limit" in r.json()["detail"], path
+    assert c.get("/api/v1/jobs", params={"limit": "1,2"}).status_code == 200
 
 
 def test_submit_lifecycle_metrics_logs_cancel(env):
