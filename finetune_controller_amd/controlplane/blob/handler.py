@@ -99,9 +99,13 @@ class S3Handler:
         return urls
 
     async def cleanup_uri_items(self, s3_uri: str) -> int:
+        """Delete the object ``s3_uri`` names, or everything under it as a directory.  A plain key-prefix
+        delete (the reference's) would also take sibling keys that merely start with the same text --
+        ``.../job-1`` sweeping ``.../job-1-retry/...``, ``data.csv`` taking ``data.csv.bak``."""
         bucket, prefix = split_s3_uri(s3_uri)
         objs = await asyncio.to_thread(self.store.list, bucket, prefix)
-        keys = [o.Key for o in objs]
+        root = prefix.rstrip("/")
+        keys = [o.Key for o in objs if o.Key == prefix or o.Key == root or o.Key.startswith(root + "/")]
         if keys:
             await asyncio.to_thread(self.store.delete, bucket, keys)
         return len(keys)

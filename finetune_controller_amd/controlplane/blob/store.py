@@ -71,8 +71,10 @@ class LocalObjectStore(ObjectStore):
         self._lock = threading.Lock()
 
     def _p(self, bucket, key):
-        p = os.path.abspath(os.path.join(self.root, bucket, key))
-        if not p.startswith(os.path.join(self.root, bucket)):
+        base = os.path.abspath(os.path.join(self.root, bucket))
+        p = os.path.abspath(os.path.join(base, key))
+        # (a bare startswith(base) would let "../<bucket>-other/..." into a sibling bucket)
+        if not (p == base or p.startswith(base + os.sep)) or not base.startswith(self.root + os.sep):
             raise ValueError("key escapes bucket")
         return p
 
