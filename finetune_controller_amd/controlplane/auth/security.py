@@ -180,17 +180,21 @@ def _token_from_scope(scope) -> str:
             cookies[k] = v
     if "bridge-user" in cookies:
         raw = cookies["bridge-user"]
-        if raw.startswith('"') and raw.endswith('"'):
-            raw = raw[1:-1].encode().decode("unicode_escape")
+        # a cookie the client controls: anything unreadable is a 401, not a server error
         try:
-            data = json.loads(raw)
-        except Exception:
-            from urllib.parse import unquote
+            if raw.startswith('"') and raw.endswith('"'):
+                raw = raw[1:-1].encode().decode("unicode_escape")
+            try:
+                data = json.loads(raw)
+            except ValueError:
+                from urllib.parse import unquote
 
-            data = json.loads(unquote(raw))
-        if not data or not data.get("token"):
-            raise HTTPAuthError(401, "Missing or invalid Authorization header")
-        return CookieData(**data).token
+                data = json.loads(unquote(raw))
+            if not isinstance(data, dict) or not data.get("token"):
+                raise ValueError("no token")
+            return CookieData(**data).token
+        except (ValueError, TypeError) as e:  # (pydantic's ValidationError is a ValueError)
+            raise HTTPAuthError(401, "Missing or invalid Authorization header") from e
     auth = headers.get("authorization", "")
     if auth.startswith("Bearer "):
         return auth.split(" ", 1)[1]

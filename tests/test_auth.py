@@ -125,6 +125,12 @@ def test_middleware_valid_invalid_missing_malformed():
     assert c.get("/api/v1/test").status_code == 401
     assert c.get("/api/v1/test", headers={"Authorization": "NotBearer token"}).status_code == 401
     assert c.get("/open").status_code == 200  # only /api/v1 is protected
+    # an unreadable bridge-user cookie is the client's problem (401), never a 500
+    for bad in ("{not json", '"\\x"', json.dumps({"token": "t"}), json.dumps([1, 2]), json.dumps({"token": ""})):
+        c.cookies.set("bridge-user", bad)
+        r = c.get("/api/v1/test")
+        assert r.status_code == 401 and r.json()["detail"] == "Missing or invalid Authorization header", bad
+    c.cookies.clear()
 
 
 def test_middleware_cookie_and_local_dev_fallback():
