@@ -55,7 +55,17 @@ def _split(token: str):
         claims = json.loads(b64url_decode(parts[1]))
     except Exception as e:
         raise JWTError(f"Invalid token encoding: {e}") from e
+    if not isinstance(header, dict) or not isinstance(claims, dict):
+        raise JWTError("Invalid token encoding: header and claims must be JSON objects")
     return parts, header, claims
+
+
+def _signature(parts) -> bytes:
+    # every malformed-token path ends in JWTError (a 401 upstream), never in a stray decoding error
+    try:
+        return b64url_decode(parts[2])
+    except Exception as e:
+        raise JWTError(f"Invalid signature encoding: {e}") from e
 
 
 def get_unverified_header(token: str) -> dict:
@@ -67,8 +77,13 @@ def get_unverified_claims(token: str) -> dict:
 
 
 def _check_claims(claims: dict, audience: str | None, verify_exp: bool, leeway: float = 0.0):
-    if verify_exp and "exp" in claims and time.time() > float(claims["exp"]) + leeway:
-        raise ExpiredSignatureError("Signature has expired")
+    if verify_exp and "exp" in claims:
+        try:
+            exp = float(claims["exp"])
+        except (TypeError, ValueError) as e:
+            raise JWTError("Invalid exp claim") from e
+        if time.time() > exp + leeway:
+            raise ExpiredSignatureError("Signature has expired")
     if audience is not None:
         aud = claims.get("aud")
         auds = aud if isinstance(aud, list) else [aud]
@@ -82,7 +97,7 @@ def decode_hs256(token: str, secret: str | bytes, audience: str | None = None, v
         raise JWTError("The specified alg value is not allowed")
     key = secret if isinstance(secret, bytes) else secret.encode()
     want = hmac.new(key, f"{parts[0]}.{parts[1]}".encode(), hashlib.sha256).digest()
-    if not hmac.compare_digest(want, b64url_decode(parts[2])):
+    if not hmac.compare_digest(want, _signature(parts)):
         raise JWTError("Signature verification failed")
     _check_claims(claims, audience, verify_exp)
     return claims
@@ -180,14 +195,17 @@ def ecdsa_p256_verify(pub: tuple[int, int], msg: bytes, sig: bytes) -> bool:
 def jwk_to_p256(jwk: dict) -> tuple[int, int]:
     if jwk.get("kty") != "EC" or jwk.get("crv") != "P-256":
         raise JWTError("unsupported JWK (need EC P-256)")
-    return int.from_bytes(b64url_decode(jwk["x"]), "big"), int.from_bytes(b64url_decode(jwk["y"]), "big")
+    try:
+        return int.from_bytes(b64url_decode(jwk["x"]), "big"), int.from_bytes(b64url_decode(jwk["y"]), "big")
+    except Exception as e:
+        raise JWTError(f"malformed EC JWK: {e}") from e
 
 
 def decode_es256(token: str, jwk: dict, audience: str | None = None, verify_exp: bool = True) -> dict:
     parts, header, claims = _split(token)
     if header.get("alg") != "ES256":
         raise JWTError("The specified alg value is not allowed")
-    if not ecdsa_p256_verify(jwk_to_p256(jwk), f"{parts[0]}.{parts[1]}".encode(), b64url_decode(parts[2])):
+    if not ecdsa_p256_verify(jwk_to_p256(jwk), f"{parts[0]}.{parts[1]}".encode(), _signature(parts)):
         raise JWTError("Signature verification failed")
     _check_claims(claims, audience, verify_exp)
     return claims

@@ -120,3 +120,23 @@ def test_alg_confusion_is_rejected():
     with pytest.raises(jose.JWTError):
         jose.decode_es256(A3_TOKEN, {"kty": "EC", "crv": "P-384", "x": A3_JWK["x"], "y": A3_JWK["y"]},
                           verify_exp=False)
+
+
+def test_every_malformed_token_is_a_jwt_error():
+    """Garbage in any segment, a non-object header / claims, a non-numeric exp or a broken JWK must all
+    surface as JWTError (a 401 upstream), never as a decoding exception (a 500)."""
+    h = jose.b64url_encode(b'{"alg":"HS256"}')
+    c = jose.b64url_encode(b'{"sub":"x"}')
+    bad_tokens = [f"{h}.{c}.a",  # signature: 1 char past a multiple of 4 -> undecodable
+                  f"{jose.b64url_encode(b'[1]')}.{c}.AAAA", f"{h}.{jose.b64url_encode(b'3')}.AAAA",
+                  f"{h}.{c}", "..", "x.y.z"]
+    for t in bad_tokens:
+        with pytest.raises(jose.JWTError):
+            jose.decode_hs256(t, b"k")
+    t = jose.encode_hs256({"sub": "x", "exp": "tomorrow"}, "k")
+    with pytest.raises(jose.JWTError, match="exp"):
+        jose.decode_hs256(t, "k")
+    with pytest.raises(jose.JWTError):
+        jose.decode_es256(A3_TOKEN, {"kty": "EC", "crv": "P-256", "x": A3_JWK["x"]}, verify_exp=False)
+    with pytest.raises(jose.JWTError):
+        jose.decode_es256(A3_TOKEN.rsplit(".", 1)[0] + ".a", A3_JWK, verify_exp=False)
