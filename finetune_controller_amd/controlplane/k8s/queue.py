@@ -1,7 +1,8 @@
 """Queue position and pod diagnostics (C18).
 
 * ``kueue_pending(kube, ns)`` -- PyTorchJob names whose Kueue ``Workload`` has ``QuotaReserved=False``,
-  oldest first (``/root/reference/app/utils/kueue_helpers.py:19-46``);
+  oldest first (``/root/reference/app/utils/kueue_helpers.py:19-46``); workloads already ``Finished``
+  are skipped (a failed job stays on the cluster and must not hold a queue slot ahead of new ones);
 * ``kubeflow_suspended(kube, ns)`` -- fallback ordering from the jobs' own ``Suspended`` condition.
   The reference compares ``type.lower()`` with ``"Suspended"`` and therefore never matches
   (``kueue_helpers.py:92``); fixed here.
@@ -27,6 +28,8 @@ def kueue_pending(kube: KubeClient, namespace: str) -> list[str]:
         if not job or not created:
             continue
         conds = (wl.get("status") or {}).get("conditions", [])
+        if any(c.get("type") == "Finished" and c.get("status") == "True" for c in conds):
+            continue  # a finished workload (e.g. of a failed job the monitor keeps) is not queued
         if any(c.get("type") == "QuotaReserved" and c.get("status") == "False" for c in conds):
             pending.append((created, md.get("_seq", 0), job))
     pending.sort()

@@ -295,6 +295,12 @@ def test_kube_client_against_api_server_json():
     assert base64.b64decode(k.read_secret("aws", "ft")["AWS_REGION"]) == b"us-east-1"
     # Kueue pending order (QuotaReserved=False, by creation time) over the same transport
     assert queue_positions(k, "ft") == {"job-b": 1, "job-c": 2}
+    # a finished workload (a failed job stays listed) never holds a queue slot, whatever its quota flag
+    api.workloads.insert(0, {"metadata": {"name": "pytorchjob-old", "creationTimestamp": "2024-01-01T00:00:00Z",
+                                          "ownerReferences": [{"kind": "PyTorchJob", "name": "job-old"}]},
+                             "status": {"conditions": [{"type": "QuotaReserved", "status": "False"},
+                                                       {"type": "Finished", "status": "True"}]}})
+    assert queue_positions(k, "ft") == {"job-b": 1, "job-c": 2}
 
 
 def test_kubeconfig_discovery(tmp_path, monkeypatch):
