@@ -12,7 +12,9 @@ container, ``s3-sync`` sidecar, Master + (N-1) Worker replicas, ``backoffLimit: 
   ``failed.txt`` has persisted for 3 sync periods (a restarted container removes it first).  The
   reference's sidecar loops forever when training fails;
 * ``imagePullPolicy`` is set on the containers (it is not a PodSpec field);
-* label values are sanitised to the Kubernetes label-value grammar (user ids may contain '@').
+* label values are sanitised to the Kubernetes label-value grammar (user ids may contain '@');
+* a job with a dataset sets ``FTC_DATASET_EXPECTED=1`` on the training container: if the dataset
+  download left the mount empty, the worker fails instead of training on synthetic tokens.
 """
 from __future__ import annotations
 
@@ -104,6 +106,9 @@ def build_pytorchjob_manifest(job: JobInput, worker: Worker, settings, namespace
             "envFrom": aws_from,
             "env": aws_env,
         })
+    # the job HAS a dataset: the worker must not fall back to synthetic tokens if the download left the
+    # mount empty (its fallback is for dataset-optional specs submitted without one)
+    expect_data = [{"name": "FTC_DATASET_EXPECTED", "value": "1"}] if job.s3_uri else []
     main = {
         "name": "pytorch",
         "image": model.image,
@@ -120,7 +125,7 @@ def build_pytorchjob_manifest(job: JobInput, worker: Worker, settings, namespace
             {"name": "NCCL_DEBUG", "value": "INFO"},  # RCCL honours the NCCL_* variables
             {"name": "LOGLEVEL", "value": "DEBUG"},
             {"name": "PL_VERBOSE_LOGGING", "value": "1"},
-        ],
+        ] + expect_data,
     }
     sidecar = {
         "name": "s3-sync",

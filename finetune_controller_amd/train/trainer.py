@@ -281,8 +281,14 @@ class Trainer:
     def data(self):
         if self._data is None:
             tc = self.tc
-            if tc.synthetic or not tc.dataset_path or not os.path.exists(tc.dataset_path) or not os.listdir(
-                    tc.dataset_path if os.path.isdir(tc.dataset_path) else os.path.dirname(tc.dataset_path)):
+            missing = not tc.dataset_path or not os.path.exists(tc.dataset_path) or not os.listdir(
+                tc.dataset_path if os.path.isdir(tc.dataset_path) else os.path.dirname(tc.dataset_path))
+            if missing and not tc.synthetic and os.environ.get("FTC_DATASET_EXPECTED") == "1":
+                # the control plane attached a dataset to this job (k8s/manifest.py): an empty mount means the
+                # download failed -- training on synthetic tokens would "complete" with a meaningless model
+                raise FileNotFoundError(f"this job has a dataset but {tc.dataset_path!r} is missing or empty "
+                                        "(did the dataset download fail?)")
+            if tc.synthetic or missing:
                 self._data = SyntheticTokens(self.cfg.vocab_size, tc.batch_size, tc.seq_len, self.device,
                                              seed=tc.seed + self.dp_rank, doc_len=tc.synthetic_doc_len,
                                              eos_id=self.eos_id() if tc.pack_documents else 2)

@@ -124,6 +124,8 @@ def test_manifest_gpu_single_node_with_queue_and_dataset():
     assert "done.txt" in main["command"][-1] and "failed.txt" in main["command"][-1]
     assert spec["initContainers"][0]["name"] == "dataset-downloader"
     assert "aws s3 cp s3://bkt/finetune_jobs/u/j/dataset/d.jsonl /data/dataset/" in spec["initContainers"][0]["args"][0]
+    # the job has a dataset: the worker is told, so an empty mount fails it instead of synthetic training
+    assert {"name": "FTC_DATASET_EXPECTED", "value": "1"} in main["env"]
     assert {"name": "dshm", "emptyDir": {"medium": "Memory"}} in spec["volumes"]
     assert spec["tolerations"] == [{"key": "amd.com/gpu", "value": "present", "effect": "NoSchedule"}]
     side = spec["containers"][1]["args"][1]
@@ -141,6 +143,7 @@ def test_manifest_cpu_no_queue_no_dataset_multinode():
     assert reps["Worker"]["replicas"] == 1
     assert [c["name"] for c in reps["Worker"]["template"]["spec"]["containers"]] == ["pytorch"]
     main = reps["Master"]["template"]["spec"]["containers"][0]
+    assert not any(e["name"] == "FTC_DATASET_EXPECTED" for e in main["env"])  # no dataset attached
     # no accelerators in the worker config -> amd.com/gpu fallback with the model's count
     assert main["resources"]["requests"]["amd.com/gpu"] == 8
     assert "--nnodes=${PET_NNODES:-1}" in main["command"][-1]

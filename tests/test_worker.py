@@ -453,6 +453,29 @@ def test_trainer_eval_synthetic(tmp_path):
     assert a == b and a == pytest.approx(np.log(512), rel=0.1)
 
 
+def test_attached_dataset_missing_fails_instead_of_synthetic(tmp_path, monkeypatch):
+    """Without a dataset a dataset-optional spec trains on synthetic tokens; with FTC_DATASET_EXPECTED=1
+    (the manifest sets it when the job has a dataset) an empty mount -- a failed download -- must fail
+    the worker rather than 'complete' on random tokens."""
+    empty = tmp_path / "dataset"
+    empty.mkdir()
+
+    def trainer():
+        return Trainer(TrainConfig(model="llama-tiny", method="lora", batch_size=2, seq_len=16,
+                                   dataset_path=str(empty), max_steps=1, checkpoint_path=str(tmp_path / "ck"),
+                                   resume=False, device="cpu", save_model=False))
+
+    monkeypatch.delenv("FTC_DATASET_EXPECTED", raising=False)
+    tr = trainer()
+    assert type(tr.data()).__name__ == "SyntheticTokens"
+    tr.close()
+    monkeypatch.setenv("FTC_DATASET_EXPECTED", "1")
+    tr = trainer()
+    with pytest.raises(FileNotFoundError, match="missing or empty"):
+        tr.data()
+    tr.close()
+
+
 def _hold_until_released(tmp, port, timeout=120.0):
     """Keep a spawned rank alive until the parent has read its queued tensors: torch shares them by
     file descriptor through the sender, so a sender that exits first resets the parent's read."""
