@@ -273,17 +273,18 @@ class S3ObjectStore(ObjectStore):
     def put_stream(self, bucket, key, chunks):
         r = self._req("POST", bucket, key, query={"uploads": ""})
         upload_id = ET.fromstring(r.text).find("{*}UploadId").text
-        parts, buf, n = [], b"", 1
+        parts, buf, n = [], bytearray(), 1  # (a bytearray: appending chunks does not re-copy the part)
         try:
             for c in chunks:
                 buf += c
                 while len(buf) >= self.PART_SIZE:
-                    part, buf = buf[: self.PART_SIZE], buf[self.PART_SIZE:]
+                    part = bytes(buf[: self.PART_SIZE])
+                    del buf[: self.PART_SIZE]
                     rr = self._req("PUT", bucket, key, query={"partNumber": n, "uploadId": upload_id}, body=part)
                     parts.append((n, rr.headers["ETag"]))
                     n += 1
             if buf or not parts:
-                rr = self._req("PUT", bucket, key, query={"partNumber": n, "uploadId": upload_id}, body=buf)
+                rr = self._req("PUT", bucket, key, query={"partNumber": n, "uploadId": upload_id}, body=bytes(buf))
                 parts.append((n, rr.headers["ETag"]))
             xml = "<CompleteMultipartUpload>" + "".join(
                 f"<Part><PartNumber>{i}</PartNumber><ETag>{e}</ETag></Part>" for i, e in parts) + \
@@ -300,8 +301,20 @@ class S3ObjectStore(ObjectStore):
         return self._req("GET", bucket, key).content
 
     def get_file(self, bucket, key, path):
-        with open(path, "wb") as f:
-            f.write(self.get_bytes(bucket, key))
+        """Streamed to disk: a multi-GB checkpoint shard never sits whole in the API server's memory."""
+        host, upath = self._target(bucket, key)
+        h = self._headers("GET", host, upath, {}, _sha256(b""))
+        url = f"{self.scheme}://{host}{_uri_encode(upath, True)}"
+        tmp = path + ".part"
+        with self.http.stream("GET", url, headers=h) as r:
+            if r.status_code == 404:
+                raise ObjectNotFound(f"s3://{bucket}/{key}")
+            if r.status_code not in (200, 206):
+                raise RuntimeError(f"S3 GET {upath} failed: {r.status_code} {r.read()[:300]!r}")
+            with open(tmp, "wb") as f:
+                for chunk in r.iter_bytes(1 << 20):
+                    f.write(chunk)
+        os.replace(tmp, path)
 
     def head(self, bucket, key):
         try:
@@ -335,7 +348,13 @@ class S3ObjectStore(ObjectStore):
                 f"<Object><Key>{_xml_escape(k)}</Key></Object>" for k in keys[i:i + 1000]) + "</Delete>"
             body = xml.encode()
             md5 = __import__("base64").b64encode(hashlib.md5(body).digest()).decode()
-            self._req("POST", bucket, query={"delete": ""}, body=body, extra={"Content-MD5": md5})
+            r = self._req("POST", bucket, query={"delete": ""}, body=body, extra={"Content-MD5": md5})
+            # DeleteObjects answers 200 even when some keys were not deleted: they are listed as <Error>
+            errs = ET.fromstring(r.text).findall("{*}Error") if r.text.strip() else []
+            if errs:
+                first = errs[0]
+                raise RuntimeError(f"S3 delete: {len(errs)} of {len(keys[i:i + 1000])} keys not deleted "
+                                   f"(e.g. {first.findtext('{*}Key')}: {first.findtext('{*}Code')})")
 
     def copy(self, src_bucket, src_key, dst_bucket, dst_key):
         self._req("PUT", dst_bucket, dst_key,

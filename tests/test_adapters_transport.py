@@ -66,6 +66,7 @@ class FakeS3:
         self.objects: dict[tuple[str, str], bytes] = {}
         self.uploads: dict[str, dict[int, bytes]] = {}
         self.requests: list[httpx.Request] = []
+        self.delete_errors: list[str] = []  # keys DeleteObjects reports as <Error> in its 200 body
 
     def _verify(self, req: httpx.Request, body: bytes):
         auth = req.headers["authorization"]
@@ -117,9 +118,14 @@ class FakeS3:
             return httpx.Response(200, text="<CompleteMultipartUploadResult/>")
         if req.method == "POST" and "delete" in q:
             assert req.headers["content-md5"] == base64.b64encode(hashlib.md5(body).digest()).decode()
+            errs = ""
             for k in ET.fromstring(body).iter("Key"):
+                if k.text in self.delete_errors:
+                    errs += f"<Error><Key>{k.text}</Key><Code>AccessDenied</Code></Error>"
+                    continue
                 self.objects.pop((bucket, k.text), None)
-            return httpx.Response(200, text="<DeleteResult/>")
+            ns = "http://s3.amazonaws.com/doc/2006-03-01/"
+            return httpx.Response(200, text=f'<DeleteResult xmlns="{ns}">{errs}</DeleteResult>')
         if req.method == "GET" and q.get("list-type") == "2":
             keys = sorted(k for b, k in self.objects if b == bucket and k.startswith(q.get("prefix", "")))
             start = int(q.get("continuation-token", "0"))
@@ -163,6 +169,17 @@ def test_s3_client_operations_over_the_wire(addressing, tmp_path, monkeypatch):
     assert fake.objects[("deploy", "models/job1/data.csv")] == b"a,b\n1,2\n"
     st.delete("bkt", [o.Key for o in listed])
     assert st.list("bkt", "finetune_jobs/alice/job 1/artifacts/") == []
+    # get_file streams to disk (through a temp name, then renamed)
+    dst = tmp_path / "dl.csv"
+    st.get_file("bkt", key, str(dst))
+    assert dst.read_bytes() == b"a,b\n1,2\n" and not (tmp_path / "dl.csv.part").exists()
+    with pytest.raises(s3.ObjectNotFound):
+        st.get_file("bkt", "missing", str(tmp_path / "x"))
+    # a DeleteObjects that reports per-key errors in its 200 body is an error, not a silent partial delete
+    fake.delete_errors = ["locked/key"]
+    with pytest.raises(RuntimeError, match="1 of 2 keys not deleted"):
+        st.delete("bkt", ["locked/key", "other"])
+    fake.delete_errors = []
     # multipart upload: parts are sent in order and re-assembled
     monkeypatch.setattr(s3.S3ObjectStore, "PART_SIZE", 16)
     st.put_stream("bkt", "big.bin", iter([b"x" * 10, b"y" * 30, b"z" * 3]))
