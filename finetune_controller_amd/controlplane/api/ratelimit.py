@@ -32,15 +32,27 @@ def remote_address(request) -> str:
 
 
 class Limiter:
+    SWEEP_EVERY = 4096  # hits between sweeps of idle (route, client) windows
+
     def __init__(self, key_func=remote_address, enabled: bool = True):
         self.key_func = key_func
         self.enabled = enabled
         self._hits: dict[tuple, deque] = defaultdict(deque)
+        self._window: dict[tuple, float] = {}
+        self._since_sweep = 0
         self._lock = threading.Lock()
 
     def reset(self):
         with self._lock:
             self._hits.clear()
+            self._window.clear()
+
+    def _sweep(self, now: float) -> None:
+        # drop the windows of clients that have not called within their window: without this every
+        # address that ever called stays in memory for the life of the worker
+        for k in [k for k, q in self._hits.items() if not q or now - q[-1] >= self._window.get(k, 0.0)]:
+            del self._hits[k]
+            self._window.pop(k, None)
 
     def hit(self, route: str, key: str, spec: str) -> None:
         if not self.enabled:
@@ -48,7 +60,12 @@ class Limiter:
         n, window = parse_limit(spec)
         now = time.monotonic()
         with self._lock:
+            self._since_sweep += 1
+            if self._since_sweep >= self.SWEEP_EVERY:
+                self._since_sweep = 0
+                self._sweep(now)
             q = self._hits[(route, key)]
+            self._window[(route, key)] = window
             while q and now - q[0] >= window:
                 q.popleft()
             if len(q) >= n:
