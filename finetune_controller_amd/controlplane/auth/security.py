@@ -139,7 +139,10 @@ class TokenValidator:
         if not info.get("active", False):
             raise HTTPAuthError(401, "Invalid token")
         if "sub" in info:
-            self._meta[info["sub"]] = (time.time(), info)
+            now = time.time()
+            if len(self._meta) >= 1024:  # users who never came back: drop their expired entries
+                self._meta = {k: v for k, v in self._meta.items() if now - v[0] <= self.metadata_cache_time}
+            self._meta[info["sub"]] = (now, info)
         return info
 
 
