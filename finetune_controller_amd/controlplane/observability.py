@@ -77,6 +77,9 @@ def get_metrics(ctx) -> ControlPlaneMetrics:
     return m
 
 
+_METHODS = frozenset({"GET", "POST", "PUT", "PATCH", "DELETE", "HEAD", "OPTIONS"})
+
+
 class PrometheusMiddleware:
     """Pure ASGI: counts HTTP requests by method / route template / status and times them."""
 
@@ -100,5 +103,7 @@ class PrometheusMiddleware:
         finally:
             route = getattr(scope.get("route"), "path", None) or "<unmatched>"
             method = scope.get("method", "?")
+            if method not in _METHODS:  # the request line is client text: keep the label set closed
+                method = "OTHER"
             self.m.http_requests.labels(method, route, str(status["code"])).inc()
             self.m.http_latency.labels(method, route).observe(time.perf_counter() - t0)

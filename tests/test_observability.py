@@ -32,6 +32,8 @@ def test_metrics_endpoint_counts_api_and_monitor(tmp_path):
             ctx.kube.reconcile()
         mon = app.state.monitor
         c.portal.call(mon.reconcile_once)
+        for verb in ("FROB", "XYZZY"):  # arbitrary request-line methods share one label value
+            c.request(verb, "/api/v1/health")
         text = c.get("/metrics").text
     s = _samples(text)
     assert s[("ftc_jobs_submitted_total", (("device", "mi355x"), ("model", "Llama3-8B-LoRA")))] == 2
@@ -43,3 +45,5 @@ def test_metrics_endpoint_counts_api_and_monitor(tmp_path):
     assert s[("ftc_monitor_reconcile_passes_total", ())] == 1
     running = sum(v for (n, lab), v in s.items() if n == "ftc_cluster_jobs")
     assert running == 2
+    methods = {dict(k[1]).get("method") for k in s if k[0] == "ftc_http_requests_total"}
+    assert "OTHER" in methods and not methods & {"FROB", "XYZZY"}
