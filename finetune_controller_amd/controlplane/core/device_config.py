@@ -93,13 +93,24 @@ class APIConfiguration(BaseModel):
 
 
 def remove_json_comments(s: str) -> str:
-    # strip // comments that are not inside a string
-    out, i, n, in_str = [], 0, len(s), False
+    """Strip ``//`` comments outside strings.  Escapes are tracked, so a string ending in an escaped
+    backslash (``"C:\\\\"``) closes where JSON says it does."""
+    out, i, n, in_str, esc = [], 0, len(s), False, False
     while i < n:
         ch = s[i]
-        if ch == '"' and (i == 0 or s[i - 1] != "\\"):
-            in_str = not in_str
-        if not in_str and s.startswith("//", i):
+        if in_str:
+            out.append(ch)
+            if esc:
+                esc = False
+            elif ch == "\\":
+                esc = True
+            elif ch == '"':
+                in_str = False
+            i += 1
+            continue
+        if ch == '"':
+            in_str = True
+        elif s.startswith("//", i):
             j = s.find("\n", i)
             i = n if j < 0 else j
             continue

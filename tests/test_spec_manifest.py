@@ -93,6 +93,10 @@ def test_lora_spec_run_cmd_and_validation():
 
 def test_device_config():
     assert "//" not in remove_json_comments('{"a": "http://x"} // c').split('"a"')[0]
+    # escapes: a string ending in an escaped backslash, an escaped quote followed by "//" inside a string
+    import json as _json
+    text = '{"a": "x\\\\", // comment\n "b": "http://h/p", "c": "q\\"//x"} // end'
+    assert _json.loads(remove_json_comments(text)) == {"a": "x\\", "b": "http://h/p", "c": 'q"//x'}
     cfg = parse_config(CFG)
     assert cfg.list_workers() == ["cpu", "mi355x", "noqueue-gpu"]
     assert cfg.get_worker("cpu").local_queue == "finetune-queue"  # default queue filled in
