@@ -112,7 +112,7 @@ class LMTrainingArguments(TrainingArguments):
     max_steps: int = Field(default=0, ge=0, description="Stop after this many optimizer steps (0 = epochs)")
     lr: float = Field(default=2e-4, gt=0, description="Peak learning rate")
     warmup_steps: int = Field(default=10, ge=0, description="Linear warmup steps")
-    schedule: str = Field(default="cosine", description="cosine | linear | constant")
+    schedule: Literal["cosine", "linear", "constant"] = Field(default="cosine", description="cosine | linear | constant")
     weight_decay: float = Field(default=0.0, ge=0, description="AdamW decoupled weight decay")
     max_grad_norm: float = Field(default=1.0, ge=0, description="Global grad-norm clip (0 = off)")
     seed: int = Field(default=1, description="Random seed")

@@ -314,3 +314,26 @@ def test_untrusted_dataset_names_cannot_inject_shell():
     assert "; rm -rf /;" not in cmd
     w = wrap_command(["/bin/bash", "-c", "python train.py"], evil)[-1]
     assert "'/data/artifacts; rm -rf //done.txt'" in w
+
+
+def test_user_argument_strings_cannot_inject_shell():
+    """Argument values come from the user's form and the command's last element runs under sh -c:
+    every rendered argument is one shell word."""
+    import shlex
+
+    from finetune_controller_amd.controlplane.spec.models.builtin import LMTrainingArguments
+
+    reg = ModelRegistry()
+    cls = reg.get("Llama3-8B-LoRA")
+    evil = "q_proj,v_proj; touch /tmp/pwned #"
+    base = cls.model_fields["training_arguments"].get_default().model_dump()
+    m = cls(training_arguments=type(cls.model_fields["training_arguments"].get_default())(
+        **{**base, "lora_targets": evil}))
+    line = m.run_cmd()[-1]
+    words = shlex.split(line)
+    assert f"--lora-targets={evil}" in words  # the whole value is one argument
+    assert "touch" not in words and "/tmp/pwned" not in words
+    # a closed vocabulary where there is one
+    import pydantic
+    with pytest.raises(pydantic.ValidationError):
+        LMTrainingArguments(schedule="cosine; reboot")
