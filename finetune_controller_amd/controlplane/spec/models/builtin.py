@@ -22,7 +22,7 @@ from __future__ import annotations
 
 from typing import Annotated, ClassVar, Literal
 
-from pydantic import Field
+from pydantic import Field, field_validator
 
 from ..finetuning import (BaseFineTuneModel, TrainingArguments, TrainingDataset, TrainingFramework,
                           TrainingResources, TrainingTask)
@@ -142,6 +142,9 @@ class LMTrainingArguments(TrainingArguments):
                                             "(0 = off); the job then restarts from its last checkpoint")
 
 
+_LORA_TARGETS = ("q_proj", "k_proj", "v_proj", "o_proj", "gate_proj", "up_proj", "down_proj")
+
+
 class LoRAArguments(LMTrainingArguments):
     lora_r: int = Field(default=16, ge=1, le=256, description="LoRA rank")
     lora_alpha: float = Field(default=32.0, gt=0, description="LoRA alpha (scale = alpha / r)")
@@ -150,6 +153,16 @@ class LoRAArguments(LMTrainingArguments):
     lora_targets: str = Field(default="q_proj,k_proj,v_proj,o_proj,gate_proj,up_proj,down_proj",
                               description="Comma-separated target modules")
     lr: float = Field(default=2e-4, gt=0, description="Peak learning rate")
+
+    @field_validator("lora_targets")
+    @classmethod
+    def _known_targets(cls, v: str) -> str:
+        # a typo would silently train fewer projections than asked (the worker has no such module)
+        names = [t.strip() for t in v.split(",") if t.strip()]
+        bad = [t for t in names if t not in _LORA_TARGETS]
+        if not names or bad:
+            raise ValueError(f"unknown LoRA target(s) {bad or v!r}; choose from {', '.join(_LORA_TARGETS)}")
+        return ",".join(names)
 
 
 class _WorkerSpec(BaseFineTuneModel):

@@ -124,6 +124,28 @@ class DecodeStep:
         return logits
 
 
+def peft_targets(tm) -> list[str]:
+    """A PEFT ``target_modules`` entry as this model's projection names: ``"all-linear"``, a list, or one
+    name / regex-like string; modules this model has no LoRA slot for (an adapter from another tool that
+    also targets ``lm_head``, say) are dropped with a warning."""
+    import sys
+
+    from .lora import ALL_LINEAR
+
+    if tm is None or tm == "all-linear":
+        return list(ALL_LINEAR)
+    names = [tm] if isinstance(tm, str) else list(tm)
+    if len(names) == 1 and names[0] not in ALL_LINEAR:
+        names = [t for t in ALL_LINEAR if t in str(names[0])] or names  # e.g. ".*(q_proj|v_proj)$"
+    kept = [t for t in names if t in ALL_LINEAR]
+    dropped = [t for t in names if t not in ALL_LINEAR]
+    if dropped:
+        print(f"[generate] adapter targets without a LoRA slot here, ignored: {dropped}", file=sys.stderr)
+    if not kept:
+        raise ValueError(f"adapter targets {tm!r} name none of {ALL_LINEAR}")
+    return kept
+
+
 def main(argv=None) -> int:
     """``python -m finetune_controller_amd.models.generate --model llama3-8b [--init-from HF_DIR]
     [--adapter ADAPTER_DIR] --prompt "..."``: continue prompts with a (fine-tuned) model."""
@@ -154,7 +176,7 @@ def main(argv=None) -> int:
 
         with open(os.path.join(a.adapter, "adapter_config.json")) as f:
             ac = json.load(f)
-        lora = LoRAConfig(r=ac["r"], alpha=ac["lora_alpha"], target_modules=list(ac["target_modules"]),
+        lora = LoRAConfig(r=ac["r"], alpha=ac["lora_alpha"], target_modules=peft_targets(ac.get("target_modules")),
                           use_rslora=bool(ac.get("use_rslora", False)))
     m = build_model(cfg, lora, device=dev, dtype=torch.bfloat16 if dev.type == "cuda" else torch.float32)
     if a.init_from:

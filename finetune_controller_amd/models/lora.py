@@ -36,6 +36,11 @@ class LoRAConfig:
     target_modules: list[str] = field(default_factory=lambda: list(ALL_LINEAR))
     use_rslora: bool = False  # rank-stabilised scaling alpha / sqrt(r) (PEFT ``use_rslora``)
 
+    def __post_init__(self):
+        bad = [t for t in self.target_modules if t not in ALL_LINEAR]
+        if bad or not self.target_modules:
+            raise ValueError(f"unknown LoRA target module(s) {bad or self.target_modules}: choose from {ALL_LINEAR}")
+
     @property
     def scale(self) -> float:
         return self.alpha / (self.r ** 0.5 if self.use_rslora else self.r)

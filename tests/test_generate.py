@@ -83,3 +83,20 @@ def test_generate_cli_loads_adapter(tmp_path, capsys):
     capsys.readouterr()
     assert main(["--model", "llama-tiny", "--adapter", str(tmp_path), "--prompt", "hi", "--max-new-tokens", "4"]) == 0
     assert capsys.readouterr().out.startswith("hi")
+
+
+def test_peft_target_forms_and_unknown_worker_targets():
+    """Adapters from other tools name their targets as "all-linear", a list (possibly with modules this
+    model has no LoRA slot for) or a regex; the trainer itself refuses a target it does not have."""
+    import pytest
+
+    from finetune_controller_amd.models.generate import peft_targets
+    from finetune_controller_amd.models.lora import ALL_LINEAR, LoRAConfig
+
+    assert peft_targets("all-linear") == ALL_LINEAR and peft_targets(None) == ALL_LINEAR
+    assert peft_targets(["q_proj", "v_proj", "lm_head"]) == ["q_proj", "v_proj"]
+    assert peft_targets(".*(q_proj|v_proj)$") == ["q_proj", "v_proj"]
+    with pytest.raises(ValueError):
+        peft_targets(["embed_tokens"])
+    with pytest.raises(ValueError, match="unknown LoRA target"):
+        LoRAConfig(target_modules=["q_proj", "qkv"])

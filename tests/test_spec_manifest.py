@@ -318,22 +318,22 @@ def test_untrusted_dataset_names_cannot_inject_shell():
 
 def test_user_argument_strings_cannot_inject_shell():
     """Argument values come from the user's form and the command's last element runs under sh -c:
-    every rendered argument is one shell word."""
+    every rendered argument is one shell word (append_args quotes; a custom spec's free-form field
+    such as docs/models.md's --target-column stays data)."""
     import shlex
 
-    from finetune_controller_amd.controlplane.spec.models.builtin import LMTrainingArguments
-
-    reg = ModelRegistry()
-    cls = reg.get("Llama3-8B-LoRA")
-    evil = "q_proj,v_proj; touch /tmp/pwned #"
-    base = cls.model_fields["training_arguments"].get_default().model_dump()
-    m = cls(training_arguments=type(cls.model_fields["training_arguments"].get_default())(
-        **{**base, "lora_targets": evil}))
-    line = m.run_cmd()[-1]
-    words = shlex.split(line)
-    assert f"--lora-targets={evil}" in words  # the whole value is one argument
-    assert "touch" not in words and "/tmp/pwned" not in words
-    # a closed vocabulary where there is one
     import pydantic
+
+    from finetune_controller_amd.controlplane.spec.models.builtin import LMTrainingArguments, LoRAArguments
+
+    m = ModelRegistry().instance("Llama3-8B-LoRA")
+    evil = "--target-column=esol; touch /tmp/pwned #"
+    words = shlex.split(m.append_args([evil, "--epochs=3"])[-1])
+    assert evil in words and "--epochs=3" in words and "touch" not in words and "/tmp/pwned" not in words
+    assert any(w.startswith("--dataset_path=") for w in words)
+    # closed vocabularies where there is one: a typo'd LoRA target or schedule is refused at submit time
     with pytest.raises(pydantic.ValidationError):
         LMTrainingArguments(schedule="cosine; reboot")
+    with pytest.raises(pydantic.ValidationError, match="unknown LoRA target"):
+        LoRAArguments(lora_targets="q_proj,v_prj")
+    assert LoRAArguments(lora_targets=" q_proj , v_proj").lora_targets == "q_proj,v_proj"
