@@ -511,7 +511,7 @@ class Trainer:
         faults = FaultInjector.from_env(self.info.rank, tc.checkpoint_path)
         self.watchdog = watchdog = StepWatchdog.from_env(tc.step_timeout_s, self.info.rank)
         metrics = MetricsCSV(os.path.join(tc.checkpoint_path, "metrics.csv"), enabled=self.is_main,
-                             resume=start > 0)
+                             resume=start > 0, resume_step=start if start > 0 else None)
         # tokens trained per optimizer step: every data-parallel replica's micro-batches (the ranks of a
         # sequence-parallel group share their sequences, so they count once)
         tok_per_step = tc.batch_size * tc.seq_len * tc.grad_accum * self.dp_world

@@ -17,12 +17,17 @@ COLUMNS = ["epoch", "step", "loss", "lr", "tokens_per_sec", "step_time_ms", "gra
 
 
 class MetricsCSV:
-    def __init__(self, path: str, enabled: bool = True, resume: bool = False):
+    def __init__(self, path: str, enabled: bool = True, resume: bool = False, resume_step: int | None = None):
+        """``resume_step``: the step the run restarts after.  Rows past it were logged by the attempt that
+        died after its last checkpoint; those steps run again, so they are dropped first (one row per
+        step in the UI's curves, not two)."""
         self.path, self.enabled = path, enabled
         if not enabled:
             return
         os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
         exists = os.path.exists(path) and os.path.getsize(path) > 0
+        if resume and exists and resume_step is not None:
+            _truncate_after(path, resume_step)
         self.f = open(path, "a" if (resume and exists) else "w", newline="")
         self.w = csv.DictWriter(self.f, fieldnames=COLUMNS, extrasaction="ignore")
         if not (resume and exists):
@@ -38,6 +43,26 @@ class MetricsCSV:
     def close(self):
         if self.enabled:
             self.f.close()
+
+
+def _truncate_after(path: str, step: int) -> None:
+    with open(path, newline="") as f:
+        rows = list(csv.reader(f))
+    if not rows or "step" not in rows[0]:
+        return
+    si = rows[0].index("step")
+    keep = [rows[0]]
+    for r in rows[1:]:
+        try:
+            if int(float(r[si])) > step:
+                continue
+        except (IndexError, ValueError):
+            continue  # a torn last line from the crash
+        keep.append(r)
+    tmp = path + ".tmp"
+    with open(tmp, "w", newline="") as f:
+        csv.writer(f).writerows(keep)
+    os.replace(tmp, path)
 
 
 def read_metrics_csv(path: str) -> list[dict]:

@@ -309,6 +309,10 @@ def test_trainer_resume(tmp_path):
     tr2.close()
     rows = open(tmp_path / "metrics.csv").read().strip().splitlines()
     assert last["step"] == 6 and rows[0].startswith("epoch,step,loss") and rows[-1].split(",")[1] == "6"
+    # the first attempt logged step 4 after its last resume checkpoint (step 2); the resumed run logs
+    # step 4 again -- the file keeps one row per step
+    steps = [int(r.split(",")[1]) for r in rows[1:]]
+    assert steps == sorted(set(steps)) and 4 in steps
 
 
 def test_dataset_formats(tmp_path):
