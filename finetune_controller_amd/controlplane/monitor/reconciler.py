@@ -53,6 +53,8 @@ class JobMonitor:
         self.stop_monitoring = False
         self.monitoring_task: asyncio.Task | None = None
         self.is_leader = False
+        self.orphan_grace_s = max(60.0, 10 * self.interval)
+        self._missing: dict[str, _dt.datetime] = {}  # job id -> first pass that did not list it
 
     # ---------------------------------------------------------------- one reconcile pass
     async def reconcile_once(self) -> int:
@@ -107,7 +109,32 @@ class JobMonitor:
                 await self.delete_job(job_id)
             elif status == KubeflowStatusEnum.failed.value:
                 logger.error("job %s failed: %s", job_id, cond.get("message"))
+        n += await self._fail_vanished(jobs)
         get_metrics(ctx).observe_pass(t0, by_status, len(queue), n)
+        return n
+
+    async def _fail_vanished(self, jobs) -> int:
+        """A job the DB still shows as queued / running whose PyTorchJob is gone from the cluster (deleted
+        with kubectl, a cluster reset) would otherwise stay 'running' in the UI forever: mark it failed
+        once it has been missing for ``orphan_grace_s`` (covers the create -> list lag of a submission)."""
+        listed = {j["metadata"]["name"] for j in jobs}
+        now = _dt.datetime.now(_dt.timezone.utc)
+        n = 0
+        for rec in await self.ctx.store.get_active_jobs():
+            if rec.job_id in listed:
+                self._missing.pop(rec.job_id, None)
+                continue
+            first = self._missing.setdefault(rec.job_id, now)
+            created = rec.created_at if rec.created_at.tzinfo else rec.created_at.replace(tzinfo=_dt.timezone.utc)
+            if (now - first).total_seconds() < self.orphan_grace_s or \
+                    (now - created).total_seconds() < self.orphan_grace_s:
+                continue
+            logger.error("job %s: its PyTorchJob is gone from the cluster; marking it failed", rec.job_id)
+            await self.ctx.store.update_job_status(rec.job_id, DatabaseStatusEnum.failed, metadata={
+                "message": "PyTorchJob no longer exists on the cluster", "reason": "PyTorchJobMissing",
+                "completion_time": now})
+            self._missing.pop(rec.job_id, None)
+            n += 1
         return n
 
     async def _process_metrics(self, job_id, info, st, completed: bool):

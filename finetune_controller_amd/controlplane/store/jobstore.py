@@ -144,6 +144,16 @@ class JobStore:
         docs = await cur.to_list(length=1)
         return JobStatus(**docs[0]) if docs else None
 
+    async def get_active_jobs(self) -> list[JobStatus]:
+        """Jobs in a running state (queued / starting / restarting / running), any user."""
+        states = [DatabaseStatusEnum.queued.value, DatabaseStatusEnum.starting.value,
+                  DatabaseStatusEnum.restarting.value, DatabaseStatusEnum.running.value]
+        out = []
+        async for d in self.jobs_collection.find({"status": {"$in": states}}):
+            d.pop("_id", None)
+            out.append(JobStatus(**d))
+        return out
+
     async def get_all_user_jobs(self, user_id: str) -> list[JobStatus]:
         out = []
         async for d in self.jobs_collection.find({"user_id": user_id}):

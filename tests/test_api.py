@@ -131,6 +131,25 @@ def test_monitor_retries_a_failed_delete_of_a_succeeded_job(env, monkeypatch):
     assert calls[:2] == [jid, jid] and ctx.kube.list_pytorchjobs(ctx.namespace) == []
 
 
+def test_monitor_fails_a_job_whose_pytorchjob_vanished(env):
+    """A PyTorchJob deleted behind the controller's back (kubectl, a cluster reset) must not leave its
+    job 'running' in the UI forever: after the grace period the monitor marks it failed."""
+    ctx, c = env
+    jid = submit(c)
+    keep = submit(c)
+    mon = JobMonitor(ctx, interval=0)
+    ctx.kube.reconcile()
+    asyncio.run(mon.reconcile_once())
+    ctx.kube.delete_pytorchjob(ctx.namespace, jid)
+    asyncio.run(mon.reconcile_once())  # first pass without it: within the grace period
+    assert c.get(f"/api/v1/jobs/{jid}").json()["status"] != "failed"
+    mon.orphan_grace_s = 0
+    asyncio.run(mon.reconcile_once())
+    j = c.get(f"/api/v1/jobs/{jid}").json()
+    assert j["status"] == "failed" and j["metadata"]["reason"] == "PyTorchJobMissing"
+    assert c.get(f"/api/v1/jobs/{keep}").json()["status"] != "failed"
+
+
 def test_failed_job_insert_takes_the_pytorchjob_back(env, monkeypatch):
     """The PyTorchJob is created before the job document; when the insert fails the submission must
     not leave a job on the cluster that no DB record (and so no monitor pass) will ever claim."""
