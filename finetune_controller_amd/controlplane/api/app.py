@@ -518,6 +518,15 @@ def create_app(ctx: AppContext, run_monitor: bool | None = None, validator_facto
             raise HTTPException(status_code=404, detail=f"Job '{job_id}' not found")
         if TrainingJobStatus.is_running(info.status):
             raise HTTPException(status_code=400, detail="Job is still running")
+        # a failed job's PyTorchJob stays on the cluster (only succeeded ones are removed by the monitor):
+        # deleting the job takes it along, or it would outlive every record of it
+        try:
+            await asyncio.to_thread(ctx.kube.delete_pytorchjob, ctx.namespace, job_id)
+        except KubeError as e:
+            if e.status != 404:
+                logger.warning("job %s: PyTorchJob delete failed: %s", job_id, e)
+        except Exception as e:  # noqa: BLE001 -- cleanup must not block the record deletion
+            logger.warning("job %s: PyTorchJob delete failed: %s", job_id, e)
         if info.promoted == PromotionStatus.COMPLETED and info.destination_uri:
             await ctx.s3.cleanup_uri_items(info.destination_uri)
         if info.atrifacts_uri:

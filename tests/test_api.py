@@ -150,6 +150,24 @@ def test_monitor_fails_a_job_whose_pytorchjob_vanished(env):
     assert c.get(f"/api/v1/jobs/{keep}").json()["status"] != "failed"
 
 
+def test_deleting_a_failed_job_removes_its_pytorchjob(env):
+    """The monitor removes succeeded PyTorchJobs only; a failed one stays for inspection until the
+    user deletes the job, which then takes the cluster object along."""
+    ctx, c = env
+    jid = submit(c)
+    mon = JobMonitor(ctx, interval=0)
+    for _ in range(40):  # every (re)start fails: backoffLimit restarts, then Failed
+        ctx.kube.fail_next(jid)
+        ctx.kube.reconcile()
+        asyncio.run(mon.reconcile_once())
+        if c.get(f"/api/v1/jobs/{jid}").json()["status"] == "failed":
+            break
+    assert c.get(f"/api/v1/jobs/{jid}").json()["status"] == "failed"
+    assert jid in [j["metadata"]["name"] for j in ctx.kube.list_pytorchjobs(ctx.namespace)]
+    r = c.request("DELETE", "/api/v1/jobs/delete", json={"job_ids": [jid]})
+    assert r.status_code == 200 and ctx.kube.list_pytorchjobs(ctx.namespace) == []
+
+
 def test_failed_job_insert_takes_the_pytorchjob_back(env, monkeypatch):
     """The PyTorchJob is created before the job document; when the insert fails the submission must
     not leave a job on the cluster that no DB record (and so no monitor pass) will ever claim."""
