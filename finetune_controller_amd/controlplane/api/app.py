@@ -65,7 +65,7 @@ from ..schemas.jobs import (Dataset, DatasetInput, DatasetMeta, Job, JobIdsReque
                             PaginatedTableResponse)
 from ..schemas.kubeflow import TrainingJobStatus
 from ..spec.finetuning import TrainingTask
-from ..tasks.services import NotFound, PromotionTask, task_builder
+from ..tasks.services import BlockedURL, NotFound, PromotionTask, task_builder
 from .forms import FormError, discard_uploads, parse_form
 from .ratelimit import Limiter, RateLimitExceeded, remote_address
 
@@ -375,6 +375,8 @@ def create_app(ctx: AppContext, run_monitor: bool | None = None, validator_facto
             return {"message": "Job started successfully", "job_id": job_id}
         except NotFound as e:
             raise HTTPException(status_code=404, detail=str(e)) from e
+        except BlockedURL as e:
+            raise HTTPException(status_code=422, detail=f"dataset_url: {e}") from e
         except KubeError as e:
             raise HTTPException(status_code=e.status, detail=f"Failed to start job {job_name} / {job_id}<br>{e}") from e
         except Exception as e:

@@ -93,6 +93,10 @@ class Settings(BaseModel):
     # [new] worker image used by the built-in MI355X model specs
     WORKER_IMAGE: str = "ghcr.io/finetune-controller-amd/worker-rocm:latest"
     CUSTOM_MODELS_DIR: str | None = None
+    # [new] dataset_url submissions are fetched BY THE API SERVER: by default a URL (or a redirect)
+    # that resolves to a loopback / private / link-local address (cluster services, the cloud metadata
+    # endpoint) is refused; set true when datasets really live on an internal host
+    DATASET_URL_ALLOW_PRIVATE: bool = False
     # [new] cached credentials (filled by load_aws_credentials)
     aws_access_key: SecretStr | None = None
     aws_secret_key: SecretStr | None = None

@@ -85,6 +85,14 @@ def test_submit_validation_errors(env):
     assert c.get("/api/v1/jobs", params={"limit": "1,2"}).status_code == 200
 
 
+def test_dataset_url_into_the_cluster_network_is_refused(env):
+    """The API server fetches dataset_url itself: the cloud metadata endpoint is not a dataset."""
+    ctx, c = env
+    r = c.post("/api/v1/jobs", data=dict(FORM, dataset_url="http://169.254.169.254/latest/meta-data/"))
+    assert r.status_code == 422 and "non-public" in r.json()["detail"]
+    assert ctx.kube.list_pytorchjobs(ctx.namespace) == []
+
+
 def test_submit_lifecycle_metrics_logs_cancel(env):
     ctx, c = env
     jid = submit(c)
@@ -231,7 +239,7 @@ def test_dataset_upload_reuse_url_and_delete(env, monkeypatch):
     def handler(req):
         return httpx.Response(200, content=b"a,b\n1,2\n", headers={"Content-Disposition": 'attachment; filename="x.csv"'})
 
-    monkeypatch.setattr(services, "_http_client", lambda: httpx.Client(transport=httpx.MockTransport(handler)))
+    monkeypatch.setattr(services, "_http_client", lambda *a, **k: httpx.Client(transport=httpx.MockTransport(handler)))
     jid3 = submit(c, dataset_url="https://example.org/data/x.csv")
     page = c.get("/api/v1/datasets", params={"page_size": 10}).json()
     assert page["total"] == 2
