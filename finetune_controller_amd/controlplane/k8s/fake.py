@@ -593,6 +593,9 @@ class FakeCluster(KubeClient):
             return
         dest = m.group(2)
         pats = re.findall(r"--include '([^']+)'", script)
+        # `aws s3 sync` filters: later ones win, so excludes written after the includes drop matches again
+        first = script[script.index("--include"):].split(";", 1)[0] if pats else ""  # one `aws s3 sync` only
+        tail_excl = re.findall(r"--exclude '([^']+)'", first)
         bucket, prefix = split_s3_uri(dest)
         art = os.path.join(p.workdir, "artifacts")
         done = os.path.join(art, "done.txt")
@@ -605,6 +608,8 @@ class FakeCluster(KubeClient):
                 if not os.path.isfile(full) or fn in ("done.txt", "failed.txt"):
                     continue
                 if not any(fnmatch.fnmatch(fn, pat) for pat in pats):
+                    continue
+                if any(fnmatch.fnmatch(fn, pat) for pat in tail_excl):
                     continue
                 mt = os.path.getmtime(full)
                 if synced.get(fn) == mt:

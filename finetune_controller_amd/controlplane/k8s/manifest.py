@@ -48,7 +48,11 @@ def wrap_command(cmd: list[str], ckpt: str) -> list[str]:
 def sync_command(ckpt: str, dest: str, patterns: list[str], interval: int) -> str:
     q = shlex.quote  # every path / URI / pattern is quoted: none of them may be shell syntax
     inc = " ".join(f"--include {q(p)}" for p in patterns)
-    s = f"aws s3 sync {q(ckpt)} {q(dest)} --exclude '*' {inc} --exclude 'done.txt' --exclude 'failed.txt'"
+    # the worker's resume checkpoints (checkpoint_step*.pt: fp32 master weights + AdamW moments, ~96 GB
+    # for an 8B full fine-tune) are read back from the pod's own volume only -- shipping every one to S3
+    # would re-upload tens of GB per save for nothing; their .tmp halves are never synced either
+    s = (f"aws s3 sync {q(ckpt)} {q(dest)} --exclude '*' {inc} --exclude 'done.txt' --exclude 'failed.txt' "
+         f"--exclude 'checkpoint_step*.pt' --exclude '*.tmp'")
     return (f"f=0; while [ ! -f {q(ckpt + '/done.txt')} ]; do {s}; sleep {int(interval)}; "
             f"if [ -f {q(ckpt + '/failed.txt')} ]; then f=$((f+1)); [ $f -ge 3 ] && break; else f=0; fi; done; "
             f"{s}; ls -la {q(ckpt)}; echo 'Training finished. Exiting sidecar.'")

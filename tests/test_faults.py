@@ -233,6 +233,10 @@ def test_lost_peer_job_restarts_and_completes(tmp_path):
         assert [t for j, t in ctx.kube.history if j == jid].count("Restarting") >= 2  # both pods
         m = c.get(f"/api/v1/jobs/{jid}/metrics").json()["metrics"]
         assert max(int(row["step"]) for row in m) == 6
+        # the sidecar ships the artifacts, never the resume checkpoints that live on the pod's volume
+        keys = [o.Key for o in ctx.objects.list(ctx.s3.bucket, "finetune_jobs/")]
+        assert any(k.endswith("metrics.csv") for k in keys)
+        assert not any("checkpoint_step" in k or k.endswith(".tmp") for k in keys), keys
 
 
 def test_first_write_registry_flushes_unwritten_weight():

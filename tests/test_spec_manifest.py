@@ -134,6 +134,10 @@ def test_manifest_gpu_single_node_with_queue_and_dataset():
     assert spec["tolerations"] == [{"key": "amd.com/gpu", "value": "present", "effect": "NoSchedule"}]
     side = spec["containers"][1]["args"][1]
     assert "--include '*.safetensors'" in side and "s3://bkt/finetune_jobs/u/j/artifacts" in side
+    # resume checkpoints stay on the pod's volume (tens of GB per save for a full fine-tune), and so do
+    # half-written files; later aws-cli filters win, so the excludes follow the includes
+    assert side.index("--exclude 'checkpoint_step*.pt'") > side.index("--include '*.pt'")
+    assert "--exclude '*.tmp'" in side
 
 
 def test_manifest_cpu_no_queue_no_dataset_multinode():
