@@ -114,11 +114,13 @@ def test_slow_final_save_does_not_trip_the_watchdog(tmp_path, monkeypatch):
 
     monkeypatch.setattr(trmod.StepWatchdog, "from_env", staticmethod(make))
     tr = Trainer(TrainConfig(model="llama-tiny", method="lora", batch_size=1, seq_len=16, synthetic=True,
-                             max_steps=2, log_interval=1, checkpoint_path=str(tmp_path), device="cpu"))
+                             max_steps=1, log_interval=1, checkpoint_path=str(tmp_path), device="cpu"))
     orig = tr.save_artifacts
 
     def slow_save():
-        time.sleep(4.5)  # 3x the step timeout (steps themselves stay well inside 1.5 s, even under xdist load)
+        # 3x the step timeout.  One step: it runs under the first-step limit (30 s), so a CPU step slowed by
+        # xdist load cannot trip the 1.5 s limit before the save phase begins
+        time.sleep(4.5)
         return orig()
 
     tr.save_artifacts = slow_save
