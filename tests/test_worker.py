@@ -15,7 +15,7 @@ from finetune_controller_amd.models import LoRAConfig, build_model, get_config
 from finetune_controller_amd.models import checkpoint as ckpt
 from finetune_controller_amd.models.lora import merge_pair_into
 from finetune_controller_amd.ops import nf4
-from finetune_controller_amd.train.data import EvalWindows, PackedTokenDataset, load_token_array
+from finetune_controller_amd.train.data import EvalWindows, PackedTokenDataset, load_token_array, load_tokens_and_mask
 from finetune_controller_amd.utils.metrics import read_metrics_csv
 from finetune_controller_amd.train.optim import FlatAdamW, lr_at
 from finetune_controller_amd.train.trainer import TrainConfig, Trainer
@@ -318,7 +318,7 @@ def test_trainer_resume(tmp_path):
 def test_dataset_formats(tmp_path):
     (tmp_path / "a.jsonl").write_text('{"text": "hello world"}\n{"prompt": "q", "completion": "a"}\n')
     arr = load_token_array(str(tmp_path / "a.jsonl"), vocab=512)
-    assert arr.dtype == np.int64 and arr.max() < 512 and len(arr) > 10
+    assert arr.dtype == np.int32 and arr.max() < 512 and len(arr) > 10  # 4 bytes per token while resident
     toks = np.arange(1000, dtype=np.uint16) % 300
     toks.tofile(tmp_path / "t.bin")
     ds = PackedTokenDataset(str(tmp_path / "t.bin"), vocab=512, batch=2, seq_len=16, device="cpu", seed=0)
@@ -326,6 +326,45 @@ def test_dataset_formats(tmp_path):
     assert x.shape == (2, 16) and torch.equal(x[:, 1:], y[:, :-1])
     (tmp_path / "c.csv").write_text("Id,SMILES,esol\na,CCO,1.0\nb,CCC,2.0\n")
     assert len(load_token_array(str(tmp_path / "c.csv"), vocab=512)) > 4
+
+
+def test_text_dataset_edge_cases(tmp_path, monkeypatch):
+    """Exports with a byte-order mark, a pretty-printed JSON array, ragged CSV rows, null fields;
+    malformed records and a tokenizer larger than the model are refused, not trained on."""
+    from finetune_controller_amd.train import data as dmod
+
+    byte_ids = lambda t: [b + 3 for b in t.encode()] + [2]  # noqa: E731  (byte-level fallback + EOS)
+    d = tmp_path / "j"
+    d.mkdir()
+    (d / "a.json").write_bytes(b"\xef\xbb\xbf\n  [\n {\"text\": \"ab\"},\n \"cd\",\n {\"prompt\": null, \"completion\": \"e\"}\n]\n")
+    assert load_token_array(str(d / "a.json"), 512).tolist() == byte_ids("ab") + byte_ids("cd") + byte_ids("e")
+    (tmp_path / "r.csv").write_text("Id,SMILES\na,CCO\nshort\n\nb,CN\n")
+    assert load_token_array(str(tmp_path / "r.csv"), 512).tolist() == byte_ids("CCO") + byte_ids("CN")
+    (tmp_path / "bad.jsonl").write_text('{"text": "ok"}\n[1, 2]\n')
+    with pytest.raises(ValueError, match="record 1 is a list"):
+        load_token_array(str(tmp_path / "bad.jsonl"), 512)
+    # batching does not change the token stream (records straddle the batch boundaries)
+    rows = [{"prompt": "p%d" % i, "completion": "c" * (i % 7)} if i % 3 else {"text": "t%d" % i} for i in range(50)]
+    (tmp_path / "m.jsonl").write_text("\n".join(json.dumps(r) for r in rows))
+    whole, wmask = load_tokens_and_mask(str(tmp_path / "m.jsonl"), 512, completion_only=True)
+    monkeypatch.setattr(dmod, "TEXT_BATCH", 4)
+    parts, pmask = load_tokens_and_mask(str(tmp_path / "m.jsonl"), 512, completion_only=True)
+    assert whole.tolist() == parts.tolist() and wmask.tolist() == pmask.tolist()
+    # a tokenizer.json of a larger vocabulary than the model's is refused (ids used to be wrapped mod vocab)
+    from tokenizers import Tokenizer as HFTok
+    from tokenizers.models import WordLevel
+    from tokenizers.pre_tokenizers import Whitespace
+
+    vocab = {"[UNK]": 0, "</s>": 1, "hello": 2, "world": 600}
+    tk = HFTok(WordLevel(vocab, unk_token="[UNK]"))
+    tk.pre_tokenizer = Whitespace()
+    t = tmp_path / "t"
+    t.mkdir()
+    tk.save(str(t / "tokenizer.json"))
+    (t / "d.txt").write_text("hello world\nhello\n")
+    assert load_token_array(str(t), 1024).tolist() == [2, 600, 1, 2, 1]
+    with pytest.raises(ValueError, match="tokenizer ids reach 600"):
+        load_token_array(str(t), 512)
 
 
 @pytest.mark.parametrize("dtype,vocab,ext", [(np.uint16, 512, "bin"), (np.uint32, 100000, "bin"),
