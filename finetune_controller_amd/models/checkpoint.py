@@ -83,18 +83,30 @@ def load_adapter(model, path: str):
     sd = load_file(path) if path.endswith(".safetensors") else torch.load(path, map_location="cpu", weights_only=True)
     pat = re.compile(r"\.(?:layers|h)\.(\d+)\..*?\.(\w+_proj)\.lora_A\.weight$")
     layers = _layers(model)
-    n = 0
+    want = {(i, seg) for i, layer in enumerate(layers) for pair in layer.lora.values() for seg in pair.names}
+    done: set[tuple[int, str]] = set()
     for k, A in sd.items():
         m = pat.search(k)
         if not m:
             continue
         i, seg = int(m.group(1)), m.group(2)
-        B = sd[k.replace("lora_A", "lora_B")]
+        kb = k[: -len("lora_A.weight")] + "lora_B.weight"
+        if (i, seg) not in want:
+            # an adapter of another model (more layers) or with targets this model was not built with:
+            # refusing beats generating from a silently partial adapter
+            raise ValueError(f"{os.path.basename(path)}: {k} has no LoRA slot in this model "
+                             f"({len(layers)} layers; targets {sorted({s for _, s in want})})")
+        if kb not in sd:
+            raise ValueError(f"{os.path.basename(path)}: {k} has no {kb.rsplit('.', 3)[-3]}.lora_B partner")
         for pair in layers[i].lora.values():
             if seg in pair.names:
-                pair.load_segment(seg, A.to(pair.A.device, pair.A.dtype), B.to(pair.B.device, pair.B.dtype))
-                n += 1
-    return n
+                pair.load_segment(seg, A.to(pair.A.device, pair.A.dtype), sd[kb].to(pair.B.device, pair.B.dtype))
+                done.add((i, seg))
+    if done != want:
+        miss = sorted(want - done)
+        raise ValueError(f"{os.path.basename(path)}: {len(miss)} of {len(want)} LoRA segments missing "
+                         f"(e.g. layer {miss[0][0]} {miss[0][1]})")
+    return len(done)
 
 
 # ---------------- full model (HF naming) ----------------
@@ -248,8 +260,30 @@ def save_resume(path: str, step: int, opt, data_state: dict, extra: dict | None 
           "opt": {k: (v.detach().cpu() if torch.is_tensor(v) else v) for k, v in opt_state.items()},
           "data": data_state, "extra": extra or {}}
     tmp = path + ".tmp"
-    torch.save(st, tmp)
+    with open(tmp, "wb") as f:
+        torch.save(st, f)
+        # on disk before the rename: the trainer deletes the previous resume point right after, so a
+        # node crash must not leave the only checkpoint as a renamed file whose data never left the
+        # page cache (the restarted pod would fail to read it on every attempt)
+        f.flush()
+        os.fsync(f.fileno())
     os.replace(tmp, path)
+    fsync_dir(os.path.dirname(path) or ".")
+
+
+def fsync_dir(d: str):
+    """Make a rename in ``d`` durable (POSIX: the directory entry is only on disk after the directory's
+    own fsync).  Best-effort where a filesystem refuses directory fsync."""
+    try:
+        fd = os.open(d, os.O_RDONLY)
+    except OSError:
+        return
+    try:
+        os.fsync(fd)
+    except OSError:
+        pass
+    finally:
+        os.close(fd)
 
 
 def latest_resume(ckpt_dir: str) -> str | None:

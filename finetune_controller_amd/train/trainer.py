@@ -635,9 +635,11 @@ class Trainer:
         p = os.path.join(self.tc.checkpoint_path, f"checkpoint_step{self.step}.pt")
         ckpt.save_resume(p, self.step, self.opt, self.data().state(), {"config": asdict(self.tc)},
                          opt_state=opt_state)
-        # keep only the newest resume point
+        # keep only the newest resume point (and no half-written .tmp left by a save a crash interrupted:
+        # each is as large as a checkpoint)
         for old in os.listdir(self.tc.checkpoint_path):
-            if old.startswith("checkpoint_step") and old.endswith(".pt") and old != os.path.basename(p):
+            if (old.startswith("checkpoint_step") and old.endswith((".pt", ".pt.tmp"))
+                    and old != os.path.basename(p)):
                 os.remove(os.path.join(self.tc.checkpoint_path, old))
 
     def save_artifacts(self) -> list[str]:

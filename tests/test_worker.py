@@ -227,6 +227,17 @@ def test_adapter_export_peft_names_and_roundtrip(tmp_path):
     m2 = build_model(cfg, lc, dtype=torch.float32)
     n = ckpt.load_adapter(m2, str(tmp_path))
     assert n == 2 * 3
+    # an adapter that does not fit the model is refused, not loaded in part
+    m3 = build_model(cfg, LoRAConfig(r=4, alpha=8, target_modules=["q_proj", "v_proj"]), dtype=torch.float32)
+    with pytest.raises(ValueError, match="down_proj.lora_A.weight has no LoRA slot"):
+        ckpt.load_adapter(m3, str(tmp_path))
+    m4 = build_model(cfg, LoRAConfig(r=4, alpha=8, target_modules=["q_proj", "v_proj", "down_proj", "o_proj"]),
+                     dtype=torch.float32)
+    with pytest.raises(ValueError, match="LoRA segments missing"):
+        ckpt.load_adapter(m4, str(tmp_path))
+    part = {k: v for k, v in sd.items() if "layers.1.mlp.down_proj.lora_B" not in k}
+    with pytest.raises(ValueError, match="no down_proj.lora_B partner"):
+        ckpt.load_adapter(m2, ckpt.save_file(part, str(tmp_path / "p.safetensors")) or str(tmp_path / "p.safetensors"))
     for a, b in zip(m.layers, m2.layers):
         for name in a.lora:
             torch.testing.assert_close(a.lora[name].B.to(torch.bfloat16).float(), b.lora[name].B)
@@ -313,6 +324,25 @@ def test_trainer_resume(tmp_path):
     # step 4 again -- the file keeps one row per step
     steps = [int(r.split(",")[1]) for r in rows[1:]]
     assert steps == sorted(set(steps)) and 4 in steps
+
+
+def test_resume_save_is_durable_and_sweeps_stale_tmp(tmp_path, monkeypatch):
+    """The resume file reaches the disk before its rename (the previous resume point is deleted right
+    after), and a .tmp a crashed save left behind -- checkpoint-sized -- is removed by the next save."""
+    from finetune_controller_amd.models import checkpoint as ckmod
+
+    events = []
+    real_fsync, real_replace = os.fsync, os.replace
+    monkeypatch.setattr(ckmod.os, "fsync", lambda fd: (events.append("fsync"), real_fsync(fd))[1])
+    monkeypatch.setattr(ckmod.os, "replace", lambda a, b: (events.append("replace"), real_replace(a, b))[1])
+    (tmp_path / "checkpoint_step1.pt.tmp").write_bytes(b"\0" * 64)  # interrupted save of a previous attempt
+    tr = Trainer(TrainConfig(model="llama-tiny", method="lora", batch_size=2, seq_len=32, synthetic=True,
+                             checkpoint_path=str(tmp_path), device="cpu", save_every=2, max_steps=3,
+                             save_model=False))
+    tr.run()
+    tr.close()
+    assert sorted(f for f in os.listdir(tmp_path) if f.startswith("checkpoint_step")) == ["checkpoint_step2.pt"]
+    assert events[:3] == ["fsync", "replace", "fsync"]  # file data, rename, directory entry
 
 
 def test_dataset_formats(tmp_path):
