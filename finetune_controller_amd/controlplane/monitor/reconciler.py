@@ -165,7 +165,7 @@ class JobMonitor:
                 self.is_leader = await self.ctx.store.acquire_lock(LEASE, self.owner, self.lease_ttl)
                 get_metrics(self.ctx).is_leader.set(1 if self.is_leader else 0)
                 if self.is_leader:
-                    await self.reconcile_once()
+                    await self._reconcile_holding_lease()
             except asyncio.CancelledError:
                 raise
             except Exception as e:
@@ -174,6 +174,33 @@ class JobMonitor:
                 await asyncio.sleep(5)
                 continue
             await asyncio.sleep(self.interval)
+
+    async def _reconcile_holding_lease(self):
+        """One pass with the lease renewed every ttl / 3 while it runs: a pass slower than the lease
+        (many jobs, a slow API server) must not let a second monitor take over and act on the same jobs
+        concurrently (double deletes, promotions, status writes)."""
+        renew = asyncio.create_task(self._renew_lease())
+        try:
+            await self.reconcile_once()
+        finally:
+            renew.cancel()
+            try:
+                await renew
+            except asyncio.CancelledError:
+                pass
+
+    async def _renew_lease(self):
+        while True:
+            await asyncio.sleep(self.lease_ttl / 3)
+            try:
+                held = await self.ctx.store.acquire_lock(LEASE, self.owner, self.lease_ttl)
+            except Exception as e:  # noqa: BLE001 -- the loop's next acquire reports a lasting outage
+                logger.warning("monitor lease renewal failed: %s", e)
+                continue
+            if not held:
+                logger.error("monitor lease lost during a reconcile pass (renewal came too late)")
+                self.is_leader = False
+                return
 
     async def start(self):
         self.stop_monitoring = False

@@ -139,6 +139,33 @@ def test_monitor_retries_a_failed_delete_of_a_succeeded_job(env, monkeypatch):
     assert calls[:2] == [jid, jid] and ctx.kube.list_pytorchjobs(ctx.namespace) == []
 
 
+def test_monitor_keeps_its_lease_through_a_slow_pass(env):
+    """A reconcile pass longer than the lease TTL renews the lease as it runs: a second monitor cannot
+    take over mid-pass and act on the same jobs."""
+    from finetune_controller_amd.controlplane.monitor.reconciler import LEASE
+
+    ctx, _ = env
+    mon = JobMonitor(ctx, interval=0, lease_ttl=0.3)
+
+    async def slow_pass():
+        await asyncio.sleep(1.0)  # > 3 x the TTL
+        return 0
+
+    mon.reconcile_once = slow_pass
+
+    async def scenario():
+        assert await ctx.store.acquire_lock(LEASE, mon.owner, mon.lease_ttl)
+        passing = asyncio.create_task(mon._reconcile_holding_lease())
+        taken = []
+        for _ in range(8):
+            await asyncio.sleep(0.1)
+            taken.append(await ctx.store.acquire_lock(LEASE, "other-replica", 0.3))
+        await passing
+        return taken
+
+    assert not any(asyncio.run(scenario()))
+
+
 def test_monitor_fails_a_job_whose_pytorchjob_vanished(env):
     """A PyTorchJob deleted behind the controller's back (kubectl, a cluster reset) must not leave its
     job 'running' in the UI forever: after the grace period the monitor marks it failed."""
