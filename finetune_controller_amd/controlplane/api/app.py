@@ -463,6 +463,9 @@ def create_app(ctx: AppContext, run_monitor: bool | None = None, validator_facto
             raise HTTPException(status_code=404, detail=f"Job '{job_id}' not found")
         if info.promoted == PromotionStatus.IN_PROGRESS:
             raise HTTPException(status_code=202, detail="Job is being promoted already")
+        if info.promoted == PromotionStatus.DELETING:
+            # a copy started now would race the running delete of the same prefix
+            raise HTTPException(status_code=409, detail="Job is being unpromoted; promote it again when that is done")
         if TrainingJobStatus.is_running(info.status):
             raise HTTPException(status_code=200, detail="Cannot promote running job")
         if not info.atrifacts_uri or not bucket:
@@ -474,6 +477,9 @@ def create_app(ctx: AppContext, run_monitor: bool | None = None, validator_facto
         if not m or not m.promotion_path:
             raise HTTPException(status_code=400, detail="Model cannot be promoted")
         dest = "s3://" + "/".join([bucket, m.promotion_path.strip("/"), job_id])
+        busy = [PromotionStatus.IN_PROGRESS, PromotionStatus.DELETING, PromotionStatus.COMPLETED]
+        if not await ctx.store.claim_job_promotion(job_id, PromotionStatus.IN_PROGRESS, dest, unless=busy):
+            raise HTTPException(status_code=409, detail="Job promotion state changed concurrently")
         background_tasks.add_task(PromotionTask.promote_job_task, ctx, job_id, info.atrifacts_uri, dest)
         return {"status": "promotion_initiated", "job_id": job_id, "message": "Job promotion started in background"}
 
@@ -489,6 +495,9 @@ def create_app(ctx: AppContext, run_monitor: bool | None = None, validator_facto
             raise HTTPException(status_code=400, detail="Model not promoted. cannot unpromote")
         if not info.destination_uri:
             raise HTTPException(status_code=400, detail="Cannot unpromote model")
+        if not await ctx.store.claim_job_promotion(job_id, PromotionStatus.DELETING, info.destination_uri,
+                                                   when=[PromotionStatus.COMPLETED]):
+            raise HTTPException(status_code=400, detail="Model not promoted. cannot unpromote")
         background_tasks.add_task(PromotionTask.unpromote_job_task, ctx, job_id, info.destination_uri)
         return {"status": "unpromotion_initiated", "job_id": job_id, "message": "Job unpromotion started in background"}
 

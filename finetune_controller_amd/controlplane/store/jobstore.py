@@ -138,6 +138,17 @@ class JobStore:
             return await self.get_job(job_id)
         return None
 
+    async def claim_job_promotion(self, job_id: str, value: PromotionStatus, destination_uri: str | None,
+                                  *, when: list[PromotionStatus] | None = None,
+                                  unless: list[PromotionStatus] | None = None) -> bool:
+        """Set the promotion state only if the current one is in ``when`` / not in ``unless``, in one
+        conditional update: of two concurrent promote (or unpromote) requests exactly one wins."""
+        cur = {"$in": _enum_values(list(when))} if when is not None else {"$nin": _enum_values(list(unless or []))}
+        res = await self.jobs_collection.update_one(
+            {"job_id": job_id, "promoted": cur},
+            {"$set": {"promoted": _enum_values(value), "destination_uri": destination_uri}})
+        return res.matched_count > 0
+
     async def get_job(self, job_id: str) -> JobStatus | None:
         pipeline = [{"$match": {"job_id": job_id}}] + self._job_pipeline_add_fields() + [{"$unset": "_id"}]
         cur = await _maybe_await(self.jobs_collection.aggregate(pipeline))

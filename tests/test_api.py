@@ -279,6 +279,33 @@ def test_dataset_upload_reuse_url_and_delete(env, monkeypatch):
     assert jid3
 
 
+def test_promotion_state_changes_are_claimed_atomically(env):
+    """Promote and unpromote claim the promotion state with one conditional update before their
+    background copy / delete runs: a promote during an unpromotion (same prefix) is refused, and of two
+    racing claims only one wins."""
+    from finetune_controller_amd.controlplane.schemas.db import PromotionStatus as PS
+
+    ctx, c = env
+    jid = submit(c)
+    settle(ctx)
+
+    async def claims():
+        dest = "s3://ftc-deploy/x/" + jid
+        busy = [PS.IN_PROGRESS, PS.DELETING, PS.COMPLETED]
+        first = await ctx.store.claim_job_promotion(jid, PS.IN_PROGRESS, dest, unless=busy)
+        second = await ctx.store.claim_job_promotion(jid, PS.IN_PROGRESS, dest, unless=busy)
+        await ctx.store.update_job_promotion(jid, PS.COMPLETED, dest)
+        un1 = await ctx.store.claim_job_promotion(jid, PS.DELETING, dest, when=[PS.COMPLETED])
+        un2 = await ctx.store.claim_job_promotion(jid, PS.DELETING, dest, when=[PS.COMPLETED])
+        return first, second, un1, un2
+
+    assert asyncio.run(claims()) == (True, False, True, False)
+    # the job is now being unpromoted: a promote would copy into the prefix being deleted
+    r = c.post(f"/api/v1/jobs/{jid}/promote")
+    assert r.status_code == 409 and "unpromoted" in r.json()["detail"]
+    assert c.get(f"/api/v1/jobs/{jid}").json()["promoted"] == "deleting"
+
+
 def test_promote_unpromote_artifacts_delete(env):
     ctx, c = env
     jid = submit(c)
