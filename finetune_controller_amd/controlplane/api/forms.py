@@ -14,6 +14,7 @@ from urllib.parse import parse_qs
 from ..schemas.jobs import UploadedFile
 
 MAX_FIELD_BYTES = 1 << 20
+MAX_URLENCODED_BYTES = 8 * MAX_FIELD_BYTES
 UPLOAD_DIR = "/tmp/ftjobs"
 
 
@@ -67,8 +68,12 @@ async def parse_form(request) -> tuple[dict[str, str], dict[str, UploadedFile]]:
 async def _parse_form(request, spooled: list[str]) -> tuple[dict[str, str], dict[str, UploadedFile]]:
     ctype = request.headers.get("content-type", "")
     if ctype.startswith("application/x-www-form-urlencoded"):
-        body = await request.body()
-        q = parse_qs(body.decode("utf-8"), keep_blank_values=True)
+        body = bytearray()
+        async for chunk in request.stream():  # bounded: an urlencoded form carries no file
+            body += chunk
+            if len(body) > MAX_URLENCODED_BYTES:
+                raise FormError("form too large")
+        q = parse_qs(body.decode("utf-8", errors="replace"), keep_blank_values=True)
         return {k: v[-1] for k, v in q.items()}, {}
     if not ctype.startswith("multipart/form-data"):
         raise FormError("expected multipart/form-data or application/x-www-form-urlencoded")
@@ -162,6 +167,8 @@ async def _parse_form(request, spooled: list[str]) -> tuple[dict[str, str], dict
                         raise FormError("form field too large")
                 finish_part()
                 state = "after_delim"
-    if state not in ("after_delim", "preamble"):
-        finish_part()
+    if state in ("headers", "body"):
+        # the body ended inside a part (no closing delimiter): a cut-off upload must not become a
+        # dataset of whatever bytes arrived
+        raise FormError("multipart body ended inside a part (truncated upload?)")
     return fields, files

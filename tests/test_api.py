@@ -245,6 +245,19 @@ def test_rejected_submissions_leave_no_spooled_upload(env, monkeypatch, tmp_path
     r = c.post("/api/v1/jobs", content=body, headers={"content-type": f"multipart/form-data; boundary={b}"})
     assert r.status_code == 422 and "too large" in r.json()["detail"]
     assert list(spool.iterdir()) == []
+    monkeypatch.setattr(forms, "MAX_FIELD_BYTES", 1 << 20)
+    # a body cut off inside the file part (no closing delimiter) is not a dataset
+    fields = "".join(f'--{b}\r\nContent-Disposition: form-data; name="{k}"\r\n\r\n{v}\r\n' for k, v in FORM.items())
+    cut = (fields + f'--{b}\r\nContent-Disposition: form-data; name="dataset"; filename="t.jsonl"\r\n\r\n'
+           + '{"text": "hel').encode()
+    r = c.post("/api/v1/jobs", content=cut, headers={"content-type": f"multipart/form-data; boundary={b}"})
+    assert r.status_code == 422 and "truncated" in r.json()["detail"]
+    assert list(spool.iterdir()) == [] and not ctx.kube.list_pytorchjobs(ctx.namespace)
+    # an urlencoded form is bounded too (it cannot carry a file)
+    monkeypatch.setattr(forms, "MAX_URLENCODED_BYTES", 1024)
+    r = c.post("/api/v1/jobs", content=b"model_name=x&arguments=" + b"a" * 4096,
+               headers={"content-type": "application/x-www-form-urlencoded"})
+    assert r.status_code == 422 and "too large" in r.json()["detail"]
 
 
 def test_dataset_upload_reuse_url_and_delete(env, monkeypatch):
