@@ -287,7 +287,9 @@ def fsync_dir(d: str):
 
 
 def latest_resume(ckpt_dir: str) -> str | None:
-    c = glob.glob(os.path.join(ckpt_dir, "checkpoint_step*.pt"))
+    # only names this trainer writes (a stray checkpoint_step_best.pt must not break the restart)
+    c = [p for p in glob.glob(os.path.join(ckpt_dir, "checkpoint_step*.pt"))
+         if re.search(r"checkpoint_step(\d+)\.pt$", p)]
     if not c:
         return None
     return max(c, key=resume_step)

@@ -22,6 +22,7 @@ from __future__ import annotations
 import json
 import logging
 import os
+import re
 import time
 from dataclasses import asdict, dataclass, field
 
@@ -638,8 +639,7 @@ class Trainer:
         # keep only the newest resume point (and no half-written .tmp left by a save a crash interrupted:
         # each is as large as a checkpoint)
         for old in os.listdir(self.tc.checkpoint_path):
-            if (old.startswith("checkpoint_step") and old.endswith((".pt", ".pt.tmp"))
-                    and old != os.path.basename(p)):
+            if re.fullmatch(r"checkpoint_step\d+\.pt(\.tmp)?", old) and old != os.path.basename(p):
                 os.remove(os.path.join(self.tc.checkpoint_path, old))
 
     def save_artifacts(self) -> list[str]:

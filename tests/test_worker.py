@@ -343,6 +343,8 @@ def test_resume_save_is_durable_and_sweeps_stale_tmp(tmp_path, monkeypatch):
     tr.close()
     assert sorted(f for f in os.listdir(tmp_path) if f.startswith("checkpoint_step")) == ["checkpoint_step2.pt"]
     assert events[:3] == ["fsync", "replace", "fsync"]  # file data, rename, directory entry
+    (tmp_path / "checkpoint_step_best.pt").write_bytes(b"")  # a name the trainer never writes
+    assert ckpt.latest_resume(str(tmp_path)).endswith("checkpoint_step2.pt")
 
 
 def test_dataset_formats(tmp_path):
