@@ -56,16 +56,24 @@ def adapter_state_dict(model) -> dict[str, torch.Tensor]:
     return sd
 
 
+def _atomic(path: str, write):
+    """``write(tmp)`` then rename onto ``path``: the s3-sync sidecar, which runs while the worker saves,
+    never uploads a half-written weights file (its ``*.tmp`` exclude skips the temporary)."""
+    tmp = path + ".tmp"
+    write(tmp)
+    os.replace(tmp, path)
+
+
 def save_adapter(model, out_dir: str, base_model_name: str, lora: LoRAConfig, write_pt: bool = True) -> list[str]:
     os.makedirs(out_dir, exist_ok=True)
     sd = adapter_state_dict(model)
     files = []
     p = os.path.join(out_dir, "adapter_model.safetensors")
-    save_file(sd, p, metadata={"format": "pt"})
+    _atomic(p, lambda t: save_file(sd, t, metadata={"format": "pt"}))
     files.append(p)
     if write_pt:
         p = os.path.join(out_dir, "adapter_model.pt")
-        torch.save(sd, p)
+        _atomic(p, lambda t: torch.save(sd, t))
         files.append(p)
     p = os.path.join(out_dir, "adapter_config.json")
     with open(p, "w") as f:
@@ -185,7 +193,7 @@ def save_full(model, out_dir: str, shard_bytes: int = 5 * 1024**3, merge_lora: b
         files, weight_map = [], {}
         for i, sh in enumerate(shards):
             fn = f"model-{i + 1:05d}-of-{len(shards):05d}.safetensors"
-            save_file(sh, os.path.join(out_dir, fn), metadata={"format": "pt"})
+            _atomic(os.path.join(out_dir, fn), lambda t, sh=sh: save_file(sh, t, metadata={"format": "pt"}))
             files.append(os.path.join(out_dir, fn))
             for k in sh:
                 weight_map[k] = fn

@@ -217,6 +217,7 @@ def test_adapter_export_peft_names_and_roundtrip(tmp_path):
                 B_s.data.normal_()
     files = ckpt.save_adapter(m, str(tmp_path), "llama-tiny", lc)
     assert {os.path.basename(f) for f in files} == {"adapter_model.safetensors", "adapter_model.pt", "adapter_config.json"}
+    assert not [f for f in os.listdir(tmp_path) if f.endswith(".tmp")]  # written as .tmp, renamed into place
     sd = ckpt.adapter_state_dict(m)
     k = "base_model.model.model.layers.0.self_attn.q_proj.lora_A.weight"
     assert k in sd and sd[k].shape == (4, cfg.dim)
