@@ -19,9 +19,13 @@ Launch modes:
   code (terminating the rest).
 
 W untimed warmup steps, then K steps bracketed by barrier + device synchronize on both sides; the
-elapsed time is the MAX over ranks; rank 0 prints one JSON line.  After the timed region (never
-inside it) the ranks measure the all-reduce bus bandwidth of one DDP-sized bucket on the process
-group's transport, and report the world size the process group saw and the RCCL version.
+elapsed time is the MAX over ranks; rank 0 prints one JSON line on stdout and flushes it right after
+the timed region.  Only then (never inside it, never before the line) do the ranks measure the
+all-reduce bus bandwidth of one DDP-sized bucket, a bucket-size and an RCCL channel sweep -- on fresh
+process groups with a 60 s collective timeout, under a total budget (``--diag-budget``, 120 s) after
+which the sweep is abandoned and the process exits 0 -- and rank 0 writes them as one JSON object
+(``{"diagnostics": ...}``) on stderr.  The default group's timeout is lowered to 300 s
+(``--collective-timeout``) so a hang inside the timed steps fails the run before a driver's limit.
 """
 from __future__ import annotations
 
@@ -32,6 +36,7 @@ import sys
 import time
 
 BASELINE_METRIC = "fine-tune tokens/sec (whole node), Llama-3-8B LoRA at 1/2/4/8 MI355X"
+DIAG_TIMEOUT_S = 60  # collective timeout of every post-headline diagnostic process group
 
 
 def _mark(op: str):
@@ -167,6 +172,12 @@ def _parse(argv):
     ap.add_argument("--profile-steps", type=int, default=0, help="extra steps under torch.profiler (not timed)")
     ap.add_argument("--launcher-timeout", type=float, default=0.0,
                     help="launcher mode: give up after this many seconds (0: never)")
+    ap.add_argument("--diag-budget", type=float, default=120.0,
+                    help="N > 1: seconds for the post-headline transport diagnostics (bucket / size / channel "
+                         "sweeps) before they are abandoned and the rank exits 0; 0 skips them")
+    ap.add_argument("--collective-timeout", type=float, default=300.0,
+                    help="process-group collective timeout (s): a hang inside the timed steps aborts the ranks "
+                         "(non-zero exit) well before a driver's limit; FTC_COLLECTIVE_TIMEOUT_S overrides")
     return ap.parse_args(argv)
 
 
@@ -203,7 +214,7 @@ def _channel_sweep(info, mb: float, counts=(2, 4, 8, 16)) -> dict:
             opts = dist.ProcessGroupNCCL.Options()
             opts.config.min_ctas = c
             opts.config.max_ctas = c
-            g = dist.new_group(backend="nccl", pg_options=opts, timeout=datetime.timedelta(seconds=120))
+            g = dist.new_group(backend="nccl", pg_options=opts, timeout=datetime.timedelta(seconds=DIAG_TIMEOUT_S))
             out[str(c)] = _bucket_busbw(info, mb, iters=5, group=g)["busbw_GBps"]
             dist.destroy_process_group(g)
         except Exception as e:  # noqa: BLE001 -- a diagnostic
@@ -236,7 +247,12 @@ def _bucket_busbw(info, mb: float, native=None, iters: int = 10, group=None) -> 
         native.reset()
     if cuda:
         torch.cuda.synchronize(info.device)
-    pdist.barrier(info)
+    if group is None:
+        pdist.barrier(info)
+    else:  # a diagnostic group: its own (short) timeout, not the default group's
+        dist.all_reduce(torch.zeros(1, device=info.device), group=group)
+        if cuda:
+            torch.cuda.synchronize(info.device)
     t0 = time.perf_counter()
     for _ in range(iters):
         run()
@@ -248,6 +264,57 @@ def _bucket_busbw(info, mb: float, native=None, iters: int = 10, group=None) -> 
     sec = max(sec, 1e-9)
     return {"bucket_mb": mb, "ms": round(sec * 1e3, 3),
             "busbw_GBps": round(numel * 2 / sec / 1e9 * 2 * (n - 1) / n, 1)}
+
+
+def _run_diagnostics(a, info, tr, dev, cuda: bool, budget_s: float) -> dict:
+    """Post-headline transport diagnostics in a daemon thread, joined for at most ``budget_s``.
+
+    Every collective runs on a fresh process group whose timeout is ``DIAG_TIMEOUT_S``.  Returns the
+    results; ``abandoned`` is set when the budget ran out (the caller then exits 0 without joining).
+    Fault hook for the tests: ``FTC_BENCH_DIAG_STALL_RANK=<r>`` parks rank r inside the sweep."""
+    import datetime
+    import threading
+
+    import torch
+    import torch.distributed as dist
+
+    res: dict = {"budget_s": budget_s, "group_timeout_s": DIAG_TIMEOUT_S}
+    done = threading.Event()
+    t0 = time.monotonic()
+
+    def work():
+        try:
+            if cuda:
+                torch.cuda.set_device(dev)  # the current device is per thread
+            g = dist.new_group(backend=info.backend, timeout=datetime.timedelta(seconds=DIAG_TIMEOUT_S))
+            stall = os.environ.get("FTC_BENCH_DIAG_STALL_RANK")
+            if stall not in (None, "") and int(stall) == info.rank:
+                time.sleep(10 ** 6)
+            res["torch"] = _bucket_busbw(info, a.bucket_mb, group=g)
+            if cuda:  # bucket-size sweep: xGMI data for tuning bucket_mb
+                res["sweep_busbw_GBps"] = {str(mb): _bucket_busbw(info, mb, iters=5, group=g)["busbw_GBps"]
+                                           for mb in (4, 16, 64, 256)}
+                res["channel_sweep_busbw_GBps"] = _channel_sweep(info, a.bucket_mb)
+            if cuda and (a.comm_ab or a.comm_engine == "native"):
+                try:
+                    native = tr.ddp._native
+                    if native is None:
+                        from finetune_controller_amd.parallel.comm import NativeComm
+
+                        native = NativeComm(device=dev)
+                    res["native"] = _bucket_busbw(info, a.bucket_mb, native=native, group=g)
+                except Exception as e:  # noqa: BLE001 -- a diagnostic
+                    res["native"] = {"error": f"{type(e).__name__}: {e}"[:200]}
+        except Exception as e:  # noqa: BLE001 -- report, never fail the run on a diagnostic
+            res["error"] = f"{type(e).__name__}: {e}"[:300]
+        finally:
+            done.set()
+
+    threading.Thread(target=work, name="ftc-bench-diag", daemon=True).start()
+    if not done.wait(budget_s):
+        res["abandoned"] = True
+    res["elapsed_s"] = round(time.monotonic() - t0, 2)
+    return res
 
 
 def main(argv=None) -> int:
@@ -277,6 +344,11 @@ def main(argv=None) -> int:
 
         rccl_log = os.path.join(tempfile.gettempdir(), f"ftc_rccl_{os.getpid()}.log")
         os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT", NCCL_DEBUG_FILE=rccl_log)
+
+    # the default process group's collective timeout (read by parallel.dist.init_distributed): a hang in
+    # the timed steps ends the ranks with a non-zero code long before a driver's limit (torch: 1800 s)
+    os.environ.setdefault("FTC_COLLECTIVE_TIMEOUT_S", str(int(a.collective_timeout)))
+    pg_timeout_s = int(float(os.environ["FTC_COLLECTIVE_TIMEOUT_S"]))
 
     import torch
     import torch.distributed as dist
@@ -339,25 +411,7 @@ def main(argv=None) -> int:
     ms = elapsed / a.steps * 1000
     flops_tok = tr.cfg.flops_per_token(a.seq_len, lora=a.method != "full")
 
-    # ---- after the timed region: transport diagnostics (never part of the metric)
-    comm = {}
-    channels = _rccl_channels(rccl_log) if info.is_main else None  # before the sweep adds communicators
-    if n > 1:
-        comm["torch"] = _bucket_busbw(info, a.bucket_mb)
-        if cuda:  # bucket-size sweep on the same process group: xGMI data for tuning bucket_mb
-            comm["sweep_busbw_GBps"] = {str(mb): _bucket_busbw(info, mb, iters=5)["busbw_GBps"]
-                                        for mb in (4, 16, 64, 256)}
-            comm["channel_sweep_busbw_GBps"] = _channel_sweep(info, a.bucket_mb)
-        if cuda and (a.comm_ab or a.comm_engine == "native"):
-            try:
-                native = tr.ddp._native
-                if native is None:
-                    from finetune_controller_amd.parallel.comm import NativeComm
-
-                    native = NativeComm(device=dev)
-                comm["native"] = _bucket_busbw(info, a.bucket_mb, native=native)
-            except Exception as e:  # report, never fail the headline on the diagnostic
-                comm["native"] = {"error": f"{type(e).__name__}: {e}"[:200]}
+    channels = _rccl_channels(rccl_log) if info.is_main else None  # before any diagnostic communicator
     rccl = None
     if cuda:
         try:
@@ -375,19 +429,8 @@ def main(argv=None) -> int:
         except Exception:
             p2p = None
 
-    if a.profile_steps:
-        from torch.profiler import ProfilerActivity, profile
-
-        acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if cuda else [])
-        with profile(activities=acts) as prof:
-            for _ in range(a.profile_steps):
-                tr.train_step(tc.lr)
-            sync()
-        if info.is_main:
-            os.makedirs("gpurun_out", exist_ok=True)
-            with open("gpurun_out/torch_profile.txt", "w") as f:
-                f.write(prof.key_averages().table(sort_by="cuda_time_total" if cuda else "cpu_time_total",
-                                                  row_limit=60))
+    # ---- the headline line FIRST: printed and flushed before any post-timed collective, so a diagnostic
+    # that stalls on a first real xGMI node can never cost the record
     if info.is_main:
         from finetune_controller_amd.ops import _backend
 
@@ -431,7 +474,6 @@ def main(argv=None) -> int:
             "rccl_channels": channels,
             "p2p_peers": p2p,
             "rank_ms_per_step": {"max": round(ms, 2), "min": round(fastest / a.steps * 1000, 2)},
-            **({"allreduce_bucket": comm} if comm else {}),
             "comm": {
                 "comm_exposed_ms": None if exposed is None else round(exposed, 3),
                 "param_sync_exposed_ms": None if psync is None else round(psync, 3),
@@ -440,6 +482,7 @@ def main(argv=None) -> int:
                 "n_buckets": tr.ddp.n_collectives(),
                 "bucket_mb": a.bucket_mb,
                 "grad_wire": str(tr.ddp.wire_dtype or tr.opt.grad_flat.dtype).replace("torch.", ""),
+                "collective_timeout_s": pg_timeout_s,
                 "env": {k: v for k, v in sorted(os.environ.items())
                         if k.startswith(("NCCL_", "RCCL_")) or k in ("HSA_ENABLE_IPC_MODE_LEGACY", "FTC_SHARE_GPU")},
             },
@@ -448,6 +491,36 @@ def main(argv=None) -> int:
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1) if cuda else None,
         }
         print(json.dumps(out), flush=True)
+    sys.stderr.flush()
+
+    # ---- after the headline: transport diagnostics (never part of the metric), on their own process
+    # groups with a short collective timeout, in a worker thread under a total budget.  Past the budget
+    # the sweep is abandoned and the rank exits 0 at once (the headline is already out); a stalled RCCL
+    # kernel of an abandoned sweep dies with the process.
+    if n > 1 and a.diag_budget > 0:
+        diag = _run_diagnostics(a, info, tr, dev, cuda, budget_s=a.diag_budget)
+        if info.is_main:
+            print(json.dumps({"diagnostics": diag}), file=sys.stderr, flush=True)
+        if diag.get("abandoned"):
+            sys.stdout.flush()
+            sys.stderr.flush()
+            if rccl_log and os.path.exists(rccl_log):
+                os.remove(rccl_log)
+            os._exit(0)
+
+    if a.profile_steps:
+        from torch.profiler import ProfilerActivity, profile
+
+        acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if cuda else [])
+        with profile(activities=acts) as prof:
+            for _ in range(a.profile_steps):
+                tr.train_step(tc.lr)
+            sync()
+        if info.is_main:
+            os.makedirs("gpurun_out", exist_ok=True)
+            with open("gpurun_out/torch_profile.txt", "w") as f:
+                f.write(prof.key_averages().table(sort_by="cuda_time_total" if cuda else "cpu_time_total",
+                                                  row_limit=60))
     tr.close()
     if rccl_log and os.path.exists(rccl_log):  # this rank's RCCL INIT log: parsed above, not kept
         os.remove(rccl_log)

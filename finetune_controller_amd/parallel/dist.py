@@ -106,10 +106,21 @@ def local_device_index(local: int, count: int, share: bool = False) -> int:
     one card), ``LOCAL_RANK mod count`` for a shared-card rehearsal."""
     if share:
         return local % count
-    if count == 1:
+    if count == 1 and _narrowed_to_one_device():
         return 0
     check_local_rank(local, count)
     return local
+
+
+def _narrowed_to_one_device() -> bool:
+    """True when this rank's single visible device is its own: the launcher narrowed the visible set
+    (``HIP_VISIBLE_DEVICES`` / ``ROCR_VISIBLE_DEVICES`` / ``CUDA_VISIBLE_DEVICES``), or the node runs one
+    rank (``LOCAL_WORLD_SIZE`` 1).  ``torchrun --nproc-per-node 2`` on a one-GPU host is neither, and gets
+    the clear ``LOCAL_RANK`` error before the rendezvous instead of RCCL's 'Duplicate GPU' after it."""
+    if any(os.environ.get(k, "").strip() for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
+                                                    "CUDA_VISIBLE_DEVICES")):
+        return True
+    return int(os.environ.get("LOCAL_WORLD_SIZE", "1") or "1") == 1
 
 
 def check_local_rank(local: int, count: int) -> None:

@@ -85,7 +85,10 @@ def test_bench_self_launches_ranks_on_cpu(tmp_path):
     assert out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 4
     assert out["value"] > 0 and out["steps"] == 2 and out["warmup"] == 1
     assert out["rank_ms_per_step"]["max"] >= out["rank_ms_per_step"]["min"] > 0
-    assert out["allreduce_bucket"]["torch"]["busbw_GBps"] > 0
+    assert out["comm"]["collective_timeout_s"] == 300
+    # the transport diagnostics come after the headline, as one JSON object on stderr
+    diag = [json.loads(ln)["diagnostics"] for ln in r.stderr.splitlines() if ln.startswith('{"diagnostics"')]
+    assert len(diag) == 1 and diag[0]["torch"]["busbw_GBps"] > 0 and not diag[0].get("abandoned")
     assert out["comm"]["n_buckets"] >= 1 and out["comm"]["wire_GB_per_step"] > 0
     assert out["comm"]["comm_exposed_ms"] is None  # device events: GPU runs only
 
@@ -108,6 +111,35 @@ def test_bench_eight_ranks_on_cpu(tmp_path):
     assert out["n_gpus"] == 8 and out["world_size_pg"] == 8
     assert out["config"]["parallelism"] == "dp8" and out["config"]["global_batch"] == 8
     assert out["config"]["zero_stage"] == 0  # LoRA: plain bucketed all-reduce
+
+
+@pytest.mark.slow
+def test_bench_headline_survives_a_stalled_diagnostic(tmp_path):
+    """VERDICT r5 Next #3: rank 3 parks inside the post-headline sweep (fault hook).  The headline line is
+    still on stdout, every rank abandons the sweep at the diagnostic budget and exits 0, and the whole run
+    ends within the budget instead of a collective timeout."""
+    import time as _time
+
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", FTC_BENCH_DIAG_STALL_RANK="3")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "FTC_INIT_METHOD",
+              "FTC_COLLECTIVE_TIMEOUT_S"):
+        env.pop(k, None)
+    t0 = _time.monotonic()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1", "--warmup", "1",
+                        "--device", "cpu", "--model", "llama-tiny", "--batch-size", "1", "--seq-len", "16",
+                        "--launcher-timeout", "400", "--diag-budget", "15"],
+                       capture_output=True, text=True, timeout=480, env=env, cwd=str(tmp_path))
+    wall = _time.monotonic() - t0
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8 and out["value"] > 0
+    diag = [json.loads(ln)["diagnostics"] for ln in r.stderr.splitlines() if ln.startswith('{"diagnostics"')]
+    assert len(diag) == 1 and diag[0]["abandoned"] is True and "torch" not in diag[0]
+    assert 15 <= diag[0]["elapsed_s"] < 40
+    # the stall costs the budget, not the 60 s group timeout or the 300 s default-group timeout
+    assert wall < 300, wall
 
 
 @pytest.mark.slow
@@ -210,8 +242,11 @@ def test_device_key_on_the_gpu():
     assert key.startswith("pci:"), key  # this image's torch reports the PCI location
 
 
-def test_distinct_device_binding_checks():
+def test_distinct_device_binding_checks(monkeypatch):
     from finetune_controller_amd.parallel import dist as pdist
+
+    for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "LOCAL_WORLD_SIZE"):
+        monkeypatch.delenv(k, raising=False)
 
     pdist.check_distinct_devices([("h0", "g0", 0), ("h0", "g1", 1), ("h1", "g0", 2)])  # per host: distinct
     with pytest.raises(RuntimeError, match="ranks 0 and 2"):
@@ -220,7 +255,15 @@ def test_distinct_device_binding_checks():
     with pytest.raises(RuntimeError, match="LOCAL_RANK 8"):
         pdist.check_local_rank(8, 8)
     assert pdist.local_device_index(5, 8) == 5
-    assert pdist.local_device_index(5, 1) == 0  # launcher gave each rank one visible device
+    # one visible device: rank 5 binds it only when the launcher narrowed the visible set to it ...
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    with pytest.raises(RuntimeError, match="LOCAL_RANK 5"):  # torchrun x8 on a 1-GPU host: fail early
+        pdist.local_device_index(5, 1)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "5")
+    assert pdist.local_device_index(5, 1) == 0
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")  # ... or the node runs one rank
+    assert pdist.local_device_index(0, 1) == 0
     assert pdist.local_device_index(5, 2, share=True) == 1
     with pytest.raises(RuntimeError, match="LOCAL_RANK 4"):
         pdist.local_device_index(4, 4)
