@@ -44,6 +44,10 @@ def _ts(s):
     return _dt.datetime.fromisoformat(str(s).replace("Z", "+00:00"))
 
 
+class LeaseLost(RuntimeError):
+    """The monitor no longer knows that it holds the lease: the pass stops before its next write."""
+
+
 class JobMonitor:
     def __init__(self, ctx: AppContext, interval: float | None = None, lease_ttl: float | None = None):
         self.ctx = ctx
@@ -55,6 +59,16 @@ class JobMonitor:
         self.is_leader = False
         self.orphan_grace_s = max(60.0, 10 * self.interval)
         self._missing: dict[str, _dt.datetime] = {}  # job id -> first pass that did not list it
+        self._leased_pass = False  # inside _reconcile_holding_lease: every write checks the lease first
+        self._lease_until = 0.0    # monotonic time the last successful acquire / renewal is good until
+
+    def _check_lease(self) -> None:
+        """Before every mutating action of a leased pass: the lease must be held AND not past the expiry
+        of the last successful acquire / renewal (a renewal that keeps failing lets it lapse silently --
+        another monitor may own it by then).  Direct ``reconcile_once`` calls (tests, one-shot tools)
+        hold no lease and are not checked."""
+        if self._leased_pass and (not self.is_leader or time.monotonic() >= self._lease_until):
+            raise LeaseLost("monitor lease lost or expired during a reconcile pass")
 
     # ---------------------------------------------------------------- one reconcile pass
     async def reconcile_once(self) -> int:
@@ -86,10 +100,12 @@ class JobMonitor:
             if TrainingJobStatus.is_stopped(prev.status) and prev.status == mapped:
                 if status == KubeflowStatusEnum.succeeded.value:
                     # already reconciled, yet still listed: an earlier pass's delete failed -- retry it
+                    self._check_lease()
                     await self.delete_job(job_id)
                 continue  # already reconciled
             if prev.status != mapped:
                 logger.info("job %s status %s -> %s", job_id, prev.status.value, mapped.value)
+            self._check_lease()
             info = await ctx.store.update_job_status(job_id, mapped, metadata={
                 "last_transition_time": _ts(cond.get("lastTransitionTime")),
                 "last_update_time": _ts(cond.get("lastUpdateTime")),
@@ -103,9 +119,11 @@ class JobMonitor:
             if info is None:
                 continue
             done = TrainingJobStatus.is_stopped(mapped)
+            self._check_lease()
             await self._process_metrics(job_id, info, st, done)
             if status == KubeflowStatusEnum.succeeded.value:
                 logger.info("job %s completed successfully, cleaning up", job_id)
+                self._check_lease()
                 await self.delete_job(job_id)
             elif status == KubeflowStatusEnum.failed.value:
                 logger.error("job %s failed: %s", job_id, cond.get("message"))
@@ -130,6 +148,7 @@ class JobMonitor:
                     (now - created).total_seconds() < self.orphan_grace_s:
                 continue
             logger.error("job %s: its PyTorchJob is gone from the cluster; marking it failed", rec.job_id)
+            self._check_lease()
             await self.ctx.store.update_job_status(rec.job_id, DatabaseStatusEnum.failed, metadata={
                 "message": "PyTorchJob no longer exists on the cluster", "reason": "PyTorchJobMissing",
                 "completion_time": now})
@@ -162,7 +181,10 @@ class JobMonitor:
         logger.info("starting job monitoring in namespace %s as %s", self.ctx.namespace, self.owner)
         while not self.stop_monitoring:
             try:
+                t_ask = time.monotonic()
                 self.is_leader = await self.ctx.store.acquire_lock(LEASE, self.owner, self.lease_ttl)
+                if self.is_leader:
+                    self._lease_until = t_ask + self.lease_ttl
                 get_metrics(self.ctx).is_leader.set(1 if self.is_leader else 0)
                 if self.is_leader:
                     await self._reconcile_holding_lease()
@@ -178,11 +200,20 @@ class JobMonitor:
     async def _reconcile_holding_lease(self):
         """One pass with the lease renewed every ttl / 3 while it runs: a pass slower than the lease
         (many jobs, a slow API server) must not let a second monitor take over and act on the same jobs
-        concurrently (double deletes, promotions, status writes)."""
+        concurrently (double deletes, promotions, status writes).  If the lease is lost or lapses anyway
+        (renewals failing or too late), the pass stops before its next write (``_check_lease``)."""
+        if self._lease_until <= time.monotonic():  # entered without the loop's acquire (tests): count from now
+            self._lease_until = time.monotonic() + self.lease_ttl
+        self.is_leader = True
         renew = asyncio.create_task(self._renew_lease())
+        self._leased_pass = True
         try:
             await self.reconcile_once()
+        except LeaseLost as e:
+            get_metrics(self.ctx).reconcile_errors.inc()
+            logger.error("%s: pass abandoned, no further writes", e)
         finally:
+            self._leased_pass = False
             renew.cancel()
             try:
                 await renew
@@ -192,12 +223,15 @@ class JobMonitor:
     async def _renew_lease(self):
         while True:
             await asyncio.sleep(self.lease_ttl / 3)
+            t_ask = time.monotonic()
             try:
                 held = await self.ctx.store.acquire_lock(LEASE, self.owner, self.lease_ttl)
-            except Exception as e:  # noqa: BLE001 -- the loop's next acquire reports a lasting outage
+            except Exception as e:  # noqa: BLE001 -- the lease then lapses at _lease_until
                 logger.warning("monitor lease renewal failed: %s", e)
                 continue
-            if not held:
+            if held:
+                self._lease_until = t_ask + self.lease_ttl
+            else:
                 logger.error("monitor lease lost during a reconcile pass (renewal came too late)")
                 self.is_leader = False
                 return

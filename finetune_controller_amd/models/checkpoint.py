@@ -83,15 +83,30 @@ def save_adapter(model, out_dir: str, base_model_name: str, lora: LoRAConfig, wr
 
 
 @torch.no_grad()
-def load_adapter(model, path: str):
-    """Load PEFT-named adapter tensors (safetensors or weights-only .pt) into the model's pairs."""
+def load_adapter(model, path: str, layers_to_transform=None):
+    """Load PEFT-named adapter tensors (safetensors or weights-only .pt) into the model's pairs.
+
+    What the adapter must hold is derived from the ADAPTER, not from the model: its own segment names on
+    the layers ``layers_to_transform`` names (argument, else ``adapter_config.json``'s, else the layers
+    its keys cover).  A key with no LoRA slot in this model, or a lora_A without its lora_B, is refused; an
+    expected (layer, segment) the file lacks (a truncated file) is refused; the model's slots the adapter
+    does not train (other layers of a ``layers_to_transform`` adapter, other projections) get B = 0."""
+    cfg_file = None
     if os.path.isdir(path):
+        cfg_file = os.path.join(path, "adapter_config.json")
         st = os.path.join(path, "adapter_model.safetensors")
         path = st if os.path.exists(st) else os.path.join(path, "adapter_model.pt")
+    else:
+        cfg_file = os.path.join(os.path.dirname(path), "adapter_config.json")
+    if layers_to_transform is None and cfg_file and os.path.exists(cfg_file):
+        with open(cfg_file) as f:
+            layers_to_transform = json.load(f).get("layers_to_transform")
+    if isinstance(layers_to_transform, int):
+        layers_to_transform = [layers_to_transform]
     sd = load_file(path) if path.endswith(".safetensors") else torch.load(path, map_location="cpu", weights_only=True)
     pat = re.compile(r"\.(?:layers|h)\.(\d+)\..*?\.(\w+_proj)\.lora_A\.weight$")
     layers = _layers(model)
-    want = {(i, seg) for i, layer in enumerate(layers) for pair in layer.lora.values() for seg in pair.names}
+    slots = {(i, seg) for i, layer in enumerate(layers) for pair in layer.lora.values() for seg in pair.names}
     done: set[tuple[int, str]] = set()
     for k, A in sd.items():
         m = pat.search(k)
@@ -99,21 +114,30 @@ def load_adapter(model, path: str):
             continue
         i, seg = int(m.group(1)), m.group(2)
         kb = k[: -len("lora_A.weight")] + "lora_B.weight"
-        if (i, seg) not in want:
+        if (i, seg) not in slots:
             # an adapter of another model (more layers) or with targets this model was not built with:
             # refusing beats generating from a silently partial adapter
             raise ValueError(f"{os.path.basename(path)}: {k} has no LoRA slot in this model "
-                             f"({len(layers)} layers; targets {sorted({s for _, s in want})})")
+                             f"({len(layers)} layers; targets {sorted({s for _, s in slots})})")
         if kb not in sd:
             raise ValueError(f"{os.path.basename(path)}: {k} has no {kb.rsplit('.', 3)[-3]}.lora_B partner")
         for pair in layers[i].lora.values():
             if seg in pair.names:
                 pair.load_segment(seg, A.to(pair.A.device, pair.A.dtype), sd[kb].to(pair.B.device, pair.B.dtype))
                 done.add((i, seg))
-    if done != want:
-        miss = sorted(want - done)
-        raise ValueError(f"{os.path.basename(path)}: {len(miss)} of {len(want)} LoRA segments missing "
+    if not done:
+        raise ValueError(f"{os.path.basename(path)}: no LoRA tensors found")
+    segs = {seg for _, seg in done}
+    on = set(layers_to_transform) if layers_to_transform is not None else {i for i, _ in done}
+    expected = {(i, seg) for i in on for seg in segs}
+    if expected - done:
+        miss = sorted(expected - done)
+        raise ValueError(f"{os.path.basename(path)}: {len(miss)} of {len(expected)} LoRA segments missing "
                          f"(e.g. layer {miss[0][0]} {miss[0][1]})")
+    for i, seg in sorted(slots - done):  # slots this adapter does not train: no contribution
+        for pair in layers[i].lora.values():
+            if seg in pair.names:
+                pair.zero_segment(seg)
     return len(done)
 
 

@@ -113,6 +113,16 @@ class LoRAPair(nn.Module):
         self.A[i * self.r:(i + 1) * self.r].copy_(A_s)
         self.B[row:row + B_s.shape[0], i * self.r:(i + 1) * self.r].copy_(B_s)
 
+    def zero_segment(self, name: str):
+        """Segment ``name`` contributes nothing (B = 0; A kept): a slot an adapter does not train."""
+        i = self.names.index(name)
+        row = 0
+        for n, rows in self.segments:
+            if n == name:
+                self.B[row:row + rows, i * self.r:(i + 1) * self.r].zero_()
+                return
+            row += rows
+
 
 def make_pairs(layer_shapes: dict[str, tuple[int, list[tuple[str, int]]]], cfg: LoRAConfig, device=None,
                dtype=torch.bfloat16) -> nn.ModuleDict:

@@ -179,10 +179,17 @@ class GradBucketer:
             self._all_reduce(self.opt.grad_flat[o:o + n])
         for w in self.works:
             w.wait()
-        for red, dst, _ in self.unstage:  # bf16 wire: the reduced sums back into the fp32 buffer
+        for red, dst, inp in self.unstage:  # bf16 wire: the reduced sums back into the fp32 buffer
             dst.copy_(red)
-            if red.is_cuda:  # staged on the launch (maybe side) stream, read here: keep the block until this copy ran
-                red.record_stream(torch.cuda.current_stream(red.device))
+            if red.is_cuda:
+                # both staging blocks were allocated on the launch (maybe side) stream and used by the
+                # collective on the comm stream (the native engine records nothing on its own stream).
+                # The current stream has waited for that collective, so recording them here keeps each
+                # block out of the side stream's pool until the collective's reads and this copy ran.
+                cur = torch.cuda.current_stream(red.device)
+                red.record_stream(cur)
+                if inp is not None:
+                    inp.record_stream(cur)
         if self._native is not None:
             self._native.reset()
         self.reset()

@@ -166,6 +166,52 @@ def test_monitor_keeps_its_lease_through_a_slow_pass(env):
     assert not any(asyncio.run(scenario()))
 
 
+@pytest.mark.parametrize("renewal", ["raises", "lost"])
+def test_monitor_stops_writing_once_its_lease_lapses(env, monkeypatch, renewal):
+    """a pass whose lease renewals fail (the lease lapses at the last good renewal's expiry) or
+    whose renewal finds the lease taken makes no further status writes or deletes in that pass."""
+    import time as _time
+
+    from finetune_controller_amd.controlplane.monitor.reconciler import LEASE
+
+    ctx, c = env
+    jid = submit(c)
+    ctx.kube.reconcile()
+    real_list = ctx.kube.list_pytorchjobs
+
+    def slow_list(ns):
+        _time.sleep(0.8)  # > the 0.3 s TTL: the lease is gone when the pass reaches its first write
+        return real_list(ns)
+
+    monkeypatch.setattr(ctx.kube, "list_pytorchjobs", slow_list)
+    mon = JobMonitor(ctx, interval=0, lease_ttl=0.3)
+    real_acquire = ctx.store.acquire_lock
+
+    async def acquire(name, owner, ttl):
+        if owner == mon.owner and renewal == "raises":
+            raise RuntimeError("mongo unreachable")
+        if owner == mon.owner:  # "lost": another replica holds it now
+            return False
+        return await real_acquire(name, owner, ttl)
+
+    writes = []
+    real_update = ctx.store.update_job_status
+
+    async def update(*a, **k):
+        writes.append(a[0])
+        return await real_update(*a, **k)
+
+    async def scenario():
+        assert await real_acquire(LEASE, mon.owner, mon.lease_ttl)
+        monkeypatch.setattr(ctx.store, "acquire_lock", acquire)
+        monkeypatch.setattr(ctx.store, "update_job_status", update)
+        await mon._reconcile_holding_lease()
+
+    asyncio.run(scenario())
+    assert writes == [], writes
+    assert c.get(f"/api/v1/jobs/{jid}").json()["status"] == "queued"
+
+
 def test_monitor_fails_a_job_whose_pytorchjob_vanished(env):
     """A PyTorchJob deleted behind the controller's back (kubectl, a cluster reset) must not leave its
     job 'running' in the UI forever: after the grace period the monitor marks it failed."""

@@ -5,6 +5,7 @@ These are the CPU rehearsals of what the driver's 8-GPU run exercises with RCCL:
 rendezvous, bucketed reductions and the rank-0 JSON contract are identical; only the transport
 differs."""
 import json
+import math
 import os
 import socket
 import subprocess
@@ -652,6 +653,35 @@ def test_zero1_rccl_update_matches_ddp(tmp_path):
     print(f"zero1 vs ddp: {moved:.3f} of sampled weights moved, max |diff| {diff:.3g}")
     assert moved > 0.5
     torch.testing.assert_close(z[0]["after"], d[0]["after"], atol=1e-6, rtol=0)
+
+
+def _zero_wire_worker(rank, world, port, tmp, q, engine):
+    os.environ["FTC_SHARE_GPU"] = "1"
+    _rank_env(rank, world, port, tmp)
+    from finetune_controller_amd.ops import linear as L
+
+    L.set_wgrad_stream(True)  # dW on the side stream: the bf16 staging is allocated there
+    tr = Trainer(TrainConfig(method="full", checkpoint_path=tmp, comm_engine=engine, grad_wire="bf16",
+                             **{**_DDP_GPU, "max_steps": 3, "lr": 1e-3, "max_grad_norm": 1.0, "zero_stage": 1}))
+    losses = [float(tr.train_step(1e-3)) for _ in range(3)]
+    tr._join_update()
+    torch.cuda.synchronize()
+    q.put((rank, {"losses": losses, "digest": _grad_digest(tr)[0]}))
+    tr.close()
+    _hold(tmp, port)
+
+
+@pytest.mark.gpu
+def test_zero1_bf16_wire_native_engine_side_stream(tmp_path):
+    """ZeRO-1 with the bf16 wire on the native RCCL engine, weight gradients on the side stream
+    (the staging buffers are allocated there and read on the engine's stream), three steps so freed
+    staging blocks get reused: the same losses and gradients as torch.distributed's path."""
+    nat = _run_ranks(_zero_wire_worker, 2, tmp_path, "native", timeout=120)
+    tor = _run_ranks(_zero_wire_worker, 2, tmp_path, "torch", timeout=120)
+    for r in (0, 1):
+        assert all(math.isfinite(x) for x in nat[r]["losses"])
+        assert nat[r]["losses"] == pytest.approx(tor[r]["losses"], rel=1e-5, abs=1e-5)
+        torch.testing.assert_close(nat[r]["digest"], tor[r]["digest"], atol=1e-6, rtol=1e-3)
 
 
 def test_rccl_channel_parse_reads_ring_lines_only(tmp_path):

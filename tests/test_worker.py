@@ -234,8 +234,30 @@ def test_adapter_export_peft_names_and_roundtrip(tmp_path):
         ckpt.load_adapter(m3, str(tmp_path))
     m4 = build_model(cfg, LoRAConfig(r=4, alpha=8, target_modules=["q_proj", "v_proj", "down_proj", "o_proj"]),
                      dtype=torch.float32)
+    for layer in m4.layers:  # stale values in the slot the adapter does not train
+        layer.lora["o_proj"].B.data.fill_(1.0) if "o_proj" in layer.lora else None
+    assert ckpt.load_adapter(m4, str(tmp_path)) == 2 * 3  # a model with MORE slots: the extra one is zeroed
+    assert all(float(layer.lora[n].B.abs().sum()) == 0 for layer in m4.layers for n in layer.lora
+               if "o_proj" in layer.lora[n].names)
+    # a truncated file (layer 1 lost its q_proj pair while keeping v / down) is refused
+    trunc = {k: v for k, v in sd.items() if "layers.1.self_attn.q_proj" not in k}
     with pytest.raises(ValueError, match="LoRA segments missing"):
-        ckpt.load_adapter(m4, str(tmp_path))
+        ckpt.load_adapter(m2, ckpt.save_file(trunc, str(tmp_path / "t.safetensors")) or str(tmp_path / "t.safetensors"))
+    # a partial-layer PEFT adapter (layers_to_transform = [0]) loads; layer 1 contributes nothing
+    only0 = {k: v for k, v in sd.items() if ".layers.0." in k}
+    os.makedirs(tmp_path / "l0")
+    ckpt.save_file(only0, str(tmp_path / "l0" / "adapter_model.safetensors"))
+    json.dump({**conf, "layers_to_transform": [0]}, open(tmp_path / "l0" / "adapter_config.json", "w"))
+    m5 = build_model(cfg, lc, dtype=torch.float32)
+    for layer in m5.layers:
+        for p in layer.lora.values():
+            for _, _, B_s in p.segment_tensors():
+                B_s.data.fill_(1.0)
+    assert ckpt.load_adapter(m5, str(tmp_path / "l0")) == 3
+    assert all(float(B_s.abs().sum()) == 0 for p in m5.layers[1].lora.values() for _, _, B_s in p.segment_tensors())
+    assert all(float(B_s.abs().sum()) > 0 for p in m5.layers[0].lora.values() for _, _, B_s in p.segment_tensors())
+    with pytest.raises(ValueError, match="LoRA segments missing"):  # it claims layer 1 but does not carry it
+        ckpt.load_adapter(m5, str(tmp_path / "l0"), layers_to_transform=[0, 1])
     part = {k: v for k, v in sd.items() if "layers.1.mlp.down_proj.lora_B" not in k}
     with pytest.raises(ValueError, match="no down_proj.lora_B partner"):
         ckpt.load_adapter(m2, ckpt.save_file(part, str(tmp_path / "p.safetensors")) or str(tmp_path / "p.safetensors"))
