@@ -46,6 +46,8 @@ class AppContext:
             kube: KubeClient = FakeCluster()
         else:
             kube = HttpKubeClient()
+        if not settings.NAMESPACE:  # the kubeconfig context's / in-cluster service account's namespace
+            settings.NAMESPACE = getattr(kube, "namespace", None) or "default"
         settings.load_aws_credentials(kube)
         objects = make_object_store(settings.OBJECT_STORE, settings)
         if settings.KUBE_BACKEND == "fake":  # the fake cluster's pods sync artifacts into the object store

@@ -53,8 +53,8 @@ class Settings(BaseModel):
     ENVIRONMENT: Literal["local", "staging", "production"] = "local"
     API_V1_STR: str = "/api/v1"
     LOG_STREAM_SEARCH_STRING: str | None = "Epoch"
-    # cluster
-    NAMESPACE: str
+    # cluster ("": the kube client's namespace -- the kubeconfig context's, or the service account's)
+    NAMESPACE: str = ""
     # CORS
     FRONTEND_URL_CORS: list[str] = Field(default_factory=list)
     # security
