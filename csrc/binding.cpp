@@ -33,21 +33,7 @@ int ftc_swiglu_bwd_wgrad(const void* da, long long da_rs, const void* gu, void* 
 int ftc_tail_gemm(void* x, long long ldx, long long rows, int K, const void* Bm, long long ldb, int nct, int Rp,
                   hipStream_t stream);
 int ftc_transpose(const void* x, long long ldx, void* y, long long ldy, int R, int C, hipStream_t stream);
-int ftc_gemm_tn_ok(const void* a, long long lda, const void* b, long long ldb, const void* c, long long ldc, int M, int N,
-                   int K);
-int ftc_gemm_tn(const void* a, long long lda, const void* b, long long ldb, void* c, long long ldc, int c_fp32, int M,
-                int N, int K, float alpha, float beta, hipStream_t stream);
-int ftc_gemm_nt_ok(const void* a, long long lda, const void* b, long long ldb, const void* c, long long ldc, int c_fp32,
-                   int M, int N, int K);
-int ftc_gemm_nt(const void* a, long long lda, const void* b, long long ldb, void* c, long long ldc, int c_fp32, int M,
-                int N, int K, float alpha, float beta, hipStream_t stream);
-void ftc_gemm_nt_config(int grid_cap, int group, int xcc);
-int ftc_gemm_nt_rope(const void* a, long long lda, const void* b, long long ldb, void* c, long long ldc, int M, int N,
-                     int K, const float* cos_t, const float* sin_t, const int* positions, int seq_len, int rot_heads,
-                     hipStream_t stream);
 int ftc_copy2d_batched(const void* jobs, int njobs, long long max_elems, hipStream_t stream);
-int ftc_gemm_tn_split(const void* a, long long lda, const void* b, long long ldb, float* parts, int M, int N, int K,
-                      int splits, hipStream_t stream);
 int ftc_splitk_sum(const float* parts, int nsplit, long long pstride, void* c, int c_fp32, long long rows, int cols,
                    long long ldc, float beta, hipStream_t stream);
 int ftc_ce_fwd_bwd(void* logits, const long long* labels, float* loss, float* lse, long long rows, int V, long long ld,
@@ -381,40 +367,6 @@ at::Tensor transpose2d(const at::Tensor& x, const c10::optional<at::Tensor>& out
   return y;
 }
 
-// ---------------- weight-gradient GEMM: c = beta c + alpha a^T b ----------------
-// a [K, M], b [K, N] bf16 row views (unit column stride); c [M, N] bf16 or fp32 row view.
-bool gemm_tn_ok(const at::Tensor& c, const at::Tensor& a, const at::Tensor& b) {
-  if (!a.is_cuda() || !b.is_cuda() || !c.is_cuda() || a.dim() != 2 || b.dim() != 2 || c.dim() != 2) return false;
-  if (a.scalar_type() != at::kBFloat16 || b.scalar_type() != at::kBFloat16) return false;
-  if (c.scalar_type() != at::kBFloat16 && c.scalar_type() != at::kFloat) return false;
-  if (a.stride(1) != 1 || b.stride(1) != 1 || c.stride(1) != 1) return false;
-  if (a.size(0) != b.size(0) || c.size(0) != a.size(1) || c.size(1) != b.size(1)) return false;
-  if (a.size(0) > INT32_MAX || a.size(1) > INT32_MAX || b.size(1) > INT32_MAX) return false;
-  return ftc_gemm_tn_ok(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
-                        (int)a.size(1), (int)b.size(1), (int)a.size(0)) != 0;
-}
-
-void gemm_tn_(at::Tensor& c, const at::Tensor& a, const at::Tensor& b, double alpha, double beta) {
-  TORCH_CHECK(gemm_tn_ok(c, a, b), "gemm_tn_: shapes / layouts outside the kernel contract (M, N % 256, K % 64, "
-              "bf16 row views a [K, M], b [K, N], c [M, N] bf16/fp32)");
-  check(ftc_gemm_tn(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
-                    c.scalar_type() == at::kFloat, (int)a.size(1), (int)b.size(1), (int)a.size(0), (float)alpha,
-                    (float)beta, cur_stream()),
-        "gemm_tn_");
-}
-
-// parts [S, M, N] fp32 contiguous = the S token slices of a^T b (a [K, M], b [K, N] bf16 row views)
-void gemm_tn_split_(at::Tensor& parts, const at::Tensor& a, const at::Tensor& b) {
-  TORCH_CHECK(parts.is_cuda() && parts.dim() == 3 && parts.is_contiguous() && parts.scalar_type() == at::kFloat &&
-                  a.dim() == 2 && b.dim() == 2 && parts.size(1) == a.size(1) && parts.size(2) == b.size(1) &&
-                  a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && a.stride(1) == 1 &&
-                  b.stride(1) == 1 && a.size(0) == b.size(0),
-              "gemm_tn_split_: parts [S, M, N] fp32, a [K, M], b [K, N] bf16 row views");
-  check(ftc_gemm_tn_split(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), parts.data_ptr<float>(),
-                          (int)a.size(1), (int)b.size(1), (int)a.size(0), (int)parts.size(0), cur_stream()),
-        "gemm_tn_split_ (shape outside the kernel contract: M, N % 256, K % (64 S))");
-}
-
 // ---------------- split-K partials: c = beta c + sum_s parts[s] ----------------
 // parts [S, M, N] fp32 contiguous; c [M, N] bf16 or fp32 row view (unit column stride)
 void splitk_sum_(at::Tensor& c, const at::Tensor& parts, double beta) {
@@ -428,57 +380,6 @@ void splitk_sum_(at::Tensor& c, const at::Tensor& parts, double beta) {
         "splitk_sum_");
 }
 
-// ---------------- projection GEMM: c = alpha a b^T + beta c ----------------
-// a [M, K], b [N, K] bf16 row views (unit column stride, K contiguous); c [M, N] bf16 or fp32 row view.
-bool gemm_nt_ok(const at::Tensor& c, const at::Tensor& a, const at::Tensor& b) {
-  if (!a.is_cuda() || !b.is_cuda() || !c.is_cuda() || a.dim() != 2 || b.dim() != 2 || c.dim() != 2) return false;
-  if (a.device() != b.device() || a.device() != c.device()) return false;
-  if (a.scalar_type() != at::kBFloat16 || b.scalar_type() != at::kBFloat16) return false;
-  if (c.scalar_type() != at::kBFloat16 && c.scalar_type() != at::kFloat) return false;
-  if (a.stride(1) != 1 || b.stride(1) != 1 || c.stride(1) != 1) return false;
-  if (a.size(1) != b.size(1) || c.size(0) != a.size(0) || c.size(1) != b.size(0)) return false;
-  if (a.size(0) > INT32_MAX || a.size(1) > INT32_MAX || b.size(0) > INT32_MAX) return false;
-  return ftc_gemm_nt_ok(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
-                        c.scalar_type() == at::kFloat, (int)a.size(0), (int)b.size(0), (int)a.size(1)) != 0;
-}
-
-void gemm_nt_(at::Tensor& c, const at::Tensor& a, const at::Tensor& b, double alpha, double beta) {
-  TORCH_CHECK(gemm_nt_ok(c, a, b), "gemm_nt_: shapes / layouts outside the kernel contract (M, N % 256, K % 32, "
-              "bf16 row views a [M, K], b [N, K], c [M, N] bf16/fp32, 16-byte aligned)");
-  check(ftc_gemm_nt(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
-                    c.scalar_type() == at::kFloat, (int)a.size(0), (int)b.size(0), (int)a.size(1), (float)alpha,
-                    (float)beta, cur_stream()),
-        "gemm_nt_");
-}
-
-// qkv projection + RoPE epilogue (head_dim 128): c = rope(a b^T) on the first rot_heads heads
-void gemm_nt_rope_(at::Tensor& c, const at::Tensor& a, const at::Tensor& b, const at::Tensor& cos_t,
-                   const at::Tensor& sin_t, const c10::optional<at::Tensor>& positions, int64_t seq_len,
-                   int64_t rot_heads) {
-  TORCH_CHECK(c.scalar_type() == at::kBFloat16 && gemm_nt_ok(c, a, b), "gemm_nt_rope_: GEMM contract (bf16 c)");
-  need(cos_t, at::kFloat, "cos");
-  need(sin_t, at::kFloat, "sin");
-  TORCH_CHECK(cos_t.dim() == 2 && cos_t.size(1) == 64 && cos_t.is_contiguous() && sin_t.sizes() == cos_t.sizes() &&
-              sin_t.is_contiguous(), "gemm_nt_rope_: cos/sin [max_pos, 64] fp32 contiguous (head_dim 128)");
-  const int* pp = nullptr;
-  if (positions.has_value()) {
-    need(*positions, at::kInt, "positions");
-    TORCH_CHECK(positions->numel() == a.size(0) && positions->is_contiguous(), "gemm_nt_rope_: positions [M]");
-    pp = positions->data_ptr<int>();
-  } else {
-    TORCH_CHECK(seq_len > 0 && seq_len <= cos_t.size(0), "gemm_nt_rope_: seq_len within the table");
-  }
-  check(ftc_gemm_nt_rope(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(), c.stride(0),
-                         (int)a.size(0), (int)b.size(0), (int)a.size(1), cos_t.data_ptr<float>(),
-                         sin_t.data_ptr<float>(), pp, (int)seq_len, (int)rot_heads, cur_stream()),
-        "gemm_nt_rope_");
-}
-
-// launch configuration of the projection GEMM (persistent grid cap, tile order, store policy); the
-// defaults are the measured best (profiles/r4/gemm_nt.md) -- tools/bench_gemm_nt.py sweeps it
-void gemm_nt_config(int64_t grid_cap, int64_t group, int64_t xcc) {
-  ftc_gemm_nt_config((int)grid_cap, (int)group, (int)xcc);
-}
 
 // ---------------- cross entropy (in place on logits) ----------------
 at::Tensor ce_fwd_bwd_(at::Tensor& logits, const at::Tensor& labels, double gscale, int64_t ignore_index) {
@@ -850,15 +751,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("tail_gemm_ok", &tail_gemm_ok);
   m.def("tail_gemm_", &tail_gemm_);
   m.def("transpose2d", &transpose2d, py::arg("x"), py::arg("out") = py::none());
-  m.def("gemm_tn_ok", &gemm_tn_ok);
-  m.def("gemm_tn_", &gemm_tn_);
   m.def("splitk_sum_", &splitk_sum_);
-  m.def("gemm_tn_split_", &gemm_tn_split_);
-  m.def("gemm_nt_ok", &gemm_nt_ok);
-  m.def("gemm_nt_rope_", &gemm_nt_rope_, py::arg("c"), py::arg("a"), py::arg("b"), py::arg("cos"), py::arg("sin"),
-        py::arg("positions"), py::arg("seq_len"), py::arg("rot_heads"));
-  m.def("gemm_nt_config", &gemm_nt_config, py::arg("grid_cap"), py::arg("group"), py::arg("xcc"));
-  m.def("gemm_nt_", &gemm_nt_, py::arg("c"), py::arg("a"), py::arg("b"), py::arg("alpha") = 1.0, py::arg("beta") = 0.0);
   m.def("ce_fwd_bwd_", &ce_fwd_bwd_);
   m.def("adamw_", &adamw_, py::arg("param"), py::arg("master"), py::arg("m"), py::arg("v"), py::arg("grad"),
         py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("step"),

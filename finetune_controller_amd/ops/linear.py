@@ -40,7 +40,6 @@ import weakref
 import torch
 
 from ._backend import ext, use_hip
-from .gemm import mm_nt, rope_nt
 
 _GRAD_READY_HOOK = None  # set by parallel.ddp to learn when a main_grad was written
 
@@ -346,22 +345,6 @@ def transpose2d(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tenso
     return x.t().contiguous()
 
 
-def own_wgrad(mg: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> bool:
-    """Whether ``mg += dy2^T x2`` runs on the hand-written gfx950 TN GEMM (csrc/kernels/gemm_tn.hip)
-    instead of hipBLASLt on a transposed copy of x.  ``FTC_GEMM_TN``: ``0`` (default) -- never;
-    ``auto`` -- only for wide activations (in-features >= 8192: the down projection's [T, 14336]
-    input, whose transposed copy alone costs 0.2 ms); ``1`` -- whenever the shape fits the kernel.
-    Measured (profiles/r2/gemm_tn.md): the kernel beats hipBLASLt on these "TT" operands as stored
-    (down 1.76 vs 1.94 ms) but not the library on a transposed x, and the full-FT step A/B gave
-    auto -0.5 % -- so the library path stays the default."""
-    mode = os.environ.get("FTC_GEMM_TN", "0")
-    if mode == "0" or not use_hip(x2):
-        return False
-    if mode == "auto" and x2.shape[1] < 8192:
-        return False
-    return bool(ext().gemm_tn_ok(mg, dy2, x2))
-
-
 def transposed_weight(W: torch.Tensor) -> torch.Tensor | None:
     """W^T for the TN backward GEMM dx = dy W (None when the TN path is off or not on the HIP backend)."""
     if not (_TN_BWD and use_hip(W) and W.dim() == 2):
@@ -433,20 +416,6 @@ def _dw_parts(device, s: int, M: int, N: int) -> torch.Tensor:
     stream it was taken on after the fold (no per-stream buffer pinned for the life of the process;
     ``utils.memplan`` counts one per dW stream in the full-FT peak)."""
     return torch.empty((s, M, N), dtype=torch.float32, device=device)
-
-
-def wgrad_tn(out: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor, beta: float = 1.0) -> torch.Tensor:
-    """``out = beta * out + dy2^T x2`` on the hand-written TN kernel (operands as stored), split along
-    the tokens like ``wgrad_mm`` when ``dw_splits`` says so (``gemm_tn_split_`` + ``splitk_sum_``)."""
-    M, N, K = dy2.shape[1], x2.shape[1], dy2.shape[0]
-    s = dw_splits(M, N, K)
-    if s == 1:
-        ext().gemm_tn_(out, dy2, x2, 1.0, float(beta))
-        return out
-    parts = _dw_parts(dy2.device, s, M, N)
-    ext().gemm_tn_split_(parts, dy2, x2)
-    ext().splitk_sum_(out, parts, float(beta))
-    return out
 
 
 # ---- first-write weight gradients (full fine-tuning).  Zeroing the 16 GB gradient buffer of Llama-3-8B
@@ -782,10 +751,7 @@ class _LoRALinearFn(torch.autograd.Function):
             if not take_prefilled("fwd", x2, aug):
                 tail_product(x2, K, Rp, aug.big[N:, :K], aug.nct)
             xa = _tail(x2, K, aug.R)  # = s * x A^T
-            if rope is not None and rope_nt(_wide(x2, K + Rp), aug.big[:N], y, rope):
-                rope = None  # RoPE applied in the GEMM epilogue (csrc/kernels/gemm_nt.hip EPI_ROPE)
-            elif not mm_nt(_wide(x2, K + Rp), aug.big[:N], y):
-                torch.mm(_wide(x2, K + Rp), aug.big[:N].t(), out=y)
+            torch.mm(_wide(x2, K + Rp), aug.big[:N].t(), out=y)  # hipBLASLt (K5 base GEMM: docs/kernels.md)
         else:
             if bias is None:
                 torch.mm(x2, W.t(), out=y)
@@ -840,7 +806,7 @@ class _LoRALinearFn(torch.autograd.Function):
         side_dw = False
         if need_w and _DW_STREAM and use_hip(x2) and not torch.cuda.is_current_stream_capturing():
             mg = getattr(W, "main_grad", None)
-            if mg is not None and not own_wgrad(mg, dy2, x2):
+            if mg is not None:
                 # issued before the input-gradient GEMM so that the two run concurrently
                 _wgrad_on_side(mg, dy2, x2, _TN_DW, take_fresh(W, mg))
                 side_dw = True
@@ -853,9 +819,7 @@ class _LoRALinearFn(torch.autograd.Function):
             dyb = _tail(dy2, N, aug.R)
             rhs = aug.bwd_operand() if _TN_BWD else aug.big[:, :aug.K]
             dx = torch.empty(dy2.shape[0], aug.K, dtype=dy2.dtype, device=dy2.device)
-            # rhs^T = bigT [K, N+Rp] row-major: the hand-written NT kernel's K-contiguous B operand
-            if not (_TN_BWD and mm_nt(_wide(dy2, N + Rp), rhs.t(), dx)):
-                torch.mm(_wide(dy2, N + Rp), rhs, out=dx)
+            torch.mm(_wide(dy2, N + Rp), rhs, out=dx)
             dx = dx.view(ctx.shp)
         else:
             if A is not None and (need_x or need_a):
@@ -874,8 +838,6 @@ class _LoRALinearFn(torch.autograd.Function):
             if mg is not None:
                 if side_dw:
                     pass  # issued above, on the side stream
-                elif own_wgrad(mg, dy2, x2):
-                    wgrad_tn(mg, dy2, x2, take_fresh(W, mg))  # both operands as stored, no copies
                 elif _TN_DW and use_hip(x2):
                     # hipBLASLt runs dW += dy^T x 14-24 % faster with x handed over transposed (K-major
                     # reduction operand, tools/bench_dw_gemm.py); the transpose streams at HBM rate

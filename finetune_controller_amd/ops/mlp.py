@@ -29,7 +29,6 @@ import torch
 
 from ._backend import ext, use_hip
 from . import linear as _L
-from .gemm import mm as gemm_mm
 from .linear import _accum_xty, _grad_ready, _spare_cols, _tail, _wide, tail_product, tn_backward
 
 _OFF = False  # True: the unfused composition (A/B by patching; profiles/r1_bench_fused_mlp*.log)
@@ -139,12 +138,12 @@ class _LoRAMLPFn(torch.autograd.Function):
         F, d = dn_p.K, dn_p.N
         # 1. gate|up projection, LoRA folded in through x's spare columns
         tail_product(x2, K, gu_p.Rp, gu_p.fwd_tail(), gu_p.nct)
-        gu = gemm_mm(_wide(x2, K + gu_p.Rp), gu_p.fwd_weight().t())
+        gu = torch.mm(_wide(x2, K + gu_p.Rp), gu_p.fwd_weight().t())
         # 2. SwiGLU + s h A_down^T into h's spare columns
         h = ext().swiglu_fwd_lora(gu, dn_p.Rp, dn_p.fwd_tail(), dn_p.nct)
         # 3. down projection
         y = torch.empty(*x.shape[:-1], d, dtype=x.dtype, device=x.device)
-        gemm_mm(_wide(h, F + dn_p.Rp), dn_p.fwd_weight().t(), out=y.view(T, d))
+        torch.mm(_wide(h, F + dn_p.Rp), dn_p.fwd_weight().t(), out=y.view(T, d))
         ctx.save_for_backward(x2, gu, h)
         ctx.params = (A_gu, B_gu, A_dn, B_dn)
         ctx.proj, ctx.shp = (gu_p, dn_p), x.shape
@@ -168,7 +167,7 @@ class _LoRAMLPFn(torch.autograd.Function):
         dyb_dn = _tail(dy2, d, dn_p.R)
         # 5. dB_down += dy^T (s h A_down^T)
         hta = _tail(h, F, dn_p.R)
-        dh = gemm_mm(_wide(dy2, d + dn_p.Rp), dn_p.bwd_weight())
+        dh = torch.mm(_wide(dy2, d + dn_p.Rp), dn_p.bwd_weight())
         _accum_xty(B_dn.main_grad, dy2, hta, 1.0)
         _grad_ready(B_dn)
         # 6. SwiGLU backward + dgu B_gu + dB_gu + dA_down
@@ -180,7 +179,7 @@ class _LoRAMLPFn(torch.autograd.Function):
         dgt = _tail(dgu, N, gu_p.R)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = gemm_mm(_wide(dgu, N + gu_p.Rp), gu_p.bwd_weight()).view(ctx.shp)
+            dx = torch.mm(_wide(dgu, N + gu_p.Rp), gu_p.bwd_weight()).view(ctx.shp)
         _accum_xty(A_gu.main_grad.t(), x2, dgt, gu_p.s)
         _grad_ready(A_gu)
         return dx, None, None, None, None, None, None

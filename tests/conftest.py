@@ -11,6 +11,7 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU and the built HIP extension")
     config.addinivalue_line("markers", "slow: long-running CPU test")
+    config.addinivalue_line("markers", "lab: lab-only kernel (tools/gemm_lab), runs with FTC_LAB=1")
 
 
 def _gpu_available() -> bool:

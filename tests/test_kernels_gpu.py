@@ -237,33 +237,6 @@ def test_grad_sumsq_paths(C, gdtype, n, offset):
 
 
 @pytest.mark.parametrize("cdtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("M,N,K,lda_pad,beta", [(256, 256, 64, 0, 0.0), (512, 768, 1024, 0, 1.0),
-                                                (768, 256, 4096, 64, 1.0), (2048, 1024, 192, 0, 0.5)])
-def test_gemm_tn(C, cdtype, M, N, K, lda_pad, beta):
-    """Weight-gradient GEMM c = beta c + alpha a^T b (a [K, M], b [K, N] as stored) vs an fp32 reference;
-    lda_pad: a is a column view of a wider buffer (the LoRA-padded activation rows)."""
-    torch.manual_seed(2)
-    abuf = (torch.rand(K, M + lda_pad, device=DEV) * 2 - 1).to(torch.bfloat16)
-    a = abuf[:, :M]
-    b = (torch.rand(K, N, device=DEV) * 2 - 1).to(torch.bfloat16)
-    c = torch.randn(M, N, device=DEV).to(cdtype)
-    ref = beta * c.float() + 0.5 * (a.float().t() @ b.float())
-    assert C.gemm_tn_ok(c, a, b)
-    C.gemm_tn_(c, a, b, 0.5, beta)
-    tol = 2e-2 * (K ** 0.5) / 8 if cdtype == torch.bfloat16 else 1e-3 * (K ** 0.5) / 8
-    torch.testing.assert_close(c.float(), ref, atol=tol, rtol=1e-2 if cdtype == torch.bfloat16 else 1e-4)
-
-
-def test_gemm_tn_rejects(C):
-    a = torch.zeros(64, 200, device=DEV, dtype=torch.bfloat16)  # M not a multiple of 256
-    b = torch.zeros(64, 256, device=DEV, dtype=torch.bfloat16)
-    c = torch.zeros(200, 256, device=DEV, dtype=torch.bfloat16)
-    assert not C.gemm_tn_ok(c, a, b)
-    with pytest.raises(RuntimeError):
-        C.gemm_tn_(c, a, b, 1.0, 0.0)
-
-
-@pytest.mark.parametrize("cdtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("splits", ["2", "4", "auto"])
 @pytest.mark.parametrize("beta", [0.0, 1.0])
 def test_wgrad_split(C, cdtype, splits, beta):
@@ -282,120 +255,14 @@ def test_wgrad_split(C, cdtype, splits, beta):
         assert L.dw_splits(M, N, T, splits) == (2 if splits == "auto" else int(splits))
         L._DW_SPLIT = splits
         tol = 2e-2 * (T ** 0.5) / 8 if cdtype == torch.bfloat16 else 1e-3 * (T ** 0.5) / 8
-        for b in (x, L.transpose2d(x).t(), None):
+        for b in (x, L.transpose2d(x).t()):
             c = torch.randn(M, N, device=DEV).to(cdtype)
             ref = beta * c.float() + dy.float().t() @ x.float()
-            if b is None:  # the hand-written TN kernel's split mode (operands as stored)
-                L.wgrad_tn(c, dy, x, beta)
-            else:
-                L.wgrad_mm(c, dy.t(), b, beta)
+            L.wgrad_mm(c, dy.t(), b, beta)
             torch.testing.assert_close(c.float(), ref, atol=tol, rtol=1e-2 if cdtype == torch.bfloat16 else 1e-4)
     finally:
         L._WAVE = old
         L._DW_SPLIT = old_split  # (later tests keep the default "auto" split-K coverage)
-
-
-@pytest.mark.parametrize("cdtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("M,N,K,pad,beta", [(256, 256, 64, 0, 0.0), (512, 768, 4160, 64, 0.0), (768, 512, 128, 8, 1.0),
-                                            (256, 1024, 1088, 0, -0.5), (512, 256, 192, 0, 0.0)])
-def test_gemm_nt(C, cdtype, M, N, K, pad, beta):
-    """Projection GEMM c = alpha a b^T + beta c (a [M, K], b [N, K] K-contiguous, a a column view of a wider
-    row buffer when pad > 0) vs an fp32 reference; asymmetric integer-valued operands first (exact
-    in fp32: any fragment / output permutation error shows as a wrong integer), then random data."""
-    torch.manual_seed(3)
-    abuf = torch.randint(-3, 4, (M, K + pad), device=DEV).to(torch.bfloat16)
-    a = abuf[:, :K]
-    b = (torch.arange(N * K, device=DEV).reshape(N, K) % 7 - 3).to(torch.bfloat16)
-    c = torch.zeros(M, N, device=DEV, dtype=cdtype)
-    assert C.gemm_nt_ok(c, a, b)
-    C.gemm_nt_(c, a, b, 1.0, 0.0)
-    exact = a.double() @ b.double().t()  # integer sums < 2^24: exact in the fp32 accumulator, one rounding
-    assert torch.equal(c, exact.to(cdtype))
-    abuf = (torch.rand(M, K + pad, device=DEV) * 2 - 1).to(torch.bfloat16)
-    a = abuf[:, :K]
-    b = (torch.rand(N, K, device=DEV) * 2 - 1).to(torch.bfloat16)
-    c = torch.randn(M, N, device=DEV).to(cdtype)
-    ref = beta * c.float() + 0.5 * (a.float() @ b.float().t())
-    C.gemm_nt_(c, a, b, 0.5, beta)
-    tol = 2e-2 * (K ** 0.5) / 8 if cdtype == torch.bfloat16 else 1e-3 * (K ** 0.5) / 8
-    torch.testing.assert_close(c.float(), ref, atol=tol, rtol=1e-2 if cdtype == torch.bfloat16 else 1e-4)
-
-
-@pytest.fixture
-def nt_config(C):
-    """Restores the projection GEMM's default launch configuration after a test that changes it."""
-    yield C
-    C.gemm_nt_config(0, -8, 32)
-
-
-@pytest.mark.parametrize("cfg", [(1, 1, 1), (3, 4, 1), (8, -2, 1), (16, 2, 2), (5, -16, 1), (4, -8, 1), (0, -8, 32)])
-@pytest.mark.parametrize("M,N,K", [(1024, 768, 64), (768, 1280, 128), (512, 1024, 448)])
-def test_gemm_nt_persistent(nt_config, cfg, M, N, K):
-    """The persistent grid walks several tiles per workgroup (grid capped below the tile count) with the
-    super-stage stream running across tile boundaries -- including K = 64 (one stage per tile: the next
-    tile's first stage is prefetched while the current one is still being read) -- under every tile
-    order: exact integer products, every tile checked."""
-    C = nt_config
-    C.gemm_nt_config(*cfg)
-    torch.manual_seed(11)
-    a = torch.randint(-3, 4, (M, K), device=DEV).to(torch.bfloat16)
-    b = (torch.arange(N * K, device=DEV).reshape(N, K) % 5 - 2).to(torch.bfloat16)
-    c = torch.full((M, N), 7.0, device=DEV, dtype=torch.bfloat16)
-    C.gemm_nt_(c, a, b, 1.0, 0.0)
-    assert torch.equal(c, (a.double() @ b.double().t()).to(torch.bfloat16))
-    cf = torch.zeros(M, N, device=DEV, dtype=torch.float32)
-    C.gemm_nt_(cf, a, b, 1.0, 0.0)
-    assert torch.equal(cf, (a.double() @ b.double().t()).float())
-
-
-@pytest.mark.parametrize("name,K,N", [("qkv_fwd", 4096 + 64, 6144), ("down_dx", 4096 + 64, 14336)])
-def test_gemm_nt_production_shape(C, name, K, N):
-    """The headline step's shapes (T = 4 x 4096 tokens, LoRA-augmented K): bit-identical to torch.mm
-    (hipBLASLt accumulates the same 16x16x32 MFMA chain in K order) and close to an fp32 reference on a
-    row sample spread over every M tile."""
-    torch.manual_seed(12)
-    M = 16384
-    a = torch.empty(M, K, device=DEV, dtype=torch.bfloat16).uniform_(-1, 1)
-    b = torch.empty(N, K, device=DEV, dtype=torch.bfloat16).uniform_(-1, 1)
-    c = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-    C.gemm_nt_(c, a, b, 1.0, 0.0)
-    lib = torch.mm(a, b.t())
-    rows = torch.arange(0, M, 97, device=DEV)
-    ref = a[rows].float() @ b.float().t()
-    torch.testing.assert_close(c[rows].float(), ref, atol=3e-2 * (K ** 0.5) / 8, rtol=1e-2)
-    assert torch.equal(c, lib), f"{name}: {(c.float() - lib.float()).abs().max().item()} max |ours - torch.mm|"
-
-
-@pytest.mark.parametrize("with_pos", [False, True])
-def test_gemm_nt_rope_epilogue(C, with_pos):
-    """qkv projection with RoPE fused into the GEMM epilogue (head_dim 128, q and k heads rotated, v not)
-    vs the fp32 product rotated by the reference RoPE."""
-    from finetune_controller_amd.ops.rope import RotaryTable, _rope_ref
-
-    torch.manual_seed(5)
-    H, KV, D, S = 4, 2, 128, 256
-    M, K = 512, 320
-    N = (H + 2 * KV) * D
-    a = (torch.rand(M, K, device=DEV) * 2 - 1).to(torch.bfloat16)
-    w = (torch.rand(N, K, device=DEV) * 2 - 1).to(torch.bfloat16)
-    tab = RotaryTable(D, 1024, 500000.0)
-    cos, sin = tab.get(DEV)
-    pos = (torch.arange(M, device=DEV, dtype=torch.int32) * 7 % 1000) if with_pos else None
-    c = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-    C.gemm_nt_rope_(c, a, w, cos, sin, pos, S, H + KV)
-    ref = _rope_ref((a.float() @ w.float().t()), cos, sin, H + KV, D, S, pos, False)
-    tol = 2e-2 * (K ** 0.5) / 8
-    torch.testing.assert_close(c.float(), ref, atol=tol, rtol=1e-2)
-
-
-def test_gemm_nt_rejects(C):
-    a = torch.zeros(256, 40, device=DEV, dtype=torch.bfloat16)  # K not a multiple of 32
-    b = torch.zeros(256, 40, device=DEV, dtype=torch.bfloat16)
-    c = torch.zeros(256, 256, device=DEV, dtype=torch.bfloat16)
-    assert not C.gemm_nt_ok(c, a, b)
-    with pytest.raises(RuntimeError):
-        C.gemm_nt_(c, a, b, 1.0, 0.0)
-    assert not C.gemm_nt_ok(c[:, :200], a, b[:200])  # N not a multiple of 256
 
 
 def test_grad_clip_coef(C):
@@ -1022,13 +889,10 @@ def test_transpose2d(C, rows, cols, pad):
     assert C.transpose2d(x, out).data_ptr() == out.data_ptr() and torch.equal(out, x.t())
 
 
-@pytest.mark.parametrize("gemm_tn", ["0", "1"])
-def test_full_ft_steps_hip_match_torch_path(C, monkeypatch, gemm_tn):
+def test_full_ft_steps_hip_match_torch_path(C, monkeypatch):
     """Full fine-tuning on the HIP path -- TN input-gradient GEMMs through per-step W^T copies, weight
-    gradients with the activation transposed (csrc/kernels/transpose.hip) or, gemm_tn = 1, on the
-    hand-written TN GEMM (csrc/kernels/gemm_tn.hip) for every projection, flat AdamW -- against the
+    gradients with the activation transposed (csrc/kernels/transpose.hip), flat AdamW -- against the
     stock-PyTorch path over two optimizer steps (the W^T cache must follow the in-place updates)."""
-    monkeypatch.setenv("FTC_GEMM_TN", gemm_tn)
     from finetune_controller_amd.models import build_model
     from finetune_controller_amd.models.config import ModelConfig
     from finetune_controller_amd.train.optim import FlatAdamW
@@ -1420,12 +1284,9 @@ def test_accum_mm_fp32_out_bf16_operands(C):
     assert err < 1e-5, err
 
 
-@pytest.mark.parametrize("gemm_tn", ["0", "1"])
-def test_full_ft_fp32_grads_hip_match_torch_path(C, monkeypatch, gemm_tn):
+def test_full_ft_fp32_grads_hip_match_torch_path(C, monkeypatch):
     """Full fine-tuning with the fp32 gradient buffer and 2 accumulated micro-batches: HIP path vs the
-    stock-PyTorch path (same fp32 accumulation semantics), losses and the summed gradient; gemm_tn = 1
-    accumulates every weight gradient with the hand-written TN GEMM straight into the fp32 buffer."""
-    monkeypatch.setenv("FTC_GEMM_TN", gemm_tn)
+    stock-PyTorch path (same fp32 accumulation semantics), losses and the summed gradient."""
     from finetune_controller_amd.models import build_model
     from finetune_controller_amd.models.config import ModelConfig
     from finetune_controller_amd.train.optim import FlatAdamW

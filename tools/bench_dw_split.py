@@ -15,6 +15,13 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def lab():
+    from tools.gemm_lab.lab import load
+
+    return load()
+
 from finetune_controller_amd.ops import linear as L  # noqa: E402
 
 T = 16384
@@ -93,10 +100,10 @@ def main():
         def tn(s):  # the hand-written TN kernel (operands as stored, no transposed copy), split s ways
             def run():
                 if s == 1:
-                    ext().gemm_tn_(c, dy, x, 1.0, 0.0)
+                    lab().gemm_tn_(c, dy, x, 1.0, 0.0)
                 else:
                     p = parts[s]
-                    ext().gemm_tn_split_(p, dy, x)
+                    lab().gemm_tn_split_(p, dy, x)
                     ext().splitk_sum_(c, p, 0.0)
             return run
 

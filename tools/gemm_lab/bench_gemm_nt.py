@@ -6,7 +6,7 @@ augmented LoRA forms of ops/linear.py (k = K + 64 forward, the transposed frozen
     python tools/bench_gemm_nt.py [--iters 20] [--rounds 5] [--shapes qkv_fwd,o_fwd] \
         [--configs "0,-8,32;0,16,2"]
 
-Each config is ``grid_cap,group,xcc`` (ext().gemm_nt_config: grid_cap 0 = one persistent workgroup per CU,
+Each config is ``grid_cap,group,xcc`` (GemmLab.gemm_nt_config: grid_cap 0 = one persistent workgroup per CU,
 a large cap = one workgroup per tile; group > 0 M-fast / < 0 N-fast tile groups; xcc logical ids per XCD
 slot).  Every config and the library are timed in
 INTERLEAVED rounds on the same uniform random [-1, 1) operands (zeros read fast: DVFS), so box-to-box
@@ -20,7 +20,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from finetune_controller_amd.ops._backend import ext  # noqa: E402
 
 T = 16384
@@ -50,7 +50,9 @@ def main():
     ap.add_argument("--configs", default=DEFAULT_CONFIGS)
     ap.add_argument("--T", type=int, default=T)
     a = ap.parse_args()
-    C = ext()
+    from tools.gemm_lab.lab import load
+
+    C = load()
     cfgs = [tuple(int(v) for v in c.split(",")) for c in a.configs.split(";") if c.strip()]
     torch.manual_seed(0)
     for name in a.shapes.split(","):

@@ -17,7 +17,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from finetune_controller_amd.ops._backend import ext  # noqa: E402
 
 SHAPES = {  # name: (M = out, N = in, K = tokens)
@@ -48,7 +48,9 @@ def main():
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--cdtype", default="bf16,fp32")
     a = ap.parse_args()
-    C = ext()
+    from tools.gemm_lab.lab import load
+
+    C = load()
     dev = "cuda"
     for name in a.shapes.split(","):
         M, N, K = SHAPES[name]

@@ -2,7 +2,7 @@
 """Lab bench for the 8-wave ping-pong projection GEMM (tools/gemm_lab/gemm_pp.hip, built by
 tools/gemm_lab/build.sh into tools/gemm_lab/libgemm_pp.so): correctness against an fp32 / exact-integer
 reference on small and production shapes, then interleaved timing rounds (same uniform random [-1, 1)
-operands) of hipBLASLt (torch.mm), the shipped 4-wave kernel (ext().gemm_nt_) and the ping-pong kernel on
+operands) of hipBLASLt (torch.mm), the lab 4-wave kernel (tools/gemm_lab/lab.py gemm_nt_) and the ping-pong kernel on
 the Llama-3-8B LoRA-step shapes (T = 16384).  One JSON line per shape.
 
     python tools/gemm_lab/bench_pp.py [--variants d0,d3,m1] [--shapes qkv_fwd,o_fwd] [--iters 20] [--rounds 5]
@@ -98,7 +98,9 @@ def main():
             check(m)
     if a.check_only:
         return
-    C = ext()
+    from tools.gemm_lab.lab import load
+
+    C = load()
     torch.manual_seed(0)
     for name in a.shapes.split(","):
         k, n = SHAPES[name]

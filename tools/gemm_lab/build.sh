@@ -10,3 +10,6 @@ build() { hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Icsrc/kernel
 for d in 0 1 2 3; do build -DPPM=0 -DDMAP=$d tools/gemm_lab/gemm_pp.hip -o tools/gemm_lab/libgemm_pp_d$d.so & done
 for m in 1 2 3; do build -DPPM=$m -DDMAP=0 tools/gemm_lab/gemm_pp.hip -o tools/gemm_lab/libgemm_pp_m$m.so & done
 wait
+# the hand-written projection (NT, with the RoPE epilogue) and weight-gradient (TN) GEMMs: lab-only since
+# round 6 (they never beat hipBLASLt on a shipped shape; tools/gemm_lab/lab.py loads this library)
+build tools/gemm_lab/gemm_nt.hip tools/gemm_lab/gemm_tn.hip -o tools/gemm_lab/libgemm_lab.so

@@ -38,7 +38,9 @@ def main():
     C = None
     if a.ours:
         from finetune_controller_amd.ops._backend import ext
-        C = ext()
+        from tools.gemm_lab.lab import load
+
+        C = load()
     bf = torch.bfloat16
     torch.manual_seed(0)
     labels = []
