@@ -445,6 +445,385 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
   }
 }
 
+
+// ==== W64: one wave per SIMD, 64 query rows per wave, software-pipelined across tiles (round 6) =========
+//
+// A workgroup = 4 waves = 256 query rows of one (batch, q head); wave w owns rows q0 + 64 w + [0, 64) as two
+// 32-row blocks j = 0, 1 (one wave per SIMD: the whole 512-register file).  Every K / V^T fragment read from
+// LDS feeds BOTH blocks' MFMAs (half the LDS bytes per FLOP of the 32-row kernel), and each wave runs its
+// softmax one phase behind its own matrix work, placed gap by gap between the MFMAs:
+//
+//   iteration i:  sync (vmcnt(0) + barrier) | O rescale if the last start asked for it (rare)
+//     X_i  32 MFMAs  S(i) = K(i) Q^T             || finish softmax(i-1): exp / row sum / bf16 pack of its
+//                                                   keys 32-63; K(i) / Q fragment reads one k-step ahead;
+//                                                   LDS-DMA of K(i+2), V(i); the first V(i-1)^T reads
+//     Y_i  32 MFMAs  O += V(i-1)^T P(i-1)^T      || start softmax(i): row max, deferred-rescale decision,
+//                                                   exp / pack of its keys 0-31; V^T reads two fragments
+//                                                   ahead; K(i+1) / Q fragments of X_{i+1}'s first k-step
+//
+// Registers: O (128) lives in accumulator registers for the whole block -- its MFMAs are inline asm on "+a"
+// operands, which the compiler never copies; S is produced in VGPRs (this file is built with
+// -mllvm -amdgpu-mfma-vgpr-form, `tools/build.py`), so the softmax reads it without v_accvgpr copies.  Q is
+// staged once per block in LDS (64 KiB) and re-read per k-step instead of pinning 64 registers.  Every gap
+// is fenced (sched_barrier): the placement below is the schedule.  K arrives two tiles ahead (3-slot ring),
+// V one (2 slots), by LDS-DMA issued as inline asm (no compiler drain before the reads of other slots);
+// one barrier per tile.  The rescale a row max asks for (the reference moves only when a max grew by more
+// than 2^8) is applied at the next iteration's seam.  Causal: a wave's last visible tile (the diagonal) is
+// the masked variant; waves whose rows end earlier keep joining the DMA and barriers.
+// Covers head_dim 128, no window / document mask / padded tail, S % 256 == 0; otherwise ftc_flash_fwd
+// runs flash_fwd_kernel.
+constexpr int W64_BQ = 256;
+
+// O^T[d][q] += V^T . P^T on accumulator registers ("+a": allocated once, never moved by the compiler)
+DEV_INLINE void w64_pv(f32x16& acc, const bf16x8& va, const bf16x8& p) {
+  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(va), "v"(p));
+}
+// wait states between the asm MFMAs that write O and compiler code that reads or writes those registers
+// (the compiler pads nothing for an asm producer / consumer); the "+a" operands also pin the order
+#define W64_O_SYNC(NOPS)                                                                                   \
+  asm volatile(NOPS : "+a"(o[0][0]), "+a"(o[0][1]), "+a"(o[0][2]), "+a"(o[0][3]), "+a"(o[1][0]), "+a"(o[1][1]), \
+               "+a"(o[1][2]), "+a"(o[1][3]))
+#define W64_GAP() __builtin_amdgcn_sched_barrier(0)
+
+template <int D>
+__global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
+  static_assert(D == 128, "W64 forward: head_dim 128");
+  constexpr int NCH = D / 8, DSTEPS = D / 16, DT = D / 32;
+  constexpr int TILE = BK * D * 2;             // 16 KiB per K or V tile
+  constexpr int NGT = TILE / 1024 / 4;         // LDS-DMA pieces per wave per tile (4)
+  constexpr int RPG = 1024 / (D * 2);          // rows per piece (4)
+  constexpr int HALF = 32 * D * 2;             // byte offset of rows 32-63 of a tile (same swizzle)
+  __shared__ __attribute__((aligned(16))) char Qs[W64_BQ * D * 2];  // 64 KiB
+  __shared__ __attribute__((aligned(16))) char Kr[3 * TILE];        // K ring, 3 slots
+  __shared__ __attribute__((aligned(16))) char Vr[2 * TILE];        // V ring, 2 slots
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = lane >> 5, lr = lane & 31;
+  int qb, b, hq, kvh;
+  decode_block(a, qb, b, hq, kvh);
+  const int S = a.S;
+  const int q0 = qb * W64_BQ, wq0 = q0 + 64 * wave;
+  const int ntiles = a.causal ? (q0 + W64_BQ) / BK : S / BK;
+  const int wtiles = a.causal ? (wq0 + 64) / BK : ntiles;
+  const float c = a.scale_log2;
+
+  const uint16_t* kbase = a.k + (long long)b * S * a.kv_rs + (long long)kvh * D;
+  const uint16_t* vbase = a.v + (long long)b * S * a.kv_rs + (long long)kvh * D;
+  const auto krs = make_rsrc(kbase), vrs = make_rsrc(vbase);
+  int voff[NGT];
+#pragma unroll
+  for (int i = 0; i < NGT; ++i) {
+    const int row = (wave * NGT + i) * RPG + lane / NCH, pc = lane % NCH;
+    voff[i] = (row * (int)a.kv_rs + ((pc ^ swz(row)) & (NCH - 1)) * 8) * 2;
+  }
+  const int tstride = BK * (int)a.kv_rs * 2;  // global bytes per 64-key tile
+  // LDS-DMA of tile t of K (slot t % 3) or V (slot t % 2): piece p of this wave's NGT
+  auto dma_k = [&](const int t, const int p, const int slot) __attribute__((always_inline)) {
+    lds_dma16(krs, Kr + slot * TILE + (wave * NGT + p) * RPG * D * 2, voff[p], t * tstride);
+  };
+  auto dma_v = [&](const int t, const int p) __attribute__((always_inline)) {
+    lds_dma16(vrs, Vr + (t & 1) * TILE + (wave * NGT + p) * RPG * D * 2, voff[p], t * tstride);
+  };
+
+  // this wave's 64 Q rows -> Qs (swizzled row image), K(0), K(1): the block prologue
+  {
+    const uint16_t* qbase = a.q + ((long long)b * S + wq0) * a.q_rs + (long long)hq * D;
+    const auto qrs = make_rsrc(qbase);
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+      const int row = p * RPG + lane / NCH, pc = lane % NCH;
+      const int qo = (row * (int)a.q_rs + ((pc ^ swz(row)) & (NCH - 1)) * 8) * 2;
+      lds_dma16(qrs, Qs + (64 * wave + p * RPG) * D * 2, qo, 0);
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < NGT; ++p) dma_k(0, p, 0);
+  if (ntiles > 1) {
+#pragma unroll
+    for (int p = 0; p < NGT; ++p) dma_k(1, p, 1);
+  }
+
+  // lane-constant LDS offsets: K / Q fragment (row lr, chunk 2 st + hh); V^T tr-read (as flash_fwd_kernel)
+  int ko[DSTEPS];
+#pragma unroll
+  for (int st = 0; st < DSTEPS; ++st) ko[st] = lds_off<D>(lr, 2 * st + hh);
+  const int gi = lane >> 4, li = lane & 15;
+  const int trq = li >> 2, trp = li & 3;
+  int vto[DT][2];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    const int col = dt * 32 + 16 * (gi & 1) + 4 * trp;
+    const int chunk = col >> 3, half8 = (col & 7) ? 8 : 0;
+    vto[dt][0] = lds_off<D>(4 * hh + trq, chunk) + half8;
+    vto[dt][1] = lds_off<D>(4 * hh + trq + 8, chunk) + half8;
+  }
+  const char* Qw = Qs + 64 * wave * D * 2;
+  auto rd_k = [&](const int t, const int kt, const int st) __attribute__((always_inline)) -> uint4 {
+    return *reinterpret_cast<const uint4*>(Kr + (t % 3) * TILE + kt * HALF + ko[st]);
+  };
+  auto rd_q = [&](const int j, const int st) __attribute__((always_inline)) -> uint4 {
+    return *reinterpret_cast<const uint4*>(Qw + j * HALF + ko[st]);
+  };
+  auto rd_v = [&](const int t, const int f, const int h) __attribute__((always_inline)) -> s16x4 {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s16x4*)(Vr + (t & 1) * TILE + vto[f >> 2][h] + (f & 3) * 16 * D * 2));
+  };
+
+  f32x16 o[2][DT];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[j][t][i] = 0.f;
+  W64_O_SYNC("s_nop 1");  // the zeros are in the accumulators before the first asm MFMA reads them
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f}, alpha[2] = {1.f, 1.f}, rs[2] = {0.f, 0.f};
+  bool resc = false;
+  f32x16 sA[2][2], sB[2][2];  // S of the tile being started / finished (parity buffers)
+  uint4 pA[2][4], pB[2][4];   // P^T fragments as packed bf16 words (parity buffers)
+  uint4 kq[2][4];             // K / Q fragments of k-steps st (slot st & 1) and st + 1: {k kt0, k kt1, q j0, q j1}
+  s16x4 vf[3][2];             // V^T fragments, ring of three (two tr-reads each)
+
+  auto sync = [&]() __attribute__((always_inline)) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMA pieces of the last iteration landed
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();        // ... everyone's; every read of a slot about to be refilled is done
+  };
+  auto rescale = [&]() __attribute__((always_inline)) {
+    if (resc) {
+      W64_O_SYNC("s_nop 7\n\ts_nop 7\n\ts_nop 7");  // the last PV MFMA's result is readable
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[j][dt][i] *= alpha[j];
+      W64_O_SYNC("s_nop 1");  // v_accvgpr_write -> MFMA operand
+      resc = false;
+    }
+  };
+  auto masked = [&](const float x, const int j, const int e, const int t, const bool mask)
+      __attribute__((always_inline)) -> float {
+    if (!mask) return x;
+    const int kt = e >> 4, i = e & 15;
+    const int off = t * BK + kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;  // key of element (kt, i)
+    return off <= wq0 + 32 * j + lr ? x : -INFINITY;
+  };
+  // one exponential of element (kt, i) of block j into the packed P word; r = row-sum partial
+  auto exp_el = [&](const f32x16 (&sv)[2][2], uint4 (&pw)[2][4], float (&r)[2], const int j, const int e,
+                    const int t, const bool mask, const float mref, float (&ev)[2][2]) __attribute__((always_inline)) {
+    const int kt = e >> 4, i = e & 15;
+    const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(masked(sv[j][kt][i], j, e, t, mask), c, -mref));
+    r[j] += p;
+    ev[j][i & 1] = p;
+    if (i & 1) {
+      const uint32_t w = pack_bf2(ev[j][0], ev[j][1]);
+      const int f = 2 * kt + (i >> 3), dw = (i & 7) >> 1;
+      if (dw == 0) pw[j][f].x = w; else if (dw == 1) pw[j][f].y = w; else if (dw == 2) pw[j][f].z = w; else pw[j][f].w = w;
+    }
+  };
+
+  // ---- one iteration (tile i).  first: no finish / PV (tile 0); mask: tile i is the wave's diagonal; more:
+  // the wave computes tile i + 1 (read its first K fragments in Y_i)
+  auto body = [&](const int i, f32x16 (&sn)[2][2], f32x16 (&so)[2][2], uint4 (&pn)[2][4], uint4 (&po)[2][4],
+                  const bool first, const bool mask, const bool more) __attribute__((always_inline)) {
+    sync();
+    rescale();
+    float mref_o[2], r[2] = {rs[0], rs[1]}, ev[2][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) mref_o[j] = (m[j] == -INFINITY) ? 0.f : m[j];
+    // ---------------- X_i
+    W64_GAP();
+#pragma unroll
+    for (int st = 0; st < DSTEPS; ++st) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int g = 4 * st + u;
+        const uint4* cur = kq[st & 1];
+        const int kt = u >> 1, j = u & 1;
+        const f32x16 zero = {};
+        sn[j][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(cur[kt]), as_bf8(cur[2 + j]), st ? sn[j][kt] : zero,
+                                                            0, 0, 0);
+        if (st + 1 < DSTEPS) {
+          kq[(st + 1) & 1][u] = u < 2 ? rd_k(i, u, st + 1) : rd_q(u - 2, st + 1);
+        } else if (!first) {
+          vf[u >> 1][u & 1] = rd_v(i - 1, u >> 1, u & 1);  // V(i-1)^T fragments 0, 1 for Y_i
+        }
+        if (!first) exp_el(so, po, r, g >> 4, 16 + (g & 15), i - 1, false, mref_o[g >> 4], ev);
+        // past the last tile the DMA repeats the last K tile into the slot K(i-1) left: nobody reads it
+        // again, and the branch-free gap keeps every wave's DMA count equal
+        if (g < NGT) {
+          dma_k(min(i + 2, ntiles - 1), g, (i + 2) % 3);
+        } else if (g < 2 * NGT) {
+          dma_v(i, g - NGT);
+        }
+        W64_GAP();
+      }
+    }
+    if (!first) {
+      l[0] += r[0];
+      l[1] += r[1];
+    }
+    // ---------------- Y_i
+    float mt[2] = {-INFINITY, -INFINITY}, mref_n[2] = {0.f, 0.f};
+    bool need_any = false;
+    r[0] = r[1] = 0.f;
+#pragma unroll
+    for (int f = 0; f < 16; ++f) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int g = 2 * f + j;
+        if (!first) {
+          const int fr = f + 2;
+          if (fr < 16) {
+            vf[fr % 3][j] = rd_v(i - 1, fr, j);
+          }
+          const s16x4 v1 = vf[f % 3][0], v2 = vf[f % 3][1];
+          const s16x8 va = {v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
+          w64_pv(o[j][f >> 2], __builtin_bit_cast(bf16x8, va), as_bf8(po[j][f & 3]));
+        }
+        if (g >= 28 && more) {  // X_{i+1}'s first k-step: K(i+1) (landed two tiles ahead) and Q
+          const int u = g - 28;
+          kq[0][u] = u < 2 ? rd_k(i + 1, u, 0) : rd_q(u - 2, 0);
+        }
+        // start softmax(i): gaps 0-7 row max (4 elements of each block per gap), 8-9 the row statistics,
+        // 10-31 exps of keys 0-31 (32 elements over 22 gaps)
+        if (g < 8) {
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+            for (int e = 4 * g; e < 4 * g + 4; ++e)
+              mt[jj] = fmaxf(mt[jj], masked(sn[jj][e >> 4][e & 15], jj, e, i, mask));
+        } else if (g == 8) {
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) mt[jj] = xhalf_max(mt[jj]) * c;
+        } else if (g == 9) {
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) {
+            const bool need = mt[jj] > m[jj] + 8.0f;
+            const float mn = need ? fmaxf(m[jj], mt[jj]) : m[jj];
+            const float al = __builtin_amdgcn_exp2f(m[jj] - ((mn == -INFINITY) ? 0.f : mn));
+            alpha[jj] = al;
+            l[jj] *= al;
+            m[jj] = mn;
+            mref_n[jj] = (mn == -INFINITY) ? 0.f : mn;
+            need_any |= need;
+          }
+        } else {
+#pragma unroll
+          for (int e2 = 0; e2 < 32; ++e2)
+            if (10 + (e2 * 22) / 32 == g) exp_el(sn, pn, r, e2 >> 4, e2 & 15, i, mask, mref_n[e2 >> 4], ev);
+        }
+        W64_GAP();
+      }
+    }
+    rs[0] = r[0];
+    rs[1] = r[1];
+    resc = __builtin_amdgcn_ballot_w64(need_any) != 0;
+  };
+  auto tail = [&](const int i, f32x16 (&so)[2][2], uint4 (&po)[2][4], const bool mask) __attribute__((always_inline)) {
+    sync();
+    rescale();
+    if (i + 2 < ntiles) {
+#pragma unroll
+      for (int p = 0; p < NGT; ++p) dma_k(i + 2, p, (i + 2) % 3);
+    }
+    if (i < ntiles) {
+#pragma unroll
+      for (int p = 0; p < NGT; ++p) dma_v(i, p);
+    }
+    float r[2] = {rs[0], rs[1]}, ev[2][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float mref = (m[j] == -INFINITY) ? 0.f : m[j];
+#pragma unroll
+      for (int e = 16; e < 32; ++e) exp_el(so, po, r, j, e, i - 1, mask, mref, ev);
+      l[j] += r[j];
+    }
+#pragma unroll
+    for (int f = 0; f < 16; ++f) {
+      const s16x4 v1 = rd_v(i - 1, f, 0), v2 = rd_v(i - 1, f, 1);
+      const s16x8 va = {v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
+      W64_GAP();
+      w64_pv(o[0][f >> 2], __builtin_bit_cast(bf16x8, va), as_bf8(po[0][f & 3]));
+      w64_pv(o[1][f >> 2], __builtin_bit_cast(bf16x8, va), as_bf8(po[1][f & 3]));
+    }
+  };
+
+  // block prologue: Q, K(0), K(1) landed; X_0's first K / Q fragments
+  sync();
+#pragma unroll
+  for (int u = 0; u < 4; ++u) kq[0][u] = u < 2 ? rd_k(0, u, 0) : rd_q(u - 2, 0);
+  body(0, sA, sB, pA, pB, true, a.causal && wtiles == 1, wtiles > 1);
+  int i = 1;
+  // steady iterations 1 .. wtiles - 2 in parity pairs; the state is back in (sA, pA) after each pair
+  for (; i + 2 < wtiles; i += 2) {
+    body(i, sB, sA, pB, pA, false, false, true);
+    body(i + 1, sA, sB, pA, pB, false, false, true);
+  }
+  if (i + 1 < wtiles) {  // one more steady iteration (odd i); then the state moves back to (sA, pA)
+    body(i, sB, sA, pB, pA, false, false, true);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      sA[j][1] = sB[j][1];
+      pA[j][0] = pB[j][0];
+      pA[j][1] = pB[j][1];
+    }
+    ++i;
+  }
+  if (i < wtiles) {  // the wave's last tile: the diagonal under the causal mask
+    body(i, sB, sA, pB, pA, false, a.causal != 0, false);
+    ++i;
+    tail(i, sB, pB, a.causal != 0);
+  } else {  // wtiles == 1
+    tail(i, sA, pA, a.causal != 0);
+  }
+  // waves whose rows ended keep joining the workgroup's DMA / barriers
+  for (++i; i <= ntiles; ++i) {
+    sync();
+    if (i + 2 < ntiles) {
+#pragma unroll
+      for (int p = 0; p < NGT; ++p) dma_k(i + 2, p, (i + 2) % 3);
+    }
+    if (i < ntiles) {
+#pragma unroll
+      for (int p = 0; p < NGT; ++p) dma_v(i, p);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // no LDS-DMA may outlive the workgroup
+  W64_O_SYNC("s_nop 7\n\ts_nop 7\n\ts_nop 7");  // the last PV MFMA's result is readable
+
+  // ---- epilogue per block: normalise, 16-byte O stores, LSE (natural log)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int qrow = wq0 + 32 * j + lr;
+    const float ltot = l[j] + __shfl_xor(l[j], 32, 64);
+    const float inv = ltot > 0.f ? 1.0f / ltot : 0.f;
+    uint16_t* op = a.o + ((long long)b * S + qrow) * a.o_rs + (long long)hq * D;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      uint32_t w[4][2];
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        w[g4][0] = pack_bf2(o[j][dt][4 * g4 + 0] * inv, o[j][dt][4 * g4 + 1] * inv);
+        w[g4][1] = pack_bf2(o[j][dt][4 * g4 + 2] * inv, o[j][dt][4 * g4 + 3] * inv);
+      }
+      const auto a0 = __builtin_amdgcn_permlane32_swap(w[0][0], w[2][0], false, false);
+      const auto a1 = __builtin_amdgcn_permlane32_swap(w[0][1], w[2][1], false, false);
+      const auto b0 = __builtin_amdgcn_permlane32_swap(w[1][0], w[3][0], false, false);
+      const auto b1 = __builtin_amdgcn_permlane32_swap(w[1][1], w[3][1], false, false);
+      const int d = dt * 32 + 16 * hh;
+      *reinterpret_cast<uint4*>(op + d) = make_uint4(a0[0], a1[0], a0[1], a1[1]);
+      *reinterpret_cast<uint4*>(op + d + 8) = make_uint4(b0[0], b1[0], b0[1], b1[1]);
+    }
+    if (hh == 0) {
+      const float lse2 = (m[j] == -INFINITY) ? -INFINITY : m[j] + __log2f(ltot);
+      a.lse[((long long)b * a.H + hq) * S + qrow] = lse2 * LN2;
+    }
+  }
+}
+
 }  // namespace
 
 // (Removed in round 5: skipping a tile a wave sees fully masked (causal diagonal) -- 0.566 / 0.559 vs
@@ -455,11 +834,29 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
 // block fenced between the other block's MFMAs, asm-DMA 3-slot ring: 0.740 vs 0.554 ms at the Llama-3-8B
 // layer, profiles/r4/attn/fwd_qb6.log; git history has the kernel.)
 
+// forward variant of every later call: 1 = W64 (default where it applies), 0 = the 32-row kernel everywhere;
+// tests and tools/bench_attention.py switch it in one process (ftc_flash_fwd_config)
+namespace {
+int& fwd_variant() {
+  static int v = 1;
+  return v;
+}
+}  // namespace
+
+extern "C" void ftc_flash_fwd_config(int variant) { fwd_variant() = variant ? 1 : 0; }
+
 extern "C" int ftc_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H,
                              int KV, int D, long long q_rs, long long kv_rs, long long o_rs, float scale, int causal,
                              int window, const int* doc_start, int kv_valid, hipStream_t stream) {
   if (S % BK != 0 || H % KV != 0 || (D != 128 && D != 64)) return -1;
   if (kv_valid <= 0 || kv_valid > S) kv_valid = S;
+  if (fwd_variant() == 1 && D == 128 && S % W64_BQ == 0 && window <= 0 && doc_start == nullptr && kv_valid == S &&
+      (o_rs & 7) == 0) {
+    FwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, q_rs, kv_rs, o_rs,
+              B, S, H, KV, S / W64_BQ, scale * LOG2E, causal, 0, nullptr, S};
+    hipLaunchKernelGGL((flash_fwd_w64_kernel<128>), dim3(a.nqb * B * H), dim3(256), 0, stream, a);
+    return (int)hipGetLastError();
+  }
   constexpr int BQ = 32 * WAVES;
   FwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, q_rs, kv_rs, o_rs,
             B, S, H, KV, (S + BQ - 1) / BQ, scale * LOG2E, causal, window, doc_start, kv_valid};

@@ -62,11 +62,18 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError(f"build step failed ({r.returncode}):\n{' '.join(cmd)}\n{r.stdout}")
 
 
+# per-source compiler flags a kernel's design depends on (its header says why):
+#   flash_attn_fwd.hip -- the W64 forward keeps O in accumulator registers through inline-asm MFMAs and wants
+#   its S MFMAs in VGPR form (the softmax reads them with no v_accvgpr copies); no SLP packing of the
+#   softmax's f32 adds into v_pk_add_f32 (an anti-lever beside MFMAs: MI355X_MICROARCH.md cycle constants)
+EXTRA_FLAGS = {"flash_attn_fwd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-slp-vectorize"]}
+
+
 def _hip_obj(src: Path, headers: list[Path], force: bool) -> Path:
     out = BUILD / (src.stem + ".hip.o")
-    if force or _newer(out, [src, *headers]):
+    if force or _newer(out, [src, *headers, Path(__file__)]):
         _run(["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", str(src), "-o", str(out),
-              "-I", str(CSRC / "kernels"), "-Wno-unused-result", "-ffp-contract=fast"])
+              "-I", str(CSRC / "kernels"), "-Wno-unused-result", "-ffp-contract=fast", *EXTRA_FLAGS.get(src.name, [])])
     return out
 
 
