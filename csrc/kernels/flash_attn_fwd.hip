@@ -473,16 +473,117 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
 // Covers head_dim 128, no window / document mask / padded tail, S % 256 == 0; otherwise ftc_flash_fwd
 // runs flash_fwd_kernel.
 constexpr int W64_BQ = 256;
+#ifndef W64_TAIL_J1FIRST
+#define W64_TAIL_J1FIRST 0
+#endif
+#ifndef W64_TAIL_NOP
+#define W64_TAIL_NOP 0
+#endif
+#ifndef W64_DEFER
+#define W64_DEFER 8.0f
+#endif
 
-// O^T[d][q] += V^T . P^T on accumulator registers ("+a": allocated once, never moved by the compiler)
-DEV_INLINE void w64_pv(f32x16& acc, const bf16x8& va, const bf16x8& p) {
-  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(va), "v"(p));
+// O lives in accumulator registers the kernel OWNS: a[128:255], tile (j, dt) at a[128 + 16 (4 j + dt) ..+15],
+// written and read only by the inline asm below (MFMAs, zeroing, rescale, epilogue reads), which lists them as
+// clobbers (that also makes the kernel descriptor allocate all 256).  The compiler never holds O, so it can
+// neither copy nor spill it: copies of "+a" operands it had inserted right after an asm MFMA read the
+// accumulators before the MFMA had written them (no hazard padding across asm) and corrupted block 1 on
+// ~0.1 % of rows.  The compiler's own accumulator use (VGPR spill slots) stays in a[0:127];
+// tools/check_asm_hazards.py --owned 128 fails the build audit if any compiler instruction touches a[128:255].
+// clobber lists of the eight 16-register O tiles (a128-a143, ..., a240-a255)
+#define W64_CLOB_T0 "a128", "a129", "a130", "a131", "a132", "a133", "a134", "a135", "a136", "a137", "a138", "a139", "a140", "a141", "a142", "a143"
+#define W64_CLOB_T1 "a144", "a145", "a146", "a147", "a148", "a149", "a150", "a151", "a152", "a153", "a154", "a155", "a156", "a157", "a158", "a159"
+#define W64_CLOB_T2 "a160", "a161", "a162", "a163", "a164", "a165", "a166", "a167", "a168", "a169", "a170", "a171", "a172", "a173", "a174", "a175"
+#define W64_CLOB_T3 "a176", "a177", "a178", "a179", "a180", "a181", "a182", "a183", "a184", "a185", "a186", "a187", "a188", "a189", "a190", "a191"
+#define W64_CLOB_T4 "a192", "a193", "a194", "a195", "a196", "a197", "a198", "a199", "a200", "a201", "a202", "a203", "a204", "a205", "a206", "a207"
+#define W64_CLOB_T5 "a208", "a209", "a210", "a211", "a212", "a213", "a214", "a215", "a216", "a217", "a218", "a219", "a220", "a221", "a222", "a223"
+#define W64_CLOB_T6 "a224", "a225", "a226", "a227", "a228", "a229", "a230", "a231", "a232", "a233", "a234", "a235", "a236", "a237", "a238", "a239"
+#define W64_CLOB_T7 "a240", "a241", "a242", "a243", "a244", "a245", "a246", "a247", "a248", "a249", "a250", "a251", "a252", "a253", "a254", "a255"
+#define W64_CLOB_ALL W64_CLOB_T0, W64_CLOB_T1, W64_CLOB_T2, W64_CLOB_T3, W64_CLOB_T4, W64_CLOB_T5, W64_CLOB_T6, W64_CLOB_T7
+
+// O tile T (= 4 j + dt) += V^T . P^T
+template <int T>
+DEV_INLINE void w64_pv(const bf16x8& va, const bf16x8& p) {
+  constexpr int B = 128 + 16 * T;
+  if constexpr (T == 0)
+    asm volatile("v_mfma_f32_32x32x16_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(va), "v"(p), "i"(B), "i"(B + 15) : W64_CLOB_T0);
+  if constexpr (T == 1)
+    asm volatile("v_mfma_f32_32x32x16_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(va), "v"(p), "i"(B), "i"(B + 15) : W64_CLOB_T1);
+  if constexpr (T == 2)
+    asm volatile("v_mfma_f32_32x32x16_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(va), "v"(p), "i"(B), "i"(B + 15) : W64_CLOB_T2);
+  if constexpr (T == 3)
+    asm volatile("v_mfma_f32_32x32x16_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(va), "v"(p), "i"(B), "i"(B + 15) : W64_CLOB_T3);
+  if constexpr (T == 4)
+    asm volatile("v_mfma_f32_32x32x16_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(va), "v"(p), "i"(B), "i"(B + 15) : W64_CLOB_T4);
+  if constexpr (T == 5)
+    asm volatile("v_mfma_f32_32x32x16_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(va), "v"(p), "i"(B), "i"(B + 15) : W64_CLOB_T5);
+  if constexpr (T == 6)
+    asm volatile("v_mfma_f32_32x32x16_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(va), "v"(p), "i"(B), "i"(B + 15) : W64_CLOB_T6);
+  if constexpr (T == 7)
+    asm volatile("v_mfma_f32_32x32x16_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]" ::"v"(va), "v"(p), "i"(B), "i"(B + 15) : W64_CLOB_T7);
 }
-// wait states between the asm MFMAs that write O and compiler code that reads or writes those registers
-// (the compiler pads nothing for an asm producer / consumer); the "+a" operands also pin the order
-#define W64_O_SYNC(NOPS)                                                                                   \
-  asm volatile(NOPS : "+a"(o[0][0]), "+a"(o[0][1]), "+a"(o[0][2]), "+a"(o[0][3]), "+a"(o[1][0]), "+a"(o[1][1]), \
-               "+a"(o[1][2]), "+a"(o[1][3]))
+// zero all of O (block start); the trailing nops cover v_accvgpr_write -> MFMA SrcC
+DEV_INLINE void w64_o_zero() {
+  asm volatile("v_accvgpr_write_b32 a128, 0\n\tv_accvgpr_write_b32 a129, 0\n\tv_accvgpr_write_b32 a130, 0\n\tv_accvgpr_write_b32 a131, 0\n\tv_accvgpr_write_b32 a132, 0\n\tv_accvgpr_write_b32 a133, 0\n\tv_accvgpr_write_b32 a134, 0\n\tv_accvgpr_write_b32 a135, 0\n\tv_accvgpr_write_b32 a136, 0\n\tv_accvgpr_write_b32 a137, 0\n\tv_accvgpr_write_b32 a138, 0\n\tv_accvgpr_write_b32 a139, 0\n\tv_accvgpr_write_b32 a140, 0\n\tv_accvgpr_write_b32 a141, 0\n\tv_accvgpr_write_b32 a142, 0\n\tv_accvgpr_write_b32 a143, 0\n\tv_accvgpr_write_b32 a144, 0\n\tv_accvgpr_write_b32 a145, 0\n\tv_accvgpr_write_b32 a146, 0\n\tv_accvgpr_write_b32 a147, 0\n\tv_accvgpr_write_b32 a148, 0\n\tv_accvgpr_write_b32 a149, 0\n\tv_accvgpr_write_b32 a150, 0\n\tv_accvgpr_write_b32 a151, 0\n\tv_accvgpr_write_b32 a152, 0\n\tv_accvgpr_write_b32 a153, 0\n\tv_accvgpr_write_b32 a154, 0\n\tv_accvgpr_write_b32 a155, 0\n\tv_accvgpr_write_b32 a156, 0\n\tv_accvgpr_write_b32 a157, 0\n\tv_accvgpr_write_b32 a158, 0\n\tv_accvgpr_write_b32 a159, 0\n\tv_accvgpr_write_b32 a160, 0\n\tv_accvgpr_write_b32 a161, 0\n\tv_accvgpr_write_b32 a162, 0\n\tv_accvgpr_write_b32 a163, 0\n\tv_accvgpr_write_b32 a164, 0\n\tv_accvgpr_write_b32 a165, 0\n\tv_accvgpr_write_b32 a166, 0\n\tv_accvgpr_write_b32 a167, 0\n\tv_accvgpr_write_b32 a168, 0\n\tv_accvgpr_write_b32 a169, 0\n\tv_accvgpr_write_b32 a170, 0\n\tv_accvgpr_write_b32 a171, 0\n\tv_accvgpr_write_b32 a172, 0\n\tv_accvgpr_write_b32 a173, 0\n\tv_accvgpr_write_b32 a174, 0\n\tv_accvgpr_write_b32 a175, 0\n\tv_accvgpr_write_b32 a176, 0\n\tv_accvgpr_write_b32 a177, 0\n\tv_accvgpr_write_b32 a178, 0\n\tv_accvgpr_write_b32 a179, 0\n\tv_accvgpr_write_b32 a180, 0\n\tv_accvgpr_write_b32 a181, 0\n\tv_accvgpr_write_b32 a182, 0\n\tv_accvgpr_write_b32 a183, 0\n\tv_accvgpr_write_b32 a184, 0\n\tv_accvgpr_write_b32 a185, 0\n\tv_accvgpr_write_b32 a186, 0\n\tv_accvgpr_write_b32 a187, 0\n\tv_accvgpr_write_b32 a188, 0\n\tv_accvgpr_write_b32 a189, 0\n\tv_accvgpr_write_b32 a190, 0\n\tv_accvgpr_write_b32 a191, 0\n\tv_accvgpr_write_b32 a192, 0\n\tv_accvgpr_write_b32 a193, 0\n\tv_accvgpr_write_b32 a194, 0\n\tv_accvgpr_write_b32 a195, 0\n\tv_accvgpr_write_b32 a196, 0\n\tv_accvgpr_write_b32 a197, 0\n\tv_accvgpr_write_b32 a198, 0\n\tv_accvgpr_write_b32 a199, 0\n\tv_accvgpr_write_b32 a200, 0\n\tv_accvgpr_write_b32 a201, 0\n\tv_accvgpr_write_b32 a202, 0\n\tv_accvgpr_write_b32 a203, 0\n\tv_accvgpr_write_b32 a204, 0\n\tv_accvgpr_write_b32 a205, 0\n\tv_accvgpr_write_b32 a206, 0\n\tv_accvgpr_write_b32 a207, 0\n\tv_accvgpr_write_b32 a208, 0\n\tv_accvgpr_write_b32 a209, 0\n\tv_accvgpr_write_b32 a210, 0\n\tv_accvgpr_write_b32 a211, 0\n\tv_accvgpr_write_b32 a212, 0\n\tv_accvgpr_write_b32 a213, 0\n\tv_accvgpr_write_b32 a214, 0\n\tv_accvgpr_write_b32 a215, 0\n\tv_accvgpr_write_b32 a216, 0\n\tv_accvgpr_write_b32 a217, 0\n\tv_accvgpr_write_b32 a218, 0\n\tv_accvgpr_write_b32 a219, 0\n\tv_accvgpr_write_b32 a220, 0\n\tv_accvgpr_write_b32 a221, 0\n\tv_accvgpr_write_b32 a222, 0\n\tv_accvgpr_write_b32 a223, 0\n\tv_accvgpr_write_b32 a224, 0\n\tv_accvgpr_write_b32 a225, 0\n\tv_accvgpr_write_b32 a226, 0\n\tv_accvgpr_write_b32 a227, 0\n\tv_accvgpr_write_b32 a228, 0\n\tv_accvgpr_write_b32 a229, 0\n\tv_accvgpr_write_b32 a230, 0\n\tv_accvgpr_write_b32 a231, 0\n\tv_accvgpr_write_b32 a232, 0\n\tv_accvgpr_write_b32 a233, 0\n\tv_accvgpr_write_b32 a234, 0\n\tv_accvgpr_write_b32 a235, 0\n\tv_accvgpr_write_b32 a236, 0\n\tv_accvgpr_write_b32 a237, 0\n\tv_accvgpr_write_b32 a238, 0\n\tv_accvgpr_write_b32 a239, 0\n\tv_accvgpr_write_b32 a240, 0\n\tv_accvgpr_write_b32 a241, 0\n\tv_accvgpr_write_b32 a242, 0\n\tv_accvgpr_write_b32 a243, 0\n\tv_accvgpr_write_b32 a244, 0\n\tv_accvgpr_write_b32 a245, 0\n\tv_accvgpr_write_b32 a246, 0\n\tv_accvgpr_write_b32 a247, 0\n\tv_accvgpr_write_b32 a248, 0\n\tv_accvgpr_write_b32 a249, 0\n\tv_accvgpr_write_b32 a250, 0\n\tv_accvgpr_write_b32 a251, 0\n\tv_accvgpr_write_b32 a252, 0\n\tv_accvgpr_write_b32 a253, 0\n\tv_accvgpr_write_b32 a254, 0\n\tv_accvgpr_write_b32 a255, 0\n\ts_nop 4" ::: W64_CLOB_ALL);
+}
+// O tile T *= alpha (per lane).  The caller put the MFMA -> v_accvgpr_read wait states in front
+// (w64_o_wait); the chain runs through one scratch VGPR; the trailing nops cover v_accvgpr_write -> MFMA SrcC
+template <int T>
+DEV_INLINE void w64_o_scale(const float alpha) {
+  float t;
+  if constexpr (T == 0) asm volatile("v_accvgpr_read_b32 %0, a128\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a128, %0\n\tv_accvgpr_read_b32 %0, a129\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a129, %0\n\tv_accvgpr_read_b32 %0, a130\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a130, %0\n\tv_accvgpr_read_b32 %0, a131\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a131, %0\n\tv_accvgpr_read_b32 %0, a132\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a132, %0\n\tv_accvgpr_read_b32 %0, a133\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a133, %0\n\tv_accvgpr_read_b32 %0, a134\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a134, %0\n\tv_accvgpr_read_b32 %0, a135\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a135, %0\n\tv_accvgpr_read_b32 %0, a136\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a136, %0\n\tv_accvgpr_read_b32 %0, a137\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a137, %0\n\tv_accvgpr_read_b32 %0, a138\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a138, %0\n\tv_accvgpr_read_b32 %0, a139\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a139, %0\n\tv_accvgpr_read_b32 %0, a140\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a140, %0\n\tv_accvgpr_read_b32 %0, a141\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a141, %0\n\tv_accvgpr_read_b32 %0, a142\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a142, %0\n\tv_accvgpr_read_b32 %0, a143\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a143, %0\n\ts_nop 2" : "=&v"(t) : "v"(alpha) : W64_CLOB_T0);
+  if constexpr (T == 1) asm volatile("v_accvgpr_read_b32 %0, a144\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a144, %0\n\tv_accvgpr_read_b32 %0, a145\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a145, %0\n\tv_accvgpr_read_b32 %0, a146\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a146, %0\n\tv_accvgpr_read_b32 %0, a147\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a147, %0\n\tv_accvgpr_read_b32 %0, a148\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a148, %0\n\tv_accvgpr_read_b32 %0, a149\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a149, %0\n\tv_accvgpr_read_b32 %0, a150\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a150, %0\n\tv_accvgpr_read_b32 %0, a151\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a151, %0\n\tv_accvgpr_read_b32 %0, a152\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a152, %0\n\tv_accvgpr_read_b32 %0, a153\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a153, %0\n\tv_accvgpr_read_b32 %0, a154\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a154, %0\n\tv_accvgpr_read_b32 %0, a155\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a155, %0\n\tv_accvgpr_read_b32 %0, a156\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a156, %0\n\tv_accvgpr_read_b32 %0, a157\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a157, %0\n\tv_accvgpr_read_b32 %0, a158\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a158, %0\n\tv_accvgpr_read_b32 %0, a159\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a159, %0\n\ts_nop 2" : "=&v"(t) : "v"(alpha) : W64_CLOB_T1);
+  if constexpr (T == 2) asm volatile("v_accvgpr_read_b32 %0, a160\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a160, %0\n\tv_accvgpr_read_b32 %0, a161\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a161, %0\n\tv_accvgpr_read_b32 %0, a162\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a162, %0\n\tv_accvgpr_read_b32 %0, a163\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a163, %0\n\tv_accvgpr_read_b32 %0, a164\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a164, %0\n\tv_accvgpr_read_b32 %0, a165\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a165, %0\n\tv_accvgpr_read_b32 %0, a166\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a166, %0\n\tv_accvgpr_read_b32 %0, a167\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a167, %0\n\tv_accvgpr_read_b32 %0, a168\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a168, %0\n\tv_accvgpr_read_b32 %0, a169\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a169, %0\n\tv_accvgpr_read_b32 %0, a170\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a170, %0\n\tv_accvgpr_read_b32 %0, a171\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a171, %0\n\tv_accvgpr_read_b32 %0, a172\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a172, %0\n\tv_accvgpr_read_b32 %0, a173\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a173, %0\n\tv_accvgpr_read_b32 %0, a174\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a174, %0\n\tv_accvgpr_read_b32 %0, a175\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a175, %0\n\ts_nop 2" : "=&v"(t) : "v"(alpha) : W64_CLOB_T2);
+  if constexpr (T == 3) asm volatile("v_accvgpr_read_b32 %0, a176\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a176, %0\n\tv_accvgpr_read_b32 %0, a177\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a177, %0\n\tv_accvgpr_read_b32 %0, a178\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a178, %0\n\tv_accvgpr_read_b32 %0, a179\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a179, %0\n\tv_accvgpr_read_b32 %0, a180\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a180, %0\n\tv_accvgpr_read_b32 %0, a181\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a181, %0\n\tv_accvgpr_read_b32 %0, a182\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a182, %0\n\tv_accvgpr_read_b32 %0, a183\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a183, %0\n\tv_accvgpr_read_b32 %0, a184\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a184, %0\n\tv_accvgpr_read_b32 %0, a185\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a185, %0\n\tv_accvgpr_read_b32 %0, a186\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a186, %0\n\tv_accvgpr_read_b32 %0, a187\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a187, %0\n\tv_accvgpr_read_b32 %0, a188\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a188, %0\n\tv_accvgpr_read_b32 %0, a189\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a189, %0\n\tv_accvgpr_read_b32 %0, a190\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a190, %0\n\tv_accvgpr_read_b32 %0, a191\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a191, %0\n\ts_nop 2" : "=&v"(t) : "v"(alpha) : W64_CLOB_T3);
+  if constexpr (T == 4) asm volatile("v_accvgpr_read_b32 %0, a192\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a192, %0\n\tv_accvgpr_read_b32 %0, a193\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a193, %0\n\tv_accvgpr_read_b32 %0, a194\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a194, %0\n\tv_accvgpr_read_b32 %0, a195\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a195, %0\n\tv_accvgpr_read_b32 %0, a196\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a196, %0\n\tv_accvgpr_read_b32 %0, a197\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a197, %0\n\tv_accvgpr_read_b32 %0, a198\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a198, %0\n\tv_accvgpr_read_b32 %0, a199\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a199, %0\n\tv_accvgpr_read_b32 %0, a200\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a200, %0\n\tv_accvgpr_read_b32 %0, a201\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a201, %0\n\tv_accvgpr_read_b32 %0, a202\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a202, %0\n\tv_accvgpr_read_b32 %0, a203\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a203, %0\n\tv_accvgpr_read_b32 %0, a204\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a204, %0\n\tv_accvgpr_read_b32 %0, a205\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a205, %0\n\tv_accvgpr_read_b32 %0, a206\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a206, %0\n\tv_accvgpr_read_b32 %0, a207\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a207, %0\n\ts_nop 2" : "=&v"(t) : "v"(alpha) : W64_CLOB_T4);
+  if constexpr (T == 5) asm volatile("v_accvgpr_read_b32 %0, a208\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a208, %0\n\tv_accvgpr_read_b32 %0, a209\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a209, %0\n\tv_accvgpr_read_b32 %0, a210\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a210, %0\n\tv_accvgpr_read_b32 %0, a211\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a211, %0\n\tv_accvgpr_read_b32 %0, a212\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a212, %0\n\tv_accvgpr_read_b32 %0, a213\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a213, %0\n\tv_accvgpr_read_b32 %0, a214\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a214, %0\n\tv_accvgpr_read_b32 %0, a215\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a215, %0\n\tv_accvgpr_read_b32 %0, a216\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a216, %0\n\tv_accvgpr_read_b32 %0, a217\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a217, %0\n\tv_accvgpr_read_b32 %0, a218\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a218, %0\n\tv_accvgpr_read_b32 %0, a219\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a219, %0\n\tv_accvgpr_read_b32 %0, a220\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a220, %0\n\tv_accvgpr_read_b32 %0, a221\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a221, %0\n\tv_accvgpr_read_b32 %0, a222\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a222, %0\n\tv_accvgpr_read_b32 %0, a223\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a223, %0\n\ts_nop 2" : "=&v"(t) : "v"(alpha) : W64_CLOB_T5);
+  if constexpr (T == 6) asm volatile("v_accvgpr_read_b32 %0, a224\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a224, %0\n\tv_accvgpr_read_b32 %0, a225\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a225, %0\n\tv_accvgpr_read_b32 %0, a226\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a226, %0\n\tv_accvgpr_read_b32 %0, a227\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a227, %0\n\tv_accvgpr_read_b32 %0, a228\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a228, %0\n\tv_accvgpr_read_b32 %0, a229\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a229, %0\n\tv_accvgpr_read_b32 %0, a230\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a230, %0\n\tv_accvgpr_read_b32 %0, a231\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a231, %0\n\tv_accvgpr_read_b32 %0, a232\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a232, %0\n\tv_accvgpr_read_b32 %0, a233\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a233, %0\n\tv_accvgpr_read_b32 %0, a234\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a234, %0\n\tv_accvgpr_read_b32 %0, a235\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a235, %0\n\tv_accvgpr_read_b32 %0, a236\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a236, %0\n\tv_accvgpr_read_b32 %0, a237\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a237, %0\n\tv_accvgpr_read_b32 %0, a238\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a238, %0\n\tv_accvgpr_read_b32 %0, a239\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a239, %0\n\ts_nop 2" : "=&v"(t) : "v"(alpha) : W64_CLOB_T6);
+  if constexpr (T == 7) asm volatile("v_accvgpr_read_b32 %0, a240\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a240, %0\n\tv_accvgpr_read_b32 %0, a241\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a241, %0\n\tv_accvgpr_read_b32 %0, a242\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a242, %0\n\tv_accvgpr_read_b32 %0, a243\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a243, %0\n\tv_accvgpr_read_b32 %0, a244\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a244, %0\n\tv_accvgpr_read_b32 %0, a245\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a245, %0\n\tv_accvgpr_read_b32 %0, a246\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a246, %0\n\tv_accvgpr_read_b32 %0, a247\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a247, %0\n\tv_accvgpr_read_b32 %0, a248\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a248, %0\n\tv_accvgpr_read_b32 %0, a249\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a249, %0\n\tv_accvgpr_read_b32 %0, a250\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a250, %0\n\tv_accvgpr_read_b32 %0, a251\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a251, %0\n\tv_accvgpr_read_b32 %0, a252\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a252, %0\n\tv_accvgpr_read_b32 %0, a253\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a253, %0\n\tv_accvgpr_read_b32 %0, a254\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a254, %0\n\tv_accvgpr_read_b32 %0, a255\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a255, %0\n\ts_nop 2" : "=&v"(t) : "v"(alpha) : W64_CLOB_T7);
+  (void)t;
+}
+DEV_INLINE void w64_pv_t(const int T, const bf16x8& va, const bf16x8& p) {
+  switch (T) {
+    case 0: w64_pv<0>(va, p); break;
+    case 1: w64_pv<1>(va, p); break;
+    case 2: w64_pv<2>(va, p); break;
+    case 3: w64_pv<3>(va, p); break;
+    case 4: w64_pv<4>(va, p); break;
+    case 5: w64_pv<5>(va, p); break;
+    case 6: w64_pv<6>(va, p); break;
+    default: w64_pv<7>(va, p); break;
+  }
+}
+// wait states between the last PV MFMA writing O and any read of it (8-pass XDL: 12; padded to 24)
+DEV_INLINE void w64_o_wait() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
+// read O tile T into registers (after w64_o_wait)
+template <int T>
+DEV_INLINE f32x16 w64_o_read() {
+  float r[16];
+  if constexpr (T == 0) asm volatile("v_accvgpr_read_b32 %0, a128\n\tv_accvgpr_read_b32 %1, a129\n\tv_accvgpr_read_b32 %2, a130\n\tv_accvgpr_read_b32 %3, a131\n\tv_accvgpr_read_b32 %4, a132\n\tv_accvgpr_read_b32 %5, a133\n\tv_accvgpr_read_b32 %6, a134\n\tv_accvgpr_read_b32 %7, a135\n\tv_accvgpr_read_b32 %8, a136\n\tv_accvgpr_read_b32 %9, a137\n\tv_accvgpr_read_b32 %10, a138\n\tv_accvgpr_read_b32 %11, a139\n\tv_accvgpr_read_b32 %12, a140\n\tv_accvgpr_read_b32 %13, a141\n\tv_accvgpr_read_b32 %14, a142\n\tv_accvgpr_read_b32 %15, a143\n\t" : "=v"(r[0]), "=v"(r[1]), "=v"(r[2]), "=v"(r[3]), "=v"(r[4]), "=v"(r[5]), "=v"(r[6]), "=v"(r[7]), "=v"(r[8]), "=v"(r[9]), "=v"(r[10]), "=v"(r[11]), "=v"(r[12]), "=v"(r[13]), "=v"(r[14]), "=v"(r[15]));
+  if constexpr (T == 1) asm volatile("v_accvgpr_read_b32 %0, a144\n\tv_accvgpr_read_b32 %1, a145\n\tv_accvgpr_read_b32 %2, a146\n\tv_accvgpr_read_b32 %3, a147\n\tv_accvgpr_read_b32 %4, a148\n\tv_accvgpr_read_b32 %5, a149\n\tv_accvgpr_read_b32 %6, a150\n\tv_accvgpr_read_b32 %7, a151\n\tv_accvgpr_read_b32 %8, a152\n\tv_accvgpr_read_b32 %9, a153\n\tv_accvgpr_read_b32 %10, a154\n\tv_accvgpr_read_b32 %11, a155\n\tv_accvgpr_read_b32 %12, a156\n\tv_accvgpr_read_b32 %13, a157\n\tv_accvgpr_read_b32 %14, a158\n\tv_accvgpr_read_b32 %15, a159\n\t" : "=v"(r[0]), "=v"(r[1]), "=v"(r[2]), "=v"(r[3]), "=v"(r[4]), "=v"(r[5]), "=v"(r[6]), "=v"(r[7]), "=v"(r[8]), "=v"(r[9]), "=v"(r[10]), "=v"(r[11]), "=v"(r[12]), "=v"(r[13]), "=v"(r[14]), "=v"(r[15]));
+  if constexpr (T == 2) asm volatile("v_accvgpr_read_b32 %0, a160\n\tv_accvgpr_read_b32 %1, a161\n\tv_accvgpr_read_b32 %2, a162\n\tv_accvgpr_read_b32 %3, a163\n\tv_accvgpr_read_b32 %4, a164\n\tv_accvgpr_read_b32 %5, a165\n\tv_accvgpr_read_b32 %6, a166\n\tv_accvgpr_read_b32 %7, a167\n\tv_accvgpr_read_b32 %8, a168\n\tv_accvgpr_read_b32 %9, a169\n\tv_accvgpr_read_b32 %10, a170\n\tv_accvgpr_read_b32 %11, a171\n\tv_accvgpr_read_b32 %12, a172\n\tv_accvgpr_read_b32 %13, a173\n\tv_accvgpr_read_b32 %14, a174\n\tv_accvgpr_read_b32 %15, a175\n\t" : "=v"(r[0]), "=v"(r[1]), "=v"(r[2]), "=v"(r[3]), "=v"(r[4]), "=v"(r[5]), "=v"(r[6]), "=v"(r[7]), "=v"(r[8]), "=v"(r[9]), "=v"(r[10]), "=v"(r[11]), "=v"(r[12]), "=v"(r[13]), "=v"(r[14]), "=v"(r[15]));
+  if constexpr (T == 3) asm volatile("v_accvgpr_read_b32 %0, a176\n\tv_accvgpr_read_b32 %1, a177\n\tv_accvgpr_read_b32 %2, a178\n\tv_accvgpr_read_b32 %3, a179\n\tv_accvgpr_read_b32 %4, a180\n\tv_accvgpr_read_b32 %5, a181\n\tv_accvgpr_read_b32 %6, a182\n\tv_accvgpr_read_b32 %7, a183\n\tv_accvgpr_read_b32 %8, a184\n\tv_accvgpr_read_b32 %9, a185\n\tv_accvgpr_read_b32 %10, a186\n\tv_accvgpr_read_b32 %11, a187\n\tv_accvgpr_read_b32 %12, a188\n\tv_accvgpr_read_b32 %13, a189\n\tv_accvgpr_read_b32 %14, a190\n\tv_accvgpr_read_b32 %15, a191\n\t" : "=v"(r[0]), "=v"(r[1]), "=v"(r[2]), "=v"(r[3]), "=v"(r[4]), "=v"(r[5]), "=v"(r[6]), "=v"(r[7]), "=v"(r[8]), "=v"(r[9]), "=v"(r[10]), "=v"(r[11]), "=v"(r[12]), "=v"(r[13]), "=v"(r[14]), "=v"(r[15]));
+  if constexpr (T == 4) asm volatile("v_accvgpr_read_b32 %0, a192\n\tv_accvgpr_read_b32 %1, a193\n\tv_accvgpr_read_b32 %2, a194\n\tv_accvgpr_read_b32 %3, a195\n\tv_accvgpr_read_b32 %4, a196\n\tv_accvgpr_read_b32 %5, a197\n\tv_accvgpr_read_b32 %6, a198\n\tv_accvgpr_read_b32 %7, a199\n\tv_accvgpr_read_b32 %8, a200\n\tv_accvgpr_read_b32 %9, a201\n\tv_accvgpr_read_b32 %10, a202\n\tv_accvgpr_read_b32 %11, a203\n\tv_accvgpr_read_b32 %12, a204\n\tv_accvgpr_read_b32 %13, a205\n\tv_accvgpr_read_b32 %14, a206\n\tv_accvgpr_read_b32 %15, a207\n\t" : "=v"(r[0]), "=v"(r[1]), "=v"(r[2]), "=v"(r[3]), "=v"(r[4]), "=v"(r[5]), "=v"(r[6]), "=v"(r[7]), "=v"(r[8]), "=v"(r[9]), "=v"(r[10]), "=v"(r[11]), "=v"(r[12]), "=v"(r[13]), "=v"(r[14]), "=v"(r[15]));
+  if constexpr (T == 5) asm volatile("v_accvgpr_read_b32 %0, a208\n\tv_accvgpr_read_b32 %1, a209\n\tv_accvgpr_read_b32 %2, a210\n\tv_accvgpr_read_b32 %3, a211\n\tv_accvgpr_read_b32 %4, a212\n\tv_accvgpr_read_b32 %5, a213\n\tv_accvgpr_read_b32 %6, a214\n\tv_accvgpr_read_b32 %7, a215\n\tv_accvgpr_read_b32 %8, a216\n\tv_accvgpr_read_b32 %9, a217\n\tv_accvgpr_read_b32 %10, a218\n\tv_accvgpr_read_b32 %11, a219\n\tv_accvgpr_read_b32 %12, a220\n\tv_accvgpr_read_b32 %13, a221\n\tv_accvgpr_read_b32 %14, a222\n\tv_accvgpr_read_b32 %15, a223\n\t" : "=v"(r[0]), "=v"(r[1]), "=v"(r[2]), "=v"(r[3]), "=v"(r[4]), "=v"(r[5]), "=v"(r[6]), "=v"(r[7]), "=v"(r[8]), "=v"(r[9]), "=v"(r[10]), "=v"(r[11]), "=v"(r[12]), "=v"(r[13]), "=v"(r[14]), "=v"(r[15]));
+  if constexpr (T == 6) asm volatile("v_accvgpr_read_b32 %0, a224\n\tv_accvgpr_read_b32 %1, a225\n\tv_accvgpr_read_b32 %2, a226\n\tv_accvgpr_read_b32 %3, a227\n\tv_accvgpr_read_b32 %4, a228\n\tv_accvgpr_read_b32 %5, a229\n\tv_accvgpr_read_b32 %6, a230\n\tv_accvgpr_read_b32 %7, a231\n\tv_accvgpr_read_b32 %8, a232\n\tv_accvgpr_read_b32 %9, a233\n\tv_accvgpr_read_b32 %10, a234\n\tv_accvgpr_read_b32 %11, a235\n\tv_accvgpr_read_b32 %12, a236\n\tv_accvgpr_read_b32 %13, a237\n\tv_accvgpr_read_b32 %14, a238\n\tv_accvgpr_read_b32 %15, a239\n\t" : "=v"(r[0]), "=v"(r[1]), "=v"(r[2]), "=v"(r[3]), "=v"(r[4]), "=v"(r[5]), "=v"(r[6]), "=v"(r[7]), "=v"(r[8]), "=v"(r[9]), "=v"(r[10]), "=v"(r[11]), "=v"(r[12]), "=v"(r[13]), "=v"(r[14]), "=v"(r[15]));
+  if constexpr (T == 7) asm volatile("v_accvgpr_read_b32 %0, a240\n\tv_accvgpr_read_b32 %1, a241\n\tv_accvgpr_read_b32 %2, a242\n\tv_accvgpr_read_b32 %3, a243\n\tv_accvgpr_read_b32 %4, a244\n\tv_accvgpr_read_b32 %5, a245\n\tv_accvgpr_read_b32 %6, a246\n\tv_accvgpr_read_b32 %7, a247\n\tv_accvgpr_read_b32 %8, a248\n\tv_accvgpr_read_b32 %9, a249\n\tv_accvgpr_read_b32 %10, a250\n\tv_accvgpr_read_b32 %11, a251\n\tv_accvgpr_read_b32 %12, a252\n\tv_accvgpr_read_b32 %13, a253\n\tv_accvgpr_read_b32 %14, a254\n\tv_accvgpr_read_b32 %15, a255\n\t" : "=v"(r[0]), "=v"(r[1]), "=v"(r[2]), "=v"(r[3]), "=v"(r[4]), "=v"(r[5]), "=v"(r[6]), "=v"(r[7]), "=v"(r[8]), "=v"(r[9]), "=v"(r[10]), "=v"(r[11]), "=v"(r[12]), "=v"(r[13]), "=v"(r[14]), "=v"(r[15]));
+  f32x16 v;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = r[i];
+  return v;
+}
+DEV_INLINE f32x16 w64_o_read_t(const int T) {
+  switch (T) {
+    case 0: return w64_o_read<0>();
+    case 1: return w64_o_read<1>();
+    case 2: return w64_o_read<2>();
+    case 3: return w64_o_read<3>();
+    case 4: return w64_o_read<4>();
+    case 5: return w64_o_read<5>();
+    case 6: return w64_o_read<6>();
+    default: return w64_o_read<7>();
+  }
+}
 #define W64_GAP() __builtin_amdgcn_sched_barrier(0)
 
 template <int D>
@@ -570,20 +671,13 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
         (lds_s16x4*)(Vr + (t & 1) * TILE + vto[f >> 2][h] + (f & 3) * 16 * D * 2));
   };
 
-  f32x16 o[2][DT];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int t = 0; t < DT; ++t)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) o[j][t][i] = 0.f;
-  W64_O_SYNC("s_nop 1");  // the zeros are in the accumulators before the first asm MFMA reads them
+  w64_o_zero();  // O: a[128:255], owned by the asm helpers above
   float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f}, alpha[2] = {1.f, 1.f}, rs[2] = {0.f, 0.f};
   bool resc = false;
   f32x16 sA[2][2], sB[2][2];  // S of the tile being started / finished (parity buffers)
   uint4 pA[2][4], pB[2][4];   // P^T fragments as packed bf16 words (parity buffers)
   uint4 kq[2][4];             // K / Q fragments of k-steps st (slot st & 1) and st + 1: {k kt0, k kt1, q j0, q j1}
-  s16x4 vf[3][2];             // V^T fragments, ring of three (two tr-reads each)
+  s16x4 vf[3][2];  // V^T fragments (two tr-reads each), ring of three, read two fragments ahead
 
   auto sync = [&]() __attribute__((always_inline)) {
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMA pieces of the last iteration landed
@@ -592,14 +686,15 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
   };
   auto rescale = [&]() __attribute__((always_inline)) {
     if (resc) {
-      W64_O_SYNC("s_nop 7\n\ts_nop 7\n\ts_nop 7");  // the last PV MFMA's result is readable
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) o[j][dt][i] *= alpha[j];
-      W64_O_SYNC("s_nop 1");  // v_accvgpr_write -> MFMA operand
+      w64_o_wait();  // the last PV MFMA's result is readable
+      w64_o_scale<0>(alpha[0]);
+      w64_o_scale<1>(alpha[0]);
+      w64_o_scale<2>(alpha[0]);
+      w64_o_scale<3>(alpha[0]);
+      w64_o_scale<4>(alpha[1]);
+      w64_o_scale<5>(alpha[1]);
+      w64_o_scale<6>(alpha[1]);
+      w64_o_scale<7>(alpha[1]);
       resc = false;
     }
   };
@@ -681,7 +776,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
           }
           const s16x4 v1 = vf[f % 3][0], v2 = vf[f % 3][1];
           const s16x8 va = {v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
-          w64_pv(o[j][f >> 2], __builtin_bit_cast(bf16x8, va), as_bf8(po[j][f & 3]));
+          w64_pv_t(4 * j + (f >> 2), __builtin_bit_cast(bf16x8, va), as_bf8(po[j][f & 3]));
         }
         if (g >= 28 && more) {  // X_{i+1}'s first k-step: K(i+1) (landed two tiles ahead) and Q
           const int u = g - 28;
@@ -701,7 +796,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
         } else if (g == 9) {
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj) {
-            const bool need = mt[jj] > m[jj] + 8.0f;
+            const bool need = mt[jj] > m[jj] + W64_DEFER;
             const float mn = need ? fmaxf(m[jj], mt[jj]) : m[jj];
             const float al = __builtin_amdgcn_exp2f(m[jj] - ((mn == -INFINITY) ? 0.f : mn));
             alpha[jj] = al;
@@ -735,19 +830,35 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     }
     float r[2] = {rs[0], rs[1]}, ev[2][2];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int jo = 0; jo < 2; ++jo) {
+      const int j = W64_TAIL_J1FIRST ? 1 - jo : jo;
       const float mref = (m[j] == -INFINITY) ? 0.f : m[j];
 #pragma unroll
       for (int e = 16; e < 32; ++e) exp_el(so, po, r, j, e, i - 1, mask, mref, ev);
       l[j] += r[j];
     }
+    if (W64_TAIL_NOP) {
+      W64_GAP();
+      asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
+      W64_GAP();
+    }
+    // the same V ring as Y_i
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      vf[f][0] = rd_v(i - 1, f, 0);
+      vf[f][1] = rd_v(i - 1, f, 1);
+    }
 #pragma unroll
     for (int f = 0; f < 16; ++f) {
-      const s16x4 v1 = rd_v(i - 1, f, 0), v2 = rd_v(i - 1, f, 1);
-      const s16x8 va = {v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
       W64_GAP();
-      w64_pv(o[0][f >> 2], __builtin_bit_cast(bf16x8, va), as_bf8(po[0][f & 3]));
-      w64_pv(o[1][f >> 2], __builtin_bit_cast(bf16x8, va), as_bf8(po[1][f & 3]));
+      if (f + 2 < 16) {
+        vf[(f + 2) % 3][0] = rd_v(i - 1, f + 2, 0);
+        vf[(f + 2) % 3][1] = rd_v(i - 1, f + 2, 1);
+      }
+      const s16x4 v1 = vf[f % 3][0], v2 = vf[f % 3][1];
+      const s16x8 va = {v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
+      w64_pv_t(f >> 2, __builtin_bit_cast(bf16x8, va), as_bf8(po[0][f & 3]));
+      w64_pv_t(4 + (f >> 2), __builtin_bit_cast(bf16x8, va), as_bf8(po[1][f & 3]));
     }
   };
 
@@ -792,7 +903,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     }
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // no LDS-DMA may outlive the workgroup
-  W64_O_SYNC("s_nop 7\n\ts_nop 7\n\ts_nop 7");  // the last PV MFMA's result is readable
+  w64_o_wait();  // the last PV MFMA's result is readable
 
   // ---- epilogue per block: normalise, 16-byte O stores, LSE (natural log)
 #pragma unroll
@@ -803,11 +914,12 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     uint16_t* op = a.o + ((long long)b * S + qrow) * a.o_rs + (long long)hq * D;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
+      const f32x16 ov = w64_o_read_t(4 * j + dt);
       uint32_t w[4][2];
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
-        w[g4][0] = pack_bf2(o[j][dt][4 * g4 + 0] * inv, o[j][dt][4 * g4 + 1] * inv);
-        w[g4][1] = pack_bf2(o[j][dt][4 * g4 + 2] * inv, o[j][dt][4 * g4 + 3] * inv);
+        w[g4][0] = pack_bf2(ov[4 * g4 + 0] * inv, ov[4 * g4 + 1] * inv);
+        w[g4][1] = pack_bf2(ov[4 * g4 + 2] * inv, ov[4 * g4 + 3] * inv);
       }
       const auto a0 = __builtin_amdgcn_permlane32_swap(w[0][0], w[2][0], false, false);
       const auto a1 = __builtin_amdgcn_permlane32_swap(w[0][1], w[2][1], false, false);

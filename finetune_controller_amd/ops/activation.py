@@ -12,7 +12,7 @@ import torch
 import torch.nn.functional as F
 
 from ._backend import ext, use_hip
-from .linear import LoRATail, mark_prefilled
+from .linear import LoRATail, gate_wgrad_stream, mark_prefilled
 
 _FUSED_OFF = False  # True: separate tail GEMMs (A/B by patching; profiles/r1_bench_fused_swiglu_tail*.log)
 
@@ -43,6 +43,7 @@ class _SwiGLUHip(torch.autograd.Function):
                                         t.split)
             mark_prefilled("bwd", dgu, t.aug)
             return dgu, None, None, None, None
+        gate_wgrad_stream()
         dgu = ext().swiglu_bwd(da2.contiguous(), gu2, ctx.grad_pad)
         return (dgu if ctx.grad_pad else dgu.view(ctx.shp)), None, None, None, None
 

@@ -27,6 +27,7 @@ import torch
 import torch.nn.functional as F
 
 from ._backend import ext, use_hip
+from .linear import gate_wgrad_stream as _gate_dw
 
 
 # flipped to True once csrc/kernels/flash_attn.hip replaces the stub launcher
@@ -216,6 +217,7 @@ class _FlashPacked(torch.autograd.Function):
         dq, dk, dv = _split(dqkv, B, S, H, KV, D)
         docs = ctx.docs
         rg = ctx.rope_grad
+        _gate_dw()
         ext().flash_bwd(q, k, v, o, do, lse, dq, dk, dv, B, S, H, KV, D, scale, causal, window,
                         docs.doc_start if docs is not None else None, docs.doc_end if docs is not None else None,
                         -1, rg.cos if rg is not None else None, rg.sin if rg is not None else None,
@@ -306,6 +308,7 @@ class _FlashPaddedTail(torch.autograd.Function):
         q, k, v = _split(qkv_p, B, Sp, H, KV, Dp)
         dq, dk, dv = _split(dqkv_p, B, Sp, H, KV, Dp)
         docs = ctx.docs
+        _gate_dw()
         ext().flash_bwd(q, k, v, o_p, do_p, lse, dq, dk, dv, B, Sp, H, KV, Dp, scale, causal, window,
                         docs.doc_start if docs is not None else None, docs.doc_end if docs is not None else None,
                         -1 if causal or Sp == S else S)

@@ -207,6 +207,24 @@ def join_wgrad_stream() -> None:
         _DW_PENDING.clear()
 
 
+# ``FTC_DW_GATE`` (VERDICT r5 Next #6): the HBM-bound backward kernels (SwiGLU, RMSNorm, flash attention
+# backward) wait for the in-flight side-stream dW before they launch, so a dW GEMM overlaps only the input-
+# gradient GEMM it was issued beside, never a stream kernel it would starve (swiglu_bwd 1.85 ms/call under
+# overlap vs 0.41 serial, profiles/r5/kernel_tables/full_ft.md).
+_DW_GATE = os.environ.get("FTC_DW_GATE", "0") == "1"
+
+
+def set_wgrad_gate(on: bool) -> None:
+    global _DW_GATE
+    _DW_GATE = bool(on)
+
+
+def gate_wgrad_stream() -> None:
+    """Called by the HBM-bound backward kernels before they launch: join the side-stream dW when gated."""
+    if _DW_GATE:
+        join_wgrad_stream()
+
+
 def wgrad_launch_stream():
     """The stream gradient collectives must be enqueued on (parallel.ddp): the side stream, after it has
     waited for the main stream, while side-stream weight gradients are in flight; else None (current)."""

@@ -11,6 +11,7 @@ import torch
 import torch.nn.functional as F
 
 from ._backend import ext, use_hip
+from .linear import gate_wgrad_stream
 
 
 def _rms_ref(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
@@ -43,6 +44,7 @@ class _AddRMSNormHip(torch.autograd.Function):
             if dres.stride(1) != 1 or dres.stride(0) % 8 or dres.data_ptr() % 16:
                 dres = dres.contiguous()  # (row-padded views from the next norm are read in place)
         need_dw = ctx.needs_input_grad[2]
+        gate_wgrad_stream()
         outs = ext().rmsnorm_bwd(dy2, hn, w, rstd, dres, need_dw, ctx.grad_pad)
         dx = outs[0] if ctx.grad_pad else outs[0].view(ctx.shp)
         dw = outs[1].to(w.dtype) if need_dw else None

@@ -5,7 +5,10 @@ hipcc pads no hazard for an `asm` statement's operands (guide §5.7 item 2).  Th
 (csrc/kernels/flash_attn_fwd.hip) issues its PV MFMAs as inline asm on VGPR A/B operands, so a VALU write
 of one of those registers within the two preceding instructions would be read stale.  This walks every
 asm MFMA (between ;;#ASMSTART / ;;#ASMEND) and fails when a VALU instruction among the previous
-`--window` instructions writes a register of its A or B operand.
+`--window` instructions writes a register of its A or B operand (RAW), and when any compiler instruction
+touches an accumulator register of the kernel-owned range (`owned` and up: the W64 forward's O).  Writes of
+an A / B register right AFTER an MFMA (WAR) are listed for information only: the hardware reads A / B at
+issue, and hipcc emits the same pattern after its own builtin MFMAs.
 
     hipcc --offload-arch=gfx950 -O3 -S --cuda-device-only ... -o fwd.s && python tools/check_asm_hazards.py fwd.s
 """
@@ -21,7 +24,16 @@ def regs(tok: str) -> set[int]:
     return {int(m.group(1))} if m else set()
 
 
-def main(path: str, window: int = 3) -> int:
+def agprs(text: str) -> set[int]:
+    out = set()
+    for lo, hi in re.findall(r"\ba\[(\d+):(\d+)\]", text):
+        out |= set(range(int(lo), int(hi) + 1))
+    for r in re.findall(r"\ba(\d+)\b", text):
+        out.add(int(r))
+    return out
+
+
+def main(path: str, window: int = 3, owned: int = 128) -> int:
     lines = [ln.strip() for ln in open(path)]
     inasm, bad, n = False, [], 0
     recent: list[str] = []  # compiler instructions before the current point
@@ -47,11 +59,43 @@ def main(path: str, window: int = 3) -> int:
                     bad.append(f"line {k + 1}: {prev}  ->  {ln}")
         if not inasm:
             recent.append(ln)
-    print(f"{n} asm MFMAs checked, {len(bad)} VALU-write -> operand hazards")
+    # WAR pass: instructions after each asm MFMA (compiler or asm) that write its A / B registers
+    war = []
+    flat = [(k, ln) for k, ln in enumerate(lines) if ln and not ln.startswith((";", ".")) and not ln.endswith(":")]
+    for idx, (k, ln) in enumerate(flat):
+        if ln.startswith("v_mfma") and "a[" in ln.split(",")[0]:
+            ops = [t.strip() for t in ln.split(None, 1)[1].split(",")]
+            used = regs(ops[1]) | regs(ops[2])
+            for k2, nxt in flat[idx + 1: idx + 1 + 2 * window]:
+                op = nxt.split(None, 1)
+                if len(op) < 2 or op[0].startswith(("s_", "v_mfma", "buffer_", "global_store", "ds_write")):
+                    continue
+                dst = regs(op[1].split(",")[0].strip())
+                if dst & used:
+                    war.append(f"line {k2 + 1}: {nxt}  after  line {k + 1}: {ln}")
+    # ownership: accumulator registers >= `owned` belong to the kernel's asm; the compiler must not touch them
+    inasm, own, comp_agpr = False, [], 0
+    for k, ln in enumerate(lines):
+        if ln.startswith(";;#ASMSTART"):
+            inasm = True
+        elif ln.startswith(";;#ASMEND"):
+            inasm = False
+        elif not inasm and ln and not ln.startswith((";", ".")) and not ln.endswith(":"):
+            regs_a = agprs(ln.split(";")[0])
+            if regs_a:
+                comp_agpr += 1
+                if max(regs_a) >= owned:
+                    own.append(f"line {k + 1}: {ln}")
+    print(f"compiler instructions touching accumulator registers: {comp_agpr}; inside the owned range a[{owned}:]: {len(own)}")
+    for o in own[:10]:
+        print("  " + o)
+    bad += own
+    print(f"{n} asm MFMAs checked, {len(bad)} write -> operand (RAW) hazards ({len(war)} WAR reuses, informational)")
     for b in bad[:20]:
         print("  " + b)
     return 1 if bad or n == 0 else 0
 
 
 if __name__ == "__main__":
-    sys.exit(main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 3))
+    sys.exit(main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 3,
+                  int(sys.argv[3]) if len(sys.argv) > 3 else 128))

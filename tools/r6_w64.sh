@@ -1,12 +1,14 @@
 #!/bin/bash
-# Round 6: W64 flash forward on one GPU -> gpurun_out/r6_w64/ (numerics first; timing only if they pass)
+# Round 6: W64 flash forward on one GPU -> gpurun_out/<out>/ (numerics first; timing only if they pass)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r6_w64}; mkdir -p $O
+timeout -k 10 120 python -u tools/w64_lab/diag.py > $O/lab_diag.log 2>&1 || { tail -20 $O/lab_diag.log; exit 1; }
+grep -v amdgpu.ids $O/lab_diag.log
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py \
   -k "flash_fwd_w64 or flash_attention_fwd_bwd or flash_lse or flash_bwd_rope or llama3_8b" > $O/pytest.log 2>&1 \
-  || { tail -40 $O/pytest.log; exit 1; }
+  || { grep -E "^E|FAILED|Error" $O/pytest.log | head -30; exit 1; }
 grep -E "passed|failed" $O/pytest.log | tail -2; grep "^w64" $O/pytest.log | head -20
 timeout -k 10 180 python -u tools/bench_fwd_variants.py > $O/fwd_ab.log 2>&1 || { tail $O/fwd_ab.log; exit 1; }
-cat $O/fwd_ab.log | grep variant
+grep variant $O/fwd_ab.log

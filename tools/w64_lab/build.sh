@@ -1,0 +1,12 @@
+#!/bin/bash
+# Build variants of the flash forward (csrc/kernels/flash_attn_fwd.hip) as standalone ctypes libraries for
+# one-call GPU A/B and numerics experiments: tools/w64_lab/lib<name>.so (extern "C" ftc_flash_fwd*).
+set -e
+cd "$(dirname "$0")/../.."
+b() { n=$1; shift; hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Icsrc/kernels -ffp-contract=fast \
+      -mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize "$@" csrc/kernels/flash_attn_fwd.hip -o tools/w64_lab/lib$n.so; }
+b base &
+
+
+
+wait
