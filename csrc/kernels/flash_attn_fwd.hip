@@ -473,6 +473,17 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
 // Covers head_dim 128, no window / document mask / padded tail, S % 256 == 0; otherwise ftc_flash_fwd
 // runs flash_fwd_kernel.
 constexpr int W64_BQ = 256;
+// timing-only ablations for tools/w64_lab (wrong results; never set by tools/build.py): no barrier in the
+// per-tile sync, no LDS-DMA in the loop, no exponentials (P packed from raw S)
+#ifndef W64_ABL_NOBAR
+#define W64_ABL_NOBAR 0
+#endif
+#ifndef W64_ABL_NODMA
+#define W64_ABL_NODMA 0
+#endif
+#ifndef W64_ABL_NOEXP
+#define W64_ABL_NOEXP 0
+#endif
 #ifndef W64_TAIL_J1FIRST
 #define W64_TAIL_J1FIRST 0
 #endif
@@ -682,7 +693,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
   auto sync = [&]() __attribute__((always_inline)) {
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMA pieces of the last iteration landed
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-    __builtin_amdgcn_s_barrier();        // ... everyone's; every read of a slot about to be refilled is done
+    if (!W64_ABL_NOBAR) __builtin_amdgcn_s_barrier();  // ... everyone's; every read of a slot about to be refilled is done
   };
   auto rescale = [&]() __attribute__((always_inline)) {
     if (resc) {
@@ -709,7 +720,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
   auto exp_el = [&](const f32x16 (&sv)[2][2], uint4 (&pw)[2][4], float (&r)[2], const int j, const int e,
                     const int t, const bool mask, const float mref, float (&ev)[2][2]) __attribute__((always_inline)) {
     const int kt = e >> 4, i = e & 15;
-    const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(masked(sv[j][kt][i], j, e, t, mask), c, -mref));
+    const float p = W64_ABL_NOEXP ? sv[j][kt][i] : __builtin_amdgcn_exp2f(__builtin_fmaf(masked(sv[j][kt][i], j, e, t, mask), c, -mref));
     r[j] += p;
     ev[j][i & 1] = p;
     if (i & 1) {
@@ -748,7 +759,8 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
         if (!first) exp_el(so, po, r, g >> 4, 16 + (g & 15), i - 1, false, mref_o[g >> 4], ev);
         // past the last tile the DMA repeats the last K tile into the slot K(i-1) left: nobody reads it
         // again, and the branch-free gap keeps every wave's DMA count equal
-        if (g < NGT) {
+        if (W64_ABL_NODMA) {
+        } else if (g < NGT) {
           dma_k(min(i + 2, ntiles - 1), g, (i + 2) % 3);
         } else if (g < 2 * NGT) {
           dma_v(i, g - NGT);

@@ -79,3 +79,25 @@ def test_run_patched_sets_module_constants_before_the_script(tmp_path):
                        capture_output=True, text=True, cwd=ROOT, timeout=120)
     assert r.returncode == 0, r.stderr
     assert "argv ['--steps', '2']" in r.stdout and "val 3" in r.stdout
+
+
+def test_w64_forward_owns_its_accumulators(tmp_path):
+    """The W64 flash forward keeps O in accumulator registers a[128:255] that only its inline asm touches
+    (csrc/kernels/flash_attn_fwd.hip): compiled with the build's own flags, no compiler instruction may
+    touch that range and no VALU write may feed an asm MFMA operand unpadded (tools/check_asm_hazards.py)."""
+    import shutil
+
+    if shutil.which("hipcc") is None:
+        pytest.skip("hipcc not available")
+    sys.path.insert(0, ROOT)
+    from finetune_controller_amd.tools.build import EXTRA_FLAGS
+
+    src = os.path.join(ROOT, "csrc", "kernels", "flash_attn_fwd.hip")
+    out = str(tmp_path / "fwd.s")
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-S", "--cuda-device-only",
+                    "-I", os.path.join(ROOT, "csrc", "kernels"), "-ffp-contract=fast",
+                    *EXTRA_FLAGS["flash_attn_fwd.hip"], src, "-o", out], check=True, capture_output=True)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_asm_hazards.py"), out],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout
+    assert "inside the owned range a[128:]: 0" in r.stdout and "0 write -> operand (RAW)" in r.stdout
