@@ -41,8 +41,7 @@ DEV_INLINE u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, int voff_bytes, int soff_b
 // completion with explicit vmcnt waits.  M0 is saved / restored inside the statement (compiler-
 // reserved).  The operands must come from SALU (kernel arguments, blockIdx / readfirstlane-derived
 // values computed well before): no VALU-written SGPR hazard is padded here.
-DEV_INLINE void lds_dma16(__amdgpu_buffer_rsrc_t r, const void* lds, int voff, int soff) {
-  const unsigned dst = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)lds;
+DEV_INLINE void lds_dma16_at(__amdgpu_buffer_rsrc_t r, unsigned dst, int voff, int soff) {
   unsigned keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
@@ -50,6 +49,17 @@ DEV_INLINE void lds_dma16(__amdgpu_buffer_rsrc_t r, const void* lds, int voff, i
       : "=&s"(keep)
       : "v"(voff), "s"(r), "s"(dst), "s"(soff)
       : "memory");
+}
+DEV_INLINE unsigned lds_addr(const void* lds) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)lds;
+}
+DEV_INLINE void lds_dma16(__amdgpu_buffer_rsrc_t r, const void* lds, int voff, int soff) {
+  lds_dma16_at(r, lds_addr(lds), voff, soff);
+}
+// the same with the LDS destination made provably wave-uniform (readfirstlane: an SGPR for the M0 write,
+// which is an SALU read of it -- no VALU-written-SGPR wait states needed, guide §5.7 item 2)
+DEV_INLINE void lds_dma16_u(__amdgpu_buffer_rsrc_t r, const void* lds, int voff, int soff) {
+  lds_dma16_at(r, __builtin_amdgcn_readfirstlane(lds_addr(lds)), voff, soff);
 }
 
 DEV_INLINE float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }

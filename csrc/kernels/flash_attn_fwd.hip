@@ -109,9 +109,9 @@ struct FwdArgs {
 };
 
 // logical block -> (qb, b, kvh, g) with heavy-first order and GQA groups co-located on one XCD
-DEV_INLINE void decode_block(const FwdArgs& a, int& qb, int& b, int& hq, int& kvh) {
+DEV_INLINE void decode_block(const FwdArgs& a, int& qb, int& b, int& hq, int& kvh, const int bid_in = -1) {
   const int G = a.H / a.KV;
-  const int bid = blockIdx.x;
+  const int bid = bid_in < 0 ? (int)blockIdx.x : bid_in;
   const int ngroups = a.nqb * a.B * a.KV;
   int j, g;
   if ((ngroups & 7) == 0) {
@@ -612,17 +612,39 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hh = lane >> 5, lr = lane & 31;
-  int qb, b, hq, kvh;
-  decode_block(a, qb, b, hq, kvh);
   const int S = a.S;
-  const int q0 = qb * W64_BQ, wq0 = q0 + 64 * wave;
-  const int ntiles = a.causal ? (q0 + W64_BQ) / BK : S / BK;
-  const int wtiles = a.causal ? (wq0 + 64) / BK : ntiles;
   const float c = a.scale_log2;
+  // persistent schedule: this workgroup's n-th block.  Rounds of gridDim blocks in decode_block's order
+  // (heaviest causal blocks first, the q heads of one kv head on one XCD); odd rounds run mirrored inside
+  // each XCD column (low three bits kept), so the causal weights even out over the rounds
+  const int total = a.nqb * a.B * a.H;
+  const int G = gridDim.x;
+  auto sched = [&](const int n) __attribute__((always_inline)) -> int {
+    const int p = blockIdx.x;
+    int pos = p;
+    if (n & 1) pos = (G & 7) == 0 ? (((G >> 3) - 1 - (p >> 3)) << 3) | (p & 7) : G - 1 - p;
+    return n * G + pos;
+  };
+  // block variables are loop-carried through the persistent loop: readfirstlane keeps them (and every DMA
+  // descriptor / offset derived from them by SALU) provably wave-uniform
+  auto rfl = [](const int x) __attribute__((always_inline)) { return __builtin_amdgcn_readfirstlane(x); };
+  int qb, b, hq, kvh;
+  decode_block(a, qb, b, hq, kvh, sched(0));
+  qb = rfl(qb);
+  b = rfl(b);
+  hq = rfl(hq);
+  kvh = rfl(kvh);
+  int q0 = qb * W64_BQ, wq0 = q0 + 64 * wave;
+  int ntiles = a.causal ? (q0 + W64_BQ) / BK : S / BK;
+  int wtiles = a.causal ? (wq0 + 64) / BK : ntiles;
+  int kslot0 = 0;  // K ring slot of this block's tile 0: the K stream runs on across blocks
+  // the next block (its K(0), K(1) and Q stream in under this block's last iterations)
+  int nqb_ = 0, nb_ = 0, nhq_ = 0, nkvh_ = 0;
+  int has_next = 0;
 
-  const uint16_t* kbase = a.k + (long long)b * S * a.kv_rs + (long long)kvh * D;
-  const uint16_t* vbase = a.v + (long long)b * S * a.kv_rs + (long long)kvh * D;
-  const auto krs = make_rsrc(kbase), vrs = make_rsrc(vbase);
+  auto kv_rsrc = [&](const uint16_t* base, const int bb, const int kh) __attribute__((always_inline)) {
+    return make_rsrc(base + (long long)bb * S * a.kv_rs + (long long)kh * D);
+  };
   int voff[NGT];
 #pragma unroll
   for (int i = 0; i < NGT; ++i) {
@@ -630,31 +652,35 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     voff[i] = (row * (int)a.kv_rs + ((pc ^ swz(row)) & (NCH - 1)) * 8) * 2;
   }
   const int tstride = BK * (int)a.kv_rs * 2;  // global bytes per 64-key tile
-  // LDS-DMA of tile t of K (slot t % 3) or V (slot t % 2): piece p of this wave's NGT
-  auto dma_k = [&](const int t, const int p, const int slot) __attribute__((always_inline)) {
-    lds_dma16(krs, Kr + slot * TILE + (wave * NGT + p) * RPG * D * 2, voff[p], t * tstride);
+  // LDS-DMA of K stream tile t (t >= ntiles: the next block's tile t - ntiles; past the last block a
+  // harmless repeat into the slot it would have used: that slot held K(t - 3), read by nobody again)
+  auto dma_k = [&](const int t, const int p) __attribute__((always_inline)) {
+    const int slot = (kslot0 + t) % 3;
+    const int nxt = (t >= ntiles) & has_next;  // integer selects (SALU), never a select of descriptors
+    const int bb = nxt ? nb_ : b, kh = nxt ? nkvh_ : kvh;
+    const int tt = t < ntiles ? t : (nxt ? t - ntiles : 0);
+    lds_dma16_u(kv_rsrc(a.k, bb, kh), Kr + slot * TILE + (wave * NGT + p) * RPG * D * 2, voff[p], tt * tstride);
   };
   auto dma_v = [&](const int t, const int p) __attribute__((always_inline)) {
-    lds_dma16(vrs, Vr + (t & 1) * TILE + (wave * NGT + p) * RPG * D * 2, voff[p], t * tstride);
+    lds_dma16_u(kv_rsrc(a.v, b, kvh), Vr + (t & 1) * TILE + (wave * NGT + p) * RPG * D * 2, voff[p], t * tstride);
   };
-
-  // this wave's 64 Q rows -> Qs (swizzled row image), K(0), K(1): the block prologue
-  {
-    const uint16_t* qbase = a.q + ((long long)b * S + wq0) * a.q_rs + (long long)hq * D;
+  // this wave's 64 Q rows of block (qb', b', hq') -> Qs (swizzled row image)
+  auto dma_q = [&](const int qbx, const int bx, const int hqx) __attribute__((always_inline)) {
+    const uint16_t* qbase = a.q + ((long long)bx * S + qbx * W64_BQ + 64 * wave) * a.q_rs + (long long)hqx * D;
     const auto qrs = make_rsrc(qbase);
 #pragma unroll
     for (int p = 0; p < 16; ++p) {
       const int row = p * RPG + lane / NCH, pc = lane % NCH;
       const int qo = (row * (int)a.q_rs + ((pc ^ swz(row)) & (NCH - 1)) * 8) * 2;
-      lds_dma16(qrs, Qs + (64 * wave + p * RPG) * D * 2, qo, 0);
+      lds_dma16_u(qrs, Qs + (64 * wave + p * RPG) * D * 2, qo, 0);
     }
-  }
+  };
+  // prologue of the first block: Q, K(0), K(1)
+  dma_q(qb, b, hq);
 #pragma unroll
-  for (int p = 0; p < NGT; ++p) dma_k(0, p, 0);
-  if (ntiles > 1) {
+  for (int p = 0; p < NGT; ++p) dma_k(0, p);
 #pragma unroll
-    for (int p = 0; p < NGT; ++p) dma_k(1, p, 1);
-  }
+  for (int p = 0; p < NGT; ++p) dma_k(1, p);
 
   // lane-constant LDS offsets: K / Q fragment (row lr, chunk 2 st + hh); V^T tr-read (as flash_fwd_kernel)
   int ko[DSTEPS];
@@ -672,7 +698,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
   }
   const char* Qw = Qs + 64 * wave * D * 2;
   auto rd_k = [&](const int t, const int kt, const int st) __attribute__((always_inline)) -> uint4 {
-    return *reinterpret_cast<const uint4*>(Kr + (t % 3) * TILE + kt * HALF + ko[st]);
+    return *reinterpret_cast<const uint4*>(Kr + ((kslot0 + t) % 3) * TILE + kt * HALF + ko[st]);
   };
   auto rd_q = [&](const int j, const int st) __attribute__((always_inline)) -> uint4 {
     return *reinterpret_cast<const uint4*>(Qw + j * HALF + ko[st]);
@@ -757,11 +783,9 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
           vf[u >> 1][u & 1] = rd_v(i - 1, u >> 1, u & 1);  // V(i-1)^T fragments 0, 1 for Y_i
         }
         if (!first) exp_el(so, po, r, g >> 4, 16 + (g & 15), i - 1, false, mref_o[g >> 4], ev);
-        // past the last tile the DMA repeats the last K tile into the slot K(i-1) left: nobody reads it
-        // again, and the branch-free gap keeps every wave's DMA count equal
         if (W64_ABL_NODMA) {
         } else if (g < NGT) {
-          dma_k(min(i + 2, ntiles - 1), g, (i + 2) % 3);
+          dma_k(i + 2, g);
         } else if (g < 2 * NGT) {
           dma_v(i, g - NGT);
         }
@@ -832,14 +856,13 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
   auto tail = [&](const int i, f32x16 (&so)[2][2], uint4 (&po)[2][4], const bool mask) __attribute__((always_inline)) {
     sync();
     rescale();
-    if (i + 2 < ntiles) {
 #pragma unroll
-      for (int p = 0; p < NGT; ++p) dma_k(i + 2, p, (i + 2) % 3);
-    }
+    for (int p = 0; p < NGT; ++p) dma_k(i + 2, p);
     if (i < ntiles) {
 #pragma unroll
       for (int p = 0; p < NGT; ++p) dma_v(i, p);
     }
+    if (has_next) dma_q(nqb_, nb_, nhq_);  // this wave's Q rows are read by nobody any more
     float r[2] = {rs[0], rs[1]}, ev[2][2];
 #pragma unroll
     for (int jo = 0; jo < 2; ++jo) {
@@ -874,78 +897,109 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     }
   };
 
-  // block prologue: Q, K(0), K(1) landed; X_0's first K / Q fragments
-  sync();
-#pragma unroll
-  for (int u = 0; u < 4; ++u) kq[0][u] = u < 2 ? rd_k(0, u, 0) : rd_q(u - 2, 0);
-  body(0, sA, sB, pA, pB, true, a.causal && wtiles == 1, wtiles > 1);
-  int i = 1;
-  // steady iterations 1 .. wtiles - 2 in parity pairs; the state is back in (sA, pA) after each pair
-  for (; i + 2 < wtiles; i += 2) {
-    body(i, sB, sA, pB, pA, false, false, true);
-    body(i + 1, sA, sB, pA, pB, false, false, true);
-  }
-  if (i + 1 < wtiles) {  // one more steady iteration (odd i); then the state moves back to (sA, pA)
-    body(i, sB, sA, pB, pA, false, false, true);
-#pragma unroll
+  auto epilogue = [&]() __attribute__((always_inline)) {
+    w64_o_wait();  // the last PV MFMA's result is readable
+  #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      sA[j][1] = sB[j][1];
-      pA[j][0] = pB[j][0];
-      pA[j][1] = pB[j][1];
+      const int qrow = wq0 + 32 * j + lr;
+      const float ltot = l[j] + __shfl_xor(l[j], 32, 64);
+      const float inv = ltot > 0.f ? 1.0f / ltot : 0.f;
+      uint16_t* op = a.o + ((long long)b * S + qrow) * a.o_rs + (long long)hq * D;
+  #pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const f32x16 ov = w64_o_read_t(4 * j + dt);
+        uint32_t w[4][2];
+  #pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          w[g4][0] = pack_bf2(ov[4 * g4 + 0] * inv, ov[4 * g4 + 1] * inv);
+          w[g4][1] = pack_bf2(ov[4 * g4 + 2] * inv, ov[4 * g4 + 3] * inv);
+        }
+        const auto a0 = __builtin_amdgcn_permlane32_swap(w[0][0], w[2][0], false, false);
+        const auto a1 = __builtin_amdgcn_permlane32_swap(w[0][1], w[2][1], false, false);
+        const auto b0 = __builtin_amdgcn_permlane32_swap(w[1][0], w[3][0], false, false);
+        const auto b1 = __builtin_amdgcn_permlane32_swap(w[1][1], w[3][1], false, false);
+        const int d = dt * 32 + 16 * hh;
+        *reinterpret_cast<uint4*>(op + d) = make_uint4(a0[0], a1[0], a0[1], a1[1]);
+        *reinterpret_cast<uint4*>(op + d + 8) = make_uint4(b0[0], b1[0], b0[1], b1[1]);
+      }
+      if (hh == 0) {
+        const float lse2 = (m[j] == -INFINITY) ? -INFINITY : m[j] + __log2f(ltot);
+        a.lse[((long long)b * a.H + hq) * S + qrow] = lse2 * LN2;
+      }
     }
-    ++i;
-  }
-  if (i < wtiles) {  // the wave's last tile: the diagonal under the causal mask
-    body(i, sB, sA, pB, pA, false, a.causal != 0, false);
-    ++i;
-    tail(i, sB, pB, a.causal != 0);
-  } else {  // wtiles == 1
-    tail(i, sA, pA, a.causal != 0);
-  }
-  // waves whose rows ended keep joining the workgroup's DMA / barriers
-  for (++i; i <= ntiles; ++i) {
+  };
+
+  for (int n = 0;; ++n) {
+    {  // the next block of this workgroup, if any
+      const int nx = sched(n + 1);
+      has_next = rfl(nx < total ? 1 : 0);
+      if (has_next) {
+        decode_block(a, nqb_, nb_, nhq_, nkvh_, nx);
+        nqb_ = rfl(nqb_);
+        nb_ = rfl(nb_);
+        nhq_ = rfl(nhq_);
+        nkvh_ = rfl(nkvh_);
+      }
+    }
+    // block start: Q, K(0), K(1) landed; X_0's first K / Q fragments
     sync();
-    if (i + 2 < ntiles) {
 #pragma unroll
-      for (int p = 0; p < NGT; ++p) dma_k(i + 2, p, (i + 2) % 3);
+    for (int u = 0; u < 4; ++u) kq[0][u] = u < 2 ? rd_k(0, u, 0) : rd_q(u - 2, 0);
+    body(0, sA, sB, pA, pB, true, a.causal && wtiles == 1, wtiles > 1);
+    int i = 1;
+    // steady iterations 1 .. wtiles - 2 in parity pairs; the state is back in (sA, pA) after each pair
+    for (; i + 2 < wtiles; i += 2) {
+      body(i, sB, sA, pB, pA, false, false, true);
+      body(i + 1, sA, sB, pA, pB, false, false, true);
     }
-    if (i < ntiles) {
+    if (i + 1 < wtiles) {  // one more steady iteration (odd i); then the state moves back to (sA, pA)
+      body(i, sB, sA, pB, pA, false, false, true);
 #pragma unroll
-      for (int p = 0; p < NGT; ++p) dma_v(i, p);
+      for (int j = 0; j < 2; ++j) {
+        sA[j][1] = sB[j][1];
+        pA[j][0] = pB[j][0];
+        pA[j][1] = pB[j][1];
+      }
+      ++i;
     }
+    if (i < wtiles) {  // the wave's last tile: the diagonal under the causal mask
+      body(i, sB, sA, pB, pA, false, a.causal != 0, false);
+      ++i;
+      tail(i, sB, pB, a.causal != 0);
+    } else {  // wtiles == 1
+      tail(i, sA, pA, a.causal != 0);
+    }
+    // this wave's rows are done: store them now, under the other waves' remaining tiles
+    epilogue();
+    w64_o_zero();
+    m[0] = m[1] = -INFINITY;
+    l[0] = l[1] = 0.f;
+    rs[0] = rs[1] = 0.f;
+    alpha[0] = alpha[1] = 1.f;
+    resc = false;
+    // waves whose rows ended keep joining the workgroup's DMA / barriers
+    for (++i; i <= ntiles; ++i) {
+      sync();
+#pragma unroll
+      for (int p = 0; p < NGT; ++p) dma_k(i + 2, p);
+      if (i < ntiles) {
+#pragma unroll
+        for (int p = 0; p < NGT; ++p) dma_v(i, p);
+      }
+    }
+    if (!has_next) break;
+    kslot0 = rfl((kslot0 + ntiles) % 3);
+    qb = nqb_;
+    b = nb_;
+    hq = nhq_;
+    kvh = nkvh_;
+    q0 = qb * W64_BQ;
+    wq0 = q0 + 64 * wave;
+    ntiles = rfl(a.causal ? (q0 + W64_BQ) / BK : S / BK);
+    wtiles = rfl(a.causal ? (wq0 + 64) / BK : ntiles);
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // no LDS-DMA may outlive the workgroup
-  w64_o_wait();  // the last PV MFMA's result is readable
 
-  // ---- epilogue per block: normalise, 16-byte O stores, LSE (natural log)
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int qrow = wq0 + 32 * j + lr;
-    const float ltot = l[j] + __shfl_xor(l[j], 32, 64);
-    const float inv = ltot > 0.f ? 1.0f / ltot : 0.f;
-    uint16_t* op = a.o + ((long long)b * S + qrow) * a.o_rs + (long long)hq * D;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      const f32x16 ov = w64_o_read_t(4 * j + dt);
-      uint32_t w[4][2];
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        w[g4][0] = pack_bf2(ov[4 * g4 + 0] * inv, ov[4 * g4 + 1] * inv);
-        w[g4][1] = pack_bf2(ov[4 * g4 + 2] * inv, ov[4 * g4 + 3] * inv);
-      }
-      const auto a0 = __builtin_amdgcn_permlane32_swap(w[0][0], w[2][0], false, false);
-      const auto a1 = __builtin_amdgcn_permlane32_swap(w[0][1], w[2][1], false, false);
-      const auto b0 = __builtin_amdgcn_permlane32_swap(w[1][0], w[3][0], false, false);
-      const auto b1 = __builtin_amdgcn_permlane32_swap(w[1][1], w[3][1], false, false);
-      const int d = dt * 32 + 16 * hh;
-      *reinterpret_cast<uint4*>(op + d) = make_uint4(a0[0], a1[0], a0[1], a1[1]);
-      *reinterpret_cast<uint4*>(op + d + 8) = make_uint4(b0[0], b1[0], b0[1], b1[1]);
-    }
-    if (hh == 0) {
-      const float lse2 = (m[j] == -INFINITY) ? -INFINITY : m[j] + __log2f(ltot);
-      a.lse[((long long)b * a.H + hq) * S + qrow] = lse2 * LN2;
-    }
-  }
 }
 
 }  // namespace
@@ -965,9 +1019,17 @@ int& fwd_variant() {
   static int v = 1;
   return v;
 }
+int& fwd_persistent() {
+  static int v = 1;
+  return v;
+}
 }  // namespace
 
-extern "C" void ftc_flash_fwd_config(int variant) { fwd_variant() = variant ? 1 : 0; }
+// variant: 1 = W64 (persistent grid), 2 = W64 with one workgroup per block, 0 = the 32-row kernel everywhere
+extern "C" void ftc_flash_fwd_config(int variant) {
+  fwd_variant() = variant ? 1 : 0;
+  fwd_persistent() = variant == 2 ? 0 : 1;
+}
 
 extern "C" int ftc_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H,
                              int KV, int D, long long q_rs, long long kv_rs, long long o_rs, float scale, int causal,
@@ -978,7 +1040,20 @@ extern "C" int ftc_flash_fwd(const void* q, const void* k, const void* v, void* 
       (o_rs & 7) == 0) {
     FwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, q_rs, kv_rs, o_rs,
               B, S, H, KV, S / W64_BQ, scale * LOG2E, causal, 0, nullptr, S};
-    hipLaunchKernelGGL((flash_fwd_w64_kernel<128>), dim3(a.nqb * B * H), dim3(256), 0, stream, a);
+    // persistent: one workgroup per CU (LDS and registers allow no second), each walking its share of the
+    // blocks heaviest-first; fewer workgroups than blocks only when there are more blocks than CUs
+    static int n_cu[64] = {0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev >= 0 && dev < 64 && n_cu[dev] == 0) {
+      int v = 0;
+      if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+      n_cu[dev] = v;
+    }
+    const int cus = (dev >= 0 && dev < 64) ? n_cu[dev] : 256;
+    const int total = a.nqb * B * H;
+    const int grid = fwd_persistent() ? (total < cus ? total : cus) : total;
+    hipLaunchKernelGGL((flash_fwd_w64_kernel<128>), dim3(grid), dim3(256), 0, stream, a);
     return (int)hipGetLastError();
   }
   constexpr int BQ = 32 * WAVES;

@@ -33,14 +33,14 @@ def main():
     q, k, v = qkv[:, :H * D], qkv[:, H * D:(H + KV) * D], qkv[:, (H + KV) * D:]
     scale = 1 / math.sqrt(D)
     flops = 4 * B * H * S * S * D / (2 if causal else 1)
-    outs, times = {}, {0: [], 1: []}
-    for var in (0, 1):
+    outs, times = {}, {0: [], 1: [], 2: []}
+    for var in (0, 1, 2):
         C.flash_fwd_config(var)
         outs[var] = C.flash_fwd(q, k, v, B, S, H, KV, D, scale, causal, 0)
     torch.cuda.synchronize()
     st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(a.rounds):
-        for var in (1, 0):
+        for var in (1, 2, 0):
             C.flash_fwd_config(var)
             st.record()
             for _ in range(a.iters):
@@ -49,11 +49,11 @@ def main():
             torch.cuda.synchronize()
             times[var].append(st.elapsed_time(en) / a.iters)
     C.flash_fwd_config(1)
-    for var in (1, 0):
+    for var in (1, 2, 0):
         ms = sorted(times[var])[len(times[var]) // 2]
         do = (outs[var][0].float() - outs[0][0].float()).abs().max().item()
         dl = (outs[var][1] - outs[0][1]).abs().max().item()
-        print(json.dumps({"variant": "w64" if var else "w32", "ms_median": round(ms, 4), "ms_min": round(min(times[var]), 4),
+        print(json.dumps({"variant": {0: "w32", 1: "w64-persistent", 2: "w64-per-block"}[var], "ms_median": round(ms, 4), "ms_min": round(min(times[var]), 4),
                           "tflops": round(flops / ms / 1e9, 1), "max_abs_diff_o_vs_w32": do, "max_abs_diff_lse_vs_w32": dl,
                           "shape": dict(B=B, S=S, H=H, KV=KV, D=D, causal=causal)}), flush=True)
 

@@ -7,8 +7,8 @@ cd "$(dirname "$0")/../.."
 b() { n=$1; shift; hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Icsrc/kernels -ffp-contract=fast \
       -mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize "$@" csrc/kernels/flash_attn_fwd.hip -o tools/w64_lab/lib$n.so; }
 b base &
-b abl_nobar -DW64_ABL_NOBAR=1 &
-b abl_nodma -DW64_ABL_NODMA=1 &
-b abl_noexp -DW64_ABL_NOEXP=1 &
-b abl_all -DW64_ABL_NOBAR=1 -DW64_ABL_NODMA=1 -DW64_ABL_NOEXP=1 &
+
+
+
+
 wait
