@@ -759,8 +759,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("gscale") = py::none(), py::arg("hp") = py::none());
   m.def("grad_sumsq", &grad_sumsq);
   m.def("flash_fwd_config", [](int64_t variant) { ftc_flash_fwd_config((int)variant); }, py::arg("variant"),
-        "flash forward variant of later calls: 1 = W64 (one wave per SIMD, 64 rows per wave) where it applies "
-        "(head_dim 128, S % 256 == 0, no window / documents / padded tail), 0 = the 32-row kernel everywhere");
+        "flash forward variant of later calls: 1 = W64 (one wave per SIMD, 64 rows per wave, persistent grid) where "
+        "it applies (head_dim 128, S % 256 == 0, no window / documents / padded tail), 2 = W64 with one workgroup "
+        "per block, 0 = the 32-row kernel everywhere, -1 = the build default");
   m.def("flash_fwd", &flash_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("B"), py::arg("S"), py::arg("H"),
         py::arg("KV"), py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("pad") = 0,
         py::arg("doc_start") = py::none(), py::arg("kv_valid") = -1);

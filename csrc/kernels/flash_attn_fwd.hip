@@ -1012,11 +1012,14 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
 // block fenced between the other block's MFMAs, asm-DMA 3-slot ring: 0.740 vs 0.554 ms at the Llama-3-8B
 // layer, profiles/r4/attn/fwd_qb6.log; git history has the kernel.)
 
-// forward variant of every later call: 1 = W64 (default where it applies), 0 = the 32-row kernel everywhere;
-// tests and tools/bench_attention.py switch it in one process (ftc_flash_fwd_config)
+// forward variant of every later call (W64_DEFAULT: the measured winner, see the W64 header); tests and
+// tools/bench_fwd_variants.py switch it in one process (ftc_flash_fwd_config)
+#ifndef W64_DEFAULT
+#define W64_DEFAULT 0
+#endif
 namespace {
 int& fwd_variant() {
-  static int v = 1;
+  static int v = W64_DEFAULT;
   return v;
 }
 int& fwd_persistent() {
@@ -1025,8 +1028,10 @@ int& fwd_persistent() {
 }
 }  // namespace
 
-// variant: 1 = W64 (persistent grid), 2 = W64 with one workgroup per block, 0 = the 32-row kernel everywhere
+// variant: 1 = W64 (persistent grid), 2 = W64 with one workgroup per block, 0 = the 32-row kernel everywhere,
+// negative = the build default
 extern "C" void ftc_flash_fwd_config(int variant) {
+  if (variant < 0) variant = W64_DEFAULT;  // back to the build's default
   fwd_variant() = variant ? 1 : 0;
   fwd_persistent() = variant == 2 ? 0 : 1;
 }

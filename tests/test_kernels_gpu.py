@@ -330,9 +330,9 @@ def test_flash_attention_fwd_bwd(C, B, S, H, KV, D, causal, window):
 
 @pytest.fixture
 def fwd_variant(C):
-    """Restores the default flash-forward variant (W64 where it applies) after a test that switches it."""
+    """Restores the build's default flash-forward variant after a test that switches it."""
     yield C
-    C.flash_fwd_config(1)
+    C.flash_fwd_config(-1)
 
 
 def _attn_ref_lse(q, k, v, B, S, H, KV, D, causal):
@@ -372,6 +372,8 @@ def test_flash_fwd_w64(fwd_variant, B, S, H, KV, causal, data):
     ref, ref_lse = _attn_ref_lse(q, k, v, B, S, H, KV, D, causal)
     C.flash_fwd_config(1)
     o, lse = C.flash_fwd(q, k, v, B, S, H, KV, D, scale, causal, 0)
+    C.flash_fwd_config(2)  # one workgroup per block (same kernel, no persistence)
+    o2, lse2 = C.flash_fwd(q, k, v, B, S, H, KV, D, scale, causal, 0)
     C.flash_fwd_config(0)
     o32, lse32 = C.flash_fwd(q, k, v, B, S, H, KV, D, scale, causal, 0)
     torch.cuda.synchronize()
@@ -383,6 +385,7 @@ def test_flash_fwd_w64(fwd_variant, B, S, H, KV, causal, data):
     torch.testing.assert_close(o.float(), ref, atol=2e-2, rtol=2e-2)
     torch.testing.assert_close(lse, ref_lse, atol=2e-3, rtol=1e-3)
     torch.testing.assert_close(lse, lse32, atol=1e-3, rtol=1e-4)
+    assert torch.equal(o, o2) and torch.equal(lse, lse2)  # persistence changes the order of blocks, not the math
 
 
 @pytest.mark.parametrize("positions", [False, True])
