@@ -484,6 +484,9 @@ constexpr int W64_BQ = 256;
 #ifndef W64_ABL_NOEXP
 #define W64_ABL_NOEXP 0
 #endif
+#ifndef W64_ABL_NOLDS  // K / Q / V^T fragments not read from LDS (lane-constant registers instead)
+#define W64_ABL_NOLDS 0
+#endif
 #ifndef W64_TAIL_J1FIRST
 #define W64_TAIL_J1FIRST 0
 #endif
@@ -552,6 +555,159 @@ DEV_INLINE void w64_o_scale(const float alpha) {
   if constexpr (T == 7) asm volatile("v_accvgpr_read_b32 %0, a240\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a240, %0\n\tv_accvgpr_read_b32 %0, a241\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a241, %0\n\tv_accvgpr_read_b32 %0, a242\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a242, %0\n\tv_accvgpr_read_b32 %0, a243\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a243, %0\n\tv_accvgpr_read_b32 %0, a244\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a244, %0\n\tv_accvgpr_read_b32 %0, a245\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a245, %0\n\tv_accvgpr_read_b32 %0, a246\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a246, %0\n\tv_accvgpr_read_b32 %0, a247\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a247, %0\n\tv_accvgpr_read_b32 %0, a248\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a248, %0\n\tv_accvgpr_read_b32 %0, a249\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a249, %0\n\tv_accvgpr_read_b32 %0, a250\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a250, %0\n\tv_accvgpr_read_b32 %0, a251\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a251, %0\n\tv_accvgpr_read_b32 %0, a252\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a252, %0\n\tv_accvgpr_read_b32 %0, a253\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a253, %0\n\tv_accvgpr_read_b32 %0, a254\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a254, %0\n\tv_accvgpr_read_b32 %0, a255\n\tv_mul_f32 %0, %0, %1\n\tv_accvgpr_write_b32 a255, %0\n\ts_nop 2" : "=&v"(t) : "v"(alpha) : W64_CLOB_T7);
   (void)t;
 }
+// Q (a[0:63]: block j, k-step st at a[4 (8 j + st)]) and K (a[64:127]: 32-key half kt, k-step st at
+// a[64 + 4 (8 kt + st)]) also live in kernel-owned accumulator registers: the S MFMA reads both operands from
+// there, its result lands in VGPRs (the softmax's), and K(i+1) is loaded a whole phase ahead (during Y_i)
+// by asm ds_reads the compiler neither counts nor sees -- the per-tile sync's lgkmcnt(0) covers them.
+#define W64_CLOB_G0 "a0", "a1", "a2", "a3"
+#define W64_CLOB_G1 "a4", "a5", "a6", "a7"
+#define W64_CLOB_G2 "a8", "a9", "a10", "a11"
+#define W64_CLOB_G3 "a12", "a13", "a14", "a15"
+#define W64_CLOB_G4 "a16", "a17", "a18", "a19"
+#define W64_CLOB_G5 "a20", "a21", "a22", "a23"
+#define W64_CLOB_G6 "a24", "a25", "a26", "a27"
+#define W64_CLOB_G7 "a28", "a29", "a30", "a31"
+#define W64_CLOB_G8 "a32", "a33", "a34", "a35"
+#define W64_CLOB_G9 "a36", "a37", "a38", "a39"
+#define W64_CLOB_G10 "a40", "a41", "a42", "a43"
+#define W64_CLOB_G11 "a44", "a45", "a46", "a47"
+#define W64_CLOB_G12 "a48", "a49", "a50", "a51"
+#define W64_CLOB_G13 "a52", "a53", "a54", "a55"
+#define W64_CLOB_G14 "a56", "a57", "a58", "a59"
+#define W64_CLOB_G15 "a60", "a61", "a62", "a63"
+#define W64_CLOB_G16 "a64", "a65", "a66", "a67"
+#define W64_CLOB_G17 "a68", "a69", "a70", "a71"
+#define W64_CLOB_G18 "a72", "a73", "a74", "a75"
+#define W64_CLOB_G19 "a76", "a77", "a78", "a79"
+#define W64_CLOB_G20 "a80", "a81", "a82", "a83"
+#define W64_CLOB_G21 "a84", "a85", "a86", "a87"
+#define W64_CLOB_G22 "a88", "a89", "a90", "a91"
+#define W64_CLOB_G23 "a92", "a93", "a94", "a95"
+#define W64_CLOB_G24 "a96", "a97", "a98", "a99"
+#define W64_CLOB_G25 "a100", "a101", "a102", "a103"
+#define W64_CLOB_G26 "a104", "a105", "a106", "a107"
+#define W64_CLOB_G27 "a108", "a109", "a110", "a111"
+#define W64_CLOB_G28 "a112", "a113", "a114", "a115"
+#define W64_CLOB_G29 "a116", "a117", "a118", "a119"
+#define W64_CLOB_G30 "a120", "a121", "a122", "a123"
+#define W64_CLOB_G31 "a124", "a125", "a126", "a127"
+template <int G>
+DEV_INLINE void w64_lda(const unsigned addr) {  // a[4 G .. 4 G + 3] = the 16 bytes at LDS addr
+  if constexpr (G == 0) asm volatile("ds_read_b128 a[0:3], %0" ::"v"(addr) : W64_CLOB_G0);
+  if constexpr (G == 1) asm volatile("ds_read_b128 a[4:7], %0" ::"v"(addr) : W64_CLOB_G1);
+  if constexpr (G == 2) asm volatile("ds_read_b128 a[8:11], %0" ::"v"(addr) : W64_CLOB_G2);
+  if constexpr (G == 3) asm volatile("ds_read_b128 a[12:15], %0" ::"v"(addr) : W64_CLOB_G3);
+  if constexpr (G == 4) asm volatile("ds_read_b128 a[16:19], %0" ::"v"(addr) : W64_CLOB_G4);
+  if constexpr (G == 5) asm volatile("ds_read_b128 a[20:23], %0" ::"v"(addr) : W64_CLOB_G5);
+  if constexpr (G == 6) asm volatile("ds_read_b128 a[24:27], %0" ::"v"(addr) : W64_CLOB_G6);
+  if constexpr (G == 7) asm volatile("ds_read_b128 a[28:31], %0" ::"v"(addr) : W64_CLOB_G7);
+  if constexpr (G == 8) asm volatile("ds_read_b128 a[32:35], %0" ::"v"(addr) : W64_CLOB_G8);
+  if constexpr (G == 9) asm volatile("ds_read_b128 a[36:39], %0" ::"v"(addr) : W64_CLOB_G9);
+  if constexpr (G == 10) asm volatile("ds_read_b128 a[40:43], %0" ::"v"(addr) : W64_CLOB_G10);
+  if constexpr (G == 11) asm volatile("ds_read_b128 a[44:47], %0" ::"v"(addr) : W64_CLOB_G11);
+  if constexpr (G == 12) asm volatile("ds_read_b128 a[48:51], %0" ::"v"(addr) : W64_CLOB_G12);
+  if constexpr (G == 13) asm volatile("ds_read_b128 a[52:55], %0" ::"v"(addr) : W64_CLOB_G13);
+  if constexpr (G == 14) asm volatile("ds_read_b128 a[56:59], %0" ::"v"(addr) : W64_CLOB_G14);
+  if constexpr (G == 15) asm volatile("ds_read_b128 a[60:63], %0" ::"v"(addr) : W64_CLOB_G15);
+  if constexpr (G == 16) asm volatile("ds_read_b128 a[64:67], %0" ::"v"(addr) : W64_CLOB_G16);
+  if constexpr (G == 17) asm volatile("ds_read_b128 a[68:71], %0" ::"v"(addr) : W64_CLOB_G17);
+  if constexpr (G == 18) asm volatile("ds_read_b128 a[72:75], %0" ::"v"(addr) : W64_CLOB_G18);
+  if constexpr (G == 19) asm volatile("ds_read_b128 a[76:79], %0" ::"v"(addr) : W64_CLOB_G19);
+  if constexpr (G == 20) asm volatile("ds_read_b128 a[80:83], %0" ::"v"(addr) : W64_CLOB_G20);
+  if constexpr (G == 21) asm volatile("ds_read_b128 a[84:87], %0" ::"v"(addr) : W64_CLOB_G21);
+  if constexpr (G == 22) asm volatile("ds_read_b128 a[88:91], %0" ::"v"(addr) : W64_CLOB_G22);
+  if constexpr (G == 23) asm volatile("ds_read_b128 a[92:95], %0" ::"v"(addr) : W64_CLOB_G23);
+  if constexpr (G == 24) asm volatile("ds_read_b128 a[96:99], %0" ::"v"(addr) : W64_CLOB_G24);
+  if constexpr (G == 25) asm volatile("ds_read_b128 a[100:103], %0" ::"v"(addr) : W64_CLOB_G25);
+  if constexpr (G == 26) asm volatile("ds_read_b128 a[104:107], %0" ::"v"(addr) : W64_CLOB_G26);
+  if constexpr (G == 27) asm volatile("ds_read_b128 a[108:111], %0" ::"v"(addr) : W64_CLOB_G27);
+  if constexpr (G == 28) asm volatile("ds_read_b128 a[112:115], %0" ::"v"(addr) : W64_CLOB_G28);
+  if constexpr (G == 29) asm volatile("ds_read_b128 a[116:119], %0" ::"v"(addr) : W64_CLOB_G29);
+  if constexpr (G == 30) asm volatile("ds_read_b128 a[120:123], %0" ::"v"(addr) : W64_CLOB_G30);
+  if constexpr (G == 31) asm volatile("ds_read_b128 a[124:127], %0" ::"v"(addr) : W64_CLOB_G31);
+}
+DEV_INLINE void w64_lda_t(const int G, const unsigned addr) {
+  switch (G) {
+    case 0: w64_lda<0>(addr); break;
+    case 1: w64_lda<1>(addr); break;
+    case 2: w64_lda<2>(addr); break;
+    case 3: w64_lda<3>(addr); break;
+    case 4: w64_lda<4>(addr); break;
+    case 5: w64_lda<5>(addr); break;
+    case 6: w64_lda<6>(addr); break;
+    case 7: w64_lda<7>(addr); break;
+    case 8: w64_lda<8>(addr); break;
+    case 9: w64_lda<9>(addr); break;
+    case 10: w64_lda<10>(addr); break;
+    case 11: w64_lda<11>(addr); break;
+    case 12: w64_lda<12>(addr); break;
+    case 13: w64_lda<13>(addr); break;
+    case 14: w64_lda<14>(addr); break;
+    case 15: w64_lda<15>(addr); break;
+    case 16: w64_lda<16>(addr); break;
+    case 17: w64_lda<17>(addr); break;
+    case 18: w64_lda<18>(addr); break;
+    case 19: w64_lda<19>(addr); break;
+    case 20: w64_lda<20>(addr); break;
+    case 21: w64_lda<21>(addr); break;
+    case 22: w64_lda<22>(addr); break;
+    case 23: w64_lda<23>(addr); break;
+    case 24: w64_lda<24>(addr); break;
+    case 25: w64_lda<25>(addr); break;
+    case 26: w64_lda<26>(addr); break;
+    case 27: w64_lda<27>(addr); break;
+    case 28: w64_lda<28>(addr); break;
+    case 29: w64_lda<29>(addr); break;
+    case 30: w64_lda<30>(addr); break;
+    case 31: w64_lda<31>(addr); break;
+  }
+}
+// S^T(j, kt) (+)= K(kt, st) . Q(j, st)^T from the owned operands into a VGPR accumulator
+template <int KR, int QR, bool FIRST>
+DEV_INLINE void w64_s(f32x16& acc) {
+  if constexpr (FIRST)
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, a[%c1:%c2], a[%c3:%c4], 0" : "=v"(acc) : "i"(KR), "i"(KR + 3), "i"(QR), "i"(QR + 3));
+  else
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, a[%c1:%c2], a[%c3:%c4], %0" : "+v"(acc) : "i"(KR), "i"(KR + 3), "i"(QR), "i"(QR + 3));
+}
+DEV_INLINE void w64_s_t(const int kt, const int st, const int j, f32x16& acc) {
+  const int idx = (kt * 8 + st) * 2 + j;
+  switch (idx) {
+    case 0: w64_s<64, 0, true>(acc); break;
+    case 1: w64_s<64, 32, true>(acc); break;
+    case 2: w64_s<68, 4, false>(acc); break;
+    case 3: w64_s<68, 36, false>(acc); break;
+    case 4: w64_s<72, 8, false>(acc); break;
+    case 5: w64_s<72, 40, false>(acc); break;
+    case 6: w64_s<76, 12, false>(acc); break;
+    case 7: w64_s<76, 44, false>(acc); break;
+    case 8: w64_s<80, 16, false>(acc); break;
+    case 9: w64_s<80, 48, false>(acc); break;
+    case 10: w64_s<84, 20, false>(acc); break;
+    case 11: w64_s<84, 52, false>(acc); break;
+    case 12: w64_s<88, 24, false>(acc); break;
+    case 13: w64_s<88, 56, false>(acc); break;
+    case 14: w64_s<92, 28, false>(acc); break;
+    case 15: w64_s<92, 60, false>(acc); break;
+    case 16: w64_s<96, 0, true>(acc); break;
+    case 17: w64_s<96, 32, true>(acc); break;
+    case 18: w64_s<100, 4, false>(acc); break;
+    case 19: w64_s<100, 36, false>(acc); break;
+    case 20: w64_s<104, 8, false>(acc); break;
+    case 21: w64_s<104, 40, false>(acc); break;
+    case 22: w64_s<108, 12, false>(acc); break;
+    case 23: w64_s<108, 44, false>(acc); break;
+    case 24: w64_s<112, 16, false>(acc); break;
+    case 25: w64_s<112, 48, false>(acc); break;
+    case 26: w64_s<116, 20, false>(acc); break;
+    case 27: w64_s<116, 52, false>(acc); break;
+    case 28: w64_s<120, 24, false>(acc); break;
+    case 29: w64_s<120, 56, false>(acc); break;
+    case 30: w64_s<124, 28, false>(acc); break;
+    case 31: w64_s<124, 60, false>(acc); break;
+  }
+}
+
 DEV_INLINE void w64_pv_t(const int T, const bf16x8& va, const bf16x8& p) {
   switch (T) {
     case 0: w64_pv<0>(va, p); break;
@@ -697,13 +853,16 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     vto[dt][1] = lds_off<D>(4 * hh + trq + 8, chunk) + half8;
   }
   const char* Qw = Qs + 64 * wave * D * 2;
-  auto rd_k = [&](const int t, const int kt, const int st) __attribute__((always_inline)) -> uint4 {
-    return *reinterpret_cast<const uint4*>(Kr + ((kslot0 + t) % 3) * TILE + kt * HALF + ko[st]);
+  const uint4 fake = make_uint4(0x3c003c00u ^ lane, 0x3c003c00u, 0x3c003c00u ^ (lane << 3), 0x3c003c00u);
+  // K fragment (kt, st) of stream tile t / Q fragment (j, st) into their owned accumulator registers
+  auto ld_k = [&](const int t, const int kt, const int st) __attribute__((always_inline)) {
+    if (!W64_ABL_NOLDS) w64_lda_t(16 + 8 * kt + st, lds_addr(Kr + ((kslot0 + t) % 3) * TILE) + kt * HALF + ko[st]);
   };
-  auto rd_q = [&](const int j, const int st) __attribute__((always_inline)) -> uint4 {
-    return *reinterpret_cast<const uint4*>(Qw + j * HALF + ko[st]);
+  auto ld_q = [&](const int j, const int st) __attribute__((always_inline)) {
+    if (!W64_ABL_NOLDS) w64_lda_t(8 * j + st, lds_addr(Qw) + j * HALF + ko[st]);
   };
   auto rd_v = [&](const int t, const int f, const int h) __attribute__((always_inline)) -> s16x4 {
+    if (W64_ABL_NOLDS) return s16x4{(short)lane, (short)f, (short)h, (short)t};
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
         (lds_s16x4*)(Vr + (t & 1) * TILE + vto[f >> 2][h] + (f & 3) * 16 * D * 2));
   };
@@ -713,8 +872,9 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
   bool resc = false;
   f32x16 sA[2][2], sB[2][2];  // S of the tile being started / finished (parity buffers)
   uint4 pA[2][4], pB[2][4];   // P^T fragments as packed bf16 words (parity buffers)
-  uint4 kq[2][4];             // K / Q fragments of k-steps st (slot st & 1) and st + 1: {k kt0, k kt1, q j0, q j1}
-  s16x4 vf[3][2];  // V^T fragments (two tr-reads each), ring of three, read two fragments ahead
+  // V(i-1)^T fragments (two tr-reads each), a ring of eight: fragments 0-7 read during X_i, fragments 8-15
+  // during Y_i's first half into the slots fragments 0-7 free (each 14+ gaps before its MFMAs)
+  s16x4 vf[8][2];
 
   auto sync = [&]() __attribute__((always_inline)) {
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMA pieces of the last iteration landed
@@ -772,16 +932,9 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int g = 4 * st + u;
-        const uint4* cur = kq[st & 1];
         const int kt = u >> 1, j = u & 1;
-        const f32x16 zero = {};
-        sn[j][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf8(cur[kt]), as_bf8(cur[2 + j]), st ? sn[j][kt] : zero,
-                                                            0, 0, 0);
-        if (st + 1 < DSTEPS) {
-          kq[(st + 1) & 1][u] = u < 2 ? rd_k(i, u, st + 1) : rd_q(u - 2, st + 1);
-        } else if (!first) {
-          vf[u >> 1][u & 1] = rd_v(i - 1, u >> 1, u & 1);  // V(i-1)^T fragments 0, 1 for Y_i
-        }
+        w64_s_t(kt, st, j, sn[j][kt]);  // operands K(i), Q in owned accumulator registers
+        if (!first && (g & 1)) vf[g >> 2][(g >> 1) & 1] = rd_v(i - 1, g >> 2, (g >> 1) & 1);  // fragments 0-7
         if (!first) exp_el(so, po, r, g >> 4, 16 + (g & 15), i - 1, false, mref_o[g >> 4], ev);
         if (W64_ABL_NODMA) {
         } else if (g < NGT) {
@@ -796,6 +949,11 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
       l[0] += r[0];
       l[1] += r[1];
     }
+    // seam: every V^T fragment landed (a compiler-known wait: no further waits in Y_i), and wait states
+    // between the last asm S MFMAs and the softmax's VALU reads of their (VGPR) results
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    W64_GAP();
     // ---------------- Y_i
     float mt[2] = {-INFINITY, -INFINITY}, mref_n[2] = {0.f, 0.f};
     bool need_any = false;
@@ -806,17 +964,18 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
       for (int j = 0; j < 2; ++j) {
         const int g = 2 * f + j;
         if (!first) {
-          const int fr = f + 2;
-          if (fr < 16) {
-            vf[fr % 3][j] = rd_v(i - 1, fr, j);
-          }
-          const s16x4 v1 = vf[f % 3][0], v2 = vf[f % 3][1];
+          const s16x4 v1 = vf[f & 7][0], v2 = vf[f & 7][1];
           const s16x8 va = {v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
           w64_pv_t(4 * j + (f >> 2), __builtin_bit_cast(bf16x8, va), as_bf8(po[j][f & 3]));
         }
-        if (g >= 28 && more) {  // X_{i+1}'s first k-step: K(i+1) (landed two tiles ahead) and Q
-          const int u = g - 28;
-          kq[0][u] = u < 2 ? rd_k(i + 1, u, 0) : rd_q(u - 2, 0);
+        // after this gap's MFMA: fragment 8 + k into the slot fragment k freed (gaps 2-17), and K(i+1) a phase
+        // ahead (landed two tiles ahead) in the other sixteen gaps
+        if (!first && g >= 2 && g < 18) {
+          const int fr = 8 + ((g - 2) >> 1), h = (g - 2) & 1;
+          vf[fr & 7][h] = rd_v(i - 1, fr, h);
+        } else if (more && (g < 2 || g >= 18)) {
+          const int kk = g < 2 ? g : g - 16;  // 0..15
+          ld_k(i + 1, kk >> 3, kk & 7);
         }
         // start softmax(i): gaps 0-7 row max (4 elements of each block per gap), 8-9 the row statistics,
         // 10-31 exps of keys 0-31 (32 elements over 22 gaps)
@@ -877,20 +1036,19 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
       asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
       W64_GAP();
     }
-    // the same V ring as Y_i
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
+    for (int f = 0; f < 8; ++f) {
       vf[f][0] = rd_v(i - 1, f, 0);
       vf[f][1] = rd_v(i - 1, f, 1);
     }
 #pragma unroll
     for (int f = 0; f < 16; ++f) {
       W64_GAP();
-      if (f + 2 < 16) {
-        vf[(f + 2) % 3][0] = rd_v(i - 1, f + 2, 0);
-        vf[(f + 2) % 3][1] = rd_v(i - 1, f + 2, 1);
+      if (f >= 1 && f + 7 < 16) {  // fragment f + 7 into the slot fragment f - 1 freed
+        vf[(f + 7) & 7][0] = rd_v(i - 1, f + 7, 0);
+        vf[(f + 7) & 7][1] = rd_v(i - 1, f + 7, 1);
       }
-      const s16x4 v1 = vf[f % 3][0], v2 = vf[f % 3][1];
+      const s16x4 v1 = vf[f & 7][0], v2 = vf[f & 7][1];
       const s16x8 va = {v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
       w64_pv_t(f >> 2, __builtin_bit_cast(bf16x8, va), as_bf8(po[0][f & 3]));
       w64_pv_t(4 + (f >> 2), __builtin_bit_cast(bf16x8, va), as_bf8(po[1][f & 3]));
@@ -944,7 +1102,13 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     // block start: Q, K(0), K(1) landed; X_0's first K / Q fragments
     sync();
 #pragma unroll
-    for (int u = 0; u < 4; ++u) kq[0][u] = u < 2 ? rd_k(0, u, 0) : rd_q(u - 2, 0);
+    for (int st = 0; st < DSTEPS; ++st) {
+      ld_q(0, st);
+      ld_q(1, st);
+      ld_k(0, 0, st);
+      ld_k(0, 1, st);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // the asm loads above (the compiler does not count them)
     body(0, sA, sB, pA, pB, true, a.causal && wtiles == 1, wtiles > 1);
     int i = 1;
     // steady iterations 1 .. wtiles - 2 in parity pairs; the state is back in (sA, pA) after each pair

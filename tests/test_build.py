@@ -82,9 +82,10 @@ def test_run_patched_sets_module_constants_before_the_script(tmp_path):
 
 
 def test_w64_forward_owns_its_accumulators(tmp_path):
-    """The W64 flash forward keeps O in accumulator registers a[128:255] that only its inline asm touches
-    (csrc/kernels/flash_attn_fwd.hip): compiled with the build's own flags, no compiler instruction may
-    touch that range and no VALU write may feed an asm MFMA operand unpadded (tools/check_asm_hazards.py)."""
+    """The W64 flash forward keeps Q, K (a[0:127]) and O (a[128:255]) in accumulator registers that only
+    its inline asm touches (csrc/kernels/flash_attn_fwd.hip): compiled with the build's own flags, no
+    compiler instruction may touch them, no VALU write may feed an asm MFMA operand unpadded and no
+    instruction may read an asm S MFMA's VGPR result early (tools/check_asm_hazards.py)."""
     import shutil
 
     if shutil.which("hipcc") is None:
@@ -97,7 +98,8 @@ def test_w64_forward_owns_its_accumulators(tmp_path):
     subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-S", "--cuda-device-only",
                     "-I", os.path.join(ROOT, "csrc", "kernels"), "-ffp-contract=fast",
                     *EXTRA_FLAGS["flash_attn_fwd.hip"], src, "-o", out], check=True, capture_output=True)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_asm_hazards.py"), out],
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_asm_hazards.py"), out, "3", "0"],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
-    assert "inside the owned range a[128:]: 0" in r.stdout and "0 write -> operand (RAW)" in r.stdout
+    assert "inside the owned range a[0:]: 0" in r.stdout and "0 write -> operand (RAW)" in r.stdout
+    assert "within 12 wait states: 0" in r.stdout

@@ -24,6 +24,16 @@ def regs(tok: str) -> set[int]:
     return {int(m.group(1))} if m else set()
 
 
+def regs_in(text: str) -> set[int]:
+    """Every VGPR named in an operand list."""
+    out = set()
+    for lo, hi in re.findall(r"\bv\[(\d+):(\d+)\]", text):
+        out |= set(range(int(lo), int(hi) + 1))
+    for r in re.findall(r"\bv(\d+)\b", text):
+        out.add(int(r))
+    return out
+
+
 def agprs(text: str) -> set[int]:
     out = set()
     for lo, hi in re.findall(r"\ba\[(\d+):(\d+)\]", text):
@@ -73,6 +83,32 @@ def main(path: str, window: int = 3, owned: int = 128) -> int:
                 dst = regs(op[1].split(",")[0].strip())
                 if dst & used:
                     war.append(f"line {k2 + 1}: {nxt}  after  line {k + 1}: {ln}")
+    # asm MFMA with a VGPR destination (the W64 S MFMAs): no instruction may read or write that destination
+    # within 12 wait states (8-pass XDL result latency; an s_nop N counts N + 1), except the next MFMA of
+    # the same accumulation chain taking it whole as SrcC
+    dres = []
+    for idx, (k, ln) in enumerate(flat):
+        if not (ln.startswith("v_mfma") and ln.split(None, 1)[1].split(",")[0].strip().startswith("v")):
+            continue
+        ops = [t.strip() for t in ln.split(None, 1)[1].split(",")]
+        dst = regs(ops[0])
+        states = 0
+        for k2, nxt in flat[idx + 1:]:
+            if states >= 12:
+                break
+            op = nxt.split(None, 1)
+            if op[0].startswith("v_mfma") and len(op) > 1:
+                o2 = [t.strip() for t in op[1].split(",")]
+                if regs(o2[0]) == dst and regs(o2[3]) == dst:
+                    break  # the chain continues: its own hazard is checked at that MFMA
+            if len(op) > 1 and op[0] != "s_nop" and (regs_in(op[1]) & dst):
+                dres.append(f"line {k2 + 1}: {nxt}  {states} states after  line {k + 1}: {ln}")
+                break
+            states += int(op[1]) + 1 if op[0] == "s_nop" else 1
+    print(f"VGPR-destination asm MFMAs: result read / overwritten within 12 wait states: {len(dres)}")
+    for d in dres[:10]:
+        print("  " + d)
+    bad += dres
     # ownership: accumulator registers >= `owned` belong to the kernel's asm; the compiler must not touch them
     inasm, own, comp_agpr = False, [], 0
     for k, ln in enumerate(lines):

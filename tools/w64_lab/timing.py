@@ -25,7 +25,7 @@ def main():
     o = torch.empty(B * S, H * D, device="cuda", dtype=torch.bfloat16)
     lse = torch.empty(B, H, S, device="cuda", dtype=torch.float32)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    arms = [(n, 1) for n in libs] + [("base", 0)]
+    arms = [(n, 1) for n in libs] + [("base", 2), ("base", 0)]
     times = {f"{n}/{v}": [] for n, v in arms}
 
     def call(L):
@@ -47,7 +47,7 @@ def main():
             torch.cuda.synchronize()
             times[f"{n}/{var}"].append(e0.elapsed_time(e1) / 20)
     for kname, t in times.items():
-        print(json.dumps({"arm": kname.replace("/1", "").replace("/0", " (w32)"), "ms_median": round(sorted(t)[3], 4)}))
+        print(json.dumps({"arm": kname.replace("/1", " (persistent)").replace("/2", " (per-block)").replace("/0", " (w32)"), "ms_median": round(sorted(t)[3], 4)}))
 
 
 if __name__ == "__main__":
