@@ -493,6 +493,18 @@ constexpr int W64_BQ = 256;
 #ifndef W64_TAIL_NOP
 #define W64_TAIL_NOP 0
 #endif
+#ifndef W64_XB  // 0: no cross-block prefetch (the next block's Q, K(0), K(1) DMA'd at its start)
+#define W64_XB 1
+#endif
+#ifndef W64_V3  // 1: a 3-slot V ring streamed one tile ahead (the whole 160 KiB of LDS); 0: 2 slots, same tile
+#define W64_V3 1
+#endif
+#ifndef W64_STAMPS  // lab only: s_memtime stamps of workgroup 0's first block, tiles 20-23 (ftc_w64_stamps)
+#define W64_STAMPS 0
+#endif
+#if W64_STAMPS
+__device__ unsigned long long w64_stamps[4][4][6];
+#endif
 #ifndef W64_DEFER
 #define W64_DEFER 8.0f
 #endif
@@ -763,7 +775,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
   constexpr int HALF = 32 * D * 2;             // byte offset of rows 32-63 of a tile (same swizzle)
   __shared__ __attribute__((aligned(16))) char Qs[W64_BQ * D * 2];  // 64 KiB
   __shared__ __attribute__((aligned(16))) char Kr[3 * TILE];        // K ring, 3 slots
-  __shared__ __attribute__((aligned(16))) char Vr[2 * TILE];        // V ring, 2 slots
+  __shared__ __attribute__((aligned(16))) char Vr[(2 + W64_V3) * TILE];  // V ring
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -793,14 +805,21 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
   int q0 = qb * W64_BQ, wq0 = q0 + 64 * wave;
   int ntiles = a.causal ? (q0 + W64_BQ) / BK : S / BK;
   int wtiles = a.causal ? (wq0 + 64) / BK : ntiles;
+  int stamp_blk = 1;  // W64_STAMPS: the first block of the workgroup
+  int vslot0 = 0;  // V ring slot of this block's tile 0 (W64_V3: the V stream runs on across blocks too)
   int kslot0 = 0;  // K ring slot of this block's tile 0: the K stream runs on across blocks
   // the next block (its K(0), K(1) and Q stream in under this block's last iterations)
   int nqb_ = 0, nb_ = 0, nhq_ = 0, nkvh_ = 0;
   int has_next = 0;
 
-  auto kv_rsrc = [&](const uint16_t* base, const int bb, const int kh) __attribute__((always_inline)) {
-    return make_rsrc(base + (long long)bb * S * a.kv_rs + (long long)kh * D);
+  // K / V element offsets of this block's and the next block's (b, kv head), set once per block; LDS
+  // destinations as plain 32-bit addresses (SALU arithmetic, no generic-pointer casts per piece)
+  auto kv_of = [&](const int bb, const int kh) __attribute__((always_inline)) -> long long {
+    return (long long)bb * S * a.kv_rs + (long long)kh * D;
   };
+  long long kof_c = kv_of(b, kvh), kof_n = 0;
+  const unsigned kr0 = lds_addr(Kr) + wave * NGT * RPG * D * 2, vr0 = lds_addr(Vr) + wave * NGT * RPG * D * 2;
+  const unsigned qs0 = lds_addr(Qs) + 64 * wave * D * 2;
   int voff[NGT];
 #pragma unroll
   for (int i = 0; i < NGT; ++i) {
@@ -812,23 +831,34 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
   // harmless repeat into the slot it would have used: that slot held K(t - 3), read by nobody again)
   auto dma_k = [&](const int t, const int p) __attribute__((always_inline)) {
     const int slot = (kslot0 + t) % 3;
-    const int nxt = (t >= ntiles) & has_next;  // integer selects (SALU), never a select of descriptors
-    const int bb = nxt ? nb_ : b, kh = nxt ? nkvh_ : kvh;
+    const int nxt = (t >= ntiles) & has_next & W64_XB;  // integer selects (SALU), never a select of descriptors
     const int tt = t < ntiles ? t : (nxt ? t - ntiles : 0);
-    lds_dma16_u(kv_rsrc(a.k, bb, kh), Kr + slot * TILE + (wave * NGT + p) * RPG * D * 2, voff[p], tt * tstride);
+    lds_dma16_at(make_rsrc(a.k + (nxt ? kof_n : kof_c)), rfl(kr0 + slot * TILE + p * RPG * D * 2), voff[p], tt * tstride);
   };
+  // LDS-DMA of V stream tile t (W64_V3: as the K stream, one tile ahead of its use instead of two)
   auto dma_v = [&](const int t, const int p) __attribute__((always_inline)) {
-    lds_dma16_u(kv_rsrc(a.v, b, kvh), Vr + (t & 1) * TILE + (wave * NGT + p) * RPG * D * 2, voff[p], t * tstride);
+    if (W64_V3) {
+      const int nxt = (t >= ntiles) & has_next & W64_XB;
+      const int tt = t < ntiles ? t : (nxt ? t - ntiles : 0);
+      lds_dma16_at(make_rsrc(a.v + (nxt ? kof_n : kof_c)), rfl(vr0 + ((vslot0 + t) % 3) * TILE + p * RPG * D * 2),
+                   voff[p], tt * tstride);
+    } else {
+      lds_dma16_at(make_rsrc(a.v + kof_c), rfl(vr0 + (t & 1) * TILE + p * RPG * D * 2), voff[p], t * tstride);
+    }
   };
-  // this wave's 64 Q rows of block (qb', b', hq') -> Qs (swizzled row image)
+  // this wave's 64 Q rows of block (qb', b', hq') -> Qs (swizzled row image).  The lane id is re-derived per
+  // call by volatile asm: hoisted as loop-invariant, the sixteen lane offsets were spilled and every reload's
+  // vmcnt(0) serialised the pieces behind the whole DMA stream (0.13 ms of the kernel at the 8B shape)
   auto dma_q = [&](const int qbx, const int bx, const int hqx) __attribute__((always_inline)) {
     const uint16_t* qbase = a.q + ((long long)bx * S + qbx * W64_BQ + 64 * wave) * a.q_rs + (long long)hqx * D;
     const auto qrs = make_rsrc(qbase);
+    int ln;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
 #pragma unroll
     for (int p = 0; p < 16; ++p) {
-      const int row = p * RPG + lane / NCH, pc = lane % NCH;
+      const int row = p * RPG + ln / NCH, pc = ln % NCH;
       const int qo = (row * (int)a.q_rs + ((pc ^ swz(row)) & (NCH - 1)) * 8) * 2;
-      lds_dma16_u(qrs, Qs + (64 * wave + p * RPG) * D * 2, qo, 0);
+      lds_dma16_at(qrs, rfl(qs0 + p * RPG * D * 2), qo, 0);
     }
   };
   // prologue of the first block: Q, K(0), K(1)
@@ -837,21 +867,31 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
   for (int p = 0; p < NGT; ++p) dma_k(0, p);
 #pragma unroll
   for (int p = 0; p < NGT; ++p) dma_k(1, p);
-
-  // lane-constant LDS offsets: K / Q fragment (row lr, chunk 2 st + hh); V^T tr-read (as flash_fwd_kernel)
-  int ko[DSTEPS];
+  if (W64_V3) {
 #pragma unroll
-  for (int st = 0; st < DSTEPS; ++st) ko[st] = lds_off<D>(lr, 2 * st + hh);
-  const int gi = lane >> 4, li = lane & 15;
-  const int trq = li >> 2, trp = li & 3;
-  int vto[DT][2];
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt) {
-    const int col = dt * 32 + 16 * (gi & 1) + 4 * trp;
-    const int chunk = col >> 3, half8 = (col & 7) ? 8 : 0;
-    vto[dt][0] = lds_off<D>(4 * hh + trq, chunk) + half8;
-    vto[dt][1] = lds_off<D>(4 * hh + trq + 8, chunk) + half8;
+    for (int p = 0; p < NGT; ++p) dma_v(0, p);
   }
+
+  // lane-constant LDS offsets: K / Q fragment (row lr, chunk 2 st + hh); V^T tr-read (as flash_fwd_kernel).
+  // Re-derived at every block start from a volatile-asm lane id, so they are dead across the epilogue and
+  // the idle iterations (kept live there, they pushed the compiler into spilling through owned registers)
+  int ko[DSTEPS], vto[DT][2];
+  auto lane_offsets = [&]() __attribute__((always_inline)) {
+    int ln;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+    const int lh = ln >> 5, ll = ln & 31;
+#pragma unroll
+    for (int st = 0; st < DSTEPS; ++st) ko[st] = lds_off<D>(ll, 2 * st + lh);
+    const int gi = ln >> 4, li = ln & 15;
+    const int trq = li >> 2, trp = li & 3;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int col = dt * 32 + 16 * (gi & 1) + 4 * trp;
+      const int chunk = col >> 3, half8 = (col & 7) ? 8 : 0;
+      vto[dt][0] = lds_off<D>(4 * lh + trq, chunk) + half8;
+      vto[dt][1] = lds_off<D>(4 * lh + trq + 8, chunk) + half8;
+    }
+  };
   const char* Qw = Qs + 64 * wave * D * 2;
   const uint4 fake = make_uint4(0x3c003c00u ^ lane, 0x3c003c00u, 0x3c003c00u ^ (lane << 3), 0x3c003c00u);
   // K fragment (kt, st) of stream tile t / Q fragment (j, st) into their owned accumulator registers
@@ -864,7 +904,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
   auto rd_v = [&](const int t, const int f, const int h) __attribute__((always_inline)) -> s16x4 {
     if (W64_ABL_NOLDS) return s16x4{(short)lane, (short)f, (short)h, (short)t};
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_s16x4*)(Vr + (t & 1) * TILE + vto[f >> 2][h] + (f & 3) * 16 * D * 2));
+        (lds_s16x4*)(Vr + (W64_V3 ? (vslot0 + t) % 3 : (t & 1)) * TILE + vto[f >> 2][h] + (f & 3) * 16 * D * 2));
   };
 
   w64_o_zero();  // O: a[128:255], owned by the asm helpers above
@@ -915,48 +955,115 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
       if (dw == 0) pw[j][f].x = w; else if (dw == 1) pw[j][f].y = w; else if (dw == 2) pw[j][f].z = w; else pw[j][f].w = w;
     }
   };
+  // the phases' exponential pipeline: element (j, e)'s exponential in one gap, its consumers (the row-sum add,
+  // the bf16 pack) in the next -- a VALU read right behind a v_exp_f32 costs a wait state (an s_nop per
+  // element).  pr: the last four exponentials by i & 3 (at most two per gap, so four are live at most)
+  float pr[4];
+  auto exp_p = [&](const f32x16 (&sv)[2][2], const int j, const int e, const int t, const bool mask, const float mref)
+      __attribute__((always_inline)) {
+    const int kt = e >> 4, i = e & 15;
+    pr[i & 3] = W64_ABL_NOEXP ? sv[j][kt][i] : __builtin_amdgcn_exp2f(__builtin_fmaf(masked(sv[j][kt][i], j, e, t, mask), c, -mref));
+  };
+  auto consume = [&](uint4 (&pw)[2][4], float (&r)[2], const int j, const int e) __attribute__((always_inline)) {
+    const int kt = e >> 4, i = e & 15;
+    r[j] += pr[i & 3];
+    if (i & 1) {
+      const uint32_t w = pack_bf2(pr[(i - 1) & 3], pr[i & 3]);
+      const int f = 2 * kt + (i >> 3), dw = (i & 7) >> 1;
+      if (dw == 0) pw[j][f].x = w; else if (dw == 1) pw[j][f].y = w; else if (dw == 2) pw[j][f].z = w; else pw[j][f].w = w;
+    }
+  };
 
   // ---- one iteration (tile i).  first: no finish / PV (tile 0); mask: tile i is the wave's diagonal; more:
   // the wave computes tile i + 1 (read its first K fragments in Y_i)
+  auto stamp = [&](const int i, const int k) __attribute__((always_inline)) {
+#if W64_STAMPS
+    if (blockIdx.x == 0 && stamp_blk && i >= 20 && i < 24) {
+      W64_GAP();
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (lane == 0) w64_stamps[wave][i - 20][k] = t;
+      W64_GAP();
+    }
+#endif
+  };
   auto body = [&](const int i, f32x16 (&sn)[2][2], f32x16 (&so)[2][2], uint4 (&pn)[2][4], uint4 (&po)[2][4],
                   const bool first, const bool mask, const bool more) __attribute__((always_inline)) {
+    stamp(i, 0);
     sync();
+    stamp(i, 1);
     rescale();
-    float mref_o[2], r[2] = {rs[0], rs[1]}, ev[2][2];
+    stamp(i, 2);
+    float mref_o[2], r[2] = {rs[0], rs[1]};
 #pragma unroll
     for (int j = 0; j < 2; ++j) mref_o[j] = (m[j] == -INFINITY) ? 0.f : m[j];
-    // ---------------- X_i
+    float mt[2] = {-INFINITY, -INFINITY}, mref_n[2] = {0.f, 0.f};
+    bool need_any = false;
+    // row statistics of block jj for tile i (l is rescaled where its tile i - 1 sum is complete)
+    auto stats = [&](const int jj) __attribute__((always_inline)) {
+      const bool need = mt[jj] > m[jj] + W64_DEFER;
+      const float mn = need ? fmaxf(m[jj], mt[jj]) : m[jj];
+      alpha[jj] = __builtin_amdgcn_exp2f(m[jj] - ((mn == -INFINITY) ? 0.f : mn));
+      m[jj] = mn;
+      mref_n[jj] = (mn == -INFINITY) ? 0.f : mn;
+      need_any |= need;
+    };
+    auto rowmax4 = [&](const int jj, const int e0) __attribute__((always_inline)) {
+#pragma unroll
+      for (int e = e0; e < e0 + 4; ++e) mt[jj] = fmaxf(mt[jj], masked(sn[jj][e >> 4][e & 15], jj, e, i, mask));
+    };
+    // ---------------- X_i: S(i) block-major (block 0's chains complete at gap 15, so its row maximum and
+    // statistics run in gaps 19-28 and Y_i can exponentiate from its first gap: one exponential per gap in
+    // both phases)
     W64_GAP();
 #pragma unroll
-    for (int st = 0; st < DSTEPS; ++st) {
+    for (int gq = 0; gq < 8; ++gq)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int g = 4 * st + u;
-        const int kt = u >> 1, j = u & 1;
-        w64_s_t(kt, st, j, sn[j][kt]);  // operands K(i), Q in owned accumulator registers
-        if (!first && (g & 1)) vf[g >> 2][(g >> 1) & 1] = rd_v(i - 1, g >> 2, (g >> 1) & 1);  // fragments 0-7
-        if (!first) exp_el(so, po, r, g >> 4, 16 + (g & 15), i - 1, false, mref_o[g >> 4], ev);
-        if (W64_ABL_NODMA) {
-        } else if (g < NGT) {
-          dma_k(i + 2, g);
-        } else if (g < 2 * NGT) {
-          dma_v(i, g - NGT);
-        }
+    for (int gu = 0; gu < 4; ++gu) {
+      const int g = 4 * gq + gu;
+      const int j = g >> 4, st = (g & 15) >> 1, kt = g & 1;
+      w64_s_t(kt, st, j, sn[j][kt]);  // operands K(i), Q in owned accumulator registers
+      if (!first && (g & 1)) vf[g >> 2][(g >> 1) & 1] = rd_v(i - 1, g >> 2, (g >> 1) & 1);  // fragments 0-7
+      if (!first) {
+        exp_p(so, g >> 4, 16 + (g & 15), i - 1, false, mref_o[g >> 4]);
+        if (g > 0) consume(po, r, (g - 1) >> 4, 16 + ((g - 1) & 15));
+      }
+      if (W64_ABL_NODMA) {
+      } else if (g < NGT) {
+        dma_k(i + 2, g);
+      } else if (g < 2 * NGT) {
+        dma_v(i + W64_V3, g - NGT);
+      }
+      if (first && g == 19) {  // tile 0's gaps carry no fillers
+        asm volatile("s_nop 7\n\ts_nop 3" ::: "memory");
         W64_GAP();
       }
+      if (g >= 19 && g < 27) rowmax4(0, 4 * (g - 19));
+      if (g == 27) mt[0] = xhalf_max(mt[0]) * c;
+      if (g == 28) stats(0);
+      W64_GAP();
     }
     if (!first) {
+      consume(po, r, 1, 31);
       l[0] += r[0];
       l[1] += r[1];
     }
-    // seam: every V^T fragment landed (a compiler-known wait: no further waits in Y_i), and wait states
-    // between the last asm S MFMAs and the softmax's VALU reads of their (VGPR) results
+    l[0] *= alpha[0];
+    stamp(i, 3);
+    // seam: every V^T fragment landed (a compiler-known wait: no further waits in Y_i); then K(i+1) a phase
+    // ahead (landed two tiles ahead), all sixteen reads issued before any of the compiler's LDS reads of Y_i --
+    // LDS returns in order, so the compiler's lgkmcnt waits (which do not count these asm reads) are neither
+    // short nor inflated by them -- and they are the wait states between the last asm S MFMAs and the
+    // softmax's VALU reads of their (VGPR) results (nops when there is no next tile)
     __builtin_amdgcn_s_waitcnt(0xC07F);
-    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    if (more) {
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) ld_k(i + 1, kk >> 3, kk & 7);
+    } else {
+      asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    }
     W64_GAP();
+    stamp(i, 4);
     // ---------------- Y_i
-    float mt[2] = {-INFINITY, -INFINITY}, mref_n[2] = {0.f, 0.f};
-    bool need_any = false;
     r[0] = r[1] = 0.f;
 #pragma unroll
     for (int f = 0; f < 16; ++f) {
@@ -968,46 +1075,26 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
           const s16x8 va = {v1[0], v1[1], v1[2], v1[3], v2[0], v2[1], v2[2], v2[3]};
           w64_pv_t(4 * j + (f >> 2), __builtin_bit_cast(bf16x8, va), as_bf8(po[j][f & 3]));
         }
-        // after this gap's MFMA: fragment 8 + k into the slot fragment k freed (gaps 2-17), and K(i+1) a phase
-        // ahead (landed two tiles ahead) in the other sixteen gaps
+        // after this gap's MFMA: fragment 8 + k into the slot fragment k freed (gaps 2-17)
         if (!first && g >= 2 && g < 18) {
           const int fr = 8 + ((g - 2) >> 1), h = (g - 2) & 1;
           vf[fr & 7][h] = rd_v(i - 1, fr, h);
-        } else if (more && (g < 2 || g >= 18)) {
-          const int kk = g < 2 ? g : g - 16;  // 0..15
-          ld_k(i + 1, kk >> 3, kk & 7);
         }
-        // start softmax(i): gaps 0-7 row max (4 elements of each block per gap), 8-9 the row statistics,
-        // 10-31 exps of keys 0-31 (32 elements over 22 gaps)
-        if (g < 8) {
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-            for (int e = 4 * g; e < 4 * g + 4; ++e)
-              mt[jj] = fmaxf(mt[jj], masked(sn[jj][e >> 4][e & 15], jj, e, i, mask));
-        } else if (g == 8) {
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj) mt[jj] = xhalf_max(mt[jj]) * c;
-        } else if (g == 9) {
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj) {
-            const bool need = mt[jj] > m[jj] + W64_DEFER;
-            const float mn = need ? fmaxf(m[jj], mt[jj]) : m[jj];
-            const float al = __builtin_amdgcn_exp2f(m[jj] - ((mn == -INFINITY) ? 0.f : mn));
-            alpha[jj] = al;
-            l[jj] *= al;
-            m[jj] = mn;
-            mref_n[jj] = (mn == -INFINITY) ? 0.f : mn;
-            need_any |= need;
-          }
-        } else {
-#pragma unroll
-          for (int e2 = 0; e2 < 32; ++e2)
-            if (10 + (e2 * 22) / 32 == g) exp_el(sn, pn, r, e2 >> 4, e2 & 15, i, mask, mref_n[e2 >> 4], ev);
+        // start softmax(i): block 0's keys 0-31 exponentiated in gaps 0-15; block 1's row maximum in gaps 0-7,
+        // its statistics in 8-9, its exponentials in 16-31 (consumers one gap behind)
+        if (g < 8) rowmax4(1, 4 * g);
+        if (g == 8) mt[1] = xhalf_max(mt[1]) * c;
+        if (g == 9) {
+          stats(1);
+          l[1] *= alpha[1];
         }
+        exp_p(sn, g >> 4, g & 15, i, mask, mref_n[g >> 4]);
+        if (g > 0) consume(pn, r, (g - 1) >> 4, (g - 1) & 15);
         W64_GAP();
       }
     }
+    consume(pn, r, 1, 15);
+    stamp(i, 5);
     rs[0] = r[0];
     rs[1] = r[1];
     resc = __builtin_amdgcn_ballot_w64(need_any) != 0;
@@ -1017,11 +1104,11 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     rescale();
 #pragma unroll
     for (int p = 0; p < NGT; ++p) dma_k(i + 2, p);
-    if (i < ntiles) {
+    if (W64_V3 || i < ntiles) {
 #pragma unroll
-      for (int p = 0; p < NGT; ++p) dma_v(i, p);
+      for (int p = 0; p < NGT; ++p) dma_v(i + W64_V3, p);
     }
-    if (has_next) dma_q(nqb_, nb_, nhq_);  // this wave's Q rows are read by nobody any more
+    if (has_next && W64_XB) dma_q(nqb_, nb_, nhq_);  // this wave's Q rows are read by nobody any more
     float r[2] = {rs[0], rs[1]}, ev[2][2];
 #pragma unroll
     for (int jo = 0; jo < 2; ++jo) {
@@ -1097,9 +1184,23 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
         nb_ = rfl(nb_);
         nhq_ = rfl(nhq_);
         nkvh_ = rfl(nkvh_);
+        kof_n = kv_of(nb_, nkvh_);
       }
     }
     // block start: Q, K(0), K(1) landed; X_0's first K / Q fragments
+    lane_offsets();
+    if (!W64_XB && n > 0) {
+      sync();  // every read of the Q rows and K slots of the last block is done
+      dma_q(qb, b, hq);
+#pragma unroll
+      for (int p = 0; p < NGT; ++p) dma_k(0, p);
+#pragma unroll
+      for (int p = 0; p < NGT; ++p) dma_k(1, p);
+      if (W64_V3) {
+#pragma unroll
+        for (int p = 0; p < NGT; ++p) dma_v(0, p);
+      }
+    }
     sync();
 #pragma unroll
     for (int st = 0; st < DSTEPS; ++st) {
@@ -1146,17 +1247,20 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
       sync();
 #pragma unroll
       for (int p = 0; p < NGT; ++p) dma_k(i + 2, p);
-      if (i < ntiles) {
+      if (W64_V3 || i < ntiles) {
 #pragma unroll
-        for (int p = 0; p < NGT; ++p) dma_v(i, p);
+        for (int p = 0; p < NGT; ++p) dma_v(i + W64_V3, p);
       }
     }
     if (!has_next) break;
+    stamp_blk = 0;
     kslot0 = rfl((kslot0 + ntiles) % 3);
+    vslot0 = rfl((vslot0 + ntiles) % 3);
     qb = nqb_;
     b = nb_;
     hq = nhq_;
     kvh = nkvh_;
+    kof_c = kof_n;
     q0 = qb * W64_BQ;
     wq0 = q0 + 64 * wave;
     ntiles = rfl(a.causal ? (q0 + W64_BQ) / BK : S / BK);
@@ -1194,6 +1298,11 @@ int& fwd_persistent() {
 
 // variant: 1 = W64 (persistent grid), 2 = W64 with one workgroup per block, 0 = the 32-row kernel everywhere,
 // negative = the build default
+#if W64_STAMPS
+extern "C" int ftc_w64_stamps(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(w64_stamps), sizeof(w64_stamps));
+}
+#endif
 extern "C" void ftc_flash_fwd_config(int variant) {
   if (variant < 0) variant = W64_DEFAULT;  // back to the build's default
   fwd_variant() = variant ? 1 : 0;
