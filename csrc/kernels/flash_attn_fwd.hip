@@ -499,11 +499,15 @@ constexpr int W64_BQ = 256;
 #ifndef W64_V3  // 1: a 3-slot V ring streamed one tile ahead (the whole 160 KiB of LDS); 0: 2 slots, same tile
 #define W64_V3 1
 #endif
+#ifndef W64_PIN
+#define W64_PIN 1
+#endif
 #ifndef W64_STAMPS  // lab only: s_memtime stamps of workgroup 0's first block, tiles 20-23 (ftc_w64_stamps)
 #define W64_STAMPS 0
 #endif
 #if W64_STAMPS
 __device__ unsigned long long w64_stamps[4][4][6];
+__device__ unsigned long long w64_bstamps[8][4][6];  // workgroup 0, blocks 0-7: per-block phase boundaries
 #endif
 #ifndef W64_DEFER
 #define W64_DEFER 8.0f
@@ -833,17 +837,17 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     const int slot = (kslot0 + t) % 3;
     const int nxt = (t >= ntiles) & has_next & W64_XB;  // integer selects (SALU), never a select of descriptors
     const int tt = t < ntiles ? t : (nxt ? t - ntiles : 0);
-    lds_dma16_at(make_rsrc(a.k + (nxt ? kof_n : kof_c)), rfl(kr0 + slot * TILE + p * RPG * D * 2), voff[p], tt * tstride);
+    lds_dma16_m0(make_rsrc(a.k + (nxt ? kof_n : kof_c)), rfl(kr0 + slot * TILE + p * RPG * D * 2), voff[p], tt * tstride);
   };
   // LDS-DMA of V stream tile t (W64_V3: as the K stream, one tile ahead of its use instead of two)
   auto dma_v = [&](const int t, const int p) __attribute__((always_inline)) {
     if (W64_V3) {
       const int nxt = (t >= ntiles) & has_next & W64_XB;
       const int tt = t < ntiles ? t : (nxt ? t - ntiles : 0);
-      lds_dma16_at(make_rsrc(a.v + (nxt ? kof_n : kof_c)), rfl(vr0 + ((vslot0 + t) % 3) * TILE + p * RPG * D * 2),
+      lds_dma16_m0(make_rsrc(a.v + (nxt ? kof_n : kof_c)), rfl(vr0 + ((vslot0 + t) % 3) * TILE + p * RPG * D * 2),
                    voff[p], tt * tstride);
     } else {
-      lds_dma16_at(make_rsrc(a.v + kof_c), rfl(vr0 + (t & 1) * TILE + p * RPG * D * 2), voff[p], t * tstride);
+      lds_dma16_m0(make_rsrc(a.v + kof_c), rfl(vr0 + (t & 1) * TILE + p * RPG * D * 2), voff[p], t * tstride);
     }
   };
   // this wave's 64 Q rows of block (qb', b', hq') -> Qs (swizzled row image).  The lane id is re-derived per
@@ -858,7 +862,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     for (int p = 0; p < 16; ++p) {
       const int row = p * RPG + ln / NCH, pc = ln % NCH;
       const int qo = (row * (int)a.q_rs + ((pc ^ swz(row)) & (NCH - 1)) * 8) * 2;
-      lds_dma16_at(qrs, rfl(qs0 + p * RPG * D * 2), qo, 0);
+      lds_dma16_m0(qrs, rfl(qs0 + p * RPG * D * 2), qo, 0);
     }
   };
   // prologue of the first block: Q, K(0), K(1)
@@ -921,6 +925,18 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     if (!W64_ABL_NOBAR) __builtin_amdgcn_s_barrier();  // ... everyone's; every read of a slot about to be refilled is done
   };
+  // a body's sync (W64_V3): the V pieces the last Y phase issued (its last NGT vector-memory operations, read
+  // only in the tile after next) stay in flight; everything older -- K(i+1), V(i) -- has landed
+  auto sync_body = [&]() __attribute__((always_inline)) {
+    if (W64_V3) {
+      static_assert(NGT == 4, "vmcnt(4) below counts the four V pieces of one Y phase");
+      __builtin_amdgcn_s_waitcnt(0x0F74);  // vmcnt(4)
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      if (!W64_ABL_NOBAR) __builtin_amdgcn_s_barrier();
+    } else {
+      sync();
+    }
+  };
   auto rescale = [&]() __attribute__((always_inline)) {
     if (resc) {
       w64_o_wait();  // the last PV MFMA's result is readable
@@ -964,11 +980,16 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     const int kt = e >> 4, i = e & 15;
     pr[i & 3] = W64_ABL_NOEXP ? sv[j][kt][i] : __builtin_amdgcn_exp2f(__builtin_fmaf(masked(sv[j][kt][i], j, e, t, mask), c, -mref));
   };
+  // W64_PIN: an empty volatile asm that takes a result as "+v" keeps its computation in the gap that
+  // produced it -- sched_barrier fences only the machine scheduler; without the pins the IR passes sank the
+  // row-sum adds to the end of Y and a whole phase's exponentials into the next tile's X
   auto consume = [&](uint4 (&pw)[2][4], float (&r)[2], const int j, const int e) __attribute__((always_inline)) {
     const int kt = e >> 4, i = e & 15;
     r[j] += pr[i & 3];
+    if (W64_PIN) asm volatile("" : "+v"(r[j]));
     if (i & 1) {
-      const uint32_t w = pack_bf2(pr[(i - 1) & 3], pr[i & 3]);
+      uint32_t w = pack_bf2(pr[(i - 1) & 3], pr[i & 3]);
+      if (W64_PIN) asm volatile("" : "+v"(w));
       const int f = 2 * kt + (i >> 3), dw = (i & 7) >> 1;
       if (dw == 0) pw[j][f].x = w; else if (dw == 1) pw[j][f].y = w; else if (dw == 2) pw[j][f].z = w; else pw[j][f].w = w;
     }
@@ -986,10 +1007,20 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     }
 #endif
   };
+  auto bstamp = [&](const int n, const int k) __attribute__((always_inline)) {
+#if W64_STAMPS
+    if (blockIdx.x == 0 && n < 8) {
+      W64_GAP();
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (lane == 0) w64_bstamps[n][wave][k] = t;
+      W64_GAP();
+    }
+#endif
+  };
   auto body = [&](const int i, f32x16 (&sn)[2][2], f32x16 (&so)[2][2], uint4 (&pn)[2][4], uint4 (&po)[2][4],
                   const bool first, const bool mask, const bool more) __attribute__((always_inline)) {
     stamp(i, 0);
-    sync();
+    sync_body();
     stamp(i, 1);
     rescale();
     stamp(i, 2);
@@ -1010,6 +1041,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     auto rowmax4 = [&](const int jj, const int e0) __attribute__((always_inline)) {
 #pragma unroll
       for (int e = e0; e < e0 + 4; ++e) mt[jj] = fmaxf(mt[jj], masked(sn[jj][e >> 4][e & 15], jj, e, i, mask));
+      if (W64_PIN) asm volatile("" : "+v"(mt[jj]));
     };
     // ---------------- X_i: S(i) block-major (block 0's chains complete at gap 15, so its row maximum and
     // statistics run in gaps 19-28 and Y_i can exponentiate from its first gap: one exponential per gap in
@@ -1022,16 +1054,17 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
       const int g = 4 * gq + gu;
       const int j = g >> 4, st = (g & 15) >> 1, kt = g & 1;
       w64_s_t(kt, st, j, sn[j][kt]);  // operands K(i), Q in owned accumulator registers
-      if (!first && (g & 1)) vf[g >> 2][(g >> 1) & 1] = rd_v(i - 1, g >> 2, (g >> 1) & 1);  // fragments 0-7
+      // V^T fragments 0-7, one read per gap in gaps 8-23 (after the DMA gaps, landed well before the seam)
+      if (!first && g >= 8 && g < 24) vf[(g - 8) >> 1][g & 1] = rd_v(i - 1, (g - 8) >> 1, g & 1);
       if (!first) {
         exp_p(so, g >> 4, 16 + (g & 15), i - 1, false, mref_o[g >> 4]);
         if (g > 0) consume(po, r, (g - 1) >> 4, 16 + ((g - 1) & 15));
       }
       if (W64_ABL_NODMA) {
-      } else if (g < NGT) {
-        dma_k(i + 2, g);
-      } else if (g < 2 * NGT) {
-        dma_v(i + W64_V3, g - NGT);
+      } else if (W64_V3 ? (g < 2 * NGT && !(g & 1)) : g < NGT) {
+        dma_k(i + 2, W64_V3 ? g >> 1 : g);
+      } else if (!W64_V3 && g < 2 * NGT) {
+        dma_v(i, g - NGT);
       }
       if (first && g == 19) {  // tile 0's gaps carry no fillers
         asm volatile("s_nop 7\n\ts_nop 3" ::: "memory");
@@ -1080,6 +1113,9 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
           const int fr = 8 + ((g - 2) >> 1), h = (g - 2) & 1;
           vf[fr & 7][h] = rd_v(i - 1, fr, h);
         }
+        // W64_V3: V(i+1) by LDS-DMA in the LDS-read-free gaps 22, 24, 26, 28 (its slot held V(i-2), whose last
+        // reads were Y_{i-1}'s); waited two syncs later (sync_body)
+        if (W64_V3 && !W64_ABL_NODMA && g >= 22 && g < 22 + 2 * NGT && !(g & 1)) dma_v(i + 1, (g - 22) >> 1);
         // start softmax(i): block 0's keys 0-31 exponentiated in gaps 0-15; block 1's row maximum in gaps 0-7,
         // its statistics in 8-9, its exponentials in 16-31 (consumers one gap behind)
         if (g < 8) rowmax4(1, 4 * g);
@@ -1188,6 +1224,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
       }
     }
     // block start: Q, K(0), K(1) landed; X_0's first K / Q fragments
+    bstamp(n, 0);
     lane_offsets();
     if (!W64_XB && n > 0) {
       sync();  // every read of the Q rows and K slots of the last block is done
@@ -1210,6 +1247,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
       ld_k(0, 1, st);
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // the asm loads above (the compiler does not count them)
+    bstamp(n, 1);
     body(0, sA, sB, pA, pB, true, a.causal && wtiles == 1, wtiles > 1);
     int i = 1;
     // steady iterations 1 .. wtiles - 2 in parity pairs; the state is back in (sA, pA) after each pair
@@ -1230,12 +1268,16 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     if (i < wtiles) {  // the wave's last tile: the diagonal under the causal mask
       body(i, sB, sA, pB, pA, false, a.causal != 0, false);
       ++i;
+      bstamp(n, 2);
       tail(i, sB, pB, a.causal != 0);
     } else {  // wtiles == 1
+      bstamp(n, 2);
       tail(i, sA, pA, a.causal != 0);
     }
+    bstamp(n, 3);
     // this wave's rows are done: store them now, under the other waves' remaining tiles
     epilogue();
+    bstamp(n, 4);
     w64_o_zero();
     m[0] = m[1] = -INFINITY;
     l[0] = l[1] = 0.f;
@@ -1252,6 +1294,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
         for (int p = 0; p < NGT; ++p) dma_v(i + W64_V3, p);
       }
     }
+    bstamp(n, 5);
     if (!has_next) break;
     stamp_blk = 0;
     kslot0 = rfl((kslot0 + ntiles) % 3);
@@ -1301,6 +1344,9 @@ int& fwd_persistent() {
 #if W64_STAMPS
 extern "C" int ftc_w64_stamps(unsigned long long* out) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(w64_stamps), sizeof(w64_stamps));
+}
+extern "C" int ftc_w64_bstamps(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(w64_bstamps), sizeof(w64_bstamps));
 }
 #endif
 extern "C" void ftc_flash_fwd_config(int variant) {

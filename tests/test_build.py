@@ -102,4 +102,4 @@ def test_w64_forward_owns_its_accumulators(tmp_path):
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
     assert "inside the owned range a[0:]: 0" in r.stdout and "0 write -> operand (RAW)" in r.stdout
-    assert "within 12 wait states: 0" in r.stdout
+    assert "within 12 wait states: 0" in r.stdout and "owns M0: 0" in r.stdout

@@ -126,6 +126,27 @@ def main(path: str, window: int = 3, owned: int = 128) -> int:
     for o in own[:10]:
         print("  " + o)
     bad += own
+    # M0: a function whose asm owns M0 (the "m0-owned" LDS-DMA pieces set it without saving it) must have no
+    # compiler instruction that reads or writes M0
+    m0bad, fn, owns, uses = [], None, False, []
+    for k, ln in enumerate(lines + ["_Zend:"]):
+        if re.match(r"^_Z\S*:", ln) or ln.startswith(".Lfunc_end"):
+            if owns and uses:
+                m0bad += [f"{fn}: {u}" for u in uses]
+            fn, owns, uses, inasm = ln, False, [], False
+            continue
+        if ln.startswith(";;#ASMSTART"):
+            inasm = True
+        elif ln.startswith(";;#ASMEND"):
+            inasm = False
+        elif inasm and "m0-owned" in ln:
+            owns = True
+        elif not inasm and ln and not ln.startswith((";", ".")) and re.search(r"\bm0\b", ln.split(";")[0]):
+            uses.append(f"line {k + 1}: {ln}")
+    print(f"compiler M0 uses in functions whose asm owns M0: {len(m0bad)}")
+    for o in m0bad[:10]:
+        print("  " + o)
+    bad += m0bad
     print(f"{n} asm MFMAs checked, {len(bad)} write -> operand (RAW) hazards ({len(war)} WAR reuses, informational)")
     for b in bad[:20]:
         print("  " + b)

@@ -34,6 +34,16 @@ def main():
         torch.cuda.synchronize()
         buf = (ctypes.c_ulonglong * 96)()
         assert L.ftc_w64_stamps(buf) == 0
+        bb = (ctypes.c_ulonglong * 192)()
+        L.ftc_w64_bstamps.argtypes = [ctypes.c_void_p]
+        assert L.ftc_w64_bstamps(bb) == 0
+        print(f"variant {var}: block wave | start-loads bodies tail epilogue idle | total (next block start - this)")
+        for n in range(8 if var == 1 else 1):
+            for w in range(4):
+                s = [bb[(n * 4 + w) * 6 + kk] for kk in range(6)]
+                d = [s[kk + 1] - s[kk] for kk in range(5)]
+                nxt = bb[((n + 1) * 4 + w) * 6] - s[0] if n < 7 and var == 1 else 0
+                print(f"  b{n} w{w} | " + " ".join(f"{x:8d}" for x in d) + f" | {s[5] - s[0]} ({nxt})")
         print(f"variant {var}: wave tile | sync rescale X seam Y | total")
         for w in range(4):
             for t in range(4):
