@@ -497,7 +497,10 @@ constexpr int W64_BQ = 256;
 #define W64_XB 1
 #endif
 #ifndef W64_V3  // 1: a 3-slot V ring streamed one tile ahead (the whole 160 KiB of LDS); 0: 2 slots, same tile
-#define W64_V3 1
+#define W64_V3 0
+#endif
+#ifndef W64_QEARLY
+#define W64_QEARLY 1
 #endif
 #ifndef W64_PIN
 #define W64_PIN 1
@@ -853,20 +856,21 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
   // this wave's 64 Q rows of block (qb', b', hq') -> Qs (swizzled row image).  The lane id is re-derived per
   // call by volatile asm: hoisted as loop-invariant, the sixteen lane offsets were spilled and every reload's
   // vmcnt(0) serialised the pieces behind the whole DMA stream (0.13 ms of the kernel at the 8B shape)
-  auto dma_q = [&](const int qbx, const int bx, const int hqx) __attribute__((always_inline)) {
+  // pieces [p0, p1) of the 16 (four rows each)
+  auto dma_q = [&](const int qbx, const int bx, const int hqx, const int p0, const int p1) __attribute__((always_inline)) {
     const uint16_t* qbase = a.q + ((long long)bx * S + qbx * W64_BQ + 64 * wave) * a.q_rs + (long long)hqx * D;
     const auto qrs = make_rsrc(qbase);
     int ln;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
 #pragma unroll
-    for (int p = 0; p < 16; ++p) {
+    for (int p = p0; p < p1; ++p) {
       const int row = p * RPG + ln / NCH, pc = ln % NCH;
       const int qo = (row * (int)a.q_rs + ((pc ^ swz(row)) & (NCH - 1)) * 8) * 2;
       lds_dma16_m0(qrs, rfl(qs0 + p * RPG * D * 2), qo, 0);
     }
   };
   // prologue of the first block: Q, K(0), K(1)
-  dma_q(qb, b, hq);
+  dma_q(qb, b, hq, 0, 16);
 #pragma unroll
   for (int p = 0; p < NGT; ++p) dma_k(0, p);
 #pragma unroll
@@ -1116,6 +1120,11 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
         // W64_V3: V(i+1) by LDS-DMA in the LDS-read-free gaps 22, 24, 26, 28 (its slot held V(i-2), whose last
         // reads were Y_{i-1}'s); waited two syncs later (sync_body)
         if (W64_V3 && !W64_ABL_NODMA && g >= 22 && g < 22 + 2 * NGT && !(g & 1)) dma_v(i + 1, (g - 22) >> 1);
+        // W64_QEARLY: the next block's Q by LDS-DMA in the first body's Y (no PV there; this wave's Q rows were
+        // read at block start; before the V pieces, so the counted body sync still leaves only V in flight) --
+        // off the last wave's critical tail
+        if (W64_QEARLY && W64_XB && !W64_ABL_NODMA && first && g >= 2 && g < 18 && has_next)
+          dma_q(nqb_, nb_, nhq_, g - 2, g - 1);
         // start softmax(i): block 0's keys 0-31 exponentiated in gaps 0-15; block 1's row maximum in gaps 0-7,
         // its statistics in 8-9, its exponentials in 16-31 (consumers one gap behind)
         if (g < 8) rowmax4(1, 4 * g);
@@ -1136,7 +1145,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     resc = __builtin_amdgcn_ballot_w64(need_any) != 0;
   };
   auto tail = [&](const int i, f32x16 (&so)[2][2], uint4 (&po)[2][4], const bool mask) __attribute__((always_inline)) {
-    sync();
+    sync_body();  // V(i) (the last Y's pieces) is read only in the next block or never
     rescale();
 #pragma unroll
     for (int p = 0; p < NGT; ++p) dma_k(i + 2, p);
@@ -1144,7 +1153,10 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
 #pragma unroll
       for (int p = 0; p < NGT; ++p) dma_v(i + W64_V3, p);
     }
-    if (has_next && W64_XB) dma_q(nqb_, nb_, nhq_);  // this wave's Q rows are read by nobody any more
+    // the next block's Q pieces its bodies 1-4 did not issue (this wave's Q rows were read at block start only)
+    if (has_next && W64_XB) {
+      if (!W64_QEARLY) dma_q(nqb_, nb_, nhq_, 0, 16);
+    }
     float r[2] = {rs[0], rs[1]}, ev[2][2];
 #pragma unroll
     for (int jo = 0; jo < 2; ++jo) {
@@ -1228,7 +1240,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     lane_offsets();
     if (!W64_XB && n > 0) {
       sync();  // every read of the Q rows and K slots of the last block is done
-      dma_q(qb, b, hq);
+      dma_q(qb, b, hq, 0, 16);
 #pragma unroll
       for (int p = 0; p < NGT; ++p) dma_k(0, p);
 #pragma unroll
