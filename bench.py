@@ -214,6 +214,7 @@ def _channel_sweep(info, mb: float, counts=(2, 4, 8, 16)) -> dict:
             opts = dist.ProcessGroupNCCL.Options()
             opts.config.min_ctas = c
             opts.config.max_ctas = c
+            opts._timeout = datetime.timedelta(seconds=DIAG_TIMEOUT_S)  # the same as the kwarg: no override warning
             g = dist.new_group(backend="nccl", pg_options=opts, timeout=datetime.timedelta(seconds=DIAG_TIMEOUT_S))
             out[str(c)] = _bucket_busbw(info, mb, iters=5, group=g)["busbw_GBps"]
             dist.destroy_process_group(g)
