@@ -47,7 +47,6 @@ int ftc_sumsq(const void* x, int is_fp32, long long n, float* partial, float* ou
 int ftc_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H, int KV, int D,
                   long long q_row_stride, long long kv_row_stride, long long o_row_stride, float scale, int causal,
                   int window, const int* doc_start, int kv_valid, hipStream_t stream);
-void ftc_flash_fwd_config(int variant);
 int ftc_flash_bwd_workspace(int B, int S, int H, int D, long long* bytes);
 long long ftc_decode_workspace_floats(int B, int H, int KV, int D, int max_len);
 int ftc_decode_attention(const void* q, void* kc, void* vc, const void* knew, const void* vnew, long long new_rs,
@@ -758,10 +757,6 @@ PYBIND11_MODULE(_C, m) {
         py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("step"),
         py::arg("gscale") = py::none(), py::arg("hp") = py::none());
   m.def("grad_sumsq", &grad_sumsq);
-  m.def("flash_fwd_config", [](int64_t variant) { ftc_flash_fwd_config((int)variant); }, py::arg("variant"),
-        "flash forward variant of later calls: 1 = W64 (one wave per SIMD, 64 rows per wave, persistent grid) where "
-        "it applies (head_dim 128, S % 256 == 0, no window / documents / padded tail), 2 = W64 with one workgroup "
-        "per block, 0 = the 32-row kernel everywhere, -1 = the build default");
   m.def("flash_fwd", &flash_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("B"), py::arg("S"), py::arg("H"),
         py::arg("KV"), py::arg("D"), py::arg("scale"), py::arg("causal"), py::arg("window"), py::arg("pad") = 0,
         py::arg("doc_start") = py::none(), py::arg("kv_valid") = -1);

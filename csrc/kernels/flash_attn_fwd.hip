@@ -448,30 +448,37 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
 
 // ==== W64: one wave per SIMD, 64 query rows per wave, software-pipelined across tiles (round 6) =========
 //
+// LAB ONLY (compiled when W64_LAB is 1: tools/w64_lab/build.sh, tests/test_build.py's audit; the package
+// build leaves it out -- it measured 0.5 % slower in the headline step than flash_fwd_kernel,
+// profiles/r6/w64/README.md).
+//
 // A workgroup = 4 waves = 256 query rows of one (batch, q head); wave w owns rows q0 + 64 w + [0, 64) as two
-// 32-row blocks j = 0, 1 (one wave per SIMD: the whole 512-register file).  Every K / V^T fragment read from
-// LDS feeds BOTH blocks' MFMAs (half the LDS bytes per FLOP of the 32-row kernel), and each wave runs its
-// softmax one phase behind its own matrix work, placed gap by gap between the MFMAs:
+// 32-row blocks j = 0, 1 (one wave per SIMD: the whole 512-register file).  Every K / V^T fragment feeds
+// BOTH blocks' MFMAs, and each wave runs its softmax one phase behind its own matrix work:
 //
-//   iteration i:  sync (vmcnt(0) + barrier) | O rescale if the last start asked for it (rare)
-//     X_i  32 MFMAs  S(i) = K(i) Q^T             || finish softmax(i-1): exp / row sum / bf16 pack of its
-//                                                   keys 32-63; K(i) / Q fragment reads one k-step ahead;
-//                                                   LDS-DMA of K(i+2), V(i); the first V(i-1)^T reads
-//     Y_i  32 MFMAs  O += V(i-1)^T P(i-1)^T      || start softmax(i): row max, deferred-rescale decision,
-//                                                   exp / pack of its keys 0-31; V^T reads two fragments
-//                                                   ahead; K(i+1) / Q fragments of X_{i+1}'s first k-step
+//   iteration i:  sync (vmcnt + barrier) | O rescale if the last start asked for it (rare)
+//     X_i  32 MFMAs  S(i) = K(i) Q^T (block-major)  || finish softmax(i-1) (keys 32-63, one exp per gap);
+//                                                    V(i-1)^T fragments 0-7; LDS-DMA of K(i+2) (and V);
+//                                                    block 0's row max / statistics of tile i
+//     seam           K(i+1) -> a[64:127] (16 asm ds_read_b128: also the S results' wait states)
+//     Y_i  32 MFMAs  O += V(i-1)^T P(i-1)^T         || start softmax(i): block 1's row max / statistics,
+//                                                    keys 0-31 of both blocks (one exp per gap);
+//                                                    V(i-1)^T fragments 8-15
 //
-// Registers: O (128) lives in accumulator registers for the whole block -- its MFMAs are inline asm on "+a"
-// operands, which the compiler never copies; S is produced in VGPRs (this file is built with
-// -mllvm -amdgpu-mfma-vgpr-form, `tools/build.py`), so the softmax reads it without v_accvgpr copies.  Q is
-// staged once per block in LDS (64 KiB) and re-read per k-step instead of pinning 64 registers.  Every gap
-// is fenced (sched_barrier): the placement below is the schedule.  K arrives two tiles ahead (3-slot ring),
-// V one (2 slots), by LDS-DMA issued as inline asm (no compiler drain before the reads of other slots);
-// one barrier per tile.  The rescale a row max asks for (the reference moves only when a max grew by more
-// than 2^8) is applied at the next iteration's seam.  Causal: a wave's last visible tile (the diagonal) is
-// the masked variant; waves whose rows end earlier keep joining the DMA and barriers.
+// Registers: the whole accumulator file is kernel-owned -- Q a[0:63] and K a[64:127] loaded by asm
+// ds_read_b128, O a[128:255] accumulated by asm MFMAs; S lands in VGPRs from asm MFMAs (this file is built
+// with -mllvm -amdgpu-mfma-vgpr-form, tools/build.py).  tools/check_asm_hazards.py audits every build: no
+// compiler instruction touches a[0:255] or M0, no VALU write feeds an asm MFMA operand unpadded, no
+// instruction reads an asm S result within 12 wait states.  Gaps are fenced by sched_barrier AND their VALU
+// results pinned by empty volatile asm (the IR passes otherwise move work across the fences).  Persistent
+// grid, heaviest causal blocks first, K / V / Q streamed across block seams; one barrier per tile; the
+// deferred rescale (a row max moves only when it grew by more than 2^8) is applied at the next seam.
 // Covers head_dim 128, no window / document mask / padded tail, S % 256 == 0; otherwise ftc_flash_fwd
 // runs flash_fwd_kernel.
+#ifndef W64_LAB
+#define W64_LAB 0
+#endif
+#if W64_LAB
 constexpr int W64_BQ = 256;
 // timing-only ablations for tools/w64_lab (wrong results; never set by tools/build.py): no barrier in the
 // per-tile sync, no LDS-DMA in the loop, no exponentials (P packed from raw S)
@@ -1324,6 +1331,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
   __builtin_amdgcn_s_waitcnt(0x0F70);  // no LDS-DMA may outlive the workgroup
 
 }
+#endif  // W64_LAB
 
 }  // namespace
 
@@ -1335,10 +1343,11 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
 // block fenced between the other block's MFMAs, asm-DMA 3-slot ring: 0.740 vs 0.554 ms at the Llama-3-8B
 // layer, profiles/r4/attn/fwd_qb6.log; git history has the kernel.)
 
-// forward variant of every later call (W64_DEFAULT: the measured winner, see the W64 header); tests and
-// tools/bench_fwd_variants.py switch it in one process (ftc_flash_fwd_config)
+#if W64_LAB
+// lab: the forward variant of every later call (W64_DEFAULT), switched in one process by the lab's
+// timing / numerics scripts (ftc_flash_fwd_config)
 #ifndef W64_DEFAULT
-#define W64_DEFAULT 0
+#define W64_DEFAULT 1
 #endif
 namespace {
 int& fwd_variant() {
@@ -1366,12 +1375,14 @@ extern "C" void ftc_flash_fwd_config(int variant) {
   fwd_variant() = variant ? 1 : 0;
   fwd_persistent() = variant == 2 ? 0 : 1;
 }
+#endif  // W64_LAB
 
 extern "C" int ftc_flash_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int S, int H,
                              int KV, int D, long long q_rs, long long kv_rs, long long o_rs, float scale, int causal,
                              int window, const int* doc_start, int kv_valid, hipStream_t stream) {
   if (S % BK != 0 || H % KV != 0 || (D != 128 && D != 64)) return -1;
   if (kv_valid <= 0 || kv_valid > S) kv_valid = S;
+#if W64_LAB
   if (fwd_variant() == 1 && D == 128 && S % W64_BQ == 0 && window <= 0 && doc_start == nullptr && kv_valid == S &&
       (o_rs & 7) == 0) {
     FwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, q_rs, kv_rs, o_rs,
@@ -1392,6 +1403,7 @@ extern "C" int ftc_flash_fwd(const void* q, const void* k, const void* v, void* 
     hipLaunchKernelGGL((flash_fwd_w64_kernel<128>), dim3(grid), dim3(256), 0, stream, a);
     return (int)hipGetLastError();
   }
+#endif
   constexpr int BQ = 32 * WAVES;
   FwdArgs a{(const uint16_t*)q, (const uint16_t*)k, (const uint16_t*)v, (uint16_t*)o, lse, q_rs, kv_rs, o_rs,
             B, S, H, KV, (S + BQ - 1) / BQ, scale * LOG2E, causal, window, doc_start, kv_valid};

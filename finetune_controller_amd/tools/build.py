@@ -62,10 +62,11 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError(f"build step failed ({r.returncode}):\n{' '.join(cmd)}\n{r.stdout}")
 
 
-# per-source compiler flags a kernel's design depends on (its header says why):
-#   flash_attn_fwd.hip -- the W64 forward keeps O in accumulator registers through inline-asm MFMAs and wants
-#   its S MFMAs in VGPR form (the softmax reads them with no v_accvgpr copies); no SLP packing of the
-#   softmax's f32 adds into v_pk_add_f32 (an anti-lever beside MFMAs: MI355X_MICROARCH.md cycle constants)
+# per-source compiler flags (the kernel's header says why):
+#   flash_attn_fwd.hip -- MFMAs in VGPR form (the softmax reads S with no v_accvgpr copies) and no SLP packing
+#   of the softmax's f32 adds into v_pk_add_f32 (an anti-lever beside MFMAs: MI355X_MICROARCH.md cycle
+#   constants); the shipped 32-row kernel was measured with them in round 6, and the lab W64 build
+#   (tools/w64_lab/build.sh, which depends on them) uses the same
 EXTRA_FLAGS = {"flash_attn_fwd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-slp-vectorize"]}
 
 

@@ -51,6 +51,9 @@ def test_extension_ships_only_the_winning_variants():
     for old in ("gemm_nt_v5_kernel", "gemm_nt_w4d_kernel", "gemm_nt_pb_kernel", "gemm_nt_pp_kernel",
                 "flash_fwd_pipe_kernel", "flash_fwd_qb2_kernel"):
         assert old not in syms, old
+    # round 6: the W64 forward lost in the headline step (profiles/r6/w64/) -- lab-only (W64_LAB, tools/w64_lab)
+    for lab in ("flash_fwd_w64_kernel", "ftc_flash_fwd_config", "w64_stamps"):
+        assert lab not in syms, lab
 
 
 def test_build_script_sets_no_diagnostic_define():
@@ -82,7 +85,8 @@ def test_run_patched_sets_module_constants_before_the_script(tmp_path):
 
 
 def test_w64_forward_owns_its_accumulators(tmp_path):
-    """The W64 flash forward keeps Q, K (a[0:127]) and O (a[128:255]) in accumulator registers that only
+    """(A lab kernel, compiled with W64_LAB as tools/w64_lab/build.sh does.)  The W64 flash forward keeps Q, K
+    (a[0:127]) and O (a[128:255]) in accumulator registers that only
     its inline asm touches (csrc/kernels/flash_attn_fwd.hip): compiled with the build's own flags, no
     compiler instruction may touch them, no VALU write may feed an asm MFMA operand unpadded and no
     instruction may read an asm S MFMA's VGPR result early (tools/check_asm_hazards.py)."""
@@ -97,7 +101,7 @@ def test_w64_forward_owns_its_accumulators(tmp_path):
     out = str(tmp_path / "fwd.s")
     subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-S", "--cuda-device-only",
                     "-I", os.path.join(ROOT, "csrc", "kernels"), "-ffp-contract=fast",
-                    *EXTRA_FLAGS["flash_attn_fwd.hip"], src, "-o", out], check=True, capture_output=True)
+                    *EXTRA_FLAGS["flash_attn_fwd.hip"], "-DW64_LAB=1", src, "-o", out], check=True, capture_output=True)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_asm_hazards.py"), out, "3", "0"],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout

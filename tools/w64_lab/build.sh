@@ -5,7 +5,7 @@
 set -e
 cd "$(dirname "$0")/../.."
 b() { n=$1; shift; hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Icsrc/kernels -ffp-contract=fast \
-      -mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize -DW64_DEFAULT=1 "$@" csrc/kernels/flash_attn_fwd.hip -o tools/w64_lab/lib$n.so; }
+      -mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize -DW64_LAB=1 "$@" csrc/kernels/flash_attn_fwd.hip -o tools/w64_lab/lib$n.so; }
 b base &
 b abl_nolds -DW64_ABL_NOLDS=1 &
 b abl_nolds_noexp -DW64_ABL_NOLDS=1 -DW64_ABL_NOEXP=1 &
