@@ -32,12 +32,11 @@ def main():
     ap.add_argument("--iters", type=int, default=6)
     ap.add_argument("--labels", default="gpurun_out/pmc_gemm_labels.json")
     ap.add_argument("--ours", action="store_true",
-                    help="also run the hand-written NT GEMM (csrc/kernels/gemm_nt.hip) on every shape, after the "
+                    help="also run the lab NT GEMM (tools/gemm_lab/gemm_nt.hip, libgemm_lab.so) on every shape, after the "
                          "library: its own kernel row in the counter table")
     a = ap.parse_args()
     C = None
     if a.ours:
-        from finetune_controller_amd.ops._backend import ext
         from tools.gemm_lab.lab import load
 
         C = load()
