@@ -506,6 +506,9 @@ constexpr int W64_BQ = 256;
 #ifndef W64_V3  // 1: a 3-slot V ring streamed one tile ahead (the whole 160 KiB of LDS); 0: 2 slots, same tile
 #define W64_V3 0
 #endif
+#ifndef W64_SEAM  // 1: the last wave carries its final tile into the next block's first body (no tail)
+#define W64_SEAM 1
+#endif
 #ifndef W64_QEARLY
 #define W64_QEARLY 1
 #endif
@@ -820,6 +823,11 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
   int ntiles = a.causal ? (q0 + W64_BQ) / BK : S / BK;
   int wtiles = a.causal ? (wq0 + 64) / BK : ntiles;
   int stamp_blk = 1;  // W64_STAMPS: the first block of the workgroup
+  // W64_SEAM: the previous block's last tile, carried into this block's first body
+  bool carry = false;
+  int tp_ = 0, wq0p_ = 0, bp_ = 0, hqp_ = 0;
+  float mp_[2] = {0.f, 0.f}, lp_[2] = {0.f, 0.f}, rsp_[2] = {0.f, 0.f};
+  static_assert(!(W64_SEAM && W64_V3), "the seam body reads the carried tile's V from slot (t & 1)");
   int vslot0 = 0;  // V ring slot of this block's tile 0 (W64_V3: the V stream runs on across blocks too)
   int kslot0 = 0;  // K ring slot of this block's tile 0: the K stream runs on across blocks
   // the next block (its K(0), K(1) and Q stream in under this block's last iterations)
@@ -962,18 +970,18 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
       resc = false;
     }
   };
-  auto masked = [&](const float x, const int j, const int e, const int t, const bool mask)
+  auto masked = [&](const float x, const int j, const int e, const int t, const bool mask, const int wq)
       __attribute__((always_inline)) -> float {
     if (!mask) return x;
     const int kt = e >> 4, i = e & 15;
     const int off = t * BK + kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;  // key of element (kt, i)
-    return off <= wq0 + 32 * j + lr ? x : -INFINITY;
+    return off <= wq + 32 * j + lr ? x : -INFINITY;  // wq: the first query row of the wave's block
   };
   // one exponential of element (kt, i) of block j into the packed P word; r = row-sum partial
   auto exp_el = [&](const f32x16 (&sv)[2][2], uint4 (&pw)[2][4], float (&r)[2], const int j, const int e,
                     const int t, const bool mask, const float mref, float (&ev)[2][2]) __attribute__((always_inline)) {
     const int kt = e >> 4, i = e & 15;
-    const float p = W64_ABL_NOEXP ? sv[j][kt][i] : __builtin_amdgcn_exp2f(__builtin_fmaf(masked(sv[j][kt][i], j, e, t, mask), c, -mref));
+    const float p = W64_ABL_NOEXP ? sv[j][kt][i] : __builtin_amdgcn_exp2f(__builtin_fmaf(masked(sv[j][kt][i], j, e, t, mask, wq0), c, -mref));
     r[j] += p;
     ev[j][i & 1] = p;
     if (i & 1) {
@@ -986,10 +994,10 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
   // the bf16 pack) in the next -- a VALU read right behind a v_exp_f32 costs a wait state (an s_nop per
   // element).  pr: the last four exponentials by i & 3 (at most two per gap, so four are live at most)
   float pr[4];
-  auto exp_p = [&](const f32x16 (&sv)[2][2], const int j, const int e, const int t, const bool mask, const float mref)
-      __attribute__((always_inline)) {
+  auto exp_p = [&](const f32x16 (&sv)[2][2], const int j, const int e, const int t, const bool mask, const float mref,
+                   const int wq) __attribute__((always_inline)) {
     const int kt = e >> 4, i = e & 15;
-    pr[i & 3] = W64_ABL_NOEXP ? sv[j][kt][i] : __builtin_amdgcn_exp2f(__builtin_fmaf(masked(sv[j][kt][i], j, e, t, mask), c, -mref));
+    pr[i & 3] = W64_ABL_NOEXP ? sv[j][kt][i] : __builtin_amdgcn_exp2f(__builtin_fmaf(masked(sv[j][kt][i], j, e, t, mask, wq), c, -mref));
   };
   // W64_PIN: an empty volatile asm that takes a result as "+v" keeps its computation in the gap that
   // produced it -- sched_barrier fences only the machine scheduler; without the pins the IR passes sank the
@@ -1028,16 +1036,22 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     }
 #endif
   };
+  // fin: the tile being finished and PV'd (not first): tile tp of the block whose first query row (this
+  // wave's) is wqp, under the causal diagonal mask maskp, with that block's row statistics mf / lf / rsf --
+  // the previous tile of this block (tp = i - 1, no mask, m / l / rs), or, in a seam body (W64_SEAM), the
+  // last tile of the previous block; q0b: the block's body 0 (issues the next block's Q)
   auto body = [&](const int i, f32x16 (&sn)[2][2], f32x16 (&so)[2][2], uint4 (&pn)[2][4], uint4 (&po)[2][4],
-                  const bool first, const bool mask, const bool more) __attribute__((always_inline)) {
+                  const bool first, const bool mask, const bool more, const int tp, const int wqp, const bool maskp,
+                  const float (&mf)[2], float (&lf)[2], const float (&rsf)[2], const bool q0b)
+      __attribute__((always_inline)) {
     stamp(i, 0);
     sync_body();
     stamp(i, 1);
     rescale();
     stamp(i, 2);
-    float mref_o[2], r[2] = {rs[0], rs[1]};
+    float mref_o[2], r[2] = {rsf[0], rsf[1]};
 #pragma unroll
-    for (int j = 0; j < 2; ++j) mref_o[j] = (m[j] == -INFINITY) ? 0.f : m[j];
+    for (int j = 0; j < 2; ++j) mref_o[j] = (mf[j] == -INFINITY) ? 0.f : mf[j];
     float mt[2] = {-INFINITY, -INFINITY}, mref_n[2] = {0.f, 0.f};
     bool need_any = false;
     // row statistics of block jj for tile i (l is rescaled where its tile i - 1 sum is complete)
@@ -1051,7 +1065,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     };
     auto rowmax4 = [&](const int jj, const int e0) __attribute__((always_inline)) {
 #pragma unroll
-      for (int e = e0; e < e0 + 4; ++e) mt[jj] = fmaxf(mt[jj], masked(sn[jj][e >> 4][e & 15], jj, e, i, mask));
+      for (int e = e0; e < e0 + 4; ++e) mt[jj] = fmaxf(mt[jj], masked(sn[jj][e >> 4][e & 15], jj, e, i, mask, wq0));
       if (W64_PIN) asm volatile("" : "+v"(mt[jj]));
     };
     // ---------------- X_i: S(i) block-major (block 0's chains complete at gap 15, so its row maximum and
@@ -1066,9 +1080,9 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
       const int j = g >> 4, st = (g & 15) >> 1, kt = g & 1;
       w64_s_t(kt, st, j, sn[j][kt]);  // operands K(i), Q in owned accumulator registers
       // V^T fragments 0-7, one read per gap in gaps 8-23 (after the DMA gaps, landed well before the seam)
-      if (!first && g >= 8 && g < 24) vf[(g - 8) >> 1][g & 1] = rd_v(i - 1, (g - 8) >> 1, g & 1);
+      if (!first && g >= 8 && g < 24) vf[(g - 8) >> 1][g & 1] = rd_v(tp, (g - 8) >> 1, g & 1);
       if (!first) {
-        exp_p(so, g >> 4, 16 + (g & 15), i - 1, false, mref_o[g >> 4]);
+        exp_p(so, g >> 4, 16 + (g & 15), tp, maskp, mref_o[g >> 4], wqp);
         if (g > 0) consume(po, r, (g - 1) >> 4, 16 + ((g - 1) & 15));
       }
       if (W64_ABL_NODMA) {
@@ -1088,8 +1102,8 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     }
     if (!first) {
       consume(po, r, 1, 31);
-      l[0] += r[0];
-      l[1] += r[1];
+      lf[0] += r[0];
+      lf[1] += r[1];
     }
     l[0] *= alpha[0];
     stamp(i, 3);
@@ -1122,7 +1136,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
         // after this gap's MFMA: fragment 8 + k into the slot fragment k freed (gaps 2-17)
         if (!first && g >= 2 && g < 18) {
           const int fr = 8 + ((g - 2) >> 1), h = (g - 2) & 1;
-          vf[fr & 7][h] = rd_v(i - 1, fr, h);
+          vf[fr & 7][h] = rd_v(tp, fr, h);
         }
         // W64_V3: V(i+1) by LDS-DMA in the LDS-read-free gaps 22, 24, 26, 28 (its slot held V(i-2), whose last
         // reads were Y_{i-1}'s); waited two syncs later (sync_body)
@@ -1130,7 +1144,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
         // W64_QEARLY: the next block's Q by LDS-DMA in the first body's Y (no PV there; this wave's Q rows were
         // read at block start; before the V pieces, so the counted body sync still leaves only V in flight) --
         // off the last wave's critical tail
-        if (W64_QEARLY && W64_XB && !W64_ABL_NODMA && first && g >= 2 && g < 18 && has_next)
+        if (W64_QEARLY && W64_XB && !W64_ABL_NODMA && q0b && g >= 2 && g < 18 && has_next)
           dma_q(nqb_, nb_, nhq_, g - 2, g - 1);
         // start softmax(i): block 0's keys 0-31 exponentiated in gaps 0-15; block 1's row maximum in gaps 0-7,
         // its statistics in 8-9, its exponentials in 16-31 (consumers one gap behind)
@@ -1140,7 +1154,7 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
           stats(1);
           l[1] *= alpha[1];
         }
-        exp_p(sn, g >> 4, g & 15, i, mask, mref_n[g >> 4]);
+        exp_p(sn, g >> 4, g & 15, i, mask, mref_n[g >> 4], wq0);
         if (g > 0) consume(pn, r, (g - 1) >> 4, (g - 1) & 15);
         W64_GAP();
       }
@@ -1197,14 +1211,16 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     }
   };
 
-  auto epilogue = [&]() __attribute__((always_inline)) {
+  // O / LSE of the wave's rows of block (bb, hqq) whose first row is wq, with its statistics mm / ll
+  auto epilogue = [&](const float (&mm)[2], const float (&ll)[2], const int wq, const int bb, const int hqq)
+      __attribute__((always_inline)) {
     w64_o_wait();  // the last PV MFMA's result is readable
   #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int qrow = wq0 + 32 * j + lr;
-      const float ltot = l[j] + __shfl_xor(l[j], 32, 64);
+      const int qrow = wq + 32 * j + lr;
+      const float ltot = ll[j] + __shfl_xor(ll[j], 32, 64);
       const float inv = ltot > 0.f ? 1.0f / ltot : 0.f;
-      uint16_t* op = a.o + ((long long)b * S + qrow) * a.o_rs + (long long)hq * D;
+      uint16_t* op = a.o + ((long long)bb * S + qrow) * a.o_rs + (long long)hqq * D;
   #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         const f32x16 ov = w64_o_read_t(4 * j + dt);
@@ -1223,8 +1239,8 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
         *reinterpret_cast<uint4*>(op + d + 8) = make_uint4(b0[0], b1[0], b0[1], b1[1]);
       }
       if (hh == 0) {
-        const float lse2 = (m[j] == -INFINITY) ? -INFINITY : m[j] + __log2f(ltot);
-        a.lse[((long long)b * a.H + hq) * S + qrow] = lse2 * LN2;
+        const float lse2 = (mm[j] == -INFINITY) ? -INFINITY : mm[j] + __log2f(ltot);
+        a.lse[((long long)bb * a.H + hqq) * S + qrow] = lse2 * LN2;
       }
     }
   };
@@ -1267,15 +1283,25 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // the asm loads above (the compiler does not count them)
     bstamp(n, 1);
-    body(0, sA, sB, pA, pB, true, a.causal && wtiles == 1, wtiles > 1);
+    if (carry) {
+      // seam body: S(0) of this block while the last tile of the previous block is finished and PV'd; that
+      // block's O is complete after it and stored here, before this block's first PV (body 1)
+      body(0, sA, sB, pA, pB, false, a.causal && wtiles == 1, wtiles > 1, tp_, wq0p_, a.causal != 0, mp_, lp_, rsp_,
+           true);
+      epilogue(mp_, lp_, wq0p_, bp_, hqp_);
+      w64_o_zero();
+      carry = false;
+    } else {
+      body(0, sA, sB, pA, pB, true, a.causal && wtiles == 1, wtiles > 1, -1, wq0, false, m, l, rs, true);
+    }
     int i = 1;
     // steady iterations 1 .. wtiles - 2 in parity pairs; the state is back in (sA, pA) after each pair
     for (; i + 2 < wtiles; i += 2) {
-      body(i, sB, sA, pB, pA, false, false, true);
-      body(i + 1, sA, sB, pA, pB, false, false, true);
+      body(i, sB, sA, pB, pA, false, false, true, i - 1, wq0, false, m, l, rs, false);
+      body(i + 1, sA, sB, pA, pB, false, false, true, i, wq0, false, m, l, rs, false);
     }
     if (i + 1 < wtiles) {  // one more steady iteration (odd i); then the state moves back to (sA, pA)
-      body(i, sB, sA, pB, pA, false, false, true);
+      body(i, sB, sA, pB, pA, false, false, true, i - 1, wq0, false, m, l, rs, false);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         sA[j][1] = sB[j][1];
@@ -1284,27 +1310,49 @@ __global__ __launch_bounds__(256, 1) void flash_fwd_w64_kernel(FwdArgs a) {
       }
       ++i;
     }
+    // W64_SEAM with a next block: the wave whose rows run to the block's last tile (every wave without the causal
+    // mask, the last one with it) hands that tile to the next block's first body instead of a tail here, and
+    // the block loses its step ntiles (its DMA -- the next block's K(2) -- is re-issued by that body anyway)
+    const bool seam_blk = W64_SEAM && has_next;
+    const bool carry_now = seam_blk && wtiles == ntiles;
     if (i < wtiles) {  // the wave's last tile: the diagonal under the causal mask
-      body(i, sB, sA, pB, pA, false, a.causal != 0, false);
+      body(i, sB, sA, pB, pA, false, a.causal != 0, false, i - 1, wq0, false, m, l, rs, false);
       ++i;
       bstamp(n, 2);
-      tail(i, sB, pB, a.causal != 0);
+      if (!carry_now) tail(i, sB, pB, a.causal != 0);
     } else {  // wtiles == 1
       bstamp(n, 2);
       tail(i, sA, pA, a.causal != 0);
     }
     bstamp(n, 3);
-    // this wave's rows are done: store them now, under the other waves' remaining tiles
-    epilogue();
+    if (carry_now) {
+      tp_ = wtiles - 1;
+      wq0p_ = wq0;
+      bp_ = b;
+      hqp_ = hq;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        mp_[j] = m[j];
+        lp_[j] = l[j];
+        rsp_[j] = rs[j];
+        m[j] = -INFINITY;  // alpha / resc stay: the seam body rescales the carried O first
+        l[j] = 0.f;
+        rs[j] = 0.f;
+      }
+      carry = true;
+    } else {
+      // this wave's rows are done: store them now, under the other waves' remaining tiles
+      epilogue(m, l, wq0, b, hq);
+      w64_o_zero();
+      m[0] = m[1] = -INFINITY;
+      l[0] = l[1] = 0.f;
+      rs[0] = rs[1] = 0.f;
+      alpha[0] = alpha[1] = 1.f;
+      resc = false;
+    }
     bstamp(n, 4);
-    w64_o_zero();
-    m[0] = m[1] = -INFINITY;
-    l[0] = l[1] = 0.f;
-    rs[0] = rs[1] = 0.f;
-    alpha[0] = alpha[1] = 1.f;
-    resc = false;
     // waves whose rows ended keep joining the workgroup's DMA / barriers
-    for (++i; i <= ntiles; ++i) {
+    for (++i; i <= ntiles - (seam_blk ? 1 : 0); ++i) {
       sync();
 #pragma unroll
       for (int p = 0; p < NGT; ++p) dma_k(i + 2, p);

@@ -12,5 +12,5 @@ b abl_nolds_noexp -DW64_ABL_NOLDS=1 -DW64_ABL_NOEXP=1 &
 b abl_all4 -DW64_ABL_NOLDS=1 -DW64_ABL_NOEXP=1 -DW64_ABL_NODMA=1 -DW64_ABL_NOBAR=1 &
 
 b stamps -DW64_STAMPS=1 &
-b v3ring -DW64_V3=1 &
+b v3ring -DW64_V3=1 -DW64_SEAM=0 &
 wait
