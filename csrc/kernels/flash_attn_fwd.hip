@@ -57,6 +57,9 @@ constexpr int BK = 64;   // keys per tile
 // packed-fp32 scale / row-sum in the online softmax (phase B1).  Measured slower (tools/pk_softmax_ab.sh,
 // profiles/r3/pk_softmax/: forward 0.605 / 0.615 vs 0.589 / 0.578 ms, headline 35,376 / 35,429 vs
 // 35,533 / 35,527 tok/s, one box) -> off
+#ifndef FWD_PIN
+#define FWD_PIN 0
+#endif
 #ifndef FWD_PK_SOFTMAX
 #define FWD_PK_SOFTMAX 0
 #endif
@@ -356,6 +359,7 @@ __global__ __launch_bounds__(64 * WAVES, 8 / WAVES) void flash_fwd_kernel(FwdArg
         const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kt][i], c, -mref));
         s[kt][i] = p;
         rs += p;
+        if (FWD_PIN) asm volatile("" : "+v"(rs));  // lab: keep the row sum in B1 (see W64_PIN)
       }
     l += rs;
 #endif

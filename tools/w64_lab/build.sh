@@ -13,4 +13,5 @@ b abl_all4 -DW64_ABL_NOLDS=1 -DW64_ABL_NOEXP=1 -DW64_ABL_NODMA=1 -DW64_ABL_NOBAR
 
 b stamps -DW64_STAMPS=1 &
 b v3ring -DW64_V3=1 -DW64_SEAM=0 &
+b w32pin -DFWD_PIN=1 &
 wait

@@ -25,7 +25,8 @@ def main():
     o = torch.empty(B * S, H * D, device="cuda", dtype=torch.bfloat16)
     lse = torch.empty(B, H, S, device="cuda", dtype=torch.float32)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    arms = [(n, 1) for n in libs] + [("base", 2), ("base", 0)]
+    arms = [(n, 1) for n in libs if n != "w32pin"] + [("base", 2), ("base", 0)] + \
+        ([("w32pin", 0)] if "w32pin" in libs else [])
     times = {f"{n}/{v}": [] for n, v in arms}
 
     def call(L):
