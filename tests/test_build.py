@@ -85,10 +85,10 @@ def test_run_patched_sets_module_constants_before_the_script(tmp_path):
 
 
 def test_w64_forward_owns_its_accumulators(tmp_path):
-    """(A lab kernel, compiled with W64_LAB as tools/w64_lab/build.sh does.)  The W64 flash forward keeps Q, K
-    (a[0:127]) and O (a[128:255]) in accumulator registers that only
-    its inline asm touches (tools/w64_lab/w64_fwd_kernel.inc via flash_attn_fwd.hip): compiled with the build's own flags, no
-    compiler instruction may touch them, no VALU write may feed an asm MFMA operand unpadded and no
+    """(A lab kernel, compiled with W64_LAB as tools/w64_lab/build.sh does.)  The W64 flash forward
+    (tools/w64_lab/w64_fwd_kernel.inc via flash_attn_fwd.hip) keeps Q, K (a[0:127]) and O (a[128:255]) in
+    accumulator registers that only its inline asm touches: compiled with the build's own flags, no
+    compiler instruction may touch them or M0, no VALU write may feed an asm MFMA operand unpadded and no
     instruction may read an asm S MFMA's VGPR result early (tools/check_asm_hazards.py)."""
     import shutil
 
